@@ -1,0 +1,314 @@
+#!/usr/bin/env python3
+"""Benchmark of the MI355X FedAvg aggregation engine (BASELINE.json metric).
+
+Metric: aggregated GB/s (device-resident) of the fused FedAvg update over K
+client model updates = algorithmic bytes / time, with algorithmic bytes
+(K+2)·P_f32·4 + (K+2)·P_i64·8.
+
+Workload (one "step" = one pass of the hot path over one batch):
+  BASELINE config C2 — 128 synthetic client updates of CIFAR ResNet-18
+  (11,183,562 fp32 + 20 int64 entries) aggregated into a new global model,
+  inputs resident in HBM.  With --gpus N (one process per GPU, launched by
+  torch.distributed.run) every rank owns one ResNet-18-sized parameter bucket
+  of 128 clients (parameter-bucket sharding): the bit-exact
+  design needs no data-path collective, so per-GPU work is fixed (weak).
+
+Reported next to it (rank 0, N=1): the roofline of the kernel (HIP events on
+the launch stream), and the reference's CPU op sequence (oracle port) timed on
+this host on the same inputs, whose result is also checked bit for bit.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+ROOT = os.path.dirname(os.path.abspath(__file__))
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--clients", type=int, default=128)
+    p.add_argument("--model", default="resnet18", choices=["resnet18", "resnet50", "lenet5", "vit"])
+    p.add_argument("--variant", type=int, default=None, help="kernel variant (tuning)")
+    p.add_argument("--sweep", action="store_true", help="time every kernel variant, interleaved")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-host-inclusive", action="store_true")
+    p.add_argument("--cpu-reps", type=int, default=3)
+    return p.parse_args()
+
+
+def model_spec(name):
+    from plato_amd import workloads
+
+    return {
+        "resnet18": lambda: workloads.resnet(18, 10),
+        "resnet50": lambda: workloads.resnet(50, 200),
+        "lenet5": lambda: workloads.lenet5(10),
+        "vit": lambda: workloads.vit_large(),
+    }[name]()
+
+
+def dist_setup(args):
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    return world, rank, local
+
+
+def barrier(world):
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def max_over_ranks(value: float, world: int) -> float:
+    if world == 1:
+        return value
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64, device="cuda")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def main():
+    args = parse()
+    world, rank, local = dist_setup(args)
+    dev = torch.device("cuda", local)
+
+    from plato_amd import _lib
+    from plato_amd.arena import ArenaLayout
+    from plato_amd.engine import ClientSlab, DeviceArena, FedAvgEngine
+    from plato_amd.synthetic import fill_baseline, fill_clients
+
+    spec = model_spec(args.model)
+    layout = ArenaLayout.from_shapes(spec)
+    k = args.clients
+    seed = args.seed + rank  # each rank owns a different bucket of the global model
+    engine = FedAvgEngine(dev, variant=args.variant)
+
+    base = DeviceArena(layout, dev)
+    slab = ClientSlab(layout, k, dev)
+    fill_baseline(base, seed)
+    fill_clients(slab, base, seed, k)
+    sys.path.insert(0, ROOT)
+    from oracle import synth  # noqa: E402  (num_samples recipe; weights are host data)
+
+    ns = synth.num_samples(k, seed)
+    total = sum(ns)
+    weights = [n / total for n in ns]
+    from plato_amd.engine import fp32_weights
+
+    w = torch.from_numpy(fp32_weights(weights)).to(dev)
+    pf, pi = slab.row_pointers(range(k))
+    tf = torch.from_numpy(pf).to(dev)
+    ti = torch.from_numpy(pi).to(dev)
+    out_f = torch.empty(layout.row_f32, dtype=torch.float32, device=dev)
+    out_i = torch.empty(layout.row_i64, dtype=torch.float32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    torch.cuda.synchronize(dev)
+
+    def step(variant=None):
+        engine.variant = args.variant if variant is None else variant
+        engine.launch_fedavg(layout, tf, ti, w, None, k, base.f32, base.i64, out_f, out_i, stream)
+
+    alg_bytes = layout.algorithmic_bytes(k)
+
+    if args.sweep:
+        nv = _lib.lib().plato_agg_tune_num_variants()
+        times = {v: [] for v in range(nv)}
+        for v in range(nv):
+            for _ in range(3):
+                step(v)
+        torch.cuda.synchronize(dev)
+        for _ in range(5):
+            for v in range(nv):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(args.steps):
+                    step(v)
+                e1.record(stream)
+                e1.synchronize()
+                times[v].append(e0.elapsed_time(e1) / args.steps)
+        if rank == 0:
+            import ctypes
+
+            for v in range(nv):
+                a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+                _lib.lib().plato_agg_tune_describe(v, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+                med = statistics.median(times[v])
+                print(json.dumps({"variant": v, "V": a.value, "U": b.value, "NT": c.value,
+                                  "ms_median": med, "ms_min": min(times[v]),
+                                  "GBps": alg_bytes / (med * 1e-3) / 1e9}), flush=True)
+        return
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize(dev)
+    barrier(world)
+    torch.cuda.synchronize(dev)
+    t1 = time.perf_counter()
+    wall = max_over_ranks(t1 - t0, world)
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps
+    kernel_ms_max = max_over_ranks(kernel_ms, world)
+
+    value_gbs = world * alg_bytes * args.steps / wall / 1e9
+    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
+
+    result = {
+        "metric": "aggregated GB/s (device-resident), K-client ResNet-18 FedAvg",
+        "value": round(value_gbs, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(wall / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (counter-based generator, SURVEY.md §8(d) C2 distributions)",
+        "config": {
+            "workload": f"C2: {k} x {args.model} client updates per GPU, fused FedAvg "
+                        "(deltas -> weighted sum -> update), parameter-bucket shard per rank",
+            "clients": k,
+            "params_f32": layout.n_f32,
+            "params_i64": layout.n_i64,
+            "algorithmic_bytes_per_step_per_gpu": alg_bytes,
+            "parallelism": f"bucket{world}",
+            "kernel_variant": args.variant if args.variant is not None else 0,
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel_ms": round(kernel_ms, 4),
+            "kernel_ms_max_over_ranks": round(kernel_ms_max, 4),
+        },
+    }
+
+    if rank == 0 and world == 1 and not args.no_host_inclusive:
+        result["host_inclusive"] = host_inclusive(engine, layout, base, slab, k, weights, dev)
+
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(layout, base, slab, k, ns, out_f, out_i, args.cpu_reps)
+        result["parity"] = result["cpu_baseline"].pop("parity")
+
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.destroy_process_group()
+
+
+def _host_state_dicts(layout, base, slab, k):
+    bf = base.f32[: layout.n_f32].cpu()
+    bi = base.i64[: layout.n_i64].cpu()
+    baseline = layout.unpack(bf, bi)
+    payloads = []
+    for c in range(k):
+        payloads.append(layout.unpack(slab.f32[c, : layout.n_f32].cpu(), slab.i64[c, : layout.n_i64].cpu()))
+    return baseline, payloads
+
+
+def host_inclusive(engine, layout, base, slab, k, weights, dev):
+    """CPU state_dicts in -> CPU state_dict out through the engine (pack, H2D, kernel, D2H)."""
+    baseline, payloads = _host_state_dicts(layout, base, slab, k)
+    times = []
+    for _ in range(3):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        engine.aggregate_weights(baseline, payloads, weights)
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times[1:])
+    return {"value": round(layout.algorithmic_bytes(k) / med / 1e9, 2), "unit": "GB/s",
+            "ms": round(med * 1e3, 2),
+            "note": "pack CPU state_dicts -> pinned -> H2D -> kernel -> D2H; median of 2 after 1 warm-up"}
+
+
+def cpu_baseline(layout, base, slab, k, ns, out_f, out_i, reps):
+    """Reference op sequence (oracle port) on the host, same inputs; bit-checks the GPU result."""
+    from oracle import fedavg_oracle as ref
+
+    baseline, payloads = _host_state_dicts(layout, base, slab, k)
+    threads = torch.get_num_threads()
+    times = []
+    upd = None
+    for r in range(reps + 1):
+        t0 = time.perf_counter()
+        upd = ref.fedavg_torch_ops(baseline, payloads, num_samples=ns)
+        dt = time.perf_counter() - t0
+        if r:
+            times.append(dt)
+    med = statistics.median(times)
+    gpu_f = out_f[: layout.n_f32].cpu()
+    gpu_i = out_i[: layout.n_i64].cpu()
+    exp_f = torch.cat([upd[e.name].reshape(-1) for e in layout.entries if e.region == "f32"])
+    exp_i = torch.cat([upd[e.name].reshape(-1) for e in layout.entries if e.region == "i64"]) \
+        if layout.n_i64 else torch.empty(0)
+    exact = bool(torch.equal(gpu_f.view(torch.int32), exp_f.view(torch.int32))
+                 and torch.equal(gpu_i.view(torch.int32), exp_i.view(torch.int32)))
+    return {
+        "value": round(layout.algorithmic_bytes(k) / med / 1e9, 3),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"full C2 job ({k} clients x {layout.n_f32 + layout.n_i64} params): torch CPU op "
+                  f"sequence sub->mul->add_->add of the reference, median of {reps} after 1 warm-up, "
+                  f"{threads} threads on {cpu_model()} (nproc {os.cpu_count()})",
+        "ms": round(med * 1e3, 1),
+        "parity": "bit-exact vs CPU reference op sequence" if exact else "MISMATCH vs CPU reference",
+    }
+
+
+if __name__ == "__main__":
+    main()

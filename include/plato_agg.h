@@ -1,0 +1,149 @@
+/*
+ * plato_agg.h — C ABI of the MI355X (gfx950) FedAvg aggregation engine.
+ *
+ * This is the drop-in boundary for Plato's server-side aggregation hot path.
+ * Every entry point takes plain device pointers, element counts and a HIP
+ * stream; nothing here allocates device memory, keeps a pointer after it
+ * returns, or synchronises the stream (so the calls can be captured in a
+ * hipGraph).  Host code (plato_amd/, ctypes) owns all buffers.
+ *
+ * Arithmetic contract (bit-exact with the reference CPU path):
+ *   for every element e, clients i = 0..K-1 in the order of `d_x`:
+ *     d   = x_i[e] - b[e]                  (fp32, RNE)       algorithms/fedavg.py:23
+ *     t   = d * w_i                        (fp32, RNE)       servers/fedavg.py:154
+ *     t   = t * s_i      (only if d_s)     (fp32, RNE)       pisces_server.py:94
+ *     acc = acc + t                        (fp32, RNE, acc starts at +0)
+ *   new[e] = b[e] + acc                    (fp32, RNE)       algorithms/fedavg.py:35
+ * No FMA contraction, no reordering of the K-sum.  int64 entries (BatchNorm
+ * num_batches_tracked) follow torch's promotion: d = x - b exactly in int64,
+ * converted to fp32 (RNE) before the multiply, new = fp32(b) + acc as fp32;
+ * load_state_dict's fp32 -> int64 truncation is plato_agg_cast_f32_i64.
+ *
+ * Errors: every call returns 0 on success or a negative PLATO_AGG_E* code;
+ * plato_agg_last_error() gives a thread-local message for the last failure.
+ * (The reference raises Python exceptions; plato_amd/_lib.py maps a non-zero
+ * return to RuntimeError/ValueError.)
+ *
+ * Reference interfaces replaced (TL-System/plato @ 2025-10-03):
+ *   plato_agg_fedavg_weights   <- Server._process_reports' deltas -> aggregate
+ *                                 -> update chain, i.e. what an
+ *                                 `aggregate_weights` hook must return
+ *                                 (plato/servers/fedavg.py:171-196,
+ *                                  plato/algorithms/fedavg.py:13-37)
+ *   plato_agg_fedavg_deltas    <- Server.aggregate_deltas
+ *                                 (plato/servers/fedavg.py:137-159)
+ *   plato_agg_compute_deltas   <- Algorithm.compute_weight_deltas
+ *                                 (plato/algorithms/fedavg.py:13-27)
+ *   plato_agg_update_weights   <- Algorithm.update_weights
+ *                                 (plato/algorithms/fedavg.py:29-37)
+ *   plato_agg_cast_f32_i64     <- Algorithm.load_weights' load_state_dict
+ *                                 fp32 -> int64 copy (plato/algorithms/fedavg.py:46-48)
+ *   plato_agg_mix_weights      <- FedAsync Algorithm.aggregate_weights
+ *                                 (examples/async/fedasync/fedasync_algorithm.py:9-20)
+ */
+#ifndef PLATO_AGG_H
+#define PLATO_AGG_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PLATO_AGG_ABI_VERSION 1
+
+#define PLATO_AGG_OK 0
+#define PLATO_AGG_EINVAL (-1)   /* bad argument (null, misaligned, K <= 0) */
+#define PLATO_AGG_EHIP (-2)     /* HIP runtime error (launch / copy)      */
+
+/* ABI version of the loaded library (== PLATO_AGG_ABI_VERSION). */
+int plato_agg_abi_version(void);
+
+/* Thread-local description of the last failure on this thread ("" if none). */
+const char* plato_agg_last_error(void);
+
+/*
+ * Fused FedAvg over K client weight arenas (a3 -> a4 -> a6 in one pass).
+ *   d_x_f32  device array of K pointers, each to n_f32 fp32 client weights
+ *            (16-byte aligned); summation order = array order.
+ *   d_x_i64  device array of K pointers to n_i64 int64 client entries, or
+ *            NULL when n_i64 == 0.
+ *   d_w      device array of K fp32 weights (fp32(n_i / N) for FedAvg).
+ *   d_s      device array of K fp32 second scalars, or NULL.
+ *   d_base_* the global model (baseline) entries.
+ *   d_out_f32   n_f32 fp32 new weights (may alias d_base_f32).
+ *   d_out_i64f  n_i64 fp32 new values of the int64 entries (the reference's
+ *               update_weights yields fp32 for them; cast with
+ *               plato_agg_cast_f32_i64 to get what load_state_dict stores).
+ */
+int plato_agg_fedavg_weights(const float* const* d_x_f32,
+                             const int64_t* const* d_x_i64,
+                             const float* d_w, const float* d_s, int K,
+                             const float* d_base_f32, const int64_t* d_base_i64,
+                             float* d_out_f32, float* d_out_i64f,
+                             size_t n_f32, size_t n_i64, hipStream_t stream);
+
+/*
+ * Weighted sum of K client delta arenas (Server.aggregate_deltas):
+ *   avg[e] = sum_i fp32(d_i[e]) * w_i  (sequential, fp32), avg is fp32 for
+ * every entry, including the int64 ones (trainers/basic.py:59-63).
+ */
+int plato_agg_fedavg_deltas(const float* const* d_d_f32,
+                            const int64_t* const* d_d_i64,
+                            const float* d_w, const float* d_s, int K,
+                            float* d_avg_f32, float* d_avg_i64f,
+                            size_t n_f32, size_t n_i64, hipStream_t stream);
+
+/* One client's deltas: out = x - base (fp32), and exact int64 x - base. */
+int plato_agg_compute_deltas(const float* d_x_f32, const int64_t* d_x_i64,
+                             const float* d_base_f32, const int64_t* d_base_i64,
+                             float* d_out_f32, int64_t* d_out_i64,
+                             size_t n_f32, size_t n_i64, hipStream_t stream);
+
+/* update_weights: out = base + avg (fp32; int64 base converted to fp32). */
+int plato_agg_update_weights(const float* d_base_f32, const int64_t* d_base_i64,
+                             const float* d_avg_f32, const float* d_avg_i64f,
+                             float* d_out_f32, float* d_out_i64f,
+                             size_t n_f32, size_t n_i64, hipStream_t stream);
+
+/*
+ * load_state_dict's fp32 -> int64 copy: truncation toward zero; NaN and
+ * values outside [-2^63, 2^63) give INT64_MIN (the x86-64 conversion result
+ * the reference CPU path produces).
+ */
+int plato_agg_cast_f32_i64(const float* d_src, int64_t* d_dst, size_t n,
+                           hipStream_t stream);
+
+/*
+ * FedAsync mixing: out = fp32(b * fp32(1 - m)) + fp32(x * fp32(m)), computed
+ * as the reference does with two fp32 scalars one_minus_m and m.
+ */
+int plato_agg_mix_weights(const float* d_x_f32, const int64_t* d_x_i64,
+                          const float* d_base_f32, const int64_t* d_base_i64,
+                          float one_minus_m, float m,
+                          float* d_out_f32, float* d_out_i64f,
+                          size_t n_f32, size_t n_i64, hipStream_t stream);
+
+/*
+ * Deterministic synthetic payloads for tests and benchmarks (a counter-based
+ * generator restated bit for bit by oracle/synth.py):
+ *   h = splitmix64(splitmix64(seed ^ (stream * 0xD1B54A32D192ED03)) + e)
+ *   r = (int32)(h >> 40) - 2^23
+ *   out[e] = (d_add ? d_add[e] : +0) + (float)r * 2^scale_log2   (fp32 add)
+ */
+int plato_agg_fill_synth_f32(float* d_out, const float* d_add, size_t n,
+                             uint64_t seed, uint64_t stream_id, int scale_log2,
+                             hipStream_t stream);
+
+/*   out[e] = (d_add ? d_add[e] : 0) + (int64)(h % modulus)   (modulus >= 1) */
+int plato_agg_fill_synth_i64(int64_t* d_out, const int64_t* d_add, size_t n,
+                             uint64_t seed, uint64_t stream_id, uint64_t modulus,
+                             hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PLATO_AGG_H */

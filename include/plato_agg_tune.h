@@ -1,0 +1,39 @@
+/*
+ * plato_agg_tune.h — benchmarking / tuning entry points of libplato_agg.so.
+ *
+ * Not part of the drop-in boundary (no reference interface behind them):
+ * bench.py and the tuning sweep use them to time the kernel variants
+ * (V float4 per lane, U clients unrolled, non-temporal loads) that the
+ * public entry points choose between.  Same argument conventions and
+ * arithmetic contract as plato_agg_fedavg_weights / _deltas in plato_agg.h.
+ */
+#ifndef PLATO_AGG_TUNE_H
+#define PLATO_AGG_TUNE_H
+
+#include <stddef.h>
+#include <stdint.h>
+#include <hip/hip_runtime_api.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int plato_agg_tune_num_variants(void);
+
+/* Writes the variant's V (float4 per lane), U (clients unrolled), NT flag. */
+int plato_agg_tune_describe(int variant, int* v, int* u, int* nt);
+
+/* has_base != 0: plato_agg_fedavg_weights; == 0: plato_agg_fedavg_deltas. */
+int plato_agg_tune_fedavg(int variant, int has_base,
+                          const float* const* d_x_f32,
+                          const int64_t* const* d_x_i64,
+                          const float* d_w, const float* d_s, int K,
+                          const float* d_base_f32, const int64_t* d_base_i64,
+                          float* d_out_f32, float* d_out_i64f,
+                          size_t n_f32, size_t n_i64, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* PLATO_AGG_TUNE_H */

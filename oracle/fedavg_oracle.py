@@ -1,0 +1,179 @@
+"""TEST INFRASTRUCTURE ONLY — the CPU oracle for the FedAvg aggregation path.
+
+Never imported by the product path (plato_amd/); only tests/, the smoke test
+in __graft_entry__.py and bench.py's ``cpu_baseline`` leg use it, as the
+checker.  Two restatements of the reference's arithmetic:
+
+1. ``fedavg_numpy`` — sequential fp32 numpy over flat arenas, one explicit
+   rounding per op (numpy ufuncs never contract to FMA):
+
+       acc = +0 ; for i in self.updates order:
+           d   = fp32(x_i - b)                  plato/algorithms/fedavg.py:23
+           t   = fp32(d * fp32(n_i / N))        plato/servers/fedavg.py:154
+           acc = fp32(acc + t)                  plato/servers/fedavg.py:154 (+=)
+       new = fp32(b + acc)                      plato/algorithms/fedavg.py:35
+       int64 keys: d = int64(x - b) -> fp32 ; new = fp32(fp32(b) + acc) ;
+       load_state_dict truncates toward zero    plato/algorithms/fedavg.py:48
+
+2. ``fedavg_torch_ops`` — the reference's own torch op sequence on CPU
+   tensors, tensor by tensor (sub -> mul(Python float) -> add_ -> add ->
+   load_state_dict copy), i.e. plato/algorithms/fedavg.py:13-48 and
+   plato/servers/fedavg.py:137-159 restated without the server object.  This
+   is the "port" CPU baseline bench.py times on the GPU box.
+
+Parity pin: tests/golden/*.json were produced by the reference itself
+(tests/golden/make_golden.py imports /root/reference and runs its
+Server.aggregate_deltas / Algorithm chain); tests/test_oracle.py checks both
+restatements against them bit for bit.
+"""
+
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Mapping, Sequence
+
+import numpy as np
+
+
+# --------------------------------------------------------------------------
+# weights
+# --------------------------------------------------------------------------
+def fedavg_weights(num_samples: Sequence[int]) -> list[float]:
+    """n_i / N in Python double (servers/fedavg.py:140,154)."""
+    total = sum(num_samples)
+    return [n / total for n in num_samples]
+
+
+def fedbuff_weights(k: int) -> list[float]:
+    """examples/async/fedbuff/fedbuff_server.py:33,45: 1 / len(updates)."""
+    return [1 / k] * k
+
+
+def port_staleness_factor(staleness: int, bound: float = 10) -> float:
+    """examples/async/port/port_server.py:135-144."""
+    return bound / (staleness + bound)
+
+
+def port_weights(num_samples: Sequence[int], staleness: Sequence[int], similarity=None,
+                 similarity_weight: float = 1, staleness_weight: float = 1,
+                 staleness_bound: float = 10) -> list[float]:
+    """examples/async/port/port_server.py:57-103 with Python-float similarities."""
+    total = sum(num_samples)
+    raw = []
+    for i, n in enumerate(num_samples):
+        sim = 1.0 if similarity is None else similarity[i]
+        factor = port_staleness_factor(staleness[i], staleness_bound)
+        raw.append(n / total * ((sim + 1) / 2 * similarity_weight + factor * staleness_weight))
+    return [r / sum(raw) for r in raw]
+
+
+def fp32(values) -> np.ndarray:
+    return np.asarray([np.float32(float(v)) for v in values], dtype=np.float32)
+
+
+# --------------------------------------------------------------------------
+# 1. numpy restatement over flat arenas
+# --------------------------------------------------------------------------
+def fedavg_numpy(base_f32: np.ndarray, base_i64: np.ndarray, clients_f32, clients_i64,
+                 weights: Sequence[float], scales: Sequence[float] | None = None):
+    """Fused FedAvg (deltas -> weighted sum -> update) on flat arenas.
+
+    Returns (new_f32, new_i64_as_f32); the int64 entries' results are fp32
+    exactly as the reference's update_weights returns them.
+    """
+    w = fp32(weights)
+    s = None if scales is None else fp32(scales)
+    acc = np.zeros(base_f32.shape, dtype=np.float32)
+    acc_i = np.zeros(base_i64.shape, dtype=np.float32)
+    for i in range(len(w)):
+        d = np.subtract(clients_f32[i], base_f32, dtype=np.float32)
+        t = np.multiply(d, w[i], dtype=np.float32)
+        if s is not None:
+            t = np.multiply(t, s[i], dtype=np.float32)
+        acc = np.add(acc, t, dtype=np.float32)
+        if base_i64.size:
+            with np.errstate(over="ignore"):
+                di = (clients_i64[i].astype(np.int64) - base_i64.astype(np.int64)).astype(np.float32)
+            ti = np.multiply(di, w[i], dtype=np.float32)
+            if s is not None:
+                ti = np.multiply(ti, s[i], dtype=np.float32)
+            acc_i = np.add(acc_i, ti, dtype=np.float32)
+    new_f = np.add(base_f32, acc, dtype=np.float32)
+    new_i = np.add(base_i64.astype(np.float32), acc_i, dtype=np.float32)
+    return new_f, new_i
+
+
+def deltas_numpy(deltas_f32, deltas_i64, weights, scales=None):
+    """Server.aggregate_deltas on flat arenas (servers/fedavg.py:143-157)."""
+    w = fp32(weights)
+    s = None if scales is None else fp32(scales)
+    acc = np.zeros(deltas_f32[0].shape, dtype=np.float32)
+    acc_i = np.zeros(np.asarray(deltas_i64[0]).shape, dtype=np.float32)
+    for i in range(len(w)):
+        t = np.multiply(deltas_f32[i], w[i], dtype=np.float32)
+        ti = np.multiply(np.asarray(deltas_i64[i]).astype(np.float32), w[i], dtype=np.float32)
+        if s is not None:
+            t = np.multiply(t, s[i], dtype=np.float32)
+            ti = np.multiply(ti, s[i], dtype=np.float32)
+        acc = np.add(acc, t, dtype=np.float32)
+        acc_i = np.add(acc_i, ti, dtype=np.float32)
+    return acc, acc_i
+
+
+def mix_numpy(base_f32, base_i64, x_f32, x_i64, mixing: float):
+    """FedAsync (fedasync_algorithm.py:15-18): b * fp32(1-m) + x * fp32(m)."""
+    om = np.float32(1 - mixing)
+    m = np.float32(mixing)
+    out = np.add(np.multiply(base_f32, om, dtype=np.float32), np.multiply(x_f32, m, dtype=np.float32),
+                 dtype=np.float32)
+    out_i = np.add(np.multiply(base_i64.astype(np.float32), om, dtype=np.float32),
+                   np.multiply(np.asarray(x_i64).astype(np.float32), m, dtype=np.float32),
+                   dtype=np.float32)
+    return out, out_i
+
+
+def trunc_to_int64(values_f32: np.ndarray) -> np.ndarray:
+    """load_state_dict fp32 -> int64 copy: truncation toward zero (x86: NaN/overflow -> INT64_MIN)."""
+    v = np.asarray(values_f32, dtype=np.float32)
+    out = np.full(v.shape, np.iinfo(np.int64).min, dtype=np.int64)
+    ok = (v >= np.float32(-(2.0**63))) & (v < np.float32(2.0**63))
+    out[ok] = np.trunc(v[ok]).astype(np.int64)
+    return out
+
+
+# --------------------------------------------------------------------------
+# 2. the reference's torch op sequence (CPU), per tensor
+# --------------------------------------------------------------------------
+def fedavg_torch_ops(baseline: Mapping, weights_received: Sequence[Mapping], num_samples=None,
+                     weights: Sequence[float] | None = None) -> "OrderedDict":
+    """compute_weight_deltas -> aggregate_deltas -> update_weights, as torch ops.
+
+    Mirrors plato/algorithms/fedavg.py:13-37 and plato/servers/fedavg.py:137-159
+    line by line (without the asyncio yields and the Server object).  Returns
+    the updated-weights dict (fp32 for every key, like update_weights).
+    """
+    import torch
+
+    deltas = []
+    for weight in weights_received:
+        delta = OrderedDict()
+        for name, current in weight.items():
+            delta[name] = current - baseline[name]
+        deltas.append(delta)
+    if weights is None:
+        total = sum(num_samples)
+        weights = [n / total for n in num_samples]
+    avg = {name: torch.zeros(d.shape) for name, d in deltas[0].items()}
+    for i, update in enumerate(deltas):
+        for name, delta in update.items():
+            avg[name] += delta * weights[i]
+    updated = OrderedDict()
+    for name, weight in baseline.items():
+        updated[name] = weight + avg[name]
+    return updated
+
+
+def load_into(model_state: Mapping, updated: Mapping) -> None:
+    """load_state_dict's per-key copy_ (fp32 -> int64 truncation included)."""
+    for name, dst in model_state.items():
+        dst.copy_(updated[name])

@@ -1,0 +1,124 @@
+"""ctypes binding of ``libplato_agg.so`` (the C ABI in ``include/plato_agg.h``).
+
+The library is the only compute path of this package: there is no CPU or
+PyTorch fallback.  If the shared object is missing or fails to load,
+:func:`lib` raises ``RuntimeError`` with the build command to run.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libplato_agg.so")
+ABI_VERSION = 1
+
+PLATO_AGG_OK = 0
+PLATO_AGG_EINVAL = -1
+PLATO_AGG_EHIP = -2
+
+_c_void_p = ctypes.c_void_p
+_c_size_t = ctypes.c_size_t
+_c_int = ctypes.c_int
+_c_float = ctypes.c_float
+_c_u64 = ctypes.c_uint64
+
+# name -> (restype, argtypes); must match include/plato_agg.h and
+# include/plato_agg_tune.h exactly (tests/test_abi.py checks the export list).
+SIGNATURES = {
+    "plato_agg_abi_version": (_c_int, []),
+    "plato_agg_last_error": (ctypes.c_char_p, []),
+    "plato_agg_fedavg_weights": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
+         _c_void_p, _c_void_p, _c_size_t, _c_size_t, _c_void_p],
+    ),
+    "plato_agg_fedavg_deltas": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
+         _c_size_t, _c_size_t, _c_void_p],
+    ),
+    "plato_agg_compute_deltas": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+         _c_size_t, _c_size_t, _c_void_p],
+    ),
+    "plato_agg_update_weights": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+         _c_size_t, _c_size_t, _c_void_p],
+    ),
+    "plato_agg_cast_f32_i64": (_c_int, [_c_void_p, _c_void_p, _c_size_t, _c_void_p]),
+    "plato_agg_mix_weights": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_float, _c_float,
+         _c_void_p, _c_void_p, _c_size_t, _c_size_t, _c_void_p],
+    ),
+    "plato_agg_fill_synth_f32": (
+        _c_int, [_c_void_p, _c_void_p, _c_size_t, _c_u64, _c_u64, _c_int, _c_void_p]
+    ),
+    "plato_agg_fill_synth_i64": (
+        _c_int, [_c_void_p, _c_void_p, _c_size_t, _c_u64, _c_u64, _c_u64, _c_void_p]
+    ),
+    # tuning / benchmarking (include/plato_agg_tune.h)
+    "plato_agg_tune_num_variants": (_c_int, []),
+    "plato_agg_tune_describe": (
+        _c_int,
+        [_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)],
+    ),
+    "plato_agg_tune_fedavg": (
+        _c_int,
+        [_c_int, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p,
+         _c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_size_t, _c_void_p],
+    ),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the engine library; raise if it is unavailable."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"plato_amd: HIP extension {LIB_PATH} is not built; run "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (or `make -C plato_amd`)"
+            )
+        try:
+            handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        except OSError as exc:  # pragma: no cover - depends on the host
+            raise RuntimeError(f"plato_amd: cannot load {LIB_PATH}: {exc}") from exc
+        for name, (restype, argtypes) in SIGNATURES.items():
+            fn = getattr(handle, name)
+            fn.restype = restype
+            fn.argtypes = argtypes
+        version = handle.plato_agg_abi_version()
+        if version != ABI_VERSION:
+            raise RuntimeError(
+                f"plato_amd: {LIB_PATH} has ABI {version}, expected {ABI_VERSION}; rebuild it"
+            )
+        _lib = handle
+        return _lib
+
+
+def check(status: int, what: str) -> None:
+    """Map a C-ABI status code to the Python exception the reference would raise."""
+    if status == PLATO_AGG_OK:
+        return
+    msg = lib().plato_agg_last_error().decode(errors="replace")
+    if status == PLATO_AGG_EINVAL:
+        raise ValueError(f"{what}: {msg}")
+    raise RuntimeError(f"{what}: {msg} (status {status})")
+
+
+def call(name: str, *args) -> None:
+    """Call a C-ABI entry point and raise on a non-zero status."""
+    check(getattr(lib(), name)(*args), name)

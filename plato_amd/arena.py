@@ -1,0 +1,152 @@
+"""Flat-arena layout of a Plato ``state_dict``.
+
+The reference aggregates tensor by tensor (122 tensors for ResNet-18, median
+256 elements: ``plato/servers/fedavg.py:152-154``).  On the GPU one launch per
+tensor would be launch-bound, so the engine packs a ``state_dict`` into two
+flat device regions and runs one kernel over the whole model:
+
+* an fp32 region holding every ``torch.float32`` entry back to back in
+  ``state_dict`` order, and
+* an int64 region holding every ``torch.int64`` entry (BatchNorm
+  ``num_batches_tracked`` counters).
+
+The key -> (region, offset, shape) map is built from the baseline's key order
+(``algorithms/fedavg.py:34``).  Client payloads must carry the same keys,
+dtypes and shapes (the reference would fail on a mismatch too:
+``algorithms/fedavg.py:20`` indexes the baseline by the client's key).
+"""
+
+from __future__ import annotations
+
+from collections import OrderedDict
+from dataclasses import dataclass
+from typing import Mapping
+
+import torch
+
+F32 = "f32"
+I64 = "i64"
+
+# Arena rows are padded to a multiple of 64 fp32 (256 B) so that every client
+# row of a [K, row] slab starts 256-byte aligned (dwordx4-friendly).
+ROW_ALIGN = 64
+
+
+@dataclass(frozen=True)
+class Entry:
+    name: str
+    region: str  # F32 or I64
+    offset: int  # element offset inside its region
+    numel: int
+    shape: tuple
+
+
+class ArenaLayout:
+    """Key -> region offsets for one model's ``state_dict``."""
+
+    def __init__(self, entries: list[Entry], n_f32: int, n_i64: int):
+        self.entries = entries
+        self.n_f32 = n_f32
+        self.n_i64 = n_i64
+        self.row_f32 = _round_up(max(n_f32, 1), ROW_ALIGN)
+        self.row_i64 = max(n_i64, 1)
+        self._by_name = {e.name: e for e in entries}
+        self.signature = tuple((e.name, e.region, e.shape) for e in entries)
+
+    # ------------------------------------------------------------------ build
+    @classmethod
+    def from_state_dict(cls, state_dict: Mapping[str, torch.Tensor]) -> "ArenaLayout":
+        entries = []
+        n_f32 = 0
+        n_i64 = 0
+        for name, tensor in state_dict.items():
+            if not isinstance(tensor, torch.Tensor):
+                raise TypeError(f"state_dict entry {name!r} is not a tensor")
+            numel = tensor.numel()
+            shape = tuple(tensor.shape)
+            if tensor.dtype == torch.float32:
+                entries.append(Entry(name, F32, n_f32, numel, shape))
+                n_f32 += numel
+            elif tensor.dtype == torch.int64:
+                entries.append(Entry(name, I64, n_i64, numel, shape))
+                n_i64 += numel
+            else:
+                raise TypeError(
+                    f"state_dict entry {name!r} has dtype {tensor.dtype}; the aggregation "
+                    "engine handles torch.float32 and torch.int64 entries"
+                )
+        return cls(entries, n_f32, n_i64)
+
+    @classmethod
+    def from_shapes(cls, spec) -> "ArenaLayout":
+        """Build from ``[(name, shape, 'f32'|'i64'), ...]`` (synthetic workloads)."""
+        entries = []
+        n = {F32: 0, I64: 0}
+        for name, shape, region in spec:
+            numel = 1
+            for dim in shape:
+                numel *= int(dim)
+            entries.append(Entry(name, region, n[region], numel, tuple(shape)))
+            n[region] += numel
+        return cls(entries, n[F32], n[I64])
+
+    # ---------------------------------------------------------------- queries
+    def __len__(self) -> int:
+        return len(self.entries)
+
+    def __getitem__(self, name: str) -> Entry:
+        return self._by_name[name]
+
+    def keys(self):
+        return [e.name for e in self.entries]
+
+    def algorithmic_bytes(self, k: int) -> int:
+        """HBM bytes of one fused FedAvg launch: read K clients + baseline, write result.
+
+        SURVEY.md §8(d): (K+2)·P_f32·4 + (K+2)·P_i64·8.
+        """
+        return (k + 2) * (self.n_f32 * 4 + self.n_i64 * 8)
+
+    def check_compatible(self, state_dict: Mapping[str, torch.Tensor], what: str) -> None:
+        if len(state_dict) != len(self.entries):
+            raise KeyError(
+                f"{what} has {len(state_dict)} entries, the baseline has {len(self.entries)}"
+            )
+        for entry in self.entries:
+            if entry.name not in state_dict:
+                raise KeyError(f"{what} is missing {entry.name!r}")
+            tensor = state_dict[entry.name]
+            want = torch.float32 if entry.region == F32 else torch.int64
+            if tensor.dtype != want or tuple(tensor.shape) != entry.shape:
+                raise ValueError(
+                    f"{what}[{entry.name!r}] is {tensor.dtype}{tuple(tensor.shape)}, "
+                    f"expected {want}{entry.shape}"
+                )
+
+    # ---------------------------------------------------------- pack / unpack
+    def pack(self, state_dict: Mapping[str, torch.Tensor], out_f32: torch.Tensor,
+             out_i64: torch.Tensor | None) -> None:
+        """Copy ``state_dict`` into flat (host or device) buffers ``out_f32``/``out_i64``."""
+        f32 = [state_dict[e.name].reshape(-1) for e in self.entries if e.region == F32]
+        i64 = [state_dict[e.name].reshape(-1) for e in self.entries if e.region == I64]
+        if f32:
+            torch.cat(f32, out=out_f32[: self.n_f32])
+        if i64:
+            torch.cat(i64, out=out_i64[: self.n_i64])
+
+    def unpack(self, flat_f32: torch.Tensor, flat_i64: torch.Tensor | None
+               ) -> "OrderedDict[str, torch.Tensor]":
+        """Views of flat buffers as an ``OrderedDict`` in baseline key order.
+
+        ``flat_i64`` holds the int64 entries' values in whatever dtype the
+        caller produced (fp32 results of update_weights, or int64 weights).
+        """
+        out = OrderedDict()
+        for e in self.entries:
+            src = flat_f32 if e.region == F32 else flat_i64
+            out[e.name] = src[e.offset : e.offset + e.numel].view(e.shape)
+        return out
+
+
+def _round_up(x: int, m: int) -> int:
+    return (x + m - 1) // m * m

@@ -1,0 +1,564 @@
+// fedavg_agg.hip — gfx950 (MI355X / CDNA4) kernels for Plato's server-side
+// FedAvg aggregation, exported through the C ABI in include/plato_agg.h.
+//
+// Design:
+//  * The hot op is an HBM-bound streaming reduction: every output element reads
+//    the same element of K client arenas plus the baseline and writes one value
+//    ((K+2)*4 bytes per fp32 element, 3K flops: ~0.75 flop/B).  No MFMA, no LDS
+//    reuse to exploit; the kernel is built to keep enough 16-byte loads in
+//    flight to saturate HBM3E.
+//  * Bit-exactness with the reference CPU path forbids splitting the K-sum
+//    across lanes/waves/GPUs: each lane owns whole elements (f4 groups) and
+//    walks the clients in order, with separately rounded sub/mul/add (the
+//    library is compiled with -ffp-contract=off; no fmaf anywhere).
+//  * Memory-level parallelism therefore comes from (a) V f4 per lane per
+//    client and (b) U clients unrolled, i.e. U*V independent dwordx4 loads per
+//    lane before the first dependent add.  Client pointers and weights are
+//    wave-uniform -> scalar (s_load) reads from the device pointer table.
+//  * The fp32 arena tail (n % 4) and the int64 entries are tiny: they run on a
+//    few extra workgroups at the end of the same grid, so one launch does the
+//    whole model.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <string>
+
+#include "plato_agg.h"
+#include "plato_agg_tune.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int check_launch(const char* what) {
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) {
+    return fail(PLATO_AGG_EHIP, std::string(what) + ": " + hipGetErrorString(err));
+  }
+  g_last_error.clear();
+  return PLATO_AGG_OK;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+// ---------------------------------------------------------------------------
+// Loads
+// ---------------------------------------------------------------------------
+// Native 4 x fp32 vector: one dwordx4 load/store; element-wise IEEE ops.
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// Client arenas are plain hipMalloc'd global memory: load through an
+// address_space(1) pointer so hipcc emits global_load_dwordx4 (vmcnt only)
+// instead of flat loads (which also tick lgkmcnt and force vmcnt(0)+lgkmcnt(0)
+// waits next to the scalar loads).
+typedef __attribute__((address_space(1))) const f4 gf4;
+typedef __attribute__((address_space(1))) const float gfloat;
+
+template <bool NT>
+__device__ __forceinline__ f4 ld4(const f4* p) {
+  gf4* g = (gf4*)p;
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(g);
+  } else {
+    return *g;
+  }
+}
+
+// Wave-uniform base + 32-bit per-lane byte offset: lets hipcc use the
+// global_load saddr form (base in SGPRs, one offset VGPR per stream).
+template <bool NT>
+__device__ __forceinline__ f4 ld4_off(const float* base, uint32_t byte_off) {
+  gf4* g = (gf4*)((__attribute__((address_space(1))) const char*)base + byte_off);
+  if constexpr (NT) {
+    return __builtin_nontemporal_load(g);
+  } else {
+    return *g;
+  }
+}
+
+// The pointer table and the weights are wave-uniform and read-only for the
+// whole launch: read them through the constant address space -> s_load
+// (scalar cache), so no VGPRs and no vector-memory round trip per client.
+template <class T>
+__device__ __forceinline__ T sld(const T* p, int i) {
+  return ((__attribute__((address_space(4))) const T*)p)[i];
+}
+
+__device__ __forceinline__ f4 f4_sub(f4 a, f4 b) { return a - b; }
+__device__ __forceinline__ f4 f4_add(f4 a, f4 b) { return a + b; }
+__device__ __forceinline__ f4 f4_scale(f4 a, float s) { return a * s; }
+__device__ __forceinline__ f4 f4_zero() { return f4{0.f, 0.f, 0.f, 0.f}; }
+
+// ---------------------------------------------------------------------------
+// Main kernel: fp32 arena body (f4 groups) + scalar work items
+// (fp32 tail and int64 entries) on extra workgroups at the end of the grid.
+// HAS_BASE: weights mode (subtract the baseline, add it back at the end);
+//           otherwise deltas mode (x are deltas, out = sum).
+// ---------------------------------------------------------------------------
+struct AggArgs {
+  const float* const* xf;      // K pointers to fp32 arenas
+  const int64_t* const* xi;    // K pointers to int64 arenas (may be null)
+  const float* w;              // K fp32 weights
+  const float* s;              // K fp32 second scalars (TWO only)
+  const float* base_f;         // baseline fp32 (HAS_BASE only)
+  const int64_t* base_i;       // baseline int64 (HAS_BASE only)
+  float* out_f;
+  float* out_if;               // fp32 results of the int64 entries
+  uint64_t n4;                 // number of f4 groups in the fp32 arena
+  uint64_t n_f32;              // fp32 elements (tail = n_f32 - 4*n4)
+  uint64_t n_i64;
+  uint32_t nb_vec;             // workgroups of the f4 body
+  uint32_t nb_vec_full;        // of which fully in range (no bounds checks)
+  int K;
+};
+
+template <int V, int U, bool HAS_BASE, bool TWO, bool NT, bool CHECK>
+__device__ __forceinline__ void vec_body(const AggArgs& a, uint32_t blk) {
+  constexpr uint64_t kChunk = uint64_t(kBlock) * V;
+  const uint64_t first = uint64_t(blk) * kChunk + threadIdx.x;
+
+  // Element groups this lane owns, as 32-bit byte offsets (host guarantees an
+  // fp32 arena < 4 GiB per launch).  In the (single) partial workgroup the
+  // out-of-range lanes load a clamped in-range address (no per-load branch:
+  // a predicated load makes hipcc branch around every load and drain vmcnt)
+  // and skip only the store.
+  uint32_t off[V];
+  bool live[V];
+  f4 b[V];
+  f4 acc[V];
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    const uint64_t e = first + uint64_t(v) * kBlock;
+    live[v] = !CHECK || e < a.n4;
+    off[v] = uint32_t((CHECK ? (e < a.n4 ? e : a.n4 - 1) : e) * 16u);
+    acc[v] = f4_zero();
+    if constexpr (HAS_BASE) b[v] = ld4_off<false>(a.base_f, off[v]);
+  }
+
+  const int K = a.K;
+  int i = 0;
+  // Client pointers for the next batch are fetched (s_load) one batch ahead
+  // so the vector loads of a batch issue without waiting on the scalar cache.
+  const float* pn[U];
+  if (U <= K) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) pn[u] = sld(a.xf, u);
+  }
+  for (; i + U <= K; i += U) {
+    f4 x[U][V];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int v = 0; v < V; ++v) x[u][v] = ld4_off<NT>(pn[u], off[v]);
+    }
+    if (i + 2 * U <= K) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) pn[u] = sld(a.xf, i + U + u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float wu = sld(a.w, i + u);
+      float su = 1.f;
+      if constexpr (TWO) su = sld(a.s, i + u);
+#pragma unroll
+      for (int v = 0; v < V; ++v) {
+        f4 d = HAS_BASE ? f4_sub(x[u][v], b[v]) : x[u][v];
+        f4 t = f4_scale(d, wu);
+        if constexpr (TWO) t = f4_scale(t, su);
+        acc[v] = f4_add(acc[v], t);
+      }
+    }
+  }
+  for (; i < K; ++i) {
+    const float* p = sld(a.xf, i);
+    const float wu = sld(a.w, i);
+    float su = 1.f;
+    if constexpr (TWO) su = sld(a.s, i);
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+      f4 x = ld4_off<NT>(p, off[v]);
+      f4 d = HAS_BASE ? f4_sub(x, b[v]) : x;
+      f4 t = f4_scale(d, wu);
+      if constexpr (TWO) t = f4_scale(t, su);
+      acc[v] = f4_add(acc[v], t);
+    }
+  }
+
+  float* out = a.out_f;
+#pragma unroll
+  for (int v = 0; v < V; ++v) {
+    if (live[v]) {
+      *(__attribute__((address_space(1))) f4*)((__attribute__((address_space(1))) char*)out + off[v]) =
+          HAS_BASE ? f4_add(b[v], acc[v]) : acc[v];
+    }
+  }
+}
+
+// One scalar work item: the fp32 tail element or an int64 entry.
+template <bool HAS_BASE, bool TWO>
+__device__ __forceinline__ void scalar_item(const AggArgs& a, uint64_t j) {
+  const uint64_t tail = a.n_f32 - 4 * a.n4;
+  const int K = a.K;
+  if (j < tail) {
+    const uint64_t e = 4 * a.n4 + j;
+    const float b = HAS_BASE ? a.base_f[e] : 0.f;
+    float acc = 0.f;
+    for (int i = 0; i < K; ++i) {
+      const float x = a.xf[i][e];
+      const float d = HAS_BASE ? x - b : x;
+      float t = d * a.w[i];
+      if constexpr (TWO) t = t * a.s[i];
+      acc = acc + t;
+    }
+    a.out_f[e] = HAS_BASE ? b + acc : acc;
+    return;
+  }
+  const uint64_t e = j - tail;
+  if (e >= a.n_i64) return;
+  const int64_t b = HAS_BASE ? a.base_i[e] : 0;
+  float acc = 0.f;
+  for (int i = 0; i < K; ++i) {
+    const int64_t x = a.xi[i][e];
+    // int64 subtraction wraps like torch's; the promotion to fp32 happens at
+    // the scalar multiply (servers/fedavg.py:154, int tensor * Python float).
+    const int64_t d = HAS_BASE ? (int64_t)((uint64_t)x - (uint64_t)b) : x;
+    float t = (float)d * a.w[i];
+    if constexpr (TWO) t = t * a.s[i];
+    acc = acc + t;
+  }
+  // update_weights: int64 weight + fp32 delta -> fp32 (float(b) + acc).
+  a.out_if[e] = HAS_BASE ? (float)b + acc : acc;
+}
+
+template <int V, int U, bool HAS_BASE, bool TWO, bool NT>
+__global__ __launch_bounds__(kBlock) void fedavg_kernel(AggArgs a) {
+  const uint32_t blk = blockIdx.x;
+  if (blk < a.nb_vec_full) {
+    vec_body<V, U, HAS_BASE, TWO, NT, false>(a, blk);
+  } else if (blk < a.nb_vec) {
+    vec_body<V, U, HAS_BASE, TWO, NT, true>(a, blk);
+  } else {
+    const uint64_t j = uint64_t(blk - a.nb_vec) * kBlock + threadIdx.x;
+    scalar_item<HAS_BASE, TWO>(a, j);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Variant table (tuning knobs: V f4 per lane, U clients unrolled, NT loads)
+// ---------------------------------------------------------------------------
+using LaunchFn = void (*)(const AggArgs&, dim3, hipStream_t);
+
+template <int V, int U, bool HAS_BASE, bool TWO, bool NT>
+void launch_one(const AggArgs& a, dim3 grid, hipStream_t st) {
+  hipLaunchKernelGGL((fedavg_kernel<V, U, HAS_BASE, TWO, NT>), grid, dim3(kBlock), 0, st, a);
+}
+
+struct Variant {
+  int V, U;
+  bool NT;
+  LaunchFn fn[2][2];  // [HAS_BASE][TWO]
+};
+
+template <int V, int U, bool NT>
+constexpr Variant make_variant() {
+  return Variant{V, U, NT,
+                 {{&launch_one<V, U, false, false, NT>, &launch_one<V, U, false, true, NT>},
+                  {&launch_one<V, U, true, false, NT>, &launch_one<V, U, true, true, NT>}}};
+}
+
+// Variant 0 is the default (chosen from the measurements in DESIGN.md §5).
+const Variant kVariants[] = {
+    make_variant<2, 8, false>(),  // 0 (default)
+    make_variant<1, 8, false>(),  // 1
+    make_variant<2, 4, false>(),  // 2
+    make_variant<4, 4, false>(),  // 3
+    make_variant<2, 8, true>(),   // 4
+    make_variant<1, 16, false>(), // 5
+    make_variant<4, 8, false>(),  // 6
+    make_variant<1, 8, true>(),   // 7
+};
+constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
+
+int run_agg(int variant, bool has_base, const float* const* xf, const int64_t* const* xi,
+            const float* w, const float* s, int K, const float* base_f, const int64_t* base_i,
+            float* out_f, float* out_if, size_t n_f32, size_t n_i64, hipStream_t st) {
+  if (variant < 0 || variant >= kNumVariants) return fail(PLATO_AGG_EINVAL, "bad variant");
+  if (K <= 0) return fail(PLATO_AGG_EINVAL, "K must be >= 1");
+  if (!w) return fail(PLATO_AGG_EINVAL, "null weight array");
+  if (n_f32 && (!xf || !out_f)) return fail(PLATO_AGG_EINVAL, "null fp32 arena pointer");
+  if (n_i64 && (!xi || !out_if)) return fail(PLATO_AGG_EINVAL, "null int64 arena pointer");
+  if (has_base && n_f32 && !base_f) return fail(PLATO_AGG_EINVAL, "null fp32 baseline");
+  if (has_base && n_i64 && !base_i) return fail(PLATO_AGG_EINVAL, "null int64 baseline");
+  if (n_f32 && (!aligned16(out_f) || (has_base && !aligned16(base_f))))
+    return fail(PLATO_AGG_EINVAL, "fp32 baseline/output must be 16-byte aligned");
+  if (n_f32 == 0 && n_i64 == 0) {
+    g_last_error.clear();
+    return PLATO_AGG_OK;
+  }
+  const Variant& vr = kVariants[variant];
+  AggArgs a{};
+  a.xf = xf;
+  a.xi = xi;
+  a.w = w;
+  a.s = s;
+  a.base_f = base_f;
+  a.base_i = base_i;
+  a.out_f = out_f;
+  a.out_if = out_if;
+  a.n4 = n_f32 / 4;
+  a.n_f32 = n_f32;
+  a.n_i64 = n_i64;
+  a.K = K;
+  const uint64_t chunk = uint64_t(kBlock) * vr.V;
+  const uint64_t nb_vec = (a.n4 + chunk - 1) / chunk;
+  const uint64_t n_scalar = (n_f32 - 4 * a.n4) + n_i64;
+  const uint64_t nb_scalar = (n_scalar + kBlock - 1) / kBlock;
+  if (nb_vec + nb_scalar > 0x7fffffffull || a.n4 * 16ull > 0xffffffffull)
+    return fail(PLATO_AGG_EINVAL, "fp32 arena must be < 4 GiB per launch (split it into buckets)");
+  a.nb_vec = uint32_t(nb_vec);
+  a.nb_vec_full = uint32_t(a.n4 / chunk);
+  dim3 grid(uint32_t(nb_vec + nb_scalar));
+  vr.fn[has_base ? 1 : 0][s ? 1 : 0](a, grid, st);
+  return check_launch("fedavg kernel launch");
+}
+
+// ---------------------------------------------------------------------------
+// Elementwise helpers (off the hot path; grid-stride, f4 where possible)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t gtid() { return uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; }
+__device__ __forceinline__ uint64_t gstride() { return uint64_t(gridDim.x) * blockDim.x; }
+
+dim3 grid_for(uint64_t work) {
+  uint64_t b = (work + kBlock - 1) / kBlock;
+  if (b < 1) b = 1;
+  if (b > 8192) b = 8192;  // grid-stride the rest (32 waves/CU x 256 CUs)
+  return dim3(uint32_t(b));
+}
+
+__global__ __launch_bounds__(kBlock) void deltas_kernel(const float* __restrict__ x, const int64_t* __restrict__ xi,
+                                                        const float* __restrict__ b, const int64_t* __restrict__ bi,
+                                                        float* __restrict__ o, int64_t* __restrict__ oi,
+                                                        uint64_t n_f32, uint64_t n_i64) {
+  const uint64_t n4 = n_f32 / 4;
+  for (uint64_t k = gtid(); k < n4; k += gstride()) {
+    reinterpret_cast<f4*>(o)[k] =
+        f4_sub(reinterpret_cast<const f4*>(x)[k], reinterpret_cast<const f4*>(b)[k]);
+  }
+  const uint64_t tail = n_f32 - 4 * n4;
+  for (uint64_t k = gtid(); k < tail + n_i64; k += gstride()) {
+    if (k < tail) {
+      o[4 * n4 + k] = x[4 * n4 + k] - b[4 * n4 + k];
+    } else {
+      const uint64_t e = k - tail;
+      oi[e] = (int64_t)((uint64_t)xi[e] - (uint64_t)bi[e]);
+    }
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void update_kernel(const float* b, const int64_t* __restrict__ bi,
+                                                        const float* avg, const float* __restrict__ avgi,
+                                                        float* o, float* __restrict__ oi, uint64_t n_f32,
+                                                        uint64_t n_i64) {
+  const uint64_t n4 = n_f32 / 4;
+  for (uint64_t k = gtid(); k < n4; k += gstride()) {
+    reinterpret_cast<f4*>(o)[k] =
+        f4_add(reinterpret_cast<const f4*>(b)[k], reinterpret_cast<const f4*>(avg)[k]);
+  }
+  const uint64_t tail = n_f32 - 4 * n4;
+  for (uint64_t k = gtid(); k < tail + n_i64; k += gstride()) {
+    if (k < tail) {
+      o[4 * n4 + k] = b[4 * n4 + k] + avg[4 * n4 + k];
+    } else {
+      const uint64_t e = k - tail;
+      oi[e] = (float)bi[e] + avgi[e];
+    }
+  }
+}
+
+__device__ __forceinline__ int64_t trunc_f32_i64(float f) {
+  // x86-64 cvttss2si semantics: NaN / out of range -> INT64_MIN.
+  if (!(f >= -9223372036854775808.0f && f < 9223372036854775808.0f)) return INT64_MIN;
+  return (int64_t)f;
+}
+
+__global__ __launch_bounds__(kBlock) void cast_kernel(const float* __restrict__ s, int64_t* __restrict__ d,
+                                                      uint64_t n) {
+  for (uint64_t k = gtid(); k < n; k += gstride()) d[k] = trunc_f32_i64(s[k]);
+}
+
+__global__ __launch_bounds__(kBlock) void mix_kernel(const float* __restrict__ x, const int64_t* __restrict__ xi,
+                                                     const float* b, const int64_t* __restrict__ bi, float om,
+                                                     float m, float* o, float* __restrict__ oi, uint64_t n_f32,
+                                                     uint64_t n_i64) {
+  const uint64_t n4 = n_f32 / 4;
+  for (uint64_t k = gtid(); k < n4; k += gstride()) {
+    f4 bb = reinterpret_cast<const f4*>(b)[k];
+    f4 xx = reinterpret_cast<const f4*>(x)[k];
+    reinterpret_cast<f4*>(o)[k] = f4_add(f4_scale(bb, om), f4_scale(xx, m));
+  }
+  const uint64_t tail = n_f32 - 4 * n4;
+  for (uint64_t k = gtid(); k < tail + n_i64; k += gstride()) {
+    if (k < tail) {
+      const uint64_t e = 4 * n4 + k;
+      o[e] = b[e] * om + x[e] * m;
+    } else {
+      const uint64_t e = k - tail;
+      oi[e] = (float)bi[e] * om + (float)xi[e] * m;
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void synth_f32_kernel(float* o, const float* add, uint64_t n, uint64_t key,
+                                                           float scale) {
+  for (uint64_t k = gtid(); k < n; k += gstride()) {
+    const uint64_t h = splitmix64(key + k);
+    const int32_t r = int32_t(h >> 40) - (1 << 23);
+    const float v = float(r) * scale;
+    o[k] = add ? add[k] + v : v;
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void synth_i64_kernel(int64_t* o, const int64_t* add, uint64_t n, uint64_t key,
+                                                           uint64_t mod) {
+  for (uint64_t k = gtid(); k < n; k += gstride()) {
+    const int64_t v = int64_t(splitmix64(key + k) % mod);
+    o[k] = add ? (int64_t)((uint64_t)add[k] + (uint64_t)v) : v;
+  }
+}
+
+uint64_t synth_key(uint64_t seed, uint64_t stream_id) {
+  uint64_t z = seed ^ (stream_id * 0xD1B54A32D192ED03ull);
+  // host copy of splitmix64
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+int plato_agg_abi_version(void) { return PLATO_AGG_ABI_VERSION; }
+
+const char* plato_agg_last_error(void) { return g_last_error.c_str(); }
+
+int plato_agg_fedavg_weights(const float* const* d_x_f32, const int64_t* const* d_x_i64, const float* d_w,
+                             const float* d_s, int K, const float* d_base_f32, const int64_t* d_base_i64,
+                             float* d_out_f32, float* d_out_i64f, size_t n_f32, size_t n_i64,
+                             hipStream_t stream) {
+  return run_agg(0, true, d_x_f32, d_x_i64, d_w, d_s, K, d_base_f32, d_base_i64, d_out_f32, d_out_i64f, n_f32,
+                 n_i64, stream);
+}
+
+int plato_agg_fedavg_deltas(const float* const* d_d_f32, const int64_t* const* d_d_i64, const float* d_w,
+                            const float* d_s, int K, float* d_avg_f32, float* d_avg_i64f, size_t n_f32,
+                            size_t n_i64, hipStream_t stream) {
+  return run_agg(0, false, d_d_f32, d_d_i64, d_w, d_s, K, nullptr, nullptr, d_avg_f32, d_avg_i64f, n_f32, n_i64,
+                 stream);
+}
+
+int plato_agg_tune_num_variants(void) { return kNumVariants; }
+
+int plato_agg_tune_describe(int variant, int* v, int* u, int* nt) {
+  if (variant < 0 || variant >= kNumVariants) return fail(PLATO_AGG_EINVAL, "bad variant");
+  *v = kVariants[variant].V;
+  *u = kVariants[variant].U;
+  *nt = kVariants[variant].NT ? 1 : 0;
+  return PLATO_AGG_OK;
+}
+
+int plato_agg_tune_fedavg(int variant, int has_base, const float* const* d_x_f32, const int64_t* const* d_x_i64,
+                          const float* d_w, const float* d_s, int K, const float* d_base_f32,
+                          const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
+                          size_t n_i64, hipStream_t stream) {
+  return run_agg(variant, has_base != 0, d_x_f32, d_x_i64, d_w, d_s, K, d_base_f32, d_base_i64, d_out_f32,
+                 d_out_i64f, n_f32, n_i64, stream);
+}
+
+int plato_agg_compute_deltas(const float* d_x_f32, const int64_t* d_x_i64, const float* d_base_f32,
+                             const int64_t* d_base_i64, float* d_out_f32, int64_t* d_out_i64, size_t n_f32,
+                             size_t n_i64, hipStream_t stream) {
+  if (n_f32 && (!d_x_f32 || !d_base_f32 || !d_out_f32)) return fail(PLATO_AGG_EINVAL, "null fp32 pointer");
+  if (n_i64 && (!d_x_i64 || !d_base_i64 || !d_out_i64)) return fail(PLATO_AGG_EINVAL, "null int64 pointer");
+  if (n_f32 && !(aligned16(d_x_f32) && aligned16(d_base_f32) && aligned16(d_out_f32)))
+    return fail(PLATO_AGG_EINVAL, "fp32 pointers must be 16-byte aligned");
+  if (n_f32 + n_i64 == 0) return PLATO_AGG_OK;
+  hipLaunchKernelGGL(deltas_kernel, grid_for(n_f32 / 4 + n_i64 + 4), dim3(kBlock), 0, stream, d_x_f32, d_x_i64,
+                     d_base_f32, d_base_i64, d_out_f32, d_out_i64, n_f32, n_i64);
+  return check_launch("compute_deltas launch");
+}
+
+int plato_agg_update_weights(const float* d_base_f32, const int64_t* d_base_i64, const float* d_avg_f32,
+                             const float* d_avg_i64f, float* d_out_f32, float* d_out_i64f, size_t n_f32,
+                             size_t n_i64, hipStream_t stream) {
+  if (n_f32 && (!d_base_f32 || !d_avg_f32 || !d_out_f32)) return fail(PLATO_AGG_EINVAL, "null fp32 pointer");
+  if (n_i64 && (!d_base_i64 || !d_avg_i64f || !d_out_i64f)) return fail(PLATO_AGG_EINVAL, "null int64 pointer");
+  if (n_f32 && !(aligned16(d_base_f32) && aligned16(d_avg_f32) && aligned16(d_out_f32)))
+    return fail(PLATO_AGG_EINVAL, "fp32 pointers must be 16-byte aligned");
+  if (n_f32 + n_i64 == 0) return PLATO_AGG_OK;
+  hipLaunchKernelGGL(update_kernel, grid_for(n_f32 / 4 + n_i64 + 4), dim3(kBlock), 0, stream, d_base_f32,
+                     d_base_i64, d_avg_f32, d_avg_i64f, d_out_f32, d_out_i64f, n_f32, n_i64);
+  return check_launch("update_weights launch");
+}
+
+int plato_agg_cast_f32_i64(const float* d_src, int64_t* d_dst, size_t n, hipStream_t stream) {
+  if (n == 0) return PLATO_AGG_OK;
+  if (!d_src || !d_dst) return fail(PLATO_AGG_EINVAL, "null pointer");
+  hipLaunchKernelGGL(cast_kernel, grid_for(n), dim3(kBlock), 0, stream, d_src, d_dst, (uint64_t)n);
+  return check_launch("cast launch");
+}
+
+int plato_agg_mix_weights(const float* d_x_f32, const int64_t* d_x_i64, const float* d_base_f32,
+                          const int64_t* d_base_i64, float one_minus_m, float m, float* d_out_f32,
+                          float* d_out_i64f, size_t n_f32, size_t n_i64, hipStream_t stream) {
+  if (n_f32 && (!d_x_f32 || !d_base_f32 || !d_out_f32)) return fail(PLATO_AGG_EINVAL, "null fp32 pointer");
+  if (n_i64 && (!d_x_i64 || !d_base_i64 || !d_out_i64f)) return fail(PLATO_AGG_EINVAL, "null int64 pointer");
+  if (n_f32 && !(aligned16(d_x_f32) && aligned16(d_base_f32) && aligned16(d_out_f32)))
+    return fail(PLATO_AGG_EINVAL, "fp32 pointers must be 16-byte aligned");
+  if (n_f32 + n_i64 == 0) return PLATO_AGG_OK;
+  hipLaunchKernelGGL(mix_kernel, grid_for(n_f32 / 4 + n_i64 + 4), dim3(kBlock), 0, stream, d_x_f32, d_x_i64,
+                     d_base_f32, d_base_i64, one_minus_m, m, d_out_f32, d_out_i64f, n_f32, n_i64);
+  return check_launch("mix launch");
+}
+
+int plato_agg_fill_synth_f32(float* d_out, const float* d_add, size_t n, uint64_t seed, uint64_t stream_id,
+                             int scale_log2, hipStream_t stream) {
+  if (n == 0) return PLATO_AGG_OK;
+  if (!d_out) return fail(PLATO_AGG_EINVAL, "null output");
+  if (scale_log2 < -126 || scale_log2 > 100) return fail(PLATO_AGG_EINVAL, "scale_log2 out of range");
+  const float scale = ldexpf(1.0f, scale_log2);
+  hipLaunchKernelGGL(synth_f32_kernel, grid_for(n), dim3(kBlock), 0, stream, d_out, d_add, (uint64_t)n,
+                     synth_key(seed, stream_id), scale);
+  return check_launch("synth_f32 launch");
+}
+
+int plato_agg_fill_synth_i64(int64_t* d_out, const int64_t* d_add, size_t n, uint64_t seed, uint64_t stream_id,
+                             uint64_t modulus, hipStream_t stream) {
+  if (n == 0) return PLATO_AGG_OK;
+  if (!d_out) return fail(PLATO_AGG_EINVAL, "null output");
+  if (modulus == 0) return fail(PLATO_AGG_EINVAL, "modulus must be >= 1");
+  hipLaunchKernelGGL(synth_i64_kernel, grid_for(n), dim3(kBlock), 0, stream, d_out, d_add, (uint64_t)n,
+                     synth_key(seed, stream_id), modulus);
+  return check_launch("synth_i64 launch");
+}
+
+}  // extern "C"

@@ -1,0 +1,355 @@
+"""Device engine: HBM arenas, host staging and launches of the HIP kernels.
+
+This is the host half of the drop-in boundary.  It takes what Plato's server
+hands to its aggregation hooks (CPU ``state_dict`` payloads in
+``self.updates`` order, the baseline from ``algorithm.extract_weights()``,
+per-client weights) and returns what the reference would return, computed by
+``libplato_agg.so`` on the GPU:
+
+* :meth:`FedAvgEngine.aggregate_weights` — the fused deltas -> weighted sum ->
+  update chain (``plato/servers/fedavg.py:184-194``), i.e. the value an
+  ``aggregate_weights`` hook must produce (``servers/fedavg.py:171-182``).
+* :meth:`FedAvgEngine.aggregate_deltas` — ``Server.aggregate_deltas``
+  (``servers/fedavg.py:137-159``) for variants that compute their own deltas.
+* :meth:`FedAvgEngine.compute_weight_deltas` / :meth:`update_weights` /
+  :meth:`mix_weights` — ``algorithms/fedavg.py:13-37`` and FedAsync's
+  ``fedasync_algorithm.py:9-20``.
+
+Everything device-side goes through the C ABI; nothing here computes model
+arithmetic on the CPU.
+"""
+
+from __future__ import annotations
+
+from collections import OrderedDict
+from typing import Mapping, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .arena import F32, I64, ArenaLayout
+
+
+def fp32_weights(values: Sequence[float]) -> np.ndarray:
+    """Round Python (double) weights to fp32 the way torch's scalar path does.
+
+    ``delta * (n_i / N)`` multiplies an fp32 tensor by a Python float; torch
+    converts the double scalar to the fp32 compute type (round to nearest even)
+    before the multiply (measured).
+    """
+    out = np.empty(len(values), dtype=np.float32)
+    for i, v in enumerate(values):
+        if isinstance(v, torch.Tensor):
+            raise TypeError("aggregation weights must be Python numbers, not tensors")
+        out[i] = np.float32(float(v))
+    return out
+
+
+def fedavg_weights(num_samples: Sequence[int]) -> list[float]:
+    """``n_i / N`` as the reference computes it (``servers/fedavg.py:140,154``)."""
+    total = sum(num_samples)
+    return [n / total for n in num_samples]
+
+
+def require_device(device=None) -> torch.device:
+    if not torch.cuda.is_available():
+        raise RuntimeError(
+            "plato_amd: no ROCm GPU visible; the aggregation engine runs only on the "
+            "HIP path (there is no CPU fallback)"
+        )
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError(f"plato_amd: device must be a GPU, got {dev}")
+    return dev
+
+
+def _ptr(t: torch.Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _stream_handle(stream: torch.cuda.Stream) -> int:
+    return stream.cuda_stream
+
+
+class DeviceArena:
+    """One model arena in HBM: fp32 region + int64 region (+ fp32 view of int64 results)."""
+
+    def __init__(self, layout: ArenaLayout, device: torch.device):
+        self.layout = layout
+        self.f32 = torch.empty(layout.row_f32, dtype=torch.float32, device=device)
+        self.i64 = torch.empty(layout.row_i64, dtype=torch.int64, device=device)
+
+
+class ClientSlab:
+    """K client arenas in HBM as two row-major slabs ``[cap, row]``."""
+
+    def __init__(self, layout: ArenaLayout, capacity: int, device: torch.device):
+        self.layout = layout
+        self.capacity = capacity
+        self.f32 = torch.empty((capacity, layout.row_f32), dtype=torch.float32, device=device)
+        self.i64 = torch.empty((capacity, layout.row_i64), dtype=torch.int64, device=device)
+
+    def row_pointers(self, rows: Sequence[int]) -> tuple[np.ndarray, np.ndarray]:
+        base_f = self.f32.data_ptr()
+        base_i = self.i64.data_ptr()
+        sf = self.layout.row_f32 * 4
+        si = self.layout.row_i64 * 8
+        rows = np.asarray(rows, dtype=np.int64)
+        return (base_f + rows * sf).astype(np.int64), (base_i + rows * si).astype(np.int64)
+
+
+class _Stager:
+    """Pinned host ring that packs CPU ``state_dict``s and copies them H2D.
+
+    Packing client j+1 (host memcpy, multi-threaded torch.cat) overlaps the
+    H2D copy of client j on a dedicated copy stream.
+    """
+
+    def __init__(self, layout: ArenaLayout, device: torch.device, depth: int = 3):
+        self.layout = layout
+        self.stream = torch.cuda.Stream(device)
+        self.bufs = [
+            (
+                torch.empty(layout.row_f32, dtype=torch.float32, pin_memory=True),
+                torch.empty(layout.row_i64, dtype=torch.int64, pin_memory=True),
+            )
+            for _ in range(depth)
+        ]
+        self.events: list[torch.cuda.Event | None] = [None] * depth
+        self.next = 0
+
+    def put(self, state_dict: Mapping[str, torch.Tensor], dst_f32: torch.Tensor,
+            dst_i64: torch.Tensor) -> None:
+        j = self.next
+        self.next = (j + 1) % len(self.bufs)
+        if self.events[j] is not None:
+            self.events[j].synchronize()
+        hf, hi = self.bufs[j]
+        self.layout.pack(state_dict, hf, hi)
+        n_f, n_i = self.layout.n_f32, self.layout.n_i64
+        with torch.cuda.stream(self.stream):
+            if n_f:
+                dst_f32[:n_f].copy_(hf[:n_f], non_blocking=True)
+            if n_i:
+                dst_i64[:n_i].copy_(hi[:n_i], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self.stream)
+        self.events[j] = ev
+
+    def fence(self, stream: torch.cuda.Stream) -> None:
+        """Make ``stream`` wait for every copy issued so far."""
+        stream.wait_stream(self.stream)
+
+
+class FedAvgEngine:
+    """HIP FedAvg aggregation on one GPU (one process per GPU)."""
+
+    def __init__(self, device=None, variant: int | None = None):
+        self.device = require_device(device)
+        self.lib = _lib.lib()
+        self.variant = variant
+        self._layout: ArenaLayout | None = None
+        self._slab: ClientSlab | None = None
+        self._base: DeviceArena | None = None
+        self._stager: _Stager | None = None
+
+    # ----------------------------------------------------------- allocation
+    def _prepare(self, template: Mapping[str, torch.Tensor], k: int) -> ArenaLayout:
+        layout = ArenaLayout.from_state_dict(template)
+        if self._layout is None or self._layout.signature != layout.signature:
+            self._layout = layout
+            self._slab = None
+            self._base = None
+            self._stager = None
+        layout = self._layout
+        if self._slab is None or self._slab.capacity < k:
+            self._slab = None
+            self._slab = ClientSlab(layout, k, self.device)
+        if self._base is None:
+            self._base = DeviceArena(layout, self.device)
+        if self._stager is None:
+            self._stager = _Stager(layout, self.device)
+        return layout
+
+    def _upload_weights(self, weights: Sequence[float], scales: Sequence[float] | None):
+        w = torch.from_numpy(fp32_weights(weights)).to(self.device, non_blocking=False)
+        s = None
+        if scales is not None:
+            if len(scales) != len(weights):
+                raise ValueError("scales must have one entry per client")
+            s = torch.from_numpy(fp32_weights(scales)).to(self.device, non_blocking=False)
+        return w, s
+
+    def _pointer_tables(self, pf: np.ndarray, pi: np.ndarray):
+        tf = torch.from_numpy(pf).to(self.device)
+        ti = torch.from_numpy(pi).to(self.device)
+        return tf, ti
+
+    # ------------------------------------------------------ raw device call
+    def launch_fedavg(self, layout: ArenaLayout, ptr_f32: torch.Tensor, ptr_i64: torch.Tensor | None,
+                      w: torch.Tensor, s: torch.Tensor | None, k: int,
+                      base_f32: torch.Tensor | None, base_i64: torch.Tensor | None,
+                      out_f32: torch.Tensor, out_i64f: torch.Tensor | None,
+                      stream: torch.cuda.Stream | None = None) -> None:
+        """Launch the fused kernel on device-resident arenas (no host traffic).
+
+        ``base_f32 is None`` selects deltas mode (``aggregate_deltas``).
+        """
+        stream = stream or torch.cuda.current_stream(self.device)
+        n_f, n_i = layout.n_f32, layout.n_i64
+        if ptr_f32.numel() < k or w.numel() < k:
+            raise ValueError("pointer table / weights shorter than K")
+        args_tail = (n_f, n_i, _stream_handle(stream))
+        ptr_i = _ptr(ptr_i64) if n_i else None
+        if self.variant is None:
+            if base_f32 is not None:
+                _lib.call("plato_agg_fedavg_weights", _ptr(ptr_f32), ptr_i, _ptr(w), _ptr(s), k,
+                          _ptr(base_f32), _ptr(base_i64) if n_i else None, _ptr(out_f32),
+                          _ptr(out_i64f) if n_i else None, *args_tail)
+            else:
+                _lib.call("plato_agg_fedavg_deltas", _ptr(ptr_f32), ptr_i, _ptr(w), _ptr(s), k,
+                          _ptr(out_f32), _ptr(out_i64f) if n_i else None, *args_tail)
+        else:
+            _lib.call("plato_agg_tune_fedavg", self.variant, int(base_f32 is not None), _ptr(ptr_f32),
+                      ptr_i, _ptr(w), _ptr(s), k, _ptr(base_f32),
+                      _ptr(base_i64) if n_i else None, _ptr(out_f32),
+                      _ptr(out_i64f) if n_i else None, *args_tail)
+
+    # ------------------------------------------------------ host-facing API
+    def stage_clients(self, payloads: Sequence[Mapping[str, torch.Tensor]], template=None,
+                      what: str = "weights_received") -> ArenaLayout:
+        """Pack and copy K CPU payloads into the client slab (rows 0..K-1)."""
+        template = template if template is not None else payloads[0]
+        layout = self._prepare(template, len(payloads))
+        for i, sd in enumerate(payloads):
+            layout.check_compatible(sd, f"{what}[{i}]")
+            self._stager.put(sd, self._slab.f32[i], self._slab.i64[i])
+        return layout
+
+    def aggregate_weights(self, baseline: Mapping[str, torch.Tensor],
+                          weights_received: Sequence[Mapping[str, torch.Tensor]],
+                          weights: Sequence[float], scales: Sequence[float] | None = None
+                          ) -> "OrderedDict[str, torch.Tensor]":
+        """``update_weights(aggregate_deltas(compute_weight_deltas(b, X)))`` on the GPU.
+
+        Returns CPU tensors in baseline key order: fp32 for every entry (int64
+        entries come back as fp32 ``float(b) + avg`` exactly like the
+        reference's ``update_weights``; ``load_weights`` truncates them).
+        """
+        k = len(weights_received)
+        if k == 0:
+            raise ValueError("no client payloads to aggregate")
+        if len(weights) != k:
+            raise ValueError("weights must have one entry per client")
+        layout = self.stage_clients(weights_received, template=baseline)
+        self._stager.put(baseline, self._base.f32, self._base.i64)
+        w, s = self._upload_weights(weights, scales)
+        pf, pi = self._slab.row_pointers(range(k))
+        tf, ti = self._pointer_tables(pf, pi)
+        stream = torch.cuda.current_stream(self.device)
+        self._stager.fence(stream)
+        out_f = torch.empty(layout.row_f32, dtype=torch.float32, device=self.device)
+        out_i = torch.empty(layout.row_i64, dtype=torch.float32, device=self.device)
+        self.launch_fedavg(layout, tf, ti, w, s, k, self._base.f32, self._base.i64, out_f, out_i,
+                           stream)
+        host_f = out_f[: layout.n_f32].to("cpu")
+        host_i = out_i[: layout.n_i64].to("cpu")
+        return layout.unpack(host_f, host_i)
+
+    def aggregate_deltas(self, deltas_received: Sequence[Mapping[str, torch.Tensor]],
+                         weights: Sequence[float], scales: Sequence[float] | None = None
+                         ) -> "OrderedDict[str, torch.Tensor]":
+        """``Server.aggregate_deltas`` on the GPU: ``avg = sum_i delta_i * w_i`` (fp32)."""
+        k = len(deltas_received)
+        if k == 0:
+            raise ValueError("no client deltas to aggregate")
+        if len(weights) != k:
+            raise ValueError("weights must have one entry per client")
+        layout = self.stage_clients(deltas_received, what="deltas_received")
+        w, s = self._upload_weights(weights, scales)
+        pf, pi = self._slab.row_pointers(range(k))
+        tf, ti = self._pointer_tables(pf, pi)
+        stream = torch.cuda.current_stream(self.device)
+        self._stager.fence(stream)
+        out_f = torch.empty(layout.row_f32, dtype=torch.float32, device=self.device)
+        out_i = torch.empty(layout.row_i64, dtype=torch.float32, device=self.device)
+        self.launch_fedavg(layout, tf, ti, w, s, k, None, None, out_f, out_i, stream)
+        return layout.unpack(out_f[: layout.n_f32].to("cpu"), out_i[: layout.n_i64].to("cpu"))
+
+    def compute_weight_deltas(self, baseline: Mapping[str, torch.Tensor],
+                              weights_received: Sequence[Mapping[str, torch.Tensor]]
+                              ) -> list["OrderedDict[str, torch.Tensor]"]:
+        """``Algorithm.compute_weight_deltas`` (``algorithms/fedavg.py:13-27``) on the GPU.
+
+        int64 entries keep int64 deltas, as ``current - baseline`` does.
+        """
+        k = len(weights_received)
+        if k == 0:
+            return []
+        layout = self.stage_clients(weights_received, template=baseline)
+        self._stager.put(baseline, self._base.f32, self._base.i64)
+        stream = torch.cuda.current_stream(self.device)
+        self._stager.fence(stream)
+        h = _stream_handle(stream)
+        out = []
+        for i in range(k):
+            df = torch.empty(layout.row_f32, dtype=torch.float32, device=self.device)
+            di = torch.empty(layout.row_i64, dtype=torch.int64, device=self.device)
+            _lib.call("plato_agg_compute_deltas", _ptr(self._slab.f32[i]), _ptr(self._slab.i64[i]),
+                      _ptr(self._base.f32), _ptr(self._base.i64), _ptr(df), _ptr(di),
+                      layout.n_f32, layout.n_i64, h)
+            out.append(layout.unpack(df[: layout.n_f32].to("cpu"), di[: layout.n_i64].to("cpu")))
+        return out
+
+    def update_weights(self, baseline: Mapping[str, torch.Tensor],
+                       deltas: Mapping[str, torch.Tensor]) -> "OrderedDict[str, torch.Tensor]":
+        """``Algorithm.update_weights`` (``algorithms/fedavg.py:29-37``): ``b + avg`` in fp32."""
+        layout = self._prepare(baseline, 1)
+        # avg is fp32 for every key (trainers/basic.py:63); stage it as a
+        # float32 row for both regions.
+        avg_f = torch.empty(layout.row_f32, dtype=torch.float32, device=self.device)
+        avg_i = torch.empty(layout.row_i64, dtype=torch.float32, device=self.device)
+        f32 = [deltas[e.name].reshape(-1).to(torch.float32) for e in layout.entries if e.region == F32]
+        i64 = [deltas[e.name].reshape(-1).to(torch.float32) for e in layout.entries if e.region == I64]
+        if f32:
+            avg_f[: layout.n_f32].copy_(torch.cat(f32))
+        if i64:
+            avg_i[: layout.n_i64].copy_(torch.cat(i64))
+        self._stager.put(baseline, self._base.f32, self._base.i64)
+        stream = torch.cuda.current_stream(self.device)
+        self._stager.fence(stream)
+        out_f = torch.empty_like(avg_f)
+        out_i = torch.empty_like(avg_i)
+        _lib.call("plato_agg_update_weights", _ptr(self._base.f32), _ptr(self._base.i64), _ptr(avg_f),
+                  _ptr(avg_i), _ptr(out_f), _ptr(out_i), layout.n_f32, layout.n_i64,
+                  _stream_handle(stream))
+        return layout.unpack(out_f[: layout.n_f32].to("cpu"), out_i[: layout.n_i64].to("cpu"))
+
+    def mix_weights(self, baseline: Mapping[str, torch.Tensor],
+                    received: Mapping[str, torch.Tensor], mixing: float
+                    ) -> "OrderedDict[str, torch.Tensor]":
+        """FedAsync: ``b * (1 - m) + x * m`` (``fedasync_algorithm.py:15-18``)."""
+        layout = self.stage_clients([received], template=baseline)
+        self._stager.put(baseline, self._base.f32, self._base.i64)
+        stream = torch.cuda.current_stream(self.device)
+        self._stager.fence(stream)
+        one_minus = float(np.float32(1 - mixing))
+        m = float(np.float32(mixing))
+        out_f = torch.empty(layout.row_f32, dtype=torch.float32, device=self.device)
+        out_i = torch.empty(layout.row_i64, dtype=torch.float32, device=self.device)
+        _lib.call("plato_agg_mix_weights", _ptr(self._slab.f32[0]), _ptr(self._slab.i64[0]),
+                  _ptr(self._base.f32), _ptr(self._base.i64), one_minus, m, _ptr(out_f),
+                  _ptr(out_i), layout.n_f32, layout.n_i64, _stream_handle(stream))
+        return layout.unpack(out_f[: layout.n_f32].to("cpu"), out_i[: layout.n_i64].to("cpu"))
+
+
+def cast_to_int64(src_f32: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:
+    """load_state_dict's fp32 -> int64 truncating copy, on the device."""
+    if not src_f32.is_cuda or src_f32.dtype != torch.float32:
+        raise ValueError("cast_to_int64 expects a CUDA float32 tensor")
+    src = src_f32.contiguous()
+    dst = torch.empty(src.shape, dtype=torch.int64, device=src.device)
+    stream = stream or torch.cuda.current_stream(src.device)
+    _lib.call("plato_agg_cast_f32_i64", _ptr(src), _ptr(dst), src.numel(), _stream_handle(stream))
+    return dst

@@ -1,0 +1,27 @@
+#!/bin/bash
+# GPU-box job: parity tests, kernel-variant sweep, bench line.
+# Each GPU step has its own time limit; a fault / abort / timeout ends the job
+# (exit codes >= 124), while an ordinary test failure (1) still lets the
+# measurement steps run so the log shows both.
+set -u
+mkdir -p gpurun_out
+run() {  # run <name> <timeout_s> <cmd...>
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*" | tee -a gpurun_out/steps.log
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc" | tee -a gpurun_out/steps.log
+  tail -5 "gpurun_out/$name.log"
+  if [ $rc -ge 124 ]; then echo "fatal rc=$rc in $name; stopping"; exit $rc; fi
+  return 0
+}
+python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { cat gpurun_out/build.log; exit 1; }
+for step in "$@"; do
+  case $step in
+    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    sweep) run sweep 600 python bench.py --sweep --steps 10 --no-cpu-baseline --no-host-inclusive ;;
+    bench) run bench 900 python bench.py ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
