@@ -168,10 +168,12 @@ def main():
             import ctypes
 
             for v in range(nv):
-                a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-                _lib.lib().plato_agg_tune_describe(v, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+                bs, a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+                _lib.lib().plato_agg_tune_describe(v, ctypes.byref(bs), ctypes.byref(a), ctypes.byref(b),
+                                                   ctypes.byref(c))
                 med = statistics.median(times[v])
-                print(json.dumps({"variant": v, "V": a.value, "U": b.value, "NT": c.value,
+                print(json.dumps({"variant": v, "B": bs.value, "V": a.value, "U": b.value,
+                                  "ntl": c.value & 1, "nts": (c.value >> 1) & 1, "pipe": (c.value >> 2) & 1,
                                   "ms_median": med, "ms_min": min(times[v]),
                                   "GBps": alg_bytes / (med * 1e-3) / 1e9}), flush=True)
         return

@@ -20,8 +20,10 @@ extern "C" {
 
 int plato_agg_tune_num_variants(void);
 
-/* Writes the variant's V (float4 per lane), U (clients unrolled), NT flag. */
-int plato_agg_tune_describe(int variant, int* v, int* u, int* nt);
+/* Writes the variant's workgroup size, V (float4 per lane), U (clients per
+ * batch) and flags: bit 0 non-temporal loads, bit 1 non-temporal stores,
+ * bit 2 software-pipelined batches. */
+int plato_agg_tune_describe(int variant, int* block, int* v, int* u, int* flags);
 
 /* has_base != 0: plato_agg_fedavg_weights; == 0: plato_agg_fedavg_deltas. */
 int plato_agg_tune_fedavg(int variant, int has_base,

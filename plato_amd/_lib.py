@@ -66,7 +66,8 @@ SIGNATURES = {
     "plato_agg_tune_num_variants": (_c_int, []),
     "plato_agg_tune_describe": (
         _c_int,
-        [_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), ctypes.POINTER(_c_int)],
+        [_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),
+         ctypes.POINTER(_c_int)],
     ),
     "plato_agg_tune_fedavg": (
         _c_int,

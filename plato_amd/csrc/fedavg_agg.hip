@@ -120,9 +120,60 @@ struct AggArgs {
   int K;
 };
 
-template <int V, int U, bool HAS_BASE, bool TWO, bool NT, bool CHECK>
+// Kernel configuration (tuning space; DESIGN.md §5 has the sweep):
+//   B   threads per workgroup      V  f4 groups per lane per client
+//   U   clients per batch          NTL/NTS  non-temporal loads / stores
+//   PIPE  software-pipelined: batch j+1's loads issue before batch j's adds
+template <int B_, int V_, int U_, bool NTL_, bool NTS_, bool PIPE_>
+struct Cfg {
+  static constexpr int B = B_, V = V_, U = U_;
+  static constexpr bool NTL = NTL_, NTS = NTS_, PIPE = PIPE_;
+};
+
+template <bool NT>
+__device__ __forceinline__ void st4_off(float* base, uint32_t byte_off, f4 v) {
+  __attribute__((address_space(1))) f4* g =
+      (__attribute__((address_space(1))) f4*)((__attribute__((address_space(1))) char*)base + byte_off);
+  if constexpr (NT) {
+    __builtin_nontemporal_store(v, g);
+  } else {
+    *g = v;
+  }
+}
+
+template <class C, bool HAS_BASE, bool TWO>
+__device__ __forceinline__ void accumulate(f4 (&acc)[C::V], const f4 (&x)[C::U][C::V], const f4 (&b)[C::V],
+                                           const AggArgs& a, int i0) {
+#pragma unroll
+  for (int u = 0; u < C::U; ++u) {
+    const float wu = sld(a.w, i0 + u);
+    float su = 1.f;
+    if constexpr (TWO) su = sld(a.s, i0 + u);
+#pragma unroll
+    for (int v = 0; v < C::V; ++v) {
+      f4 d = HAS_BASE ? f4_sub(x[u][v], b[v]) : x[u][v];
+      f4 t = f4_scale(d, wu);
+      if constexpr (TWO) t = f4_scale(t, su);
+      acc[v] = f4_add(acc[v], t);
+    }
+  }
+}
+
+template <class C>
+__device__ __forceinline__ void load_batch(f4 (&x)[C::U][C::V], const AggArgs& a, int i0,
+                                           const uint32_t (&off)[C::V]) {
+#pragma unroll
+  for (int u = 0; u < C::U; ++u) {
+    const float* p = sld(a.xf, i0 + u);
+#pragma unroll
+    for (int v = 0; v < C::V; ++v) x[u][v] = ld4_off<C::NTL>(p, off[v]);
+  }
+}
+
+template <class C, bool HAS_BASE, bool TWO, bool CHECK>
 __device__ __forceinline__ void vec_body(const AggArgs& a, uint32_t blk) {
-  constexpr uint64_t kChunk = uint64_t(kBlock) * V;
+  constexpr int V = C::V, U = C::U;
+  constexpr uint64_t kChunk = uint64_t(C::B) * V;
   const uint64_t first = uint64_t(blk) * kChunk + threadIdx.x;
 
   // Element groups this lane owns, as 32-bit byte offsets (host guarantees an
@@ -136,55 +187,44 @@ __device__ __forceinline__ void vec_body(const AggArgs& a, uint32_t blk) {
   f4 acc[V];
 #pragma unroll
   for (int v = 0; v < V; ++v) {
-    const uint64_t e = first + uint64_t(v) * kBlock;
+    const uint64_t e = first + uint64_t(v) * C::B;
     live[v] = !CHECK || e < a.n4;
     off[v] = uint32_t((CHECK ? (e < a.n4 ? e : a.n4 - 1) : e) * 16u);
     acc[v] = f4_zero();
-    if constexpr (HAS_BASE) b[v] = ld4_off<false>(a.base_f, off[v]);
+    b[v] = HAS_BASE ? ld4_off<false>(a.base_f, off[v]) : f4_zero();
   }
 
   const int K = a.K;
-  int i = 0;
-  // Client pointers for the next batch are fetched (s_load) one batch ahead
-  // so the vector loads of a batch issue without waiting on the scalar cache.
-  const float* pn[U];
-  if (U <= K) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) pn[u] = sld(a.xf, u);
-  }
-  for (; i + U <= K; i += U) {
-    f4 x[U][V];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-#pragma unroll
-      for (int v = 0; v < V; ++v) x[u][v] = ld4_off<NT>(pn[u], off[v]);
-    }
-    if (i + 2 * U <= K) {
-#pragma unroll
-      for (int u = 0; u < U; ++u) pn[u] = sld(a.xf, i + U + u);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const float wu = sld(a.w, i + u);
-      float su = 1.f;
-      if constexpr (TWO) su = sld(a.s, i + u);
-#pragma unroll
-      for (int v = 0; v < V; ++v) {
-        f4 d = HAS_BASE ? f4_sub(x[u][v], b[v]) : x[u][v];
-        f4 t = f4_scale(d, wu);
-        if constexpr (TWO) t = f4_scale(t, su);
-        acc[v] = f4_add(acc[v], t);
+  const int nbatch = K / U;
+  if constexpr (C::PIPE) {
+    if (nbatch > 0) {
+      f4 x0[U][V], x1[U][V];
+      load_batch<C>(x0, a, 0, off);
+      int j = 0;
+      // Two named register sets (no runtime-indexed arrays -> no scratch).
+      for (; j + 2 <= nbatch; j += 2) {
+        load_batch<C>(x1, a, (j + 1) * U, off);
+        accumulate<C, HAS_BASE, TWO>(acc, x0, b, a, j * U);
+        if (j + 2 < nbatch) load_batch<C>(x0, a, (j + 2) * U, off);
+        accumulate<C, HAS_BASE, TWO>(acc, x1, b, a, (j + 1) * U);
       }
+      if (j < nbatch) accumulate<C, HAS_BASE, TWO>(acc, x0, b, a, j * U);
+    }
+  } else {
+    for (int j = 0; j < nbatch; ++j) {
+      f4 x[U][V];
+      load_batch<C>(x, a, j * U, off);
+      accumulate<C, HAS_BASE, TWO>(acc, x, b, a, j * U);
     }
   }
-  for (; i < K; ++i) {
+  for (int i = nbatch * U; i < K; ++i) {
     const float* p = sld(a.xf, i);
     const float wu = sld(a.w, i);
     float su = 1.f;
     if constexpr (TWO) su = sld(a.s, i);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      f4 x = ld4_off<NT>(p, off[v]);
+      f4 x = ld4_off<C::NTL>(p, off[v]);
       f4 d = HAS_BASE ? f4_sub(x, b[v]) : x;
       f4 t = f4_scale(d, wu);
       if constexpr (TWO) t = f4_scale(t, su);
@@ -192,13 +232,9 @@ __device__ __forceinline__ void vec_body(const AggArgs& a, uint32_t blk) {
     }
   }
 
-  float* out = a.out_f;
 #pragma unroll
   for (int v = 0; v < V; ++v) {
-    if (live[v]) {
-      *(__attribute__((address_space(1))) f4*)((__attribute__((address_space(1))) char*)out + off[v]) =
-          HAS_BASE ? f4_add(b[v], acc[v]) : acc[v];
-    }
+    if (live[v]) st4_off<C::NTS>(a.out_f, off[v], HAS_BASE ? f4_add(b[v], acc[v]) : acc[v]);
   }
 }
 
@@ -212,10 +248,10 @@ __device__ __forceinline__ void scalar_item(const AggArgs& a, uint64_t j) {
     const float b = HAS_BASE ? a.base_f[e] : 0.f;
     float acc = 0.f;
     for (int i = 0; i < K; ++i) {
-      const float x = a.xf[i][e];
+      const float x = sld(a.xf, i)[e];
       const float d = HAS_BASE ? x - b : x;
-      float t = d * a.w[i];
-      if constexpr (TWO) t = t * a.s[i];
+      float t = d * sld(a.w, i);
+      if constexpr (TWO) t = t * sld(a.s, i);
       acc = acc + t;
     }
     a.out_f[e] = HAS_BASE ? b + acc : acc;
@@ -226,64 +262,71 @@ __device__ __forceinline__ void scalar_item(const AggArgs& a, uint64_t j) {
   const int64_t b = HAS_BASE ? a.base_i[e] : 0;
   float acc = 0.f;
   for (int i = 0; i < K; ++i) {
-    const int64_t x = a.xi[i][e];
+    const int64_t x = sld(a.xi, i)[e];
     // int64 subtraction wraps like torch's; the promotion to fp32 happens at
     // the scalar multiply (servers/fedavg.py:154, int tensor * Python float).
     const int64_t d = HAS_BASE ? (int64_t)((uint64_t)x - (uint64_t)b) : x;
-    float t = (float)d * a.w[i];
-    if constexpr (TWO) t = t * a.s[i];
+    float t = (float)d * sld(a.w, i);
+    if constexpr (TWO) t = t * sld(a.s, i);
     acc = acc + t;
   }
   // update_weights: int64 weight + fp32 delta -> fp32 (float(b) + acc).
   a.out_if[e] = HAS_BASE ? (float)b + acc : acc;
 }
 
-template <int V, int U, bool HAS_BASE, bool TWO, bool NT>
-__global__ __launch_bounds__(kBlock) void fedavg_kernel(AggArgs a) {
+template <class C, bool HAS_BASE, bool TWO>
+__global__ __launch_bounds__(C::B) void fedavg_kernel(AggArgs a) {
   const uint32_t blk = blockIdx.x;
   if (blk < a.nb_vec_full) {
-    vec_body<V, U, HAS_BASE, TWO, NT, false>(a, blk);
+    vec_body<C, HAS_BASE, TWO, false>(a, blk);
   } else if (blk < a.nb_vec) {
-    vec_body<V, U, HAS_BASE, TWO, NT, true>(a, blk);
+    vec_body<C, HAS_BASE, TWO, true>(a, blk);
   } else {
-    const uint64_t j = uint64_t(blk - a.nb_vec) * kBlock + threadIdx.x;
+    const uint64_t j = uint64_t(blk - a.nb_vec) * C::B + threadIdx.x;
     scalar_item<HAS_BASE, TWO>(a, j);
   }
 }
 
 // ---------------------------------------------------------------------------
-// Variant table (tuning knobs: V f4 per lane, U clients unrolled, NT loads)
+// Variant table
 // ---------------------------------------------------------------------------
 using LaunchFn = void (*)(const AggArgs&, dim3, hipStream_t);
 
-template <int V, int U, bool HAS_BASE, bool TWO, bool NT>
+template <class C, bool HAS_BASE, bool TWO>
 void launch_one(const AggArgs& a, dim3 grid, hipStream_t st) {
-  hipLaunchKernelGGL((fedavg_kernel<V, U, HAS_BASE, TWO, NT>), grid, dim3(kBlock), 0, st, a);
+  hipLaunchKernelGGL((fedavg_kernel<C, HAS_BASE, TWO>), grid, dim3(C::B), 0, st, a);
 }
 
 struct Variant {
-  int V, U;
-  bool NT;
+  int B, V, U;
+  bool NTL, NTS, PIPE;
   LaunchFn fn[2][2];  // [HAS_BASE][TWO]
 };
 
-template <int V, int U, bool NT>
+template <class C>
 constexpr Variant make_variant() {
-  return Variant{V, U, NT,
-                 {{&launch_one<V, U, false, false, NT>, &launch_one<V, U, false, true, NT>},
-                  {&launch_one<V, U, true, false, NT>, &launch_one<V, U, true, true, NT>}}};
+  return Variant{C::B, C::V, C::U, C::NTL, C::NTS, C::PIPE,
+                 {{&launch_one<C, false, false>, &launch_one<C, false, true>},
+                  {&launch_one<C, true, false>, &launch_one<C, true, true>}}};
 }
 
-// Variant 0 is the default (chosen from the measurements in DESIGN.md §5).
+// Variant 0 is the default of the public entry points (fastest in the
+// interleaved sweep on MI355X).
 const Variant kVariants[] = {
-    make_variant<2, 8, false>(),  // 0 (default)
-    make_variant<1, 8, false>(),  // 1
-    make_variant<2, 4, false>(),  // 2
-    make_variant<4, 4, false>(),  // 3
-    make_variant<2, 8, true>(),   // 4
-    make_variant<1, 16, false>(), // 5
-    make_variant<4, 8, false>(),  // 6
-    make_variant<1, 8, true>(),   // 7
+    make_variant<Cfg<256, 1, 8, true, false, false>>(),   // 0 (default)
+    make_variant<Cfg<256, 2, 8, false, false, false>>(),  // 1 first version
+    make_variant<Cfg<256, 1, 8, false, false, false>>(),  // 2
+    make_variant<Cfg<256, 1, 4, true, false, false>>(),   // 3
+    make_variant<Cfg<256, 1, 16, true, false, false>>(),  // 4
+    make_variant<Cfg<256, 1, 8, true, true, false>>(),    // 5
+    make_variant<Cfg<256, 1, 8, true, false, true>>(),    // 6
+    make_variant<Cfg<256, 1, 4, true, false, true>>(),    // 7
+    make_variant<Cfg<512, 1, 8, true, false, false>>(),   // 8
+    make_variant<Cfg<128, 1, 8, true, false, false>>(),   // 9
+    make_variant<Cfg<256, 2, 8, true, false, false>>(),   // 10
+    make_variant<Cfg<256, 2, 4, true, false, true>>(),    // 11
+    make_variant<Cfg<1024, 1, 8, true, false, false>>(),  // 12
+    make_variant<Cfg<256, 1, 32, true, false, false>>(),  // 13
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -317,10 +360,10 @@ int run_agg(int variant, bool has_base, const float* const* xf, const int64_t* c
   a.n_f32 = n_f32;
   a.n_i64 = n_i64;
   a.K = K;
-  const uint64_t chunk = uint64_t(kBlock) * vr.V;
+  const uint64_t chunk = uint64_t(vr.B) * vr.V;
   const uint64_t nb_vec = (a.n4 + chunk - 1) / chunk;
   const uint64_t n_scalar = (n_f32 - 4 * a.n4) + n_i64;
-  const uint64_t nb_scalar = (n_scalar + kBlock - 1) / kBlock;
+  const uint64_t nb_scalar = (n_scalar + vr.B - 1) / vr.B;
   if (nb_vec + nb_scalar > 0x7fffffffull || a.n4 * 16ull > 0xffffffffull)
     return fail(PLATO_AGG_EINVAL, "fp32 arena must be < 4 GiB per launch (split it into buckets)");
   a.nb_vec = uint32_t(nb_vec);
@@ -478,11 +521,13 @@ int plato_agg_fedavg_deltas(const float* const* d_d_f32, const int64_t* const* d
 
 int plato_agg_tune_num_variants(void) { return kNumVariants; }
 
-int plato_agg_tune_describe(int variant, int* v, int* u, int* nt) {
+int plato_agg_tune_describe(int variant, int* block, int* v, int* u, int* flags) {
   if (variant < 0 || variant >= kNumVariants) return fail(PLATO_AGG_EINVAL, "bad variant");
-  *v = kVariants[variant].V;
-  *u = kVariants[variant].U;
-  *nt = kVariants[variant].NT ? 1 : 0;
+  const Variant& vr = kVariants[variant];
+  *block = vr.B;
+  *v = vr.V;
+  *u = vr.U;
+  *flags = (vr.NTL ? 1 : 0) | (vr.NTS ? 2 : 0) | (vr.PIPE ? 4 : 0);
   return PLATO_AGG_OK;
 }
 
