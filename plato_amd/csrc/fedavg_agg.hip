@@ -313,20 +313,20 @@ constexpr Variant make_variant() {
 // Variant 0 is the default of the public entry points (fastest in the
 // interleaved sweep on MI355X).
 const Variant kVariants[] = {
-    make_variant<Cfg<256, 1, 8, true, false, false>>(),   // 0 (default)
+    make_variant<Cfg<256, 1, 8, true, true, false>>(),    // 0 (default): NT loads + NT stores
     make_variant<Cfg<256, 2, 8, false, false, false>>(),  // 1 first version
-    make_variant<Cfg<256, 1, 8, false, false, false>>(),  // 2
-    make_variant<Cfg<256, 1, 4, true, false, false>>(),   // 3
-    make_variant<Cfg<256, 1, 16, true, false, false>>(),  // 4
-    make_variant<Cfg<256, 1, 8, true, true, false>>(),    // 5
-    make_variant<Cfg<256, 1, 8, true, false, true>>(),    // 6
-    make_variant<Cfg<256, 1, 4, true, false, true>>(),    // 7
-    make_variant<Cfg<512, 1, 8, true, false, false>>(),   // 8
-    make_variant<Cfg<128, 1, 8, true, false, false>>(),   // 9
-    make_variant<Cfg<256, 2, 8, true, false, false>>(),   // 10
-    make_variant<Cfg<256, 2, 4, true, false, true>>(),    // 11
-    make_variant<Cfg<1024, 1, 8, true, false, false>>(),  // 12
-    make_variant<Cfg<256, 1, 32, true, false, false>>(),  // 13
+    make_variant<Cfg<256, 1, 8, false, false, false>>(),  // 2 plain loads
+    make_variant<Cfg<256, 1, 8, true, false, false>>(),   // 3 NT loads only
+    make_variant<Cfg<256, 1, 4, true, true, false>>(),    // 4
+    make_variant<Cfg<256, 1, 16, true, true, false>>(),   // 5
+    make_variant<Cfg<256, 1, 8, true, true, true>>(),     // 6 pipelined
+    make_variant<Cfg<256, 1, 4, true, true, true>>(),     // 7 pipelined
+    make_variant<Cfg<512, 1, 8, true, true, false>>(),    // 8
+    make_variant<Cfg<1024, 1, 8, true, true, false>>(),   // 9
+    make_variant<Cfg<256, 2, 8, true, true, false>>(),    // 10
+    make_variant<Cfg<256, 1, 32, true, true, false>>(),   // 11
+    make_variant<Cfg<64, 1, 8, true, true, false>>(),     // 12
+    make_variant<Cfg<128, 1, 16, true, true, false>>(),   // 13
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
