@@ -93,6 +93,30 @@ def max_over_ranks(value: float, world: int) -> float:
     return float(t.item())
 
 
+def pmc_traffic(alg_bytes: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload.
+
+    PMC counters cannot be read from inside a timed run; scripts/profile.sh
+    collects FETCH_SIZE / WRITE_SIZE in their own passes of this same command
+    and scripts/summarize_profile.py writes profiles/<tag>_summary.json.
+    """
+    import glob
+
+    best = None
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
+        try:
+            with open(path) as f:
+                summ = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if summ.get("algorithmic_bytes") == alg_bytes:
+            best = (path, summ)
+    if best is None:
+        return None, None
+    path, summ = best
+    return summ["pmc"]["hbm_bytes"], os.path.relpath(path, ROOT)
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -199,6 +223,7 @@ def main():
     kernel_ms_max = max_over_ranks(kernel_ms, world)
 
     value_gbs = world * alg_bytes * args.steps / wall / 1e9
+    traffic, traffic_src = pmc_traffic(alg_bytes) if (args.variant in (None, 0)) else (None, None)
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
 
     result = {
@@ -230,7 +255,9 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": traffic,
+            "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC)",
+            "traffic_source": traffic_src,
             "kernel_ms": round(kernel_ms, 4),
             "kernel_ms_max_over_ranks": round(kernel_ms_max, 4),
         },
