@@ -217,6 +217,16 @@ class FedAvgEngine:
                       _ptr(out_i64f) if n_i else None, *args_tail)
 
     # ------------------------------------------------------ host-facing API
+    def begin(self, template: Mapping[str, torch.Tensor], capacity: int) -> "AggregationRound":
+        """Start a round: device arenas for up to ``capacity`` client payloads."""
+        if capacity <= 0:
+            raise ValueError("no client payloads to aggregate")
+        layout = self._prepare(template, capacity)
+        # The previous round's kernel may still read the slab / baseline arena:
+        # order this round's H2D copies (copy stream) after it.
+        self._stager.stream.wait_stream(torch.cuda.current_stream(self.device))
+        return AggregationRound(self, layout, capacity)
+
     def stage_clients(self, payloads: Sequence[Mapping[str, torch.Tensor]], template=None,
                       what: str = "weights_received") -> ArenaLayout:
         """Pack and copy K CPU payloads into the client slab (rows 0..K-1)."""
@@ -242,20 +252,12 @@ class FedAvgEngine:
             raise ValueError("no client payloads to aggregate")
         if len(weights) != k:
             raise ValueError("weights must have one entry per client")
-        layout = self.stage_clients(weights_received, template=baseline)
-        self._stager.put(baseline, self._base.f32, self._base.i64)
-        w, s = self._upload_weights(weights, scales)
-        pf, pi = self._slab.row_pointers(range(k))
-        tf, ti = self._pointer_tables(pf, pi)
-        stream = torch.cuda.current_stream(self.device)
-        self._stager.fence(stream)
-        out_f = torch.empty(layout.row_f32, dtype=torch.float32, device=self.device)
-        out_i = torch.empty(layout.row_i64, dtype=torch.float32, device=self.device)
-        self.launch_fedavg(layout, tf, ti, w, s, k, self._base.f32, self._base.i64, out_f, out_i,
-                           stream)
-        host_f = out_f[: layout.n_f32].to("cpu")
-        host_i = out_i[: layout.n_i64].to("cpu")
-        return layout.unpack(host_f, host_i)
+        rnd = self.begin(baseline, k)
+        rnd.put_baseline(baseline)
+        for i, sd in enumerate(weights_received):
+            rnd.put_client(i, sd)
+        rnd.launch(weights, scales)
+        return rnd.result()
 
     def aggregate_deltas(self, deltas_received: Sequence[Mapping[str, torch.Tensor]],
                          weights: Sequence[float], scales: Sequence[float] | None = None
@@ -266,16 +268,11 @@ class FedAvgEngine:
             raise ValueError("no client deltas to aggregate")
         if len(weights) != k:
             raise ValueError("weights must have one entry per client")
-        layout = self.stage_clients(deltas_received, what="deltas_received")
-        w, s = self._upload_weights(weights, scales)
-        pf, pi = self._slab.row_pointers(range(k))
-        tf, ti = self._pointer_tables(pf, pi)
-        stream = torch.cuda.current_stream(self.device)
-        self._stager.fence(stream)
-        out_f = torch.empty(layout.row_f32, dtype=torch.float32, device=self.device)
-        out_i = torch.empty(layout.row_i64, dtype=torch.float32, device=self.device)
-        self.launch_fedavg(layout, tf, ti, w, s, k, None, None, out_f, out_i, stream)
-        return layout.unpack(out_f[: layout.n_f32].to("cpu"), out_i[: layout.n_i64].to("cpu"))
+        rnd = self.begin(deltas_received[0], k)
+        for i, sd in enumerate(deltas_received):
+            rnd.put_client(i, sd, what="deltas_received")
+        rnd.launch(weights, scales, deltas=True)
+        return rnd.result()
 
     def compute_weight_deltas(self, baseline: Mapping[str, torch.Tensor],
                               weights_received: Sequence[Mapping[str, torch.Tensor]]
@@ -342,6 +339,82 @@ class FedAvgEngine:
                   _ptr(self._base.f32), _ptr(self._base.i64), one_minus, m, _ptr(out_f),
                   _ptr(out_i), layout.n_f32, layout.n_i64, _stream_handle(stream))
         return layout.unpack(out_f[: layout.n_f32].to("cpu"), out_i[: layout.n_i64].to("cpu"))
+
+
+class AggregationRound:
+    """One aggregation: client rows staged H2D (in any order), then one launch.
+
+    Rows are slots; the summation order is given at :meth:`launch` time by
+    ``order`` (default: slot order), matching ``self.updates`` order in the
+    reference regardless of the order payloads arrived in.
+    """
+
+    def __init__(self, engine: FedAvgEngine, layout: ArenaLayout, capacity: int):
+        self.engine = engine
+        self.layout = layout
+        self.capacity = capacity
+        self.staged = [False] * capacity
+        self.has_baseline = False
+        self.event: torch.cuda.Event | None = None
+        self._out = None
+
+    def put_baseline(self, baseline: Mapping[str, torch.Tensor]) -> None:
+        self.layout.check_compatible(baseline, "baseline_weights")
+        eng = self.engine
+        eng._stager.put(baseline, eng._base.f32, eng._base.i64)
+        self.has_baseline = True
+
+    def put_client(self, slot: int, payload: Mapping[str, torch.Tensor],
+                   what: str = "weights_received") -> None:
+        if not 0 <= slot < self.capacity:
+            raise IndexError(f"slot {slot} outside [0, {self.capacity})")
+        self.layout.check_compatible(payload, f"{what}[{slot}]")
+        eng = self.engine
+        eng._stager.put(payload, eng._slab.f32[slot], eng._slab.i64[slot])
+        self.staged[slot] = True
+
+    def launch(self, weights: Sequence[float], scales: Sequence[float] | None = None,
+               order: Sequence[int] | None = None, deltas: bool = False) -> None:
+        """Enqueue the fused kernel (stream-ordered after every staged copy)."""
+        order = list(range(len(weights))) if order is None else list(order)
+        if len(order) != len(weights):
+            raise ValueError("order and weights must have the same length")
+        for slot in order:
+            if not (0 <= slot < self.capacity and self.staged[slot]):
+                raise ValueError(f"client slot {slot} was not staged")
+        if not deltas and not self.has_baseline:
+            raise ValueError("baseline not staged")
+        eng = self.engine
+        lay = self.layout
+        w, s = eng._upload_weights(weights, scales)
+        pf, pi = eng._slab.row_pointers(order)
+        tf, ti = eng._pointer_tables(pf, pi)
+        stream = torch.cuda.current_stream(eng.device)
+        eng._stager.fence(stream)
+        out_f = torch.empty(lay.row_f32, dtype=torch.float32, device=eng.device)
+        out_i = torch.empty(lay.row_i64, dtype=torch.float32, device=eng.device)
+        eng.launch_fedavg(lay, tf, ti, w, s, len(order), None if deltas else eng._base.f32,
+                          None if deltas else eng._base.i64, out_f, out_i, stream)
+        # D2H into fresh pinned buffers, still stream-ordered; result() only waits.
+        host_f = torch.empty(lay.n_f32, dtype=torch.float32, pin_memory=True)
+        host_i = torch.empty(lay.n_i64, dtype=torch.float32, pin_memory=True)
+        host_f.copy_(out_f[: lay.n_f32], non_blocking=True)
+        host_i.copy_(out_i[: lay.n_i64], non_blocking=True)
+        self.event = torch.cuda.Event()
+        self.event.record(stream)
+        # keep device buffers alive until the copies finish
+        self._out = (host_f, host_i, out_f, out_i, tf, ti, w, s)
+
+    def ready(self) -> bool:
+        return self.event is not None and self.event.query()
+
+    def result(self) -> "OrderedDict[str, torch.Tensor]":
+        if self.event is None:
+            raise RuntimeError("launch() first")
+        self.event.synchronize()
+        host_f, host_i = self._out[0], self._out[1]
+        self._out = None
+        return self.layout.unpack(host_f, host_i)
 
 
 def cast_to_int64(src_f32: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:

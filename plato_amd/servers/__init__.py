@@ -1,0 +1,3 @@
+"""Server-side plugin surface: GPU-backed aggregation hooks for Plato servers."""
+
+from .fedavg import DeltasAggregationMixin, FusedAggregationMixin, make_server  # noqa: F401

@@ -1,0 +1,127 @@
+"""FedAvg-family server variants on the same GPU kernel (weights differ only).
+
+Each mixin overrides :meth:`aggregation_weights` with the reference variant's
+per-client numbers (plato_amd/weights.py has the formulas and citations) and
+inherits the fused ``aggregate_weights`` hook.  Compose with the reference's
+own variant server when its other behaviour (client selection, saving models)
+is wanted, e.g. ``class Server(PortWeights, FusedAggregationMixin, port_server.Server)``.
+"""
+
+from __future__ import annotations
+
+import os
+
+from .. import weights as W
+from .fedavg import FusedAggregationMixin, _EngineHolder
+
+
+def _config_server():
+    try:
+        from plato.config import Config
+
+        return Config().server
+    except Exception:  # Plato not importable: defaults below apply
+        return None
+
+
+def _cfg(name, default):
+    server = _config_server()
+    if server is not None and hasattr(server, name):
+        return getattr(server, name)
+    return default
+
+
+class FedBuffWeights(_EngineHolder):
+    """examples/async/fedbuff/fedbuff_server.py:31-50: every update weighs 1/K."""
+
+    def aggregation_weights(self, updates):
+        return W.fedbuff(len(updates)), None
+
+
+class PortWeights(_EngineHolder):
+    """examples/async/port/port_server.py:54-124 (+ staleness_function :134-144).
+
+    The cosine-similarity term is 1.0 unless staleness > 1 and the global model
+    of round ``current_round - 2`` exists on disk (``port_server.py:28-34``);
+    that case needs the similarity reduction, which :meth:`port_similarities`
+    computes on the GPU.
+    """
+
+    def port_similarities(self, updates):
+        sims = []
+        model_path = None
+        try:
+            from plato.config import Config
+
+            model_path = f"{Config().params['model_path']}/model_{self.current_round - 2}.pth"
+        except Exception:
+            pass
+        for update in updates:
+            if update.staleness > 1 and model_path is not None and os.path.exists(model_path):
+                raise NotImplementedError(
+                    "Port cosine similarity against a stored stale model is not on the GPU path yet"
+                )
+            sims.append(1.0)
+        return sims
+
+    def aggregation_weights(self, updates):
+        self.total_samples = sum(u.report.num_samples for u in updates)
+        return W.port(
+            [u.report.num_samples for u in updates],
+            [u.staleness for u in updates],
+            similarities=self.port_similarities(updates),
+            similarity_weight=_cfg("similarity_weight", 1),
+            staleness_weight=_cfg("staleness_weight", 1),
+            staleness_bound=_cfg("staleness_bound", 10),
+        ), None
+
+
+class PiscesWeights(_EngineHolder):
+    """examples/client_selection/pisces/pisces_server.py:73-100.
+
+    ``delta * (n/N) * staleness_factor``: two successive fp32 multiplies, so
+    the factor goes to the kernel's second-scalar slot.  Appends each update's
+    staleness to ``self.client_staleness`` exactly like the reference.
+    """
+
+    def aggregation_weights(self, updates):
+        self.total_samples = sum(u.report.num_samples for u in updates)
+        exponent = getattr(self, "staleness_factor", _cfg("staleness_factor", 1))
+        histories = []
+        for update in updates:
+            hist = self.client_staleness.setdefault(update.client_id, [])
+            hist.append(update.staleness)
+            histories.append(list(hist))
+        first, second = W.pisces([u.report.num_samples for u in updates], histories, exponent)
+        return first, second
+
+
+class FedAsyncMixing(_EngineHolder):
+    """examples/async/fedasync: ``b*(1-m) + x_0*m`` with staleness-adapted m."""
+
+    mixing_hyperparam = 0.9
+    adaptive_mixing = False
+
+    async def aggregate_weights(self, updates, baseline_weights, weights_received):
+        if self.adaptive_mixing:
+            fn = _cfg("staleness_weighting_function", None)
+            if fn is None:
+                self.mixing_hyperparam = W.fedasync_mixing(self.mixing_hyperparam, updates[0].staleness)
+            else:
+                self.mixing_hyperparam = W.fedasync_mixing(
+                    self.mixing_hyperparam, updates[0].staleness, fn.type,
+                    getattr(fn, "a", 1), getattr(fn, "b", 0))
+        return self.aggregation_engine().mix_weights(baseline_weights, weights_received[0],
+                                                     self.mixing_hyperparam)
+
+
+class FedBuffServerMixin(FedBuffWeights, FusedAggregationMixin):
+    pass
+
+
+class PortServerMixin(PortWeights, FusedAggregationMixin):
+    pass
+
+
+class PiscesServerMixin(PiscesWeights, FusedAggregationMixin):
+    pass

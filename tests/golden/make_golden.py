@@ -1,0 +1,470 @@
+#!/usr/bin/env python3
+"""Generate the golden fixtures under tests/golden/ by running the REFERENCE.
+
+Run here (the build container), never on the GPU box:
+
+    python tests/golden/make_golden.py [--reference /root/reference]
+
+It imports TL-System/plato from --reference and drives its own server-side
+aggregation code on inputs made by the counter-based generator of
+oracle/synth.py (which the tests, the GPU kernels and bench.py restate bit for
+bit), then records only data: recipes, SHA-256 digests of the reference's
+outputs, sampled output values, and (for the small LeNet-5 / toy cases) full
+output arrays.  Nothing from the reference's sources is copied.
+
+Reference code paths exercised (file:line in the reference):
+  * fedavg.Server._process_reports            plato/servers/fedavg.py:161-229
+    -> Algorithm.compute_weight_deltas        plato/algorithms/fedavg.py:13-27
+    -> Server.aggregate_deltas                plato/servers/fedavg.py:137-159
+    -> Algorithm.update_weights / load_weights plato/algorithms/fedavg.py:29-48
+  * FedBuff aggregate_deltas                  examples/async/fedbuff/fedbuff_server.py:31-50
+  * Port aggregate_deltas                     examples/async/port/port_server.py:54-124
+  * Pisces aggregate_deltas                   examples/client_selection/pisces/pisces_server.py:73-99
+  * FedAsync aggregate_weights                examples/async/fedasync/fedasync_server.py:67-78,
+                                              fedasync_algorithm.py:9-20
+  * the reference's own known-answer test     tests/fedavg_tests.py:44-175
+Missing third-party packages that the reference imports but this path never
+uses (socketio, torchvision, zstd, ...) are replaced by inert module stubs.
+"""
+
+from __future__ import annotations
+
+import argparse
+import asyncio
+import copy
+import hashlib
+import importlib.abc
+import importlib.machinery
+import json
+import os
+import sys
+import tempfile
+import types
+from collections import OrderedDict
+from unittest import mock
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+
+from oracle import synth  # noqa: E402
+
+STUBBED = [
+    "socketio", "torchvision", "zstd", "lightly", "opacus", "torch_optimizer", "gym", "boto3",
+    "botocore", "evaluate", "tenseal", "cv2", "pycocotools", "skimage", "ultralytics", "h5py",
+    "timm", "mmcv", "wandb", "torchmetrics",
+]
+
+CANON_NAN = np.uint32(0x7FC00000)
+
+
+class _StubFinder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
+    """Inert modules for missing packages the aggregation path never calls."""
+
+    def find_spec(self, name, path, target=None):
+        if name.split(".")[0] in STUBBED:
+            return importlib.machinery.ModuleSpec(name, self, is_package=True)
+        return None
+
+    def create_module(self, spec):
+        mod = mock.MagicMock(name=spec.name)
+        mod.__path__ = []
+        mod.__spec__ = spec
+        return mod
+
+    def exec_module(self, module):
+        return None
+
+
+CONFIG = """
+clients:
+    type: simple
+    total_clients: 1024
+    per_round: 1024
+    do_test: false
+server:
+    address: 127.0.0.1
+    port: 8000
+    do_test: false
+    synchronous: true
+    similarity_weight: 1
+    staleness_weight: 3
+    staleness_bound: 10
+    staleness_factor: 0.5
+    exploration_factor: 0.3
+    exploration_decaying_factor: 0.99
+    min_explore_factor: 0.1
+    mixing_hyperparameter: 0.9
+    adaptive_mixing: true
+    staleness_weighting_function:
+        type: hinge
+        a: 10
+        b: 4
+data:
+    datasource: MNIST
+    partition_size: 20000
+    sampler: iid
+    random_seed: 1
+trainer:
+    type: basic
+    rounds: 1
+    max_concurrency: 1
+    epochs: 1
+    batch_size: 32
+    optimizer: SGD
+    model_name: resnet_18
+algorithm:
+    type: fedavg
+parameters:
+    model:
+        num_classes: 10
+    optimizer:
+        lr: 0.01
+        momentum: 0.9
+        weight_decay: 0.0
+"""
+
+
+def boot_reference(ref_root: str, workdir: str):
+    sys.meta_path.insert(0, _StubFinder())
+    cfg = os.path.join(workdir, "golden.yml")
+    with open(cfg, "w") as f:
+        f.write(CONFIG)
+    os.environ["config_file"] = cfg
+    sys.argv = ["make_golden", "-b", workdir]
+    sys.path.insert(0, ref_root)
+    for sub in ("examples/async/fedbuff", "examples/async/port", "examples/async/fedasync",
+                "examples/client_selection/pisces"):
+        sys.path.insert(0, os.path.join(ref_root, sub))
+    from plato.config import Config
+
+    Config()
+
+
+# --------------------------------------------------------------------------
+def canon(a: np.ndarray) -> np.ndarray:
+    a = np.ascontiguousarray(a, dtype=np.float32).copy()
+    bits = a.view(np.uint32)
+    bits[np.isnan(a)] = CANON_NAN
+    return a
+
+
+def sha(a: np.ndarray) -> str:
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def f32hex(x) -> str:
+    return "%08x" % int(np.float32(x).view(np.uint32))
+
+
+def layout_of(state_dict):
+    entries = []
+    nf = ni = 0
+    for name, t in state_dict.items():
+        if t.dtype == torch.float32:
+            entries.append((name, "f32", nf, t.numel(), list(t.shape)))
+            nf += t.numel()
+        elif t.dtype == torch.int64:
+            entries.append((name, "i64", ni, t.numel(), list(t.shape)))
+            ni += t.numel()
+        else:
+            raise TypeError(name)
+    return entries, nf, ni
+
+
+def unpack(entries, flat_f, flat_i):
+    out = OrderedDict()
+    for name, reg, off, n, shape in entries:
+        src = flat_f if reg == "f32" else flat_i
+        out[name] = src[off : off + n].reshape(shape)
+    return out
+
+
+def flatten(entries, sd, region, dtype):
+    parts = [sd[name].reshape(-1).to(dtype) for name, reg, *_ in entries if reg == region]
+    return torch.cat(parts).numpy() if parts else np.zeros(0, dtype=np.float32)
+
+
+def apply_overrides(bf, bi, xs_f, xs_i, overrides):
+    for tgt, region, idx, val in overrides:
+        if region == "f32":
+            arr = bf if tgt == "base" else xs_f[tgt]
+            arr.view(np.uint32)[idx] = np.uint32(int(val, 16))
+        else:
+            arr = bi if tgt == "base" else xs_i[tgt]
+            arr[idx] = np.int64(int(val))
+
+
+def make_model(name):
+    from plato.models import lenet5, resnet
+
+    if name == "lenet5":
+        return lenet5.Model(num_classes=10)
+    if name == "resnet18":
+        return resnet.Model.get("resnet_18", num_classes=10)
+    if name == "resnet50_200":
+        return resnet.Model.get("resnet_50", num_classes=200)
+    raise ValueError(name)
+
+
+def make_updates(num_samples, payloads, order, staleness):
+    ups = []
+    for pos, c in enumerate(order):
+        ups.append(types.SimpleNamespace(
+            client_id=c + 1,
+            report=types.SimpleNamespace(client_id=c + 1, num_samples=num_samples[c], accuracy=0.5,
+                                         training_time=0, processing_time=0, comm_time=0,
+                                         update_response=False, statistical_utility=1.0,
+                                         start_round=0),
+            payload=payloads[c],
+            staleness=staleness[c],
+        ))
+    return ups
+
+
+def server_class(mode):
+    if mode == "fedavg":
+        from plato.servers import fedavg
+        return fedavg.Server
+    if mode == "fedbuff":
+        import fedbuff_server
+        return fedbuff_server.Server
+    if mode == "port":
+        import port_server
+        return port_server.Server
+    if mode == "pisces":
+        import pisces_server
+        return pisces_server.Server
+    if mode == "fedasync":
+        import fedasync_server
+        return fedasync_server.Server
+    raise ValueError(mode)
+
+
+def run_case(case):
+    """Run the reference on one recipe; return the recorded outputs."""
+    model = make_model(case["model"])
+    entries, nf, ni = layout_of(model.state_dict())
+    k, seed = case["k"], case["seed"]
+    bf, bi = synth.baseline_arena(nf, ni, seed)
+    xs = [synth.client_arena(bf, bi, seed, c) for c in range(k)]
+    xs_f = [x[0] for x in xs]
+    xs_i = [x[1] for x in xs]
+    apply_overrides(bf, bi, xs_f, xs_i, case.get("overrides", []))
+    baseline = unpack(entries, torch.from_numpy(bf), torch.from_numpy(bi))
+    payloads = [unpack(entries, torch.from_numpy(xs_f[c]), torch.from_numpy(xs_i[c]))
+                for c in range(k)]
+    order = case.get("order", list(range(k)))
+    staleness = case.get("staleness", [0] * k)
+    mode = case.get("mode", "fedavg")
+
+    cls = server_class(mode)
+    if mode == "fedasync":
+        from fedasync_algorithm import Algorithm as FedAsyncAlgorithm
+
+        server = cls(model=lambda: model, algorithm=FedAsyncAlgorithm)
+        server.init_trainer()
+        # what FedAsync's configure() reads from the config (fedasync_server.py:37-65)
+        server.mixing_hyperparam = 0.9
+        server.adaptive_mixing = True
+    else:
+        server = cls(model=lambda: model)
+        server.init_trainer()
+    if mode == "pisces":
+        server.client_staleness = {c + 1: [] for c in range(k)}
+    server.algorithm.load_weights(copy.deepcopy(baseline))
+    server.updates = make_updates(case["num_samples"], payloads, order, staleness)
+    server.current_round = case.get("current_round", 0)
+
+    captured = {}
+    orig_agg = server.aggregate_deltas if mode != "fedasync" else None
+    if orig_agg is not None:
+        async def spy_agg(updates, deltas):
+            avg = await orig_agg(updates, deltas)
+            captured["avg"] = {n: t.clone() for n, t in avg.items()}
+            return avg
+        server.aggregate_deltas = spy_agg
+    orig_load = server.algorithm.load_weights
+
+    def spy_load(weights):
+        captured["updated"] = OrderedDict((n, t.clone()) for n, t in weights.items())
+        return orig_load(weights)
+    server.algorithm.load_weights = spy_load
+
+    if mode in ("fedavg", "fedbuff", "port", "fedasync"):
+        asyncio.run(server._process_reports())
+    else:  # pisces: drive the hot path directly (its weights_aggregated needs client selection state)
+        weights_received = [u.payload for u in server.updates]
+        base_w = server.algorithm.extract_weights()
+        deltas = server.algorithm.compute_weight_deltas(base_w, weights_received)
+        avg = asyncio.run(server.aggregate_deltas(server.updates, deltas))
+        server.algorithm.load_weights(server.algorithm.update_weights(avg))
+
+    loaded = model.state_dict()
+    upd = captured["updated"]
+    out = {
+        "layout": {"n_f32": nf, "n_i64": ni, "tensors": len(entries)},
+        "updated_f32_sha256": sha(canon(flatten(entries, upd, "f32", torch.float32))),
+        "updated_i64f_sha256": sha(canon(flatten(entries, upd, "i64", torch.float32))),
+        "loaded_i64_sha256": sha(flatten(entries, loaded, "i64", torch.int64)),
+    }
+    uf = flatten(entries, upd, "f32", torch.float32)
+    rng = np.random.default_rng(1234)
+    idx = np.unique(np.concatenate([np.arange(min(64, nf)), rng.integers(0, nf, 192), [nf - 1]]))
+    out["samples_f32"] = [[int(i), f32hex(uf[i])] for i in idx]
+    ui = flatten(entries, upd, "i64", torch.float32)
+    out["samples_i64f"] = [[int(i), f32hex(ui[i])] for i in range(min(ni, 64))]
+    li = flatten(entries, loaded, "i64", torch.int64)
+    out["samples_loaded_i64"] = [[int(i), int(li[i])] for i in range(min(ni, 64))]
+    if "avg" in captured:
+        out["avg_f32_sha256"] = sha(canon(flatten(entries, captured["avg"], "f32", torch.float32)))
+        out["avg_i64f_sha256"] = sha(canon(flatten(entries, captured["avg"], "i64", torch.float32)))
+    if case.get("full"):
+        out["_full"] = {"updated_f32": uf, "updated_i64f": ui, "loaded_i64": li}
+        if "avg" in captured:
+            out["_full"]["avg_f32"] = flatten(entries, captured["avg"], "f32", torch.float32)
+    return out, entries
+
+
+def cases():
+    c2_ns = synth.num_samples(128, 0)
+    ovr_edge = [
+        [3, "f32", 5, "7fc00000"],    # NaN in one client
+        [1, "f32", 6, "7f800000"],    # +Inf
+        [2, "f32", 7, "ff800000"],    # -Inf
+        ["base", "f32", 8, "00000001"],  # smallest denormal baseline
+        [0, "f32", 8, "80000003"],    # denormal client
+        ["base", "f32", 9, "80000000"],  # -0 baseline
+        [0, "f32", 9, "00000000"],
+        [1, "f32", 9, "80000000"],
+        [4, "f32", 10, "7f7fffff"],   # FLT_MAX -> overflow in the sum
+        [5, "f32", 10, "7f7fffff"],
+        ["base", "f32", 11, "3f800000"],
+        [0, "f32", 11, "3f800001"],   # 1 ulp deltas
+        [6, "f32", 12, "00800000"],   # FLT_MIN normal
+    ]
+    ovr_i64 = [
+        ["base", "i64", 0, str(2**40 + 3)], [0, "i64", 0, str(2**40 + 11)],
+        [1, "i64", 0, str(2**40 + 1)], [2, "i64", 0, str(2**40 - 7)], [3, "i64", 0, str(2**40 + 3)],
+        [4, "i64", 0, str(2**40 + 5)],
+        ["base", "i64", 1, "5000"], [0, "i64", 1, "4000"], [1, "i64", 1, "3"], [2, "i64", 1, "-20"],
+        ["base", "i64", 2, str(2**24 + 1)], [3, "i64", 2, str(2**24 + 2**20)],
+        ["base", "i64", 3, str(-1)], [1, "i64", 3, str(2**63 - 1)],  # int64 wrap in x - b
+    ]
+    return [
+        dict(name="C1_lenet5_k10_iid", model="lenet5", k=10, seed=1, num_samples=[20000] * 10, full=True),
+        dict(name="lenet5_k10_skewed", model="lenet5", k=10, seed=2,
+             num_samples=synth.num_samples(10, 2), full=True),
+        dict(name="lenet5_k7_edge_values", model="lenet5", k=7, seed=9,
+             num_samples=[300, 10, 7, 1000, 55, 55, 2], overrides=ovr_edge, full=True),
+        dict(name="resnet18_k16", model="resnet18", k=16, seed=3, num_samples=synth.num_samples(16, 3)),
+        dict(name="resnet18_k16_permuted", model="resnet18", k=16, seed=3,
+             num_samples=synth.num_samples(16, 3), order=[5, 0, 15, 3, 2, 9, 1, 14, 4, 8, 11, 7, 6, 13, 10, 12]),
+        dict(name="resnet18_k1", model="resnet18", k=1, seed=5, num_samples=[777]),
+        dict(name="resnet18_k5_int64_edges", model="resnet18", k=5, seed=6,
+             num_samples=[10, 20, 30, 40, 50], overrides=ovr_i64),
+        dict(name="C2_resnet18_k128", model="resnet18", k=128, seed=0, num_samples=c2_ns),
+        dict(name="C2_resnet18_k128_equal", model="resnet18", k=128, seed=0, num_samples=[1000] * 128),
+        dict(name="C3_resnet50_200cls_k8", model="resnet50_200", k=8, seed=4,
+             num_samples=synth.num_samples(8, 4)),
+        dict(name="fedbuff_resnet18_k16", model="resnet18", k=16, seed=7, mode="fedbuff",
+             num_samples=synth.num_samples(16, 7)),
+        dict(name="port_resnet18_k16", model="resnet18", k=16, seed=8, mode="port",
+             num_samples=synth.num_samples(16, 8), staleness=[i % 11 for i in range(16)]),
+        dict(name="pisces_resnet18_k8", model="resnet18", k=8, seed=10, mode="pisces",
+             num_samples=synth.num_samples(8, 10), staleness=[0, 1, 2, 3, 5, 8, 13, 1]),
+        dict(name="fedasync_resnet18_k1", model="resnet18", k=1, seed=12, mode="fedasync",
+             num_samples=[500], staleness=[7]),
+        dict(name="C4_port_resnet18_k256", model="resnet18", k=256, seed=13, mode="port",
+             num_samples=synth.num_samples(256, 13), staleness=[(7 * i) % 11 for i in range(256)]),
+    ]
+
+
+def dump_shapes(out_dir):
+    for name in ("lenet5", "resnet18", "resnet50_200"):
+        sd = make_model(name).state_dict()
+        spec = [[k, list(v.shape), "f32" if v.dtype == torch.float32 else "i64"] for k, v in sd.items()]
+        with open(os.path.join(out_dir, f"shapes_{name}.json"), "w") as f:
+            json.dump(spec, f)
+
+
+def run_reference_known_answer(ref_root):
+    """tests/fedavg_tests.py's aggregation: record the 4 payloads and the server model after FedAvg."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("ref_fedavg_tests",
+                                                  os.path.join(ref_root, "tests", "fedavg_tests.py"))
+    # The test module re-points config_file at its own yml; keep ours.
+    saved = os.environ["config_file"]
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    os.environ["config_file"] = saved
+    from plato.servers import fedavg as fedavg_server
+
+    captured = {}
+    orig = fedavg_server.Server.aggregate_deltas
+
+    async def spy(self, updates, deltas):
+        captured["payloads"] = [copy.deepcopy(u.payload) for u in updates]
+        captured["num_samples"] = [u.report.num_samples for u in updates]
+        captured["server"] = self
+        return await orig(self, updates, deltas)
+
+    fedavg_server.Server.aggregate_deltas = spy
+    try:
+        test = mod.FedAvgTest("test_fedavg_aggregation")
+        test.setUp()
+        test.test_fedavg_aggregation()
+    finally:
+        fedavg_server.Server.aggregate_deltas = orig
+    server_model = captured["server"].trainer.model
+    result = {
+        "source": "reference tests/fedavg_tests.py:44-175 (aggregated server model, never asserted there)",
+        "num_samples": captured["num_samples"],
+        "baseline": {"layer.weight": [f32hex(v) for v in np.arange(10, dtype=np.float32)],
+                     "head.weight": [f32hex(1.0)]},
+        "payloads": [{n: [f32hex(v) for v in t.reshape(-1).numpy()] for n, t in p.items()}
+                     for p in captured["payloads"]],
+        "aggregated": {n: [f32hex(v) for v in t.reshape(-1).numpy()]
+                       for n, t in server_model.state_dict().items()},
+    }
+    return result
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reference", default="/root/reference")
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+    workdir = tempfile.mkdtemp(prefix="golden_")
+    boot_reference(args.reference, workdir)
+    os.chdir(workdir)
+    dump_shapes(HERE)
+    ka = run_reference_known_answer(args.reference)
+    with open(os.path.join(HERE, "known_answer_fedavg_tests.json"), "w") as f:
+        json.dump(ka, f, indent=1)
+    results = []
+    full = {}
+    for case in cases():
+        if args.only and case["name"] != args.only:
+            continue
+        print("case", case["name"], flush=True)
+        out, _ = run_case(case)
+        arrays = out.pop("_full", None)
+        if arrays:
+            for key, arr in arrays.items():
+                full[f"{case['name']}/{key}"] = arr
+        results.append({"recipe": case, "expected": out})
+    with open(os.path.join(HERE, "fedavg_cases.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py", "synth": "oracle/synth.py",
+                   "nan_policy": "NaN outputs canonicalised to 0x7fc00000 before hashing",
+                   "cases": results}, f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "fedavg_full_small.npz"), **full)
+    print("wrote", len(results), "cases")
+
+
+if __name__ == "__main__":
+    main()
