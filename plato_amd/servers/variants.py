@@ -64,15 +64,24 @@ class PortWeights(_EngineHolder):
             sims.append(1.0)
         return sims
 
+    #: Port hyper-parameters; None = Config().server.<name>, else the reference default
+    similarity_weight = None
+    staleness_weight = None
+    staleness_bound = None
+
+    def _port_param(self, name, default):
+        value = getattr(self, name)
+        return _cfg(name, default) if value is None else value
+
     def aggregation_weights(self, updates):
         self.total_samples = sum(u.report.num_samples for u in updates)
         return W.port(
             [u.report.num_samples for u in updates],
             [u.staleness for u in updates],
             similarities=self.port_similarities(updates),
-            similarity_weight=_cfg("similarity_weight", 1),
-            staleness_weight=_cfg("staleness_weight", 1),
-            staleness_bound=_cfg("staleness_bound", 10),
+            similarity_weight=self._port_param("similarity_weight", 1),
+            staleness_weight=self._port_param("staleness_weight", 1),
+            staleness_bound=self._port_param("staleness_bound", 10),
         ), None
 
 
