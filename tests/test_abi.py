@@ -1,0 +1,72 @@
+"""The C-ABI library loads on the CPU host and exports exactly what include/*.h declares."""
+
+import ctypes
+import glob
+import os
+import re
+
+import pytest
+
+from plato_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    names = set()
+    for header in glob.glob(os.path.join(ROOT, "include", "*.h")):
+        text = open(header).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        names.update(re.findall(r"\b(plato_agg_\w+)\s*\(", text))
+    return names
+
+
+def test_headers_declare_the_boundary():
+    names = declared_symbols()
+    for required in ("plato_agg_fedavg_weights", "plato_agg_fedavg_deltas", "plato_agg_compute_deltas",
+                     "plato_agg_update_weights", "plato_agg_cast_f32_i64", "plato_agg_mix_weights",
+                     "plato_agg_last_error", "plato_agg_abi_version"):
+        assert required in names
+
+
+def test_library_exports_every_declared_symbol():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built (run __graft_entry__.build())")
+    handle = ctypes.CDLL(_lib.LIB_PATH)
+    for name in declared_symbols():
+        assert hasattr(handle, name), name
+    # and the Python binding knows the signature of each
+    assert declared_symbols() == set(_lib.SIGNATURES)
+
+
+def test_binding_loads_and_reports_abi():
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    lib = _lib.lib()
+    assert lib.plato_agg_abi_version() == _lib.ABI_VERSION
+    assert lib.plato_agg_tune_num_variants() >= 1
+
+
+def test_argument_errors_are_raised_without_gpu_work():
+    """Invalid arguments are rejected on the host (no launch), mapped to ValueError."""
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("library not built")
+    with pytest.raises(ValueError, match="K must be"):
+        _lib.call("plato_agg_fedavg_weights", None, None, None, None, 0, None, None, None, None, 16, 0, None)
+    with pytest.raises(ValueError, match="null"):
+        _lib.call("plato_agg_fedavg_weights", None, None, 8, None, 2, None, None, None, None, 16, 0, None)
+    with pytest.raises(ValueError, match="aligned"):
+        _lib.call("plato_agg_fedavg_weights", 8, None, 8, None, 2, 4, None, 4, None, 16, 0, None)
+    with pytest.raises(ValueError, match="modulus"):
+        _lib.call("plato_agg_fill_synth_i64", 8, None, 4, 0, 0, 0, None)
+
+
+def test_engine_refuses_without_gpu():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from plato_amd.engine import FedAvgEngine
+
+    with pytest.raises(RuntimeError, match="no ROCm GPU"):
+        FedAvgEngine()

@@ -1,0 +1,68 @@
+"""Multi-rank paths: bucket plan, gloo world_size-2 runs of the sharding logic."""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+from plato_amd.distributed import BucketPlan, client_shard
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _run(mode, world, tmp_path, timeout=300):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "dist_worker.py"), mode, str(tmp_path)]
+    env = dict(os.environ, OMP_NUM_THREADS="2", PYTHONPATH=ROOT)
+    proc = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    return [json.load(open(os.path.join(tmp_path, f"rank{r}.json"))) for r in range(world)]
+
+
+@pytest.mark.parametrize("n_f32,world", [(61706, 1), (61706, 2), (61706, 3), (11183562, 8), (10, 8), (0, 2)])
+def test_bucket_plan_covers_arena_once(n_f32, world):
+    plan = BucketPlan.make(n_f32, 20, world)
+    assert plan.per % 64 == 0
+    seen = 0
+    for r in range(world):
+        lo, hi = plan.f32_range(r)
+        assert lo == min(seen, n_f32) and hi - lo <= plan.per
+        seen = hi
+    assert seen == n_f32
+    assert plan.i64_range(0) == (0, 20) and all(plan.i64_range(r) == (0, 0) for r in range(1, world))
+    assert sum(plan.bucket_bytes(r, 5) for r in range(world)) == 7 * (n_f32 * 4 + 20 * 8)
+
+
+def test_client_shard_partition():
+    shards = [client_shard(10, 3, r) for r in range(3)]
+    assert sorted(sum(shards, [])) == list(range(10))
+
+
+def test_gloo_bucket_sharding_bit_exact(tmp_path):
+    outs = _run("cpu-bucket", 2, tmp_path)
+    assert all(o["bit_exact"] for o in outs)
+
+
+def test_gloo_client_sharding_normwise(tmp_path):
+    outs = _run("cpu-client", 2, tmp_path)
+    for o in outs:
+        assert o["normwise"] <= 1e-6, o
+
+
+@pytest.mark.gpu
+def test_two_ranks_bucket_aggregator_on_gpu(tmp_path):
+    outs = _run("gpu-bucket", 2, tmp_path)
+    for o in outs:
+        assert o["f32_match"] and o["i64_match"], o
