@@ -39,8 +39,9 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--clients", type=int, default=128)
-    p.add_argument("--model", default="resnet18", choices=["resnet18", "resnet50", "lenet5", "vit"])
+    p.add_argument("--config", default="C2", choices=sorted(CONFIGS),
+                   help="BASELINE.json configuration (C2 = the headline metric's workload)")
+    p.add_argument("--clients", type=int, default=None, help="override K")
     p.add_argument("--variant", type=int, default=None, help="kernel variant (tuning)")
     p.add_argument("--sweep", action="store_true", help="time every kernel variant, interleaved")
     p.add_argument("--seed", type=int, default=0)
@@ -50,14 +51,29 @@ def parse():
     return p.parse_args()
 
 
+# name -> (model, K, scaling).  "weak": each rank aggregates its own
+# model-sized parameter bucket (per-GPU work fixed, the C2/C4 one-GPU configs);
+# "strong": one model is bucket-sharded across the ranks (C3, C5).
+CONFIGS = {
+    "C1": ("lenet5", 10, "weak"),
+    "C2": ("resnet18", 128, "weak"),
+    "C3": ("resnet50_200", 1024, "strong"),
+    "C4": ("resnet18", 256, "weak"),
+    "C5": ("vit_large", 32, "strong"),
+    "C5-gpt2": ("gpt2_medium", 32, "strong"),
+}
+BASELINE_METRIC = "aggregated GB/s (device-resident), K-client ResNet-18 FedAvg at 1/2/4/8 GPUs"
+
+
 def model_spec(name):
     from plato_amd import workloads
 
     return {
         "resnet18": lambda: workloads.resnet(18, 10),
-        "resnet50": lambda: workloads.resnet(50, 200),
+        "resnet50_200": lambda: workloads.resnet(50, 200),
         "lenet5": lambda: workloads.lenet5(10),
-        "vit": lambda: workloads.vit_large(),
+        "vit_large": lambda: workloads.vit_large(),
+        "gpt2_medium": lambda: workloads.gpt2_medium(),
     }[name]()
 
 
@@ -138,24 +154,38 @@ def main():
     from plato_amd.engine import ClientSlab, DeviceArena, FedAvgEngine
     from plato_amd.synthetic import fill_baseline, fill_clients
 
-    spec = model_spec(args.model)
-    layout = ArenaLayout.from_shapes(spec)
-    k = args.clients
-    seed = args.seed + rank  # each rank owns a different bucket of the global model
+    model, k_default, scaling = CONFIGS[args.config]
+    k = args.clients or k_default
+    full_layout = ArenaLayout.from_shapes(model_spec(model))
+    if scaling == "strong" and world > 1:
+        # one model, parameter-bucket sharded: this rank holds bucket `rank`
+        from plato_amd.distributed import BucketPlan
+
+        plan = BucketPlan.for_layout(full_layout, world)
+        lo, hi = plan.f32_range(rank)
+        a, b = plan.i64_range(rank)
+        layout = ArenaLayout([], hi - lo, b - a)
+        job_bytes = full_layout.algorithmic_bytes(k)
+    else:
+        layout = full_layout
+        job_bytes = world * full_layout.algorithmic_bytes(k)
+    seed = args.seed + rank  # distinct synthetic data per bucket
     engine = FedAvgEngine(dev, variant=args.variant)
 
     base = DeviceArena(layout, dev)
     slab = ClientSlab(layout, k, dev)
     fill_baseline(base, seed)
     fill_clients(slab, base, seed, k)
-    sys.path.insert(0, ROOT)
-    from oracle import synth  # noqa: E402  (num_samples recipe; weights are host data)
 
-    ns = synth.num_samples(k, seed)
-    total = sum(ns)
-    weights = [n / total for n in ns]
+    from plato_amd import synthetic
+    from plato_amd import weights as W
     from plato_amd.engine import fp32_weights
 
+    ns = synthetic.num_samples(k, seed)
+    if args.config == "C4":  # async staleness-weighted (Port, examples/async/port/port_cifar10.yml)
+        weights = W.port(ns, synthetic.staleness(k, seed), similarity_weight=1, staleness_weight=3)
+    else:
+        weights = W.fedavg(ns)
     w = torch.from_numpy(fp32_weights(weights)).to(dev)
     pf, pi = slab.row_pointers(range(k))
     tf = torch.from_numpy(pf).to(dev)
@@ -222,12 +252,12 @@ def main():
     kernel_ms = ev0.elapsed_time(ev1) / args.steps
     kernel_ms_max = max_over_ranks(kernel_ms, world)
 
-    value_gbs = world * alg_bytes * args.steps / wall / 1e9
+    value_gbs = job_bytes * args.steps / wall / 1e9
     traffic, traffic_src = pmc_traffic(alg_bytes) if (args.variant in (None, 0)) else (None, None)
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
 
     result = {
-        "metric": "aggregated GB/s (device-resident), K-client ResNet-18 FedAvg",
+        "metric": BASELINE_METRIC,
         "value": round(value_gbs, 2),
         "unit": "GB/s",
         "n_gpus": world,
@@ -235,17 +265,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(wall / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (counter-based generator, SURVEY.md §8(d) C2 distributions)",
         "config": {
-            "workload": f"C2: {k} x {args.model} client updates per GPU, fused FedAvg "
-                        "(deltas -> weighted sum -> update), parameter-bucket shard per rank",
+            "workload": f"{args.config}: {k} x {model} client updates, fused FedAvg "
+                        "(deltas -> weighted sum -> update), inputs resident in HBM; "
+                        + ("each rank aggregates its own model-sized parameter bucket"
+                           if scaling == "weak" else f"one model bucket-sharded over {world} GPU(s)"),
             "clients": k,
-            "params_f32": layout.n_f32,
-            "params_i64": layout.n_i64,
+            "params_f32_per_gpu": layout.n_f32,
+            "params_i64_per_gpu": layout.n_i64,
             "algorithmic_bytes_per_step_per_gpu": alg_bytes,
+            "algorithmic_bytes_per_step_job": job_bytes,
             "parallelism": f"bucket{world}",
             "kernel_variant": args.variant if args.variant is not None else 0,
         },
@@ -267,7 +300,8 @@ def main():
         result["host_inclusive"] = host_inclusive(engine, layout, base, slab, k, weights, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(layout, base, slab, k, ns, out_f, out_i, args.cpu_reps)
+        result["cpu_baseline"] = cpu_baseline(layout, base, slab, k, weights, out_f, out_i, args.cpu_reps,
+                                              args.config)
         result["parity"] = result["cpu_baseline"].pop("parity")
 
     if rank == 0:
@@ -290,6 +324,8 @@ def _host_state_dicts(layout, base, slab, k):
 
 def host_inclusive(engine, layout, base, slab, k, weights, dev):
     """CPU state_dicts in -> CPU state_dict out through the engine (pack, H2D, kernel, D2H)."""
+    if k * (layout.n_f32 * 4 + layout.n_i64 * 8) > 16e9:
+        return None  # would need the whole job's payloads in host memory
     baseline, payloads = _host_state_dicts(layout, base, slab, k)
     times = []
     for _ in range(3):
@@ -304,38 +340,49 @@ def host_inclusive(engine, layout, base, slab, k, weights, dev):
             "note": "pack CPU state_dicts -> pinned -> H2D -> kernel -> D2H; median of 2 after 1 warm-up"}
 
 
-def cpu_baseline(layout, base, slab, k, ns, out_f, out_i, reps):
-    """Reference op sequence (oracle port) on the host, same inputs; bit-checks the GPU result."""
+def cpu_baseline(layout, base, slab, k, weights, out_f, out_i, reps, config):
+    """Reference op sequence (oracle port) on the host on a bounded sample of the job.
+
+    The sample is the first k_s clients of the same device inputs (all K for
+    C2), sized to ~6 GB of client payload so the leg stays within tens of
+    seconds; the GPU result is checked bit for bit when k_s == K.
+    """
     from oracle import fedavg_oracle as ref
 
-    baseline, payloads = _host_state_dicts(layout, base, slab, k)
+    per_client = layout.n_f32 * 4 + layout.n_i64 * 8
+    k_s = max(1, min(k, int(6e9 // max(per_client, 1))))
+    baseline, payloads = _host_state_dicts(layout, base, slab, k_s)
+    w_s = weights[:k_s]
     threads = torch.get_num_threads()
     times = []
     upd = None
     for r in range(reps + 1):
         t0 = time.perf_counter()
-        upd = ref.fedavg_torch_ops(baseline, payloads, num_samples=ns)
+        upd = ref.fedavg_torch_ops(baseline, payloads, weights=w_s)
         dt = time.perf_counter() - t0
         if r:
             times.append(dt)
     med = statistics.median(times)
-    gpu_f = out_f[: layout.n_f32].cpu()
-    gpu_i = out_i[: layout.n_i64].cpu()
-    exp_f = torch.cat([upd[e.name].reshape(-1) for e in layout.entries if e.region == "f32"])
-    exp_i = torch.cat([upd[e.name].reshape(-1) for e in layout.entries if e.region == "i64"]) \
-        if layout.n_i64 else torch.empty(0)
-    exact = bool(torch.equal(gpu_f.view(torch.int32), exp_f.view(torch.int32))
-                 and torch.equal(gpu_i.view(torch.int32), exp_i.view(torch.int32)))
+    parity = "not checked (sampled subset of clients)"
+    if k_s == k:
+        gpu_f = out_f[: layout.n_f32].cpu()
+        gpu_i = out_i[: layout.n_i64].cpu()
+        exp_f = torch.cat([upd[e.name].reshape(-1) for e in layout.entries if e.region == "f32"])
+        exp_i = torch.cat([upd[e.name].reshape(-1) for e in layout.entries if e.region == "i64"]) \
+            if layout.n_i64 else torch.empty(0)
+        exact = bool(torch.equal(gpu_f.view(torch.int32), exp_f.view(torch.int32))
+                     and torch.equal(gpu_i.view(torch.int32), exp_i.view(torch.int32)))
+        parity = "bit-exact vs CPU reference op sequence" if exact else "MISMATCH vs CPU reference"
     return {
-        "value": round(layout.algorithmic_bytes(k) / med / 1e9, 3),
+        "value": round(layout.algorithmic_bytes(k_s) / med / 1e9, 3),
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"full C2 job ({k} clients x {layout.n_f32 + layout.n_i64} params): torch CPU op "
-                  f"sequence sub->mul->add_->add of the reference, median of {reps} after 1 warm-up, "
-                  f"{threads} threads on {cpu_model()} (nproc {os.cpu_count()})",
+        "sample": f"{config}: {k_s} of {k} clients x {layout.n_f32 + layout.n_i64} params; the "
+                  f"reference's torch CPU op sequence sub->mul->add_->add per tensor, median of {reps} "
+                  f"after 1 warm-up, {threads} threads on {cpu_model()} (nproc {os.cpu_count()})",
         "ms": round(med * 1e3, 1),
-        "parity": "bit-exact vs CPU reference op sequence" if exact else "MISMATCH vs CPU reference",
+        "parity": parity,
     }
 
 

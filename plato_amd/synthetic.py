@@ -26,6 +26,38 @@ I64_BASE_MOD = 10001
 I64_CLIENT_MOD = 9
 
 
+def _splitmix64(z: int) -> int:
+    mask = (1 << 64) - 1
+    z = (z + 0x9E3779B97F4A7C15) & mask
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & mask
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & mask
+    return z ^ (z >> 31)
+
+
+def num_samples(k: int, seed: int, equal: bool = False) -> list[int]:
+    """Synthetic ``report.num_samples`` per client: int(1000 * U(0.1, 2.0)).
+
+    A Dirichlet-partition analogue (plato/samplers/dirichlet.py:47-60); same
+    counter generator (stream 0xFFFF) as the payloads.
+    """
+    if equal:
+        return [1000] * k
+    mask = (1 << 64) - 1
+    key = _splitmix64((seed ^ ((0xFFFF * 0xD1B54A32D192ED03) & mask)) & mask)
+    out = []
+    for c in range(k):
+        u = (_splitmix64((key + c) & mask) >> 11) * (2.0**-53)
+        out.append(int(1000 * (0.1 + 1.9 * u)))
+    return out
+
+
+def staleness(k: int, seed: int, bound: int = 10) -> list[int]:
+    """Synthetic staleness in U{0..bound} per client (C4 async workloads)."""
+    mask = (1 << 64) - 1
+    key = _splitmix64((seed ^ ((0xFFFE * 0xD1B54A32D192ED03) & mask)) & mask)
+    return [_splitmix64((key + c) & mask) % (bound + 1) for c in range(k)]
+
+
 def _h(stream) -> int:
     return stream.cuda_stream
 

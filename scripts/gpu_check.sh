@@ -22,6 +22,7 @@ for step in "$@"; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     sweep) run sweep 600 python bench.py --sweep --steps 10 --no-cpu-baseline --no-host-inclusive ;;
     bench) run bench 900 python bench.py ;;
+    configs) for c in C1 C3 C4 C5 C5-gpt2; do run bench_$c 600 python bench.py --config $c --steps 10 --warmup 3; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
