@@ -1,0 +1,123 @@
+"""Run the product's server hooks inside the REAL reference server (CPU, this container).
+
+Launched as a subprocess by tests/test_reference_integration.py, only where
+/root/reference exists.  It boots TL-System/plato like the fixture generator
+does, builds ``class Server(FusedAggregationMixin, plato.servers.fedavg.Server)``
+and lets the reference's own ``_process_reports`` (plato/servers/fedavg.py:161)
+dispatch to the product hook, call ``algorithm.load_weights`` and fire its
+callbacks.  No GPU exists here, so the engine is replaced by a test double with
+the same begin/put/launch/ready/result API whose arithmetic is the oracle; the
+point is the wiring (hook signature, dispatch, returned dict, load_weights
+truncation, total_samples), the numerics are covered on the GPU.
+"""
+
+import asyncio
+import json
+import os
+import sys
+import tempfile
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+import make_golden as MG  # noqa: E402  (boot helpers: stubs + config)
+from oracle import fedavg_oracle as ref  # noqa: E402
+from oracle import synth  # noqa: E402
+from plato_amd.arena import ArenaLayout  # noqa: E402
+
+
+class OracleRound:
+    def __init__(self, layout, capacity):
+        self.layout, self.slots, self.base = layout, {}, None
+
+    def put_baseline(self, sd):
+        self.base = sd
+
+    def put_client(self, slot, sd, what=None):
+        self.slots[slot] = sd
+
+    def launch(self, weights, scales=None, order=None, deltas=False):
+        flat = lambda sd, r: torch.cat([sd[e.name].reshape(-1) for e in self.layout.entries if e.region == r])  # noqa
+        xs = [self.slots[i] for i in range(len(weights))]
+        bf = flat(self.base, "f32").numpy()
+        bi = flat(self.base, "i64").numpy()
+        nf, ni = ref.fedavg_numpy(bf, bi, [flat(x, "f32").numpy() for x in xs],
+                                  [flat(x, "i64").numpy() for x in xs], weights, scales)
+        self.out = self.layout.unpack(torch.from_numpy(nf), torch.from_numpy(ni))
+
+    def ready(self):
+        return True
+
+    def result(self):
+        return self.out
+
+
+class OracleEngine:
+    def begin(self, template, capacity):
+        return OracleRound(ArenaLayout.from_state_dict(template), capacity)
+
+
+def main():
+    out_path = sys.argv[1]
+    workdir = tempfile.mkdtemp(prefix="refint_")
+    MG.boot_reference(os.environ.get("PLATO_REFERENCE", "/root/reference"), workdir)
+    os.chdir(workdir)
+    from plato.servers import fedavg
+
+    from plato_amd.servers import FusedAggregationMixin
+
+    calls = {"hook": 0, "load": 0, "cb_received": 0, "cb_aggregated": 0}
+
+    class Server(FusedAggregationMixin, fedavg.Server):
+        def aggregation_engine(self):
+            calls["hook"] += 1
+            return OracleEngine()
+
+    model = MG.make_model("resnet18")
+    server = Server(model=lambda: model)
+    server.init_trainer()
+    entries, nf_, ni_ = MG.layout_of(model.state_dict())
+    k, seed = 6, 31
+    bf, bi = synth.baseline_arena(nf_, ni_, seed)
+    xs = [synth.client_arena(bf, bi, seed, c) for c in range(k)]
+    baseline = MG.unpack(entries, torch.from_numpy(bf), torch.from_numpy(bi))
+    payloads = [MG.unpack(entries, torch.from_numpy(x[0]), torch.from_numpy(x[1])) for x in xs]
+    server.algorithm.load_weights({n: t.clone() for n, t in baseline.items()})
+    ns = synth.num_samples(k, seed)
+    server.updates = MG.make_updates(ns, payloads, list(range(k)), [0] * k)
+    orig_load = server.algorithm.load_weights
+
+    def spy_load(w):
+        calls["load"] += 1
+        calls["load_dtypes"] = sorted({str(t.dtype) for t in w.values()})
+        return orig_load(w)
+
+    server.algorithm.load_weights = spy_load
+
+    class CB:
+        def __getattr__(self, name):
+            def f(*a, **kw):
+                if name == "on_weights_received":
+                    calls["cb_received"] += 1
+                if name == "on_weights_aggregated":
+                    calls["cb_aggregated"] += 1
+            return f
+
+    server.callback_handler.add_callbacks([CB()])
+    asyncio.run(server._process_reports())
+    state = model.state_dict()
+    exp = ref.fedavg_torch_ops(baseline, payloads, num_samples=ns)
+    same = all(torch.equal(state[n], exp[n].to(state[n].dtype)) for n in state)
+    calls["model_matches_reference_chain"] = bool(same)
+    calls["total_samples"] = server.total_samples == sum(ns)
+    with open(out_path, "w") as f:
+        json.dump(calls, f)
+
+
+if __name__ == "__main__":
+    main()

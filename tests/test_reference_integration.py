@@ -1,0 +1,32 @@
+"""The product's aggregate_weights hook inside the real reference server (CPU wiring test).
+
+Runs only where TL-System/plato is present (this build container); see
+tests/ref_integration.py.  Numerics of the same hook on the GPU are covered by
+tests/test_golden_gpu.py::test_server_hooks_match_reference.
+"""
+
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REFERENCE = os.environ.get("PLATO_REFERENCE", "/root/reference")
+
+
+@pytest.mark.skipif(not os.path.isdir(os.path.join(REFERENCE, "plato")), reason="reference not present")
+def test_hook_dispatch_in_reference_process_reports(tmp_path):
+    out = tmp_path / "calls.json"
+    proc = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "ref_integration.py"), str(out)],
+                          capture_output=True, text=True, timeout=600,
+                          env=dict(os.environ, PYTHONPATH=ROOT, OMP_NUM_THREADS="4"))
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    calls = json.loads(out.read_text())
+    assert calls["hook"] == 1                 # _process_reports took the aggregate_weights branch
+    assert calls["load"] == 1                 # ... and loaded what the hook returned
+    assert calls["load_dtypes"] == ["torch.float32"]  # update_weights' dtypes (int keys as fp32)
+    assert calls["cb_received"] == 1 and calls["cb_aggregated"] == 1
+    assert calls["model_matches_reference_chain"]
+    assert calls["total_samples"]
