@@ -40,6 +40,11 @@
  *                                 fp32 -> int64 copy (plato/algorithms/fedavg.py:46-48)
  *   plato_agg_mix_weights      <- FedAsync Algorithm.aggregate_weights
  *                                 (examples/async/fedasync/fedasync_algorithm.py:9-20)
+ *   plato_agg_client_dots      <- the model-wide reductions of Port's
+ *                                 cosine_similarity (examples/async/port/
+ *                                 port_server.py:24-52, F.cosine_similarity over
+ *                                 the flattened models) and of the norm-based
+ *                                 variants (Polaris, FedAdp, FedAtt)
  */
 #ifndef PLATO_AGG_H
 #define PLATO_AGG_H
@@ -125,6 +130,25 @@ int plato_agg_mix_weights(const float* d_x_f32, const int64_t* d_x_i64,
                           float one_minus_m, float m,
                           float* d_out_f32, float* d_out_i64f,
                           size_t n_f32, size_t n_i64, hipStream_t stream);
+
+/*
+ * Per-client model-wide reductions (Port cosine similarity, norms) over the
+ * whole arena, int64 entries included as torch.cat promotes them (fp32):
+ *   d_i = x_i - base (fp32, as compute_weight_deltas; int64: fp32(x - b)),
+ *         or x_i if d_base is NULL
+ *   d_out[i]     = sum_e d_i[e] * v[e]         (0 <= i < K)
+ *   d_out[K + i] = sum_e d_i[e]^2
+ *   d_out[2K]    = sum_e v[e]^2                (v's int64 entries as fp32)
+ * accumulated in fp64 in a fixed order (bitwise reproducible run to run; it
+ * matches torch's fp32 CPU reductions within tolerance, not bit for bit).
+ * d_workspace must hold plato_agg_client_dots_workspace(K, n_f32) bytes.
+ */
+size_t plato_agg_client_dots_workspace(int K, size_t n_f32);
+int plato_agg_client_dots(const float* const* d_x, const int64_t* const* d_x_i64, int K,
+                          const float* d_base, const int64_t* d_base_i64,
+                          const float* d_v, const int64_t* d_v_i64,
+                          size_t n_f32, size_t n_i64, double* d_workspace,
+                          double* d_out, hipStream_t stream);
 
 /*
  * Deterministic synthetic payloads for tests and benchmarks (a counter-based

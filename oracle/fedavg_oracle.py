@@ -67,8 +67,38 @@ def port_weights(num_samples: Sequence[int], staleness: Sequence[int], similarit
     return [r / sum(raw) for r in raw]
 
 
+def port_weights_torch(num_samples, staleness, similarity, similarity_weight=1, staleness_weight=1,
+                       staleness_bound=10):
+    """examples/async/port/port_server.py:57-103 evaluated as written, with the
+    similarities as the reference holds them: the Python float 1.0, or a 0-dim
+    fp32 torch tensor from F.cosine_similarity."""
+    import torch
+
+    total = sum(num_samples)
+    raw = []
+    for i, n in enumerate(num_samples):
+        sim = similarity[i]
+        if not isinstance(sim, float):
+            sim = torch.tensor(np.float32(sim))
+        factor = port_staleness_factor(staleness[i], staleness_bound)
+        raw.append(n / total * ((sim + 1) / 2 * similarity_weight + factor * staleness_weight))
+    return [r / sum(raw) for r in raw]
+
+
+def cosine_similarity_fp64(current_minus_previous: np.ndarray, delta: np.ndarray, eps: float = 1e-8) -> float:
+    """F.cosine_similarity(a, b, dim=0) restated in fp64 (port_server.py:50)."""
+    a = current_minus_previous.astype(np.float64)
+    b = delta.astype(np.float64)
+    return float(np.dot(a, b) / (max(np.linalg.norm(a), eps) * max(np.linalg.norm(b), eps)))
+
+
 def fp32(values) -> np.ndarray:
-    return np.asarray([np.float32(float(v)) for v in values], dtype=np.float32)
+    out = []
+    for v in values:
+        if hasattr(v, "item") and not isinstance(v, np.floating):
+            v = v.item()  # 0-dim torch tensor (fp32): exact
+        out.append(np.float32(float(v)))
+    return np.asarray(out, dtype=np.float32)
 
 
 # --------------------------------------------------------------------------

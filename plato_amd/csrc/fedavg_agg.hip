@@ -24,17 +24,28 @@
 #include <cstdio>
 #include <string>
 
+#include "common.h"
 #include "plato_agg.h"
 #include "plato_agg_tune.h"
 
 namespace {
-
 thread_local std::string g_last_error;
+}  // namespace
 
-int fail(int code, const std::string& msg) {
+namespace plato_agg_internal {
+int set_error(int code, const std::string& msg) {
   g_last_error = msg;
   return code;
 }
+int clear_error() {
+  g_last_error.clear();
+  return PLATO_AGG_OK;
+}
+}  // namespace plato_agg_internal
+
+namespace {
+
+int fail(int code, const std::string& msg) { return plato_agg_internal::set_error(code, msg); }
 
 int check_launch(const char* what) {
   hipError_t err = hipGetLastError();

@@ -405,6 +405,52 @@ class AggregationRound:
         # keep device buffers alive until the copies finish
         self._out = (host_f, host_i, out_f, out_i, tf, ti, w, s)
 
+    def model_similarities(self, reference: Mapping[str, torch.Tensor], slots: Sequence[int],
+                           eps: float = 1e-8) -> list[np.float32]:
+        """Port's cosine similarity of each client delta with ``baseline - reference``.
+
+        ``F.cosine_similarity(current - previous, delta, dim=0)`` over the
+        flattened models (examples/async/port/port_server.py:38-50), from the
+        device reductions of ``plato_agg_client_dots`` (fp64, fixed order):
+        ``dot / (max(|v|, eps) * max(|d|, eps))``, returned as fp32 like the
+        reference's 0-dim tensor.
+        """
+        if not self.has_baseline:
+            raise ValueError("baseline not staged")
+        slots = list(slots)
+        for slot in slots:
+            if not (0 <= slot < self.capacity and self.staged[slot]):
+                raise ValueError(f"client slot {slot} was not staged")
+        if not slots:
+            return []
+        eng = self.engine
+        lay = self.layout
+        lay.check_compatible(reference, "reference model")
+        stream = torch.cuda.current_stream(eng.device)
+        prev = DeviceArena(lay, eng.device)
+        eng._stager.put(reference, prev.f32, prev.i64)
+        eng._stager.fence(stream)
+        v = DeviceArena(lay, eng.device)
+        h = _stream_handle(stream)
+        _lib.call("plato_agg_compute_deltas", _ptr(eng._base.f32), _ptr(eng._base.i64), _ptr(prev.f32),
+                  _ptr(prev.i64), _ptr(v.f32), _ptr(v.i64), lay.n_f32, lay.n_i64, h)
+        pf, pi = eng._slab.row_pointers(slots)
+        tf, ti = eng._pointer_tables(pf, pi)
+        k = len(slots)
+        ws_bytes = self.engine.lib.plato_agg_client_dots_workspace(k, lay.n_f32)
+        ws = torch.empty((ws_bytes + 7) // 8, dtype=torch.float64, device=eng.device)
+        out = torch.empty(2 * k + 1, dtype=torch.float64, device=eng.device)
+        _lib.call("plato_agg_client_dots", _ptr(tf), _ptr(ti) if lay.n_i64 else None, k, _ptr(eng._base.f32),
+                  _ptr(eng._base.i64) if lay.n_i64 else None, _ptr(v.f32), _ptr(v.i64) if lay.n_i64 else None,
+                  lay.n_f32, lay.n_i64, _ptr(ws), _ptr(out), h)
+        res = out.cpu().numpy()
+        vnorm = max(float(np.sqrt(res[2 * k])), eps)
+        sims = []
+        for i in range(k):
+            dnorm = max(float(np.sqrt(res[k + i])), eps)
+            sims.append(np.float32(res[i] / (vnorm * dnorm)))
+        return sims
+
     def ready(self) -> bool:
         return self.event is not None and self.event.query()
 

@@ -56,7 +56,6 @@ class FusedAggregationMixin(_EngineHolder):
     """``aggregate_weights`` hook: fused deltas -> weighted sum -> update on the GPU."""
 
     async def aggregate_weights(self, updates, baseline_weights, weights_received):
-        weights, scales = self.aggregation_weights(updates)
         engine = self.aggregation_engine()
         rnd = engine.begin(baseline_weights, len(weights_received))
         rnd.put_baseline(baseline_weights)
@@ -65,6 +64,12 @@ class FusedAggregationMixin(_EngineHolder):
             # Yield to other tasks in the server between clients, as the
             # reference does per client (servers/fedavg.py:157).
             await asyncio.sleep(0)
+        # weights may need the staged arenas (Port's similarity reduction)
+        self._plato_amd_round = rnd
+        try:
+            weights, scales = self.aggregation_weights(updates)
+        finally:
+            self._plato_amd_round = None
         rnd.launch(weights, scales)
         while not rnd.ready():
             await asyncio.sleep(0)

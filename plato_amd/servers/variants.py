@@ -47,22 +47,32 @@ class PortWeights(_EngineHolder):
     computes on the GPU.
     """
 
-    def port_similarities(self, updates):
-        sims = []
-        model_path = None
+    def port_previous_model_path(self):
+        """Where the reference looks for the round-(r-2) global model (port_server.py:28-30)."""
         try:
             from plato.config import Config
 
-            model_path = f"{Config().params['model_path']}/model_{self.current_round - 2}.pth"
-        except Exception:
-            pass
-        for update in updates:
-            if update.staleness > 1 and model_path is not None and os.path.exists(model_path):
-                raise NotImplementedError(
-                    "Port cosine similarity against a stored stale model is not on the GPU path yet"
-                )
-            sims.append(1.0)
-        return sims
+            return f"{Config().params['model_path']}/model_{self.current_round - 2}.pth"
+        except Exception:  # Plato not importable / not configured
+            return None
+
+    def port_similarities(self, updates):
+        """1.0, or the fp32 cosine similarity computed on the GPU (port_server.py:24-52)."""
+        path = self.port_previous_model_path()
+        need = [i for i, u in enumerate(updates) if u.staleness > 1]
+        if not need or path is None or not os.path.exists(path):
+            return [1.0] * len(updates)
+        rnd = getattr(self, "_plato_amd_round", None)
+        if rnd is None:
+            raise RuntimeError("Port similarities need the staged round (use the fused aggregate_weights hook)")
+        import torch
+
+        previous = torch.load(path, map_location="cpu", weights_only=True)
+        sims = rnd.model_similarities(previous, need)
+        out = [1.0] * len(updates)
+        for i, sim in zip(need, sims):
+            out[i] = sim
+        return out
 
     #: Port hyper-parameters; None = Config().server.<name>, else the reference default
     similarity_weight = None

@@ -36,17 +36,65 @@ def port_staleness_factor(staleness: int, staleness_bound: float = 10) -> float:
     return staleness_bound / (staleness + staleness_bound)
 
 
+class _F32:
+    """A 0-dim fp32 torch tensor's scalar arithmetic, restated with numpy float32.
+
+    Port's cosine similarity is a 0-dim fp32 tensor (F.cosine_similarity), so
+    every weight expression it enters follows tensor semantics: Python numbers
+    are cast to fp32 at each op, ``number / tensor`` is
+    ``tensor.reciprocal() * number`` (torch/_tensor.py ``__rdiv__``).
+    """
+
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = np.float32(v)
+
+    @staticmethod
+    def _f(x):
+        return x.v if isinstance(x, _F32) else np.float32(x)
+
+    def __add__(self, o):
+        return _F32(self.v + self._f(o))
+
+    __radd__ = __add__
+
+    def __mul__(self, o):
+        return _F32(self.v * self._f(o))
+
+    __rmul__ = __mul__
+
+    def __truediv__(self, o):
+        return _F32(self.v / self._f(o))
+
+    def __rtruediv__(self, o):
+        return _F32((np.float32(1) / self.v) * self._f(o))
+
+
 def port(num_samples: Sequence[int], staleness: Sequence[int], similarities=None,
          similarity_weight: float = 1, staleness_weight: float = 1,
          staleness_bound: float = 10) -> list[float]:
-    """Port's normalised weights; ``similarities`` default to 1.0 (no stale model on disk)."""
+    """Port's normalised weights, evaluated with the reference's expression order.
+
+    ``similarities[i]`` is the Python float 1.0 when the reference skips the
+    cosine similarity, else the fp32 value of F.cosine_similarity (pass a
+    ``numpy.float32``): then that client's weight and every weight normalised by
+    the (now tensor-valued) sum follow fp32 tensor arithmetic, as in the reference.
+    """
     total = sum(num_samples)
     raw = []
     for i, n in enumerate(num_samples):
         sim = 1.0 if similarities is None else similarities[i]
+        if isinstance(sim, np.floating) and sim.dtype == np.float32:
+            sim = _F32(sim)
         factor = port_staleness_factor(staleness[i], staleness_bound)
         raw.append(n / total * ((sim + 1) / 2 * similarity_weight + factor * staleness_weight))
-    return [r / sum(raw) for r in raw]
+    denom = sum(raw)
+    out = []
+    for r in raw:
+        w = r / denom
+        out.append(float(w.v) if isinstance(w, _F32) else w)
+    return out
 
 
 def pisces_staleness_factor(history: Sequence[int], exponent: float) -> float:

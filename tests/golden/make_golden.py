@@ -278,6 +278,17 @@ def run_case(case):
     server.algorithm.load_weights(copy.deepcopy(baseline))
     server.updates = make_updates(case["num_samples"], payloads, order, staleness)
     server.current_round = case.get("current_round", 0)
+    if "previous" in case:
+        # the round-(r-2) global model Port compares against (port_server.py:28-36)
+        from plato.config import Config
+
+        pv = case["previous"]
+        prev_f = synth.synth_f32(nf, seed, pv["stream"], pv["scale"], add=bf)
+        prev_i = synth.synth_i64(ni, seed, pv["stream"], 3, add=bi)
+        model_path = Config().params["model_path"]
+        os.makedirs(model_path, exist_ok=True)
+        torch.save(unpack(entries, torch.from_numpy(prev_f), torch.from_numpy(prev_i)),
+                   f"{model_path}/model_{server.current_round - 2}.pth")
 
     captured = {}
     orig_agg = server.aggregate_deltas if mode != "fedasync" else None
@@ -287,6 +298,15 @@ def run_case(case):
             captured["avg"] = {n: t.clone() for n, t in avg.items()}
             return avg
         server.aggregate_deltas = spy_agg
+    if mode == "port":
+        orig_cs = server.cosine_similarity
+
+        async def spy_cs(update, st):
+            sim = await orig_cs(update, st)
+            captured.setdefault("sims", []).append(
+                f32hex(sim.item()) if isinstance(sim, torch.Tensor) else float(sim))
+            return sim
+        server.cosine_similarity = spy_cs
     orig_load = server.algorithm.load_weights
 
     def spy_load(weights):
@@ -319,6 +339,8 @@ def run_case(case):
     out["samples_i64f"] = [[int(i), f32hex(ui[i])] for i in range(min(ni, 64))]
     li = flatten(entries, loaded, "i64", torch.int64)
     out["samples_loaded_i64"] = [[int(i), int(li[i])] for i in range(min(ni, 64))]
+    if "sims" in captured:
+        out["port_similarities"] = captured["sims"]
     if "avg" in captured:
         out["avg_f32_sha256"] = sha(canon(flatten(entries, captured["avg"], "f32", torch.float32)))
         out["avg_i64f_sha256"] = sha(canon(flatten(entries, captured["avg"], "i64", torch.float32)))
@@ -378,6 +400,12 @@ def cases():
              num_samples=synth.num_samples(8, 10), staleness=[0, 1, 2, 3, 5, 8, 13, 1]),
         dict(name="fedasync_resnet18_k1", model="resnet18", k=1, seed=12, mode="fedasync",
              num_samples=[500], staleness=[7]),
+        dict(name="port_similarity_lenet5_k8", model="lenet5", k=8, seed=14, mode="port",
+             num_samples=synth.num_samples(8, 14), staleness=[0, 1, 2, 3, 5, 2, 0, 4],
+             current_round=5, previous={"stream": 999, "scale": -26}, full=True),
+        dict(name="port_similarity_resnet18_k4", model="resnet18", k=4, seed=15, mode="port",
+             num_samples=synth.num_samples(4, 15), staleness=[3, 0, 2, 7],
+             current_round=9, previous={"stream": 998, "scale": -25}),
         dict(name="C4_port_resnet18_k256", model="resnet18", k=256, seed=13, mode="port",
              num_samples=synth.num_samples(256, 13), staleness=[(7 * i) % 11 for i in range(256)]),
     ]
@@ -442,12 +470,20 @@ def main():
     workdir = tempfile.mkdtemp(prefix="golden_")
     boot_reference(args.reference, workdir)
     os.chdir(workdir)
-    dump_shapes(HERE)
-    ka = run_reference_known_answer(args.reference)
-    with open(os.path.join(HERE, "known_answer_fedavg_tests.json"), "w") as f:
-        json.dump(ka, f, indent=1)
+    if not args.only:
+        dump_shapes(HERE)
+        ka = run_reference_known_answer(args.reference)
+        with open(os.path.join(HERE, "known_answer_fedavg_tests.json"), "w") as f:
+            json.dump(ka, f, indent=1)
+    cases_path = os.path.join(HERE, "fedavg_cases.json")
+    full_path = os.path.join(HERE, "fedavg_full_small.npz")
     results = []
     full = {}
+    if args.only and os.path.exists(cases_path):  # merge into the existing fixtures
+        with open(cases_path) as f:
+            results = [c for c in json.load(f)["cases"] if c["recipe"]["name"] != args.only]
+        with np.load(full_path, allow_pickle=False) as z:
+            full = {k: z[k] for k in z.files if not k.startswith(args.only + "/")}
     for case in cases():
         if args.only and case["name"] != args.only:
             continue
@@ -458,11 +494,13 @@ def main():
             for key, arr in arrays.items():
                 full[f"{case['name']}/{key}"] = arr
         results.append({"recipe": case, "expected": out})
-    with open(os.path.join(HERE, "fedavg_cases.json"), "w") as f:
+    order = {c["name"]: i for i, c in enumerate(cases())}
+    results.sort(key=lambda c: order.get(c["recipe"]["name"], 1 << 30))
+    with open(cases_path, "w") as f:
         json.dump({"generator": "tests/golden/make_golden.py", "synth": "oracle/synth.py",
                    "nan_policy": "NaN outputs canonicalised to 0x7fc00000 before hashing",
                    "cases": results}, f, indent=1)
-    np.savez_compressed(os.path.join(HERE, "fedavg_full_small.npz"), **full)
+    np.savez_compressed(full_path, **full)
     print("wrote", len(results), "cases")
 
 

@@ -57,7 +57,15 @@ def order_of(recipe):
     return recipe.get("order", list(range(recipe["k"])))
 
 
-def weights_for(recipe, impl):
+def reference_similarities(case):
+    """Port similarities the reference computed: 1.0 or np.float32 (from fp32 hex)."""
+    sims = case["expected"].get("port_similarities")
+    if sims is None:
+        return None
+    return [s if isinstance(s, float) else hexf(s) for s in sims]
+
+
+def weights_for(recipe, impl, similarities=None):
     """(weights, scales) in update order.  ``impl`` is plato_amd.weights or an oracle shim."""
     order = order_of(recipe)
     ns = [recipe["num_samples"][c] for c in order]
@@ -68,7 +76,8 @@ def weights_for(recipe, impl):
     if mode == "fedbuff":
         return impl.fedbuff(len(ns)), None
     if mode == "port":
-        return impl.port(ns, st, similarity_weight=1, staleness_weight=3, staleness_bound=10), None
+        return impl.port(ns, st, similarities, similarity_weight=1, staleness_weight=3,
+                         staleness_bound=10), None
     if mode == "pisces":
         first, second = impl.pisces(ns, [[s] for s in st], 0.5)
         return first, second

@@ -75,7 +75,8 @@ def test_kernel_matches_reference(engine, case):
     recipe, exp = case["recipe"], case["expected"]
     layout, base, slab = _device_inputs(recipe)
     order = G.order_of(recipe)
-    weights, scales = G.weights_for(recipe, W)
+    # Port with a stored stale model: the reference's own similarity values
+    weights, scales = G.weights_for(recipe, W, G.reference_similarities(case))
     out_f, out_i = _launch(engine, layout, base, slab, order, weights, scales)
     got_f = out_f[: layout.n_f32].cpu().numpy()
     got_i = out_i[: layout.n_i64].cpu().numpy()
@@ -115,7 +116,7 @@ def test_full_arrays_small_cases(engine):
         if not recipe.get("full"):
             continue
         layout, base, slab = _device_inputs(recipe)
-        weights, scales = G.weights_for(recipe, W)
+        weights, scales = G.weights_for(recipe, W, G.reference_similarities(case))
         out_f, _ = _launch(engine, layout, base, slab, G.order_of(recipe), weights, scales)
         got = G.canon(out_f[: layout.n_f32].cpu().numpy())
         assert got.tobytes() == G.canon(full[f"{recipe['name']}/updated_f32"]).tobytes(), recipe["name"]
@@ -208,3 +209,56 @@ def test_fedasync_mixing_matches_reference():
     updated = asyncio.run(server.aggregate_weights(_updates(recipe, payloads), baseline, payloads))
     assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
     assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+
+
+def _previous(recipe, layout):
+    pv = recipe["previous"]
+    bf, bi = synth.baseline_arena(layout.n_f32, layout.n_i64, recipe["seed"])
+    prev_f = synth.synth_f32(layout.n_f32, recipe["seed"], pv["stream"], pv["scale"], add=bf)
+    prev_i = synth.synth_i64(layout.n_i64, recipe["seed"], pv["stream"], 3, add=bi)
+    return layout.unpack(torch.from_numpy(prev_f), torch.from_numpy(prev_i))
+
+
+@pytest.mark.parametrize("name", ["port_similarity_lenet5_k8", "port_similarity_resnet18_k4"])
+def test_device_similarities_match_reference(engine, name):
+    """plato_agg_client_dots (wave shuffles + LDS, fp64) vs the reference's F.cosine_similarity."""
+    case = next(c for c in CASES if c["recipe"]["name"] == name)
+    recipe = case["recipe"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    rnd = engine.begin(baseline, recipe["k"])
+    rnd.put_baseline(baseline)
+    for c in range(recipe["k"]):
+        rnd.put_client(c, payloads[c])
+    sims = rnd.model_similarities(_previous(recipe, layout), range(recipe["k"]))
+    ref_sims = G.reference_similarities(case)
+    st = recipe["staleness"]
+    for i in range(recipe["k"]):
+        if st[i] > 1:  # the reference computed it; tolerance: see test_oracle
+            assert abs(float(sims[i]) - float(ref_sims[i])) <= 1e-5, (i, sims[i], ref_sims[i])
+    # run to run the device reduction is bitwise reproducible (fixed order)
+    again = rnd.model_similarities(_previous(recipe, layout), range(recipe["k"]))
+    assert [np.float32(a).tobytes() for a in sims] == [np.float32(b).tobytes() for b in again]
+
+
+def test_port_server_with_stale_model_matches_reference(tmp_path):
+    """PortServerMixin end to end with a stored round-(r-2) model: normwise <= 1e-6 of the reference."""
+    from plato_amd.servers.variants import PortServerMixin
+
+    case = next(c for c in CASES if c["recipe"]["name"] == "port_similarity_lenet5_k8")
+    recipe = case["recipe"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    path = tmp_path / f"model_{recipe['current_round'] - 2}.pth"
+    torch.save(_previous(recipe, layout), path)
+
+    class Server(PortServerMixin):
+        aggregation_device = DEV
+        staleness_weight = 3
+        current_round = recipe["current_round"]
+
+        def port_previous_model_path(self):
+            return str(path)
+
+    updated = asyncio.run(Server().aggregate_weights(_updates(recipe, payloads), baseline, payloads))
+    got = _flat(layout, updated, "f32").astype(np.float64)
+    exp = G.load_full()[f"{recipe['name']}/updated_f32"].astype(np.float64)
+    assert np.max(np.abs(got - exp)) / np.max(np.abs(exp)) <= 1e-6

@@ -29,8 +29,10 @@ class OracleWeights:
     fedbuff = staticmethod(ref.fedbuff_weights)
 
     @staticmethod
-    def port(ns, st, similarity_weight, staleness_weight, staleness_bound):
-        return ref.port_weights(ns, st, None, similarity_weight, staleness_weight, staleness_bound)
+    def port(ns, st, sims, similarity_weight, staleness_weight, staleness_bound):
+        if sims is None:
+            return ref.port_weights(ns, st, None, similarity_weight, staleness_weight, staleness_bound)
+        return ref.port_weights_torch(ns, st, sims, similarity_weight, staleness_weight, staleness_bound)
 
     @staticmethod
     def pisces(ns, histories, a):
@@ -94,8 +96,9 @@ def test_oracle_reproduces_reference(case):
     if G.case_size(recipe) > 4e8 and not SLOW:
         pytest.skip("large case: PLATO_AGG_SLOW=1 (covered on the GPU)")
     inputs = _inputs(recipe)
-    w_prod = G.weights_for(recipe, product_weights)
-    w_orac = G.weights_for(recipe, OracleWeights)
+    sims = G.reference_similarities(case)  # Port with a stored stale model: the reference's values
+    w_prod = G.weights_for(recipe, product_weights, sims)
+    w_orac = G.weights_for(recipe, OracleWeights, sims)
     assert ref.fp32(w_prod[0]).tobytes() == ref.fp32(w_orac[0]).tobytes()
     _check_case(case, inputs, *w_prod)
 
@@ -158,3 +161,30 @@ def test_order_changes_bits():
 def test_trunc_semantics():
     vals = np.array([5.9999, -0.5, -7.99, 3.0, -3.0, 0.0], dtype=np.float32)
     assert list(ref.trunc_to_int64(vals)) == [5, 0, -7, 3, -3, 0]
+
+
+@pytest.mark.parametrize("name", ["port_similarity_lenet5_k8", "port_similarity_resnet18_k4"])
+def test_oracle_cosine_similarity_matches_reference(name):
+    """fp64 restatement of F.cosine_similarity vs the reference's fp32 values.
+
+    Tolerance 1e-5 absolute: the reference normalises and sums 11M fp32
+    products (torch CPU reduction order), so its own error is a few 1e-6 on
+    ResNet-18; the weights it feeds move the model by ~1e-7 normwise.
+    """
+    case = next(c for c in CASES if c["recipe"]["name"] == name)
+    recipe = case["recipe"]
+    layout, bf, bi, xs_f, xs_i = _inputs(recipe)
+    pv = recipe["previous"]
+    prev_f = synth.synth_f32(layout.n_f32, recipe["seed"], pv["stream"], pv["scale"], add=bf)
+    prev_i = synth.synth_i64(layout.n_i64, recipe["seed"], pv["stream"], 3, add=bi)
+    # state_dict order interleaves fp32 and int64 keys; the cosine is order-free
+    v = np.concatenate([np.subtract(bf, prev_f, dtype=np.float32),
+                        bi.astype(np.float32) - prev_i.astype(np.float32)])
+    sims = G.reference_similarities(case)
+    st = [recipe["staleness"][c] for c in G.order_of(recipe)]
+    for i, s in enumerate(sims):
+        if st[i] <= 1:
+            assert s == 1.0
+            continue
+        d = np.concatenate([np.subtract(xs_f[i], bf, dtype=np.float32), (xs_i[i] - bi).astype(np.float32)])
+        assert abs(ref.cosine_similarity_fp64(v, d) - float(s)) <= 1e-5
