@@ -128,6 +128,7 @@ struct AggArgs {
   uint64_t n_i64;
   uint32_t nb_vec;             // workgroups of the f4 body
   uint32_t nb_vec_full;        // of which fully in range (no bounds checks)
+  uint32_t nb_grid;            // PERSIST: workgroups striding over the chunks
   int K;
 };
 
@@ -135,11 +136,21 @@ struct AggArgs {
 //   B   threads per workgroup      V  f4 groups per lane per client
 //   U   clients per batch          NTL/NTS  non-temporal loads / stores
 //   PIPE  software-pipelined: batch j+1's loads issue before batch j's adds
-template <int B_, int V_, int U_, bool NTL_, bool NTS_, bool PIPE_>
+//   BUF   buffer_load_dwordx4 (SRD per client, 32-bit voffset) instead of global_load
+//   PERSIST  0: one workgroup per chunk; N: N workgroups per CU-slot grid-stride
+//            over the chunks (grid = min(chunks, 256*N))
+template <int B_, int V_, int U_, bool NTL_, bool NTS_, bool PIPE_, bool BUF_ = false, int PERSIST_ = 0>
 struct Cfg {
   static constexpr int B = B_, V = V_, U = U_;
-  static constexpr bool NTL = NTL_, NTS = NTS_, PIPE = PIPE_;
+  static constexpr bool NTL = NTL_, NTS = NTS_, PIPE = PIPE_, BUF = BUF_;
+  static constexpr int PERSIST = PERSIST_;
 };
+
+template <bool NT>
+__device__ __forceinline__ f4 ld4_buf(const float* base, uint32_t byte_off, uint32_t bytes) {
+  __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, (short)0, (int)bytes, 0x00020000);
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, NT ? 2 : 0));
+}
 
 template <bool NT>
 __device__ __forceinline__ void st4_off(float* base, uint32_t byte_off, f4 v) {
@@ -171,13 +182,22 @@ __device__ __forceinline__ void accumulate(f4 (&acc)[C::V], const f4 (&x)[C::U][
 }
 
 template <class C>
+__device__ __forceinline__ f4 ld_client(const float* p, uint32_t off, const AggArgs& a) {
+  if constexpr (C::BUF) {
+    return ld4_buf<C::NTL>(p, off, uint32_t(a.n4 * 16u));
+  } else {
+    return ld4_off<C::NTL>(p, off);
+  }
+}
+
+template <class C>
 __device__ __forceinline__ void load_batch(f4 (&x)[C::U][C::V], const AggArgs& a, int i0,
                                            const uint32_t (&off)[C::V]) {
 #pragma unroll
   for (int u = 0; u < C::U; ++u) {
     const float* p = sld(a.xf, i0 + u);
 #pragma unroll
-    for (int v = 0; v < C::V; ++v) x[u][v] = ld4_off<C::NTL>(p, off[v]);
+    for (int v = 0; v < C::V; ++v) x[u][v] = ld_client<C>(p, off[v], a);
   }
 }
 
@@ -235,7 +255,7 @@ __device__ __forceinline__ void vec_body(const AggArgs& a, uint32_t blk) {
     if constexpr (TWO) su = sld(a.s, i);
 #pragma unroll
     for (int v = 0; v < V; ++v) {
-      f4 x = ld4_off<C::NTL>(p, off[v]);
+      f4 x = ld_client<C>(p, off[v], a);
       f4 d = HAS_BASE ? f4_sub(x, b[v]) : x;
       f4 t = f4_scale(d, wu);
       if constexpr (TWO) t = f4_scale(t, su);
@@ -288,13 +308,29 @@ __device__ __forceinline__ void scalar_item(const AggArgs& a, uint64_t j) {
 template <class C, bool HAS_BASE, bool TWO>
 __global__ __launch_bounds__(C::B) void fedavg_kernel(AggArgs a) {
   const uint32_t blk = blockIdx.x;
-  if (blk < a.nb_vec_full) {
-    vec_body<C, HAS_BASE, TWO, false>(a, blk);
-  } else if (blk < a.nb_vec) {
-    vec_body<C, HAS_BASE, TWO, true>(a, blk);
+  if constexpr (C::PERSIST > 0) {
+    // a.nb_grid workgroups stride over the nb_vec chunks; the rest do scalars
+    if (blk < a.nb_grid) {
+      for (uint32_t c = blk; c < a.nb_vec; c += a.nb_grid) {
+        if (c < a.nb_vec_full) {
+          vec_body<C, HAS_BASE, TWO, false>(a, c);
+        } else {
+          vec_body<C, HAS_BASE, TWO, true>(a, c);
+        }
+      }
+    } else {
+      const uint64_t j = uint64_t(blk - a.nb_grid) * C::B + threadIdx.x;
+      scalar_item<HAS_BASE, TWO>(a, j);
+    }
   } else {
-    const uint64_t j = uint64_t(blk - a.nb_vec) * C::B + threadIdx.x;
-    scalar_item<HAS_BASE, TWO>(a, j);
+    if (blk < a.nb_vec_full) {
+      vec_body<C, HAS_BASE, TWO, false>(a, blk);
+    } else if (blk < a.nb_vec) {
+      vec_body<C, HAS_BASE, TWO, true>(a, blk);
+    } else {
+      const uint64_t j = uint64_t(blk - a.nb_vec) * C::B + threadIdx.x;
+      scalar_item<HAS_BASE, TWO>(a, j);
+    }
   }
 }
 
@@ -310,13 +346,14 @@ void launch_one(const AggArgs& a, dim3 grid, hipStream_t st) {
 
 struct Variant {
   int B, V, U;
-  bool NTL, NTS, PIPE;
+  bool NTL, NTS, PIPE, BUF;
+  int PERSIST;
   LaunchFn fn[2][2];  // [HAS_BASE][TWO]
 };
 
 template <class C>
 constexpr Variant make_variant() {
-  return Variant{C::B, C::V, C::U, C::NTL, C::NTS, C::PIPE,
+  return Variant{C::B, C::V, C::U, C::NTL, C::NTS, C::PIPE, C::BUF, C::PERSIST,
                  {{&launch_one<C, false, false>, &launch_one<C, false, true>},
                   {&launch_one<C, true, false>, &launch_one<C, true, true>}}};
 }
@@ -324,20 +361,20 @@ constexpr Variant make_variant() {
 // Variant 0 is the default of the public entry points (fastest in the
 // interleaved sweep on MI355X).
 const Variant kVariants[] = {
-    make_variant<Cfg<256, 1, 8, true, true, false>>(),    // 0 (default): NT loads + NT stores
-    make_variant<Cfg<256, 2, 8, false, false, false>>(),  // 1 first version
-    make_variant<Cfg<256, 1, 8, false, false, false>>(),  // 2 plain loads
-    make_variant<Cfg<256, 1, 8, true, false, false>>(),   // 3 NT loads only
-    make_variant<Cfg<256, 1, 4, true, true, false>>(),    // 4
-    make_variant<Cfg<256, 1, 16, true, true, false>>(),   // 5
-    make_variant<Cfg<256, 1, 8, true, true, true>>(),     // 6 pipelined
-    make_variant<Cfg<256, 1, 4, true, true, true>>(),     // 7 pipelined
-    make_variant<Cfg<512, 1, 8, true, true, false>>(),    // 8
-    make_variant<Cfg<1024, 1, 8, true, true, false>>(),   // 9
-    make_variant<Cfg<256, 2, 8, true, true, false>>(),    // 10
-    make_variant<Cfg<256, 1, 32, true, true, false>>(),   // 11
-    make_variant<Cfg<64, 1, 8, true, true, false>>(),     // 12
-    make_variant<Cfg<128, 1, 16, true, true, false>>(),   // 13
+    make_variant<Cfg<256, 1, 8, true, true, false>>(),              // 0 (default): NT loads + NT stores
+    make_variant<Cfg<256, 2, 8, false, false, false>>(),            // 1 first version
+    make_variant<Cfg<256, 1, 8, false, false, false>>(),            // 2 plain loads
+    make_variant<Cfg<256, 1, 8, true, false, false>>(),             // 3 NT loads only
+    make_variant<Cfg<256, 1, 4, true, true, false>>(),              // 4
+    make_variant<Cfg<256, 1, 16, true, true, false>>(),             // 5
+    make_variant<Cfg<256, 1, 8, true, true, true>>(),               // 6 pipelined
+    make_variant<Cfg<64, 1, 8, true, true, false>>(),               // 7
+    make_variant<Cfg<256, 1, 8, true, true, false, true>>(),        // 8 buffer loads (nt)
+    make_variant<Cfg<256, 1, 4, true, true, false, true>>(),        // 9 buffer loads (nt)
+    make_variant<Cfg<256, 1, 8, true, true, false, false, 8>>(),    // 10 persistent 8/CU
+    make_variant<Cfg<256, 1, 8, true, true, false, false, 4>>(),    // 11 persistent 4/CU
+    make_variant<Cfg<256, 1, 8, true, true, false, true, 8>>(),     // 12 buffer + persistent 8/CU
+    make_variant<Cfg<256, 1, 8, false, true, false, true>>(),       // 13 buffer, plain loads
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -379,7 +416,12 @@ int run_agg(int variant, bool has_base, const float* const* xf, const int64_t* c
     return fail(PLATO_AGG_EINVAL, "fp32 arena must be < 4 GiB per launch (split it into buckets)");
   a.nb_vec = uint32_t(nb_vec);
   a.nb_vec_full = uint32_t(a.n4 / chunk);
-  dim3 grid(uint32_t(nb_vec + nb_scalar));
+  a.nb_grid = a.nb_vec;
+  if (vr.PERSIST > 0) {
+    const uint64_t cap = uint64_t(256) * vr.PERSIST;  // 256 CUs on MI355X
+    a.nb_grid = uint32_t(nb_vec < cap ? nb_vec : cap);
+  }
+  dim3 grid(uint32_t(a.nb_grid + nb_scalar));
   vr.fn[has_base ? 1 : 0][s ? 1 : 0](a, grid, st);
   return check_launch("fedavg kernel launch");
 }
@@ -538,7 +580,7 @@ int plato_agg_tune_describe(int variant, int* block, int* v, int* u, int* flags)
   *block = vr.B;
   *v = vr.V;
   *u = vr.U;
-  *flags = (vr.NTL ? 1 : 0) | (vr.NTS ? 2 : 0) | (vr.PIPE ? 4 : 0);
+  *flags = (vr.NTL ? 1 : 0) | (vr.NTS ? 2 : 0) | (vr.PIPE ? 4 : 0) | (vr.BUF ? 8 : 0) | (vr.PERSIST << 4);
   return PLATO_AGG_OK;
 }
 
