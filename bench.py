@@ -218,8 +218,34 @@ def main():
                 e1.record(stream)
                 e1.synchronize()
                 times[v].append(e0.elapsed_time(e1) / args.steps)
+        # measured streaming ceilings over the same byte count (5.8 GB for C2)
+        n_probe = (alg_bytes // 4) // 4 * 4
+        src = torch.empty(n_probe, dtype=torch.float32, device=dev)
+        src.fill_(1.0)
+        dst = torch.empty(n_probe // 2 + 64, dtype=torch.float32, device=dev)
+        probes = {}
+        for mode, name, nbytes in ((1, "read", n_probe * 4), (0, "copy", (n_probe // 2) * 8)):
+            for blocks in (1024, 2048, 4096, 8192):
+                n_el = n_probe if mode == 1 else n_probe // 2
+                _lib.call("plato_agg_tune_stream", mode, src.data_ptr(), dst.data_ptr(), n_el, blocks,
+                          stream.cuda_stream)
+                torch.cuda.synchronize(dev)
+                ts = []
+                for _ in range(5):
+                    e0 = torch.cuda.Event(enable_timing=True)
+                    e1 = torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    _lib.call("plato_agg_tune_stream", mode, src.data_ptr(), dst.data_ptr(), n_el, blocks,
+                              stream.cuda_stream)
+                    e1.record(stream)
+                    e1.synchronize()
+                    ts.append(e0.elapsed_time(e1))
+                probes[f"{name}_b{blocks}"] = nbytes / (statistics.median(ts) * 1e-3) / 1e9
+        del src, dst
         if rank == 0:
             import ctypes
+
+            print(json.dumps({"ceilings_GBps": {k: round(v, 1) for k, v in probes.items()}}), flush=True)
 
             for v in range(nv):
                 bs, a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()

@@ -35,6 +35,13 @@ int plato_agg_tune_fedavg(int variant, int has_base,
                           float* d_out_f32, float* d_out_i64f,
                           size_t n_f32, size_t n_i64, hipStream_t stream);
 
+/* Ceiling probes: mode 0 = non-temporal copy src -> dst, mode 1 = non-temporal
+ * read of src only; n fp32 elements (n % 4 == 0), `blocks` workgroups of 256
+ * grid-striding (<= 0: 2048).  bench.py --sweep reports them as the measured
+ * streaming ceilings of the device next to the FedAvg kernel variants. */
+int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n,
+                          int blocks, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

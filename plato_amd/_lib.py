@@ -75,6 +75,7 @@ SIGNATURES = {
         [_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),
          ctypes.POINTER(_c_int)],
     ),
+    "plato_agg_tune_stream": (_c_int, [_c_int, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_void_p]),
     "plato_agg_tune_fedavg": (
         _c_int,
         [_c_int, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p,

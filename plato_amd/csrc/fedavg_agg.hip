@@ -427,6 +427,44 @@ int run_agg(int variant, bool has_base, const float* const* xf, const int64_t* c
 }
 
 // ---------------------------------------------------------------------------
+// Ceiling probes (tuning only): how fast this chip streams the same bytes with
+// no arithmetic dependence.  mode 0: NT read + NT write copy; mode 1: NT read
+// only (per-lane xor kept live by a conditional store that never fires).
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256) void stream_probe(const f4* __restrict__ src, f4* __restrict__ dst, uint64_t n4,
+                                                    uint32_t unroll) {
+  const uint64_t stride = uint64_t(gridDim.x) * 256;
+  uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+  for (; i + 7 * stride < n4; i += 8 * stride) {
+    f4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = __builtin_nontemporal_load((gf4*)src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if constexpr (MODE == 0) {
+        __builtin_nontemporal_store(v[u], (__attribute__((address_space(1))) f4*)dst + i + u * stride);
+      } else {
+        acc += v[u];
+      }
+    }
+  }
+  for (; i < n4; i += stride) {
+    f4 v = __builtin_nontemporal_load((gf4*)src + i);
+    if constexpr (MODE == 0) {
+      __builtin_nontemporal_store(v, (__attribute__((address_space(1))) f4*)dst + i);
+    } else {
+      acc += v;
+    }
+  }
+  if constexpr (MODE == 1) {
+    if (acc.x == 1234.5f && acc.y == -1234.5f) dst[0] = acc;  // keeps the loads live
+  }
+  (void)unroll;
+}
+
+// ---------------------------------------------------------------------------
 // Elementwise helpers (off the hot path; grid-stride, f4 where possible)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint64_t gtid() { return uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; }
@@ -590,6 +628,18 @@ int plato_agg_tune_fedavg(int variant, int has_base, const float* const* d_x_f32
                           size_t n_i64, hipStream_t stream) {
   return run_agg(variant, has_base != 0, d_x_f32, d_x_i64, d_w, d_s, K, d_base_f32, d_base_i64, d_out_f32,
                  d_out_i64f, n_f32, n_i64, stream);
+}
+
+int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n, int blocks, hipStream_t stream) {
+  if (!d_src || !d_dst || (n & 3)) return fail(PLATO_AGG_EINVAL, "stream probe: null pointer or n % 4 != 0");
+  if (blocks <= 0) blocks = 2048;
+  const uint64_t n4 = n / 4;
+  if (mode == 0) {
+    hipLaunchKernelGGL(stream_probe<0>, dim3(blocks), dim3(256), 0, stream, (const f4*)d_src, (f4*)d_dst, n4, 8u);
+  } else {
+    hipLaunchKernelGGL(stream_probe<1>, dim3(blocks), dim3(256), 0, stream, (const f4*)d_src, (f4*)d_dst, n4, 8u);
+  }
+  return check_launch("stream probe launch");
 }
 
 int plato_agg_compute_deltas(const float* d_x_f32, const int64_t* d_x_i64, const float* d_base_f32,
