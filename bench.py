@@ -219,7 +219,7 @@ def main():
                 e1.synchronize()
                 times[v].append(e0.elapsed_time(e1) / args.steps)
         # measured streaming ceilings over the same byte count (5.8 GB for C2)
-        n_probe = (alg_bytes // 4) // 4 * 4
+        n_probe = (alg_bytes // 4) // 8 * 8
         src = torch.empty(n_probe, dtype=torch.float32, device=dev)
         src.fill_(1.0)
         dst = torch.empty(n_probe // 2 + 64, dtype=torch.float32, device=dev)
