@@ -362,9 +362,41 @@ def host_inclusive(engine, layout, base, slab, k, weights, dev):
         torch.cuda.synchronize(dev)
         times.append(time.perf_counter() - t0)
     med = statistics.median(times[1:])
-    return {"value": round(layout.algorithmic_bytes(k) / med / 1e9, 2), "unit": "GB/s",
-            "ms": round(med * 1e3, 2),
-            "note": "pack CPU state_dicts -> pinned -> H2D -> kernel -> D2H; median of 2 after 1 warm-up"}
+    out = {"value": round(layout.algorithmic_bytes(k) / med / 1e9, 2), "unit": "GB/s",
+           "ms": round(med * 1e3, 2),
+           "note": "pack CPU state_dicts -> pinned -> H2D -> kernel -> D2H; median of 2 after 1 warm-up"}
+    # from the wire: pickled payload bytes (what the server receives, servers/base.py:821)
+    import pickle
+
+    from plato_amd import ingest
+
+    wire = [pickle.dumps(p) for p in payloads]
+    del payloads
+    t_wire = []
+    t_pickle = None
+    for r in range(3):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        rnd = engine.begin(baseline, k)
+        rnd.put_baseline(baseline)
+        for slot, data in enumerate(wire):
+            rnd.put_client(slot, ingest.loads(data, layout=layout, pin=True))
+        rnd.launch(weights)
+        rnd.result()
+        t_wire.append(time.perf_counter() - t0)
+    t0 = time.perf_counter()
+    for data in wire[:8]:
+        pickle.loads(data)
+    t_pickle = (time.perf_counter() - t0) / 8
+    med_w = statistics.median(t_wire[1:])
+    out["from_wire"] = {
+        "value": round(layout.algorithmic_bytes(k) / med_w / 1e9, 2), "unit": "GB/s",
+        "ms": round(med_w * 1e3, 2),
+        "native_parse_ms_per_payload": round(med_w * 1e3 / k, 3),
+        "pickle_loads_ms_per_payload": round(t_pickle * 1e3, 3),
+        "note": "pickled payload bytes -> libplato_ingest parse + gather into pinned arenas -> H2D -> "
+                "kernel -> D2H (replaces pickle.loads at servers/base.py:822)"}
+    return out
 
 
 def cpu_baseline(layout, base, slab, k, weights, out_f, out_i, reps, config):

@@ -121,13 +121,23 @@ class _Stager:
 
     def put(self, state_dict: Mapping[str, torch.Tensor], dst_f32: torch.Tensor,
             dst_i64: torch.Tensor) -> None:
+        n_f, n_i = self.layout.n_f32, self.layout.n_i64
+        arena_f = getattr(state_dict, "arena_f32", None)
+        if arena_f is not None and getattr(state_dict, "layout_signature", None) == self.layout.signature:
+            # Already laid out as the arena (plato_amd.ingest.loads): copy it as is.
+            arena_i = state_dict.arena_i64
+            with torch.cuda.stream(self.stream):
+                if n_f:
+                    dst_f32[:n_f].copy_(arena_f[:n_f], non_blocking=arena_f.is_pinned())
+                if n_i:
+                    dst_i64[:n_i].copy_(arena_i[:n_i], non_blocking=arena_i.is_pinned())
+            return
         j = self.next
         self.next = (j + 1) % len(self.bufs)
         if self.events[j] is not None:
             self.events[j].synchronize()
         hf, hi = self.bufs[j]
         self.layout.pack(state_dict, hf, hi)
-        n_f, n_i = self.layout.n_f32, self.layout.n_i64
         with torch.cuda.stream(self.stream):
             if n_f:
                 dst_f32[:n_f].copy_(hf[:n_f], non_blocking=True)

@@ -1,0 +1,198 @@
+"""Payload ingestion: pickled ``state_dict`` bytes -> tensors in one flat (pinned) arena.
+
+Replaces ``pickle.loads`` of a client payload on the server
+(plato/servers/base.py:822; ``pickle.load`` at :791-792 for comm_simulation)
+with ``libplato_ingest.so`` (include/plato_ingest.h): a C++ parser that only
+recognises a pickled dict of CPU tensors and executes nothing, and a
+multi-threaded gather of the tensor bytes straight into the arena the engine
+copies to HBM.  With a layout, the result is an :class:`ArenaStateDict` whose
+tensors are views of that arena, so staging it needs no pack step.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from collections import OrderedDict
+
+import numpy as np
+import torch
+
+from .arena import F32, I64, ArenaLayout
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libplato_ingest.so")
+MAX_DIMS = 8
+
+DTYPES = {
+    0: torch.float32, 1: torch.int64, 2: torch.float64, 3: torch.float16, 4: torch.bfloat16,
+    5: torch.int32, 6: torch.int16, 7: torch.int8, 8: torch.uint8, 9: torch.bool,
+}
+
+
+class TensorInfo(ctypes.Structure):
+    _fields_ = [
+        ("name_offset", ctypes.c_uint64),
+        ("name_len", ctypes.c_uint32),
+        ("dtype", ctypes.c_int32),
+        ("ndim", ctypes.c_int32),
+        ("contiguous", ctypes.c_int32),
+        ("shape", ctypes.c_int64 * MAX_DIMS),
+        ("stride", ctypes.c_int64 * MAX_DIMS),
+        ("numel", ctypes.c_uint64),
+        ("storage_offset", ctypes.c_uint64),
+        ("storage_numel", ctypes.c_uint64),
+        ("data_offset", ctypes.c_uint64),
+        ("storage_id", ctypes.c_int32),
+        ("element_size", ctypes.c_int32),
+    ]
+
+
+class IngestError(ValueError):
+    """The bytes are not a pickled dict of CPU tensors this parser accepts."""
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"plato_amd: {LIB_PATH} is not built; run __graft_entry__.build()")
+            h = ctypes.CDLL(LIB_PATH)
+            h.plato_ingest_last_error.restype = ctypes.c_char_p
+            h.plato_ingest_last_error.argtypes = []
+            h.plato_ingest_parse.restype = ctypes.c_int
+            h.plato_ingest_parse.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(TensorInfo),
+                                             ctypes.c_int]
+            h.plato_ingest_gather.restype = ctypes.c_int
+            h.plato_ingest_gather.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(TensorInfo),
+                                              ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
+                                              ctypes.c_size_t, ctypes.c_int]
+            _lib = h
+    return _lib
+
+
+class ArenaStateDict(OrderedDict):
+    """A ``state_dict`` whose tensors are views of one flat arena (layout order).
+
+    ``arena_f32`` / ``arena_i64`` are the backing buffers (pinned when built
+    for staging) and ``layout_signature`` identifies the layout; the engine's
+    stager copies them to HBM directly instead of packing tensor by tensor.
+    """
+
+    arena_f32: torch.Tensor | None = None
+    arena_i64: torch.Tensor | None = None
+    layout_signature: tuple | None = None
+
+    def __reduce__(self):  # pickles (e.g. for payload-size accounting) as a plain OrderedDict
+        return (OrderedDict, (list(self.items()),))
+
+
+def _buffer(data):
+    """(address, length, keepalive) of a bytes-like object without copying."""
+    if isinstance(data, (bytes, bytearray)):
+        arr = np.frombuffer(data, dtype=np.uint8)
+    else:
+        arr = np.frombuffer(memoryview(data), dtype=np.uint8)
+    return arr.ctypes.data, arr.size, arr
+
+
+def parse(data) -> tuple[list[TensorInfo], list[str], object]:
+    """Parse pickled payload bytes; returns (tensor infos, keys, keepalive)."""
+    addr, n, keep = _buffer(data)
+    h = lib()
+    cap = 64
+    while True:
+        out = (TensorInfo * cap)()
+        rc = h.plato_ingest_parse(addr, n, out, cap)
+        if rc == -5:  # capacity
+            cap *= 8
+            continue
+        if rc < 0:
+            raise IngestError(f"payload rejected ({rc}): {h.plato_ingest_last_error().decode()}")
+        infos = list(out[:rc])
+        keys = [bytes(keep[t.name_offset : t.name_offset + t.name_len]).decode("utf-8") for t in infos]
+        return infos, keys, keep
+
+
+def _gather(keep, addr, n, infos, offsets, dst: torch.Tensor, threads: int):
+    arr = (TensorInfo * len(infos))(*infos)
+    offs = (ctypes.c_uint64 * len(infos))(*offsets)
+    rc = lib().plato_ingest_gather(addr, n, arr, len(infos), offs, dst.data_ptr(),
+                                   dst.numel() * dst.element_size(), threads)
+    if rc < 0:
+        raise IngestError(f"gather failed ({rc}): {lib().plato_ingest_last_error().decode()}")
+
+
+def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: int = 0) -> OrderedDict:
+    """``pickle.loads`` for a pickled ``state_dict`` of CPU tensors, natively.
+
+    Without ``layout``: an ``OrderedDict`` of fresh contiguous tensors (one
+    backing buffer).  With ``layout`` (the engine's arena for the baseline):
+    an :class:`ArenaStateDict` laid out exactly as the arena, fp32 entries in
+    the fp32 region and int64 entries in the int64 region; raises
+    ``KeyError``/``ValueError`` if the payload does not match the layout.
+    """
+    infos, keys, keep = parse(data)
+    addr, n = keep.ctypes.data, keep.size
+    if layout is None:
+        offsets, total = [], 0
+        for t in infos:
+            total = (total + 63) // 64 * 64
+            offsets.append(total)
+            total += t.numel * t.element_size
+        buf = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=pin)
+        _gather(keep, addr, n, infos, offsets, buf, threads)
+        out = OrderedDict()
+        for key, t, off in zip(keys, infos, offsets):
+            dt = DTYPES[t.dtype]
+            shape = tuple(t.shape[: t.ndim])
+            view = buf[off : off + t.numel * t.element_size].view(dt).view(shape)
+            out[key] = view
+        return out
+
+    if len(keys) != len(layout.entries):
+        raise KeyError(f"payload has {len(keys)} entries, the layout has {len(layout.entries)}")
+    f32 = torch.empty(layout.row_f32, dtype=torch.float32, pin_memory=pin)
+    i64 = torch.empty(layout.row_i64, dtype=torch.int64, pin_memory=pin)
+    f_infos, f_offs, i_infos, i_offs = [], [], [], []
+    for key, t in zip(keys, infos):
+        if key not in layout._by_name:
+            raise KeyError(f"payload entry {key!r} is not in the layout")
+        e = layout[key]
+        want = 0 if e.region == F32 else 1
+        shape = tuple(t.shape[: t.ndim])
+        if t.dtype != want or shape != e.shape:
+            raise ValueError(f"payload[{key!r}] is {DTYPES[t.dtype]}{shape}, expected "
+                             f"{'torch.float32' if want == 0 else 'torch.int64'}{e.shape}")
+        if e.region == F32:
+            f_infos.append(t)
+            f_offs.append(e.offset * 4)
+        else:
+            i_infos.append(t)
+            i_offs.append(e.offset * 8)
+    if f_infos:
+        _gather(keep, addr, n, f_infos, f_offs, f32, threads)
+    if i_infos:
+        _gather(keep, addr, n, i_infos, i_offs, i64, threads)
+    out = ArenaStateDict()
+    for key in keys:
+        e = layout[key]
+        src = f32 if e.region == F32 else i64
+        out[key] = src[e.offset : e.offset + e.numel].view(e.shape)
+    out.arena_f32, out.arena_i64 = f32, i64
+    out.layout_signature = layout.signature
+    return out
+
+
+def load_file(path: str, layout: ArenaLayout | None = None, pin: bool = False) -> OrderedDict:
+    """``pickle.load(open(path, 'rb'))`` of a comm_simulation payload file, natively."""
+    data = np.fromfile(path, dtype=np.uint8)
+    return loads(data, layout=layout, pin=pin)

@@ -1,0 +1,61 @@
+"""Server-side payload ingestion hook: native parsing of arriving payload bytes.
+
+The reference joins a client's socket.io chunks and calls ``pickle.loads``
+on them (plato/servers/base.py:817-831).  :class:`WireIngestMixin` overrides
+that one method so the bytes are parsed by libplato_ingest.so directly into a
+pinned arena laid out like the engine's (baseline key order).  The result is a
+real ``OrderedDict`` of CPU tensors (an :class:`~plato_amd.ingest.ArenaStateDict`),
+so every later step of the reference — inbound processors, ``weights_received``,
+size accounting, ``self.updates`` — sees what ``pickle.loads`` would have
+produced, and the aggregation hook stages it to HBM without packing.
+
+Payloads that are not a plain dict of tensors (algorithms that send extra
+objects) are handed to ``pickle.loads`` exactly as the reference does.
+"""
+
+from __future__ import annotations
+
+import pickle
+
+from .. import ingest
+from ..arena import ArenaLayout
+
+
+class WireIngestMixin:
+    #: pin the per-payload arenas (async H2D); False keeps them pageable
+    ingest_pinned = True
+
+    def _ingest_layout(self):
+        try:
+            baseline = self.algorithm.extract_weights()
+            layout = ArenaLayout.from_state_dict(baseline)
+        except (AttributeError, TypeError):
+            return None
+        cached = getattr(self, "_plato_amd_ingest_layout", None)
+        if cached is not None and cached.signature == layout.signature:
+            return cached
+        self._plato_amd_ingest_layout = layout
+        return layout
+
+    def ingest_payload(self, payload: bytes):
+        """Native ``pickle.loads`` of one payload (falls back for non-tensor payloads)."""
+        try:
+            return ingest.loads(payload, layout=self._ingest_layout(), pin=self.ingest_pinned)
+        except (ingest.IngestError, KeyError, ValueError):
+            return pickle.loads(payload)
+
+    async def _client_payload_arrived(self, sid, client_id):
+        """plato/servers/base.py:817-831 with the unpickle done natively."""
+        assert len(self.client_chunks[sid]) > 0 and client_id in self.training_clients
+
+        payload = b"".join(self.client_chunks[sid])
+        _data = self.ingest_payload(payload)
+        self.client_chunks[sid] = []
+
+        if self.client_payload[sid] is None:
+            self.client_payload[sid] = _data
+        elif isinstance(self.client_payload[sid], list):
+            self.client_payload[sid].append(_data)
+        else:
+            self.client_payload[sid] = [self.client_payload[sid]]
+            self.client_payload[sid].append(_data)

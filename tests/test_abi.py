@@ -12,12 +12,12 @@ from plato_amd import _lib
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
+def declared_symbols(pattern="plato_agg*.h"):
     names = set()
-    for header in glob.glob(os.path.join(ROOT, "include", "*.h")):
+    for header in glob.glob(os.path.join(ROOT, "include", pattern)):
         text = open(header).read()
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-        names.update(re.findall(r"\b(plato_agg_\w+)\s*\(", text))
+        names.update(re.findall(r"\b(plato_(?:agg|ingest)_\w+)\s*\(", text))
     return names
 
 
@@ -37,6 +37,18 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(handle, name), name
     # and the Python binding knows the signature of each
     assert declared_symbols() == set(_lib.SIGNATURES)
+
+
+def test_ingest_library_exports_its_header():
+    from plato_amd import ingest
+
+    if not os.path.exists(ingest.LIB_PATH):
+        pytest.skip("ingest library not built")
+    handle = ctypes.CDLL(ingest.LIB_PATH)
+    names = declared_symbols("plato_ingest.h")
+    assert names == {"plato_ingest_last_error", "plato_ingest_parse", "plato_ingest_gather"}
+    for name in names:
+        assert hasattr(handle, name), name
 
 
 def test_binding_loads_and_reports_abi():

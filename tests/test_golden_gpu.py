@@ -262,3 +262,22 @@ def test_port_server_with_stale_model_matches_reference(tmp_path):
     got = _flat(layout, updated, "f32").astype(np.float64)
     exp = G.load_full()[f"{recipe['name']}/updated_f32"].astype(np.float64)
     assert np.max(np.abs(got - exp)) / np.max(np.abs(exp)) <= 1e-6
+
+
+def test_wire_ingested_payloads_match_reference(engine):
+    """Pickled payload bytes -> native ingest (pinned arenas) -> engine: reference digest."""
+    import pickle
+
+    from plato_amd import ingest
+
+    case = next(c for c in CASES if c["recipe"]["name"] == "resnet18_k16_permuted")
+    recipe, exp = case["recipe"], case["expected"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    order = G.order_of(recipe)
+    wire = [pickle.dumps(payloads[c]) for c in order]
+    received = [ingest.loads(w, layout=layout, pin=True) for w in wire]
+    assert all(isinstance(r, ingest.ArenaStateDict) for r in received)
+    weights, _ = G.weights_for(recipe, W)
+    updated = engine.aggregate_weights(baseline, received, weights)
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]

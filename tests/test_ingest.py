@@ -1,0 +1,205 @@
+"""Native payload ingestion (libplato_ingest.so) vs pickle.loads, on the CPU.
+
+The reference server turns payload bytes back into a state_dict with
+pickle.loads (plato/servers/base.py:822).  The native parser must produce the
+same keys, dtypes, shapes and values, land them in the engine's arena layout,
+and refuse (never execute) anything that is not a pickled dict of tensors.
+"""
+
+import io
+import os
+import pickle
+import random
+import subprocess
+import sys
+import time
+from collections import OrderedDict
+
+import numpy as np
+import pytest
+import torch
+
+from plato_amd import ingest, workloads
+from plato_amd.arena import ArenaLayout
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.skipif(not os.path.exists(ingest.LIB_PATH), reason="libplato_ingest.so not built")
+
+
+def state_dict(spec, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    out = OrderedDict()
+    for name, shape, region in spec:
+        if region == "f32":
+            out[name] = torch.randn(shape, generator=g)
+        else:
+            out[name] = torch.randint(0, 10**6, shape, generator=g)
+    return out
+
+
+def assert_same(a, b):
+    assert list(a.keys()) == list(b.keys())
+    for k in a:
+        assert a[k].dtype == b[k].dtype, k
+        assert tuple(a[k].shape) == tuple(b[k].shape), k
+        assert torch.equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("proto", [3, 4, 5])
+def test_matches_pickle_loads_resnet18(proto):
+    sd = state_dict(workloads.resnet(18), 1)
+    data = pickle.dumps(sd, protocol=proto)
+    assert_same(ingest.loads(data), pickle.loads(data))
+
+
+def test_protocol2_is_refused_cleanly():
+    """Protocol 2 has no bytes opcode (storage blobs become _codecs.encode calls): refused."""
+    with pytest.raises(ingest.IngestError, match="_codecs"):
+        ingest.loads(pickle.dumps(state_dict(workloads.lenet5()), protocol=2))
+
+
+def test_arena_layout_matches_pack():
+    spec = workloads.resnet(18)
+    sd = state_dict(spec, 2)
+    layout = ArenaLayout.from_shapes(spec)
+    got = ingest.loads(pickle.dumps(sd), layout=layout)
+    assert isinstance(got, ingest.ArenaStateDict) and got.layout_signature == layout.signature
+    f = torch.empty(layout.row_f32)
+    i = torch.empty(layout.row_i64, dtype=torch.int64)
+    layout.pack(sd, f, i)
+    assert torch.equal(got.arena_f32[: layout.n_f32], f[: layout.n_f32])
+    assert torch.equal(got.arena_i64[: layout.n_i64], i[: layout.n_i64])
+    assert_same(got, sd)
+    # and it pickles back like the plain dict the reference sizes (servers/base.py:839-846)
+    assert_same(pickle.loads(pickle.dumps(got)), sd)
+
+
+def test_odd_tensors():
+    base = torch.arange(24, dtype=torch.float32).reshape(4, 6)
+    sd = OrderedDict()
+    sd["tied_a"] = base
+    sd["tied_b"] = base                      # shared storage (tied weights)
+    sd["transposed"] = base.t()              # non-contiguous
+    sd["slice"] = base[1:3, 2:5]             # storage offset + strides
+    sd["scalar_i64"] = torch.tensor(7)
+    sd["empty"] = torch.empty(0, 3)
+    sd["half"] = torch.randn(5).half()
+    sd["bf16"] = torch.randn(5).bfloat16()
+    sd["f64"] = torch.randn(3, dtype=torch.float64)
+    sd["bool"] = torch.tensor([True, False, True])
+    sd["u8"] = torch.arange(7, dtype=torch.uint8)
+    sd["i32"] = torch.arange(-3, 3, dtype=torch.int32)
+    data = pickle.dumps(sd)
+    assert_same(ingest.loads(data), pickle.loads(data))
+    plain = dict(sd)
+    assert_same(ingest.loads(pickle.dumps(plain)), plain)
+
+
+def test_layout_mismatch_is_rejected():
+    layout = ArenaLayout.from_shapes(workloads.lenet5())
+    sd = state_dict(workloads.lenet5())
+    sd["fc5.bias"] = torch.zeros(11)
+    with pytest.raises(ValueError):
+        ingest.loads(pickle.dumps(sd), layout=layout)
+    del sd["fc5.bias"]
+    with pytest.raises(KeyError):
+        ingest.loads(pickle.dumps(sd), layout=layout)
+
+
+class Evil:
+    def __reduce__(self):
+        return (os.system, ("touch /tmp/plato_ingest_pwned",))
+
+
+def test_never_executes_and_rejects_foreign_objects():
+    if os.path.exists("/tmp/plato_ingest_pwned"):
+        os.remove("/tmp/plato_ingest_pwned")
+    for obj in [OrderedDict(a=Evil()), Evil(), [torch.zeros(2)], OrderedDict(a=[1, 2]), {"a": 1.5},
+                OrderedDict(a=torch.zeros(2), b="x")]:
+        with pytest.raises(ingest.IngestError):
+            ingest.loads(pickle.dumps(obj))
+    assert not os.path.exists("/tmp/plato_ingest_pwned")
+
+
+def test_truncation_and_corruption_fuzz():
+    """Every prefix and random byte flips: error or a result, never a crash (subprocess)."""
+    code = r'''
+import pickle, random, sys
+from collections import OrderedDict
+import torch
+sys.path.insert(0, sys.argv[1])
+from plato_amd import ingest
+sd = OrderedDict(w=torch.randn(3, 4), b=torch.arange(5), n=torch.tensor(3))
+data = pickle.dumps(sd)
+ok = err = 0
+for cut in range(len(data)):
+    try:
+        ingest.loads(data[:cut]); ok += 1
+    except (ingest.IngestError, KeyError, ValueError):
+        err += 1
+rnd = random.Random(0)
+for _ in range(3000):
+    b = bytearray(data)
+    for _ in range(rnd.randint(1, 4)):
+        b[rnd.randrange(len(b))] = rnd.randrange(256)
+    try:
+        ingest.loads(bytes(b)); ok += 1
+    except (ingest.IngestError, KeyError, ValueError, RuntimeError, OverflowError):
+        err += 1
+print("OK", ok, err)
+'''
+    proc = subprocess.run([sys.executable, "-c", code, ROOT], capture_output=True, text=True, timeout=300)
+    assert proc.returncode == 0 and "OK" in proc.stdout, proc.stderr[-2000:]
+
+
+def test_faster_than_pickle_loads():
+    sd = state_dict(workloads.resnet(18), 3)
+    layout = ArenaLayout.from_shapes(workloads.resnet(18))
+    data = pickle.dumps(sd)
+    ingest.loads(data, layout=layout)
+    t0 = time.perf_counter()
+    for _ in range(5):
+        pickle.loads(data)
+    t_pickle = (time.perf_counter() - t0) / 5
+    t0 = time.perf_counter()
+    for _ in range(5):
+        ingest.loads(data, layout=layout)
+    t_native = (time.perf_counter() - t0) / 5
+    print(f"pickle.loads {t_pickle * 1e3:.1f} ms, native {t_native * 1e3:.1f} ms")
+    assert t_native < t_pickle
+
+
+def test_wire_ingest_mixin_replaces_pickle_loads():
+    """The overridden _client_payload_arrived (servers/base.py:817-831) yields the same payload."""
+    import asyncio
+
+    from plato_amd.servers import WireIngestMixin
+
+    spec = workloads.resnet(18)
+    base = state_dict(spec, 5)
+    client = state_dict(spec, 6)
+    data = pickle.dumps(client)
+
+    class Algo:
+        def extract_weights(self):
+            return base
+
+    class S(WireIngestMixin):
+        ingest_pinned = False
+
+        def __init__(self):
+            self.algorithm = Algo()
+            self.client_chunks = {"sid": [data[i:i + 2**20] for i in range(0, len(data), 2**20)]}
+            self.client_payload = {"sid": None}
+            self.training_clients = {3: 1}
+
+    s = S()
+    asyncio.run(s._client_payload_arrived("sid", 3))
+    got = s.client_payload["sid"]
+    assert isinstance(got, ingest.ArenaStateDict)
+    assert_same(got, client)
+    # a non-state-dict payload goes through pickle.loads like the reference
+    s.client_chunks["sid"] = [pickle.dumps(["features", 1, 2])]
+    s.client_payload["sid"] = None
+    asyncio.run(s._client_payload_arrived("sid", 3))
+    assert s.client_payload["sid"] == ["features", 1, 2]
