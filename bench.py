@@ -370,7 +370,9 @@ def host_inclusive(engine, layout, base, slab, k, weights, dev):
 
     from plato_amd import ingest
 
-    wire = [pickle.dumps(p) for p in payloads]
+    # clients pickle model.state_dict(): one storage per tensor (views of one
+    # arena would each serialise the whole arena)
+    wire = [pickle.dumps(type(p)((n, t.clone()) for n, t in p.items())) for p in payloads]
     del payloads
     t_wire = []
     t_pickle = None

@@ -274,7 +274,9 @@ def test_wire_ingested_payloads_match_reference(engine):
     recipe, exp = case["recipe"], case["expected"]
     layout, baseline, payloads = _host_payloads(recipe)
     order = G.order_of(recipe)
-    wire = [pickle.dumps(payloads[c]) for c in order]
+    # one storage per tensor, like a client's model.state_dict() (views of one
+    # arena would each pickle the whole arena)
+    wire = [pickle.dumps(type(payloads[c])((n, t.clone()) for n, t in payloads[c].items())) for c in order]
     received = [ingest.loads(w, layout=layout, pin=True) for w in wire]
     assert all(isinstance(r, ingest.ArenaStateDict) for r in received)
     weights, _ = G.weights_for(recipe, W)
