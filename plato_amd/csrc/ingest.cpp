@@ -9,6 +9,9 @@
 // checked against [buf, buf + len).
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
 #include <cstdint>
 #include <cstring>
 #include <memory>
@@ -434,6 +437,73 @@ struct Piece {
   size_t bytes;
 };
 
+// Persistent copy workers: creating threads in every gather call cost more
+// than the copies (~20 us per thread, two gathers per payload).
+class Pool {
+ public:
+  static Pool& get() {
+    static Pool* p = new Pool();  // never destroyed: no teardown ordering at exit
+    return *p;
+  }
+
+  // Runs fn(0 .. n_tasks-1) on up to `width` threads, the caller included.
+  void run(size_t n_tasks, int width, const std::function<void(size_t)>& fn) {
+    std::lock_guard<std::mutex> call(call_mu_);  // one parallel gather at a time
+    const int helpers = std::max(0, std::min(width, kMax) - 1);
+    std::atomic<size_t> next{0};
+    std::function<void()> body = [&]() {
+      for (size_t k = next.fetch_add(1); k < n_tasks; k = next.fetch_add(1)) fn(k);
+    };
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      while (int(spawned_) < helpers) {
+        const int id = spawned_++;
+        std::thread([this, id] { loop(id); }).detach();
+      }
+      job_ = &body;
+      participants_ = helpers;
+      remaining_ = helpers;
+      ++gen_;
+    }
+    cv_.notify_all();
+    body();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return remaining_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  static constexpr int kMax = 32;
+
+  void loop(int id) {
+    uint64_t seen = 0;
+    for (;;) {
+      std::function<void()>* job = nullptr;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        if (id >= participants_) continue;
+        job = job_;
+      }
+      (*job)();
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        --remaining_;
+      }
+      done_cv_.notify_all();
+    }
+  }
+
+  std::mutex call_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void()>* job_ = nullptr;
+  int spawned_ = 0;
+  int participants_ = 0;
+  int remaining_ = 0;
+  uint64_t gen_ = 0;
+};
+
 void copy_strided(const uint8_t* base, const plato_ingest_tensor& t, uint8_t* dst) {
   const size_t es = size_t(t.element_size);
   int64_t idx[PLATO_INGEST_MAX_DIMS] = {0};
@@ -518,16 +588,13 @@ int plato_ingest_gather(const uint8_t* buf, size_t len, const plato_ingest_tenso
   for (auto& p : pieces) total += p.bytes;
   int nt = threads > 0 ? threads : int(std::max(1u, std::thread::hardware_concurrency()));
   nt = int(std::min<size_t>(size_t(nt), std::max<size_t>(1, total / (size_t(4) << 20))));
-  nt = std::min(nt, 32);
-  std::atomic<size_t> next{0};
-  auto worker = [&]() {
-    for (size_t k = next.fetch_add(1); k < pieces.size(); k = next.fetch_add(1))
-      std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].bytes);
-  };
-  std::vector<std::thread> pool;
-  for (int w = 1; w < nt; ++w) pool.emplace_back(worker);
-  worker();
-  for (auto& th : pool) th.join();
+  nt = std::min(nt, 16);
+  if (nt <= 1 || pieces.size() <= 1) {
+    for (auto& p : pieces) std::memcpy(p.dst, p.src, p.bytes);
+  } else {
+    Pool::get().run(pieces.size(), nt,
+                    [&](size_t k) { std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].bytes); });
+  }
   for (int i : strided) copy_strided(buf + t[i].data_offset, t[i], dst + dst_byte_offset[i]);
   g_err.clear();
   return 0;
