@@ -84,11 +84,21 @@ def dist_setup(args):
     if world != args.gpus:
         if world == 1 and args.gpus > 1:
             raise SystemExit("--gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    backend = os.environ.get("PLATO_BENCH_BACKEND", "nccl")
+    ndev = torch.cuda.device_count()
+    if local >= ndev:
+        if backend != "gloo":
+            raise SystemExit(f"rank {rank}: LOCAL_RANK {local} but only {ndev} GPU(s); one process per GPU "
+                             "(set PLATO_BENCH_BACKEND=gloo to rehearse several ranks on one GPU)")
+        local = local % ndev  # rehearsal only: ranks share a GPU
     torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":  # RCCL over xGMI
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     return world, rank, local
 
 
@@ -104,7 +114,8 @@ def max_over_ranks(value: float, world: int) -> float:
         return value
     import torch.distributed as dist
 
-    t = torch.tensor([value], dtype=torch.float64, device="cuda")
+    dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+    t = torch.tensor([value], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
