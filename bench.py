@@ -42,6 +42,8 @@ def parse():
     p.add_argument("--config", default="C2", choices=sorted(CONFIGS),
                    help="BASELINE.json configuration (C2 = the headline metric's workload)")
     p.add_argument("--clients", type=int, default=None, help="override K")
+    p.add_argument("--codec", default="native", choices=["native", "bf16"],
+                   help="payload codec: bf16 = model_quantize'd payloads, kept bf16 in HBM")
     p.add_argument("--variant", type=int, default=None, help="kernel variant (tuning)")
     p.add_argument("--sweep", action="store_true", help="time every kernel variant, interleaved")
     p.add_argument("--seed", type=int, default=0)
@@ -187,6 +189,13 @@ def main():
     slab = ClientSlab(layout, k, dev)
     fill_baseline(base, seed)
     fill_clients(slab, base, seed, k)
+    if args.codec == "bf16":  # model_quantize'd payloads (every entry .to(bfloat16))
+        slab16 = ClientSlab(layout, k, dev, codec="bf16")
+        slab16.f32.copy_(slab.f32.to(torch.bfloat16))
+        slab16.i64.copy_(slab.i64.to(torch.bfloat16))
+        del slab
+        torch.cuda.empty_cache()
+        slab = slab16
 
     from plato_amd import synthetic
     from plato_amd import weights as W
@@ -207,10 +216,18 @@ def main():
     torch.cuda.synchronize(dev)
 
     def step(variant=None):
+        if args.codec == "bf16":
+            _lib.call("plato_agg_fedavg_weights_bf16", tf.data_ptr(), ti.data_ptr(), w.data_ptr(), None, k,
+                      base.f32.data_ptr(), base.i64.data_ptr(), out_f.data_ptr(), out_i.data_ptr(),
+                      layout.n_f32, layout.n_i64, stream.cuda_stream)
+            return
         engine.variant = args.variant if variant is None else variant
         engine.launch_fedavg(layout, tf, ti, w, None, k, base.f32, base.i64, out_f, out_i, stream)
 
     alg_bytes = layout.algorithmic_bytes(k)
+    if args.codec == "bf16":  # K bf16 client arenas + fp32 baseline and result
+        alg_bytes = k * 2 * (layout.n_f32 + layout.n_i64) + 2 * (layout.n_f32 * 4 + layout.n_i64 * 8)
+        job_bytes = alg_bytes * (world if scaling == "weak" else 1)
 
     if args.sweep:
         nv = _lib.lib().plato_agg_tune_num_variants()
@@ -319,6 +336,7 @@ def main():
             "algorithmic_bytes_per_step_job": job_bytes,
             "parallelism": f"bucket{world}",
             "kernel_variant": args.variant if args.variant is not None else 0,
+            "payload_codec": args.codec,
         },
         "roofline": {
             "bound": "hbm",
@@ -334,6 +352,8 @@ def main():
         },
     }
 
+    if args.codec != "native":
+        args.no_host_inclusive = args.no_cpu_baseline = True
     if rank == 0 and world == 1 and not args.no_host_inclusive:
         result["host_inclusive"] = host_inclusive(engine, layout, base, slab, k, weights, dev)
 

@@ -38,6 +38,9 @@
  *                                 (plato/algorithms/fedavg.py:29-37)
  *   plato_agg_cast_f32_i64     <- Algorithm.load_weights' load_state_dict
  *                                 fp32 -> int64 copy (plato/algorithms/fedavg.py:46-48)
+ *   plato_agg_fedavg_weights_bf16 <- the model_dequantize inbound processor
+ *                                 (plato/processors/model_dequantize.py:15-18)
+ *                                 followed by the same chain, on bf16 payloads
  *   plato_agg_mix_weights      <- FedAsync Algorithm.aggregate_weights
  *                                 (examples/async/fedasync/fedasync_algorithm.py:9-20)
  *   plato_agg_client_dots      <- the model-wide reductions of Port's
@@ -100,6 +103,25 @@ int plato_agg_fedavg_deltas(const float* const* d_d_f32,
                             const float* d_w, const float* d_s, int K,
                             float* d_avg_f32, float* d_avg_i64f,
                             size_t n_f32, size_t n_i64, hipStream_t stream);
+
+/*
+ * Fused FedAvg over K bf16-quantized client payloads (Plato's model_quantize
+ * codec: every entry .to(bfloat16), plato/processors/model_quantize.py:15),
+ * equal to dequantizing them on the server (model_dequantize.py:15-18,
+ * .to(float32), exact) and running plato_agg_fedavg_weights: the payload
+ * stays bf16 through PCIe and HBM and is widened in registers.  The int64
+ * entries' payload values are bf16 as well; as in the reference, they are
+ * subtracted from the int64 baseline in fp32: d = fp32(x) - fp32(b).
+ *   d_x_bf16      K pointers to n_f32 bf16 values (16-byte aligned)
+ *   d_x_i64_bf16  K pointers to n_i64 bf16 values (or NULL if n_i64 == 0)
+ * Other arguments as plato_agg_fedavg_weights.
+ */
+int plato_agg_fedavg_weights_bf16(const uint16_t* const* d_x_bf16,
+                                  const uint16_t* const* d_x_i64_bf16,
+                                  const float* d_w, const float* d_s, int K,
+                                  const float* d_base_f32, const int64_t* d_base_i64,
+                                  float* d_out_f32, float* d_out_i64f,
+                                  size_t n_f32, size_t n_i64, hipStream_t stream);
 
 /* One client's deltas: out = x - base (fp32), and exact int64 x - base. */
 int plato_agg_compute_deltas(const float* d_x_f32, const int64_t* d_x_i64,

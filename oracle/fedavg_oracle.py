@@ -122,8 +122,13 @@ def fedavg_numpy(base_f32: np.ndarray, base_i64: np.ndarray, clients_f32, client
             t = np.multiply(t, s[i], dtype=np.float32)
         acc = np.add(acc, t, dtype=np.float32)
         if base_i64.size:
-            with np.errstate(over="ignore"):
-                di = (clients_i64[i].astype(np.int64) - base_i64.astype(np.int64)).astype(np.float32)
+            if clients_i64[i].dtype == np.float32:
+                # dequantized (bf16 codec) payload: fp32 tensor - int64 tensor
+                # promotes to fp32 (plato/algorithms/fedavg.py:23)
+                di = np.subtract(clients_i64[i], base_i64.astype(np.float32), dtype=np.float32)
+            else:
+                with np.errstate(over="ignore"):
+                    di = (clients_i64[i].astype(np.int64) - base_i64.astype(np.int64)).astype(np.float32)
             ti = np.multiply(di, w[i], dtype=np.float32)
             if s is not None:
                 ti = np.multiply(ti, s[i], dtype=np.float32)
@@ -160,6 +165,14 @@ def mix_numpy(base_f32, base_i64, x_f32, x_i64, mixing: float):
                    np.multiply(np.asarray(x_i64).astype(np.float32), m, dtype=np.float32),
                    dtype=np.float32)
     return out, out_i
+
+
+def bf16_roundtrip(values: np.ndarray) -> np.ndarray:
+    """model_quantize then model_dequantize (processors/model_quantize.py:15,
+    model_dequantize.py:15-18): .to(bfloat16).to(float32), via torch's CPU cast."""
+    import torch
+
+    return torch.from_numpy(np.ascontiguousarray(values)).to(torch.bfloat16).to(torch.float32).numpy()
 
 
 def trunc_to_int64(values_f32: np.ndarray) -> np.ndarray:

@@ -35,6 +35,11 @@ SIGNATURES = {
         [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
          _c_void_p, _c_void_p, _c_size_t, _c_size_t, _c_void_p],
     ),
+    "plato_agg_fedavg_weights_bf16": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
+         _c_void_p, _c_void_p, _c_size_t, _c_size_t, _c_void_p],
+    ),
     "plato_agg_fedavg_deltas": (
         _c_int,
         [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,

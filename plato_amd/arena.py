@@ -31,6 +31,19 @@ I64 = "i64"
 # row of a [K, row] slab starts 256-byte aligned (dwordx4-friendly).
 ROW_ALIGN = 64
 
+# Payload codecs: element dtypes of (fp32 region, int64 region) as the client
+# sends them.  "native": the model's own dtypes.  "bf16": Plato's
+# model_quantize outbound processor (plato/processors/model_quantize.py:15)
+# casts every entry to bfloat16.
+CODECS = {"native": (torch.float32, torch.int64), "bf16": (torch.bfloat16, torch.bfloat16)}
+
+
+def payload_codec(state_dict) -> str:
+    """The codec a payload arrives in (all-bf16 entries -> "bf16")."""
+    for tensor in state_dict.values():
+        return "bf16" if isinstance(tensor, torch.Tensor) and tensor.dtype == torch.bfloat16 else "native"
+    return "native"
+
 
 @dataclass(frozen=True)
 class Entry:
@@ -107,7 +120,8 @@ class ArenaLayout:
         """
         return (k + 2) * (self.n_f32 * 4 + self.n_i64 * 8)
 
-    def check_compatible(self, state_dict: Mapping[str, torch.Tensor], what: str) -> None:
+    def check_compatible(self, state_dict: Mapping[str, torch.Tensor], what: str,
+                         codec: str = "native") -> None:
         if len(state_dict) != len(self.entries):
             raise KeyError(
                 f"{what} has {len(state_dict)} entries, the baseline has {len(self.entries)}"
@@ -116,7 +130,7 @@ class ArenaLayout:
             if entry.name not in state_dict:
                 raise KeyError(f"{what} is missing {entry.name!r}")
             tensor = state_dict[entry.name]
-            want = torch.float32 if entry.region == F32 else torch.int64
+            want = CODECS[codec][0] if entry.region == F32 else CODECS[codec][1]
             if tensor.dtype != want or tuple(tensor.shape) != entry.shape:
                 raise ValueError(
                     f"{what}[{entry.name!r}] is {tensor.dtype}{tuple(tensor.shape)}, "

@@ -427,6 +427,137 @@ int run_agg(int variant, bool has_base, const float* const* xf, const int64_t* c
 }
 
 // ---------------------------------------------------------------------------
+// bf16 client payloads (Plato's model_quantize / model_dequantize codec,
+// plato/processors/model_quantize.py:15, model_dequantize.py:15-18): the
+// server dequantizes with .to(float32) before aggregating, which is exact, so
+// the kernel keeps the payload in bf16 through PCIe and HBM and widens in
+// registers (bits << 16).  Each lane owns 8 elements: one 16-byte bf16 load
+// per client, two float4 for the baseline and the result.  int64 entries
+// arrive as bf16 too (model_quantize converts every layer), and the
+// reference then subtracts the int64 baseline in fp32 (tensor promotion):
+// d = fp32(x) - fp32(b).
+// ---------------------------------------------------------------------------
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const u4 gu4;
+
+__device__ __forceinline__ float bf16_lo(unsigned int w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float bf16_hi(unsigned int w) { return __uint_as_float(w & 0xffff0000u); }
+__device__ __forceinline__ float bf16_at(const uint16_t* p, uint64_t e) {
+  return __uint_as_float(uint32_t(p[e]) << 16);
+}
+
+struct Bf16Args {
+  const uint16_t* const* xf;   // K pointers to n_f32 bf16
+  const uint16_t* const* xi;   // K pointers to n_i64 bf16 (int64 entries, quantized)
+  const float* w;
+  const float* s;
+  const float* base_f;
+  const int64_t* base_i;
+  float* out_f;
+  float* out_if;
+  uint64_t n8, n_f32, n_i64;
+  uint32_t nb_vec, nb_vec_full;
+  int K;
+};
+
+template <bool TWO, bool CHECK, int U>
+__device__ __forceinline__ void bf16_body(const Bf16Args& a, uint32_t blk) {
+  const uint64_t e8 = uint64_t(blk) * 256 + threadIdx.x;
+  const bool live = !CHECK || e8 < a.n8;
+  const uint64_t g = CHECK ? (e8 < a.n8 ? e8 : a.n8 - 1) : e8;
+  const uint32_t xoff = uint32_t(g * 16u);   // bf16 bytes
+  const uint32_t foff = uint32_t(g * 32u);   // fp32 bytes
+  const f4 b0 = ld4_off<false>(a.base_f, foff);
+  const f4 b1 = ld4_off<false>(a.base_f, foff + 16u);
+  f4 acc0 = f4_zero(), acc1 = f4_zero();
+  const int K = a.K;
+  int i = 0;
+  for (; i + U <= K; i += U) {
+    u4 q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint16_t* p = sld(a.xf, i + u);
+      q[u] = __builtin_nontemporal_load((gu4*)((__attribute__((address_space(1))) const char*)p + xoff));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float wu = sld(a.w, i + u);
+      float su = 1.f;
+      if constexpr (TWO) su = sld(a.s, i + u);
+      const f4 x0 = f4{bf16_lo(q[u].x), bf16_hi(q[u].x), bf16_lo(q[u].y), bf16_hi(q[u].y)};
+      const f4 x1 = f4{bf16_lo(q[u].z), bf16_hi(q[u].z), bf16_lo(q[u].w), bf16_hi(q[u].w)};
+      f4 t0 = f4_scale(x0 - b0, wu), t1 = f4_scale(x1 - b1, wu);
+      if constexpr (TWO) {
+        t0 = f4_scale(t0, su);
+        t1 = f4_scale(t1, su);
+      }
+      acc0 = acc0 + t0;
+      acc1 = acc1 + t1;
+    }
+  }
+  for (; i < K; ++i) {
+    const uint16_t* p = sld(a.xf, i);
+    const u4 q = __builtin_nontemporal_load((gu4*)((__attribute__((address_space(1))) const char*)p + xoff));
+    const float wu = sld(a.w, i);
+    float su = 1.f;
+    if constexpr (TWO) su = sld(a.s, i);
+    const f4 x0 = f4{bf16_lo(q.x), bf16_hi(q.x), bf16_lo(q.y), bf16_hi(q.y)};
+    const f4 x1 = f4{bf16_lo(q.z), bf16_hi(q.z), bf16_lo(q.w), bf16_hi(q.w)};
+    f4 t0 = f4_scale(x0 - b0, wu), t1 = f4_scale(x1 - b1, wu);
+    if constexpr (TWO) {
+      t0 = f4_scale(t0, su);
+      t1 = f4_scale(t1, su);
+    }
+    acc0 = acc0 + t0;
+    acc1 = acc1 + t1;
+  }
+  if (live) {
+    st4_off<true>(a.out_f, foff, b0 + acc0);
+    st4_off<true>(a.out_f, foff + 16u, b1 + acc1);
+  }
+}
+
+template <bool TWO>
+__device__ __forceinline__ void bf16_scalar(const Bf16Args& a, uint64_t j) {
+  const uint64_t tail = a.n_f32 - 8 * a.n8;
+  const int K = a.K;
+  if (j < tail) {
+    const uint64_t e = 8 * a.n8 + j;
+    const float b = a.base_f[e];
+    float acc = 0.f;
+    for (int i = 0; i < K; ++i) {
+      float t = (bf16_at(sld(a.xf, i), e) - b) * sld(a.w, i);
+      if constexpr (TWO) t = t * sld(a.s, i);
+      acc = acc + t;
+    }
+    a.out_f[e] = b + acc;
+    return;
+  }
+  const uint64_t e = j - tail;
+  if (e >= a.n_i64) return;
+  const float b = (float)a.base_i[e];
+  float acc = 0.f;
+  for (int i = 0; i < K; ++i) {
+    float t = (bf16_at(sld(a.xi, i), e) - b) * sld(a.w, i);
+    if constexpr (TWO) t = t * sld(a.s, i);
+    acc = acc + t;
+  }
+  a.out_if[e] = b + acc;
+}
+
+template <bool TWO>
+__global__ __launch_bounds__(256) void fedavg_bf16_kernel(Bf16Args a) {
+  const uint32_t blk = blockIdx.x;
+  if (blk < a.nb_vec_full) {
+    bf16_body<TWO, false, 8>(a, blk);
+  } else if (blk < a.nb_vec) {
+    bf16_body<TWO, true, 8>(a, blk);
+  } else {
+    bf16_scalar<TWO>(a, uint64_t(blk - a.nb_vec) * 256 + threadIdx.x);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Ceiling probes (tuning only): how fast this chip streams the same bytes with
 // no arithmetic dependence.  mode 0: NT read + NT write copy; mode 1: NT read
 // only (per-lane xor kept live by a conditional store that never fires).
@@ -608,6 +739,46 @@ int plato_agg_fedavg_deltas(const float* const* d_d_f32, const int64_t* const* d
                             size_t n_i64, hipStream_t stream) {
   return run_agg(0, false, d_d_f32, d_d_i64, d_w, d_s, K, nullptr, nullptr, d_avg_f32, d_avg_i64f, n_f32, n_i64,
                  stream);
+}
+
+int plato_agg_fedavg_weights_bf16(const uint16_t* const* d_x_bf16, const uint16_t* const* d_x_i64_bf16,
+                                  const float* d_w, const float* d_s, int K, const float* d_base_f32,
+                                  const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
+                                  size_t n_i64, hipStream_t stream) {
+  if (K <= 0) return fail(PLATO_AGG_EINVAL, "K must be >= 1");
+  if (!d_w) return fail(PLATO_AGG_EINVAL, "null weight array");
+  if (n_f32 && (!d_x_bf16 || !d_base_f32 || !d_out_f32)) return fail(PLATO_AGG_EINVAL, "null fp32 pointer");
+  if (n_i64 && (!d_x_i64_bf16 || !d_base_i64 || !d_out_i64f)) return fail(PLATO_AGG_EINVAL, "null int64 pointer");
+  if (n_f32 && (!aligned16(d_base_f32) || !aligned16(d_out_f32)))
+    return fail(PLATO_AGG_EINVAL, "fp32 baseline/output must be 16-byte aligned");
+  if (n_f32 + n_i64 == 0) return plato_agg_internal::clear_error();
+  Bf16Args a{};
+  a.xf = d_x_bf16;
+  a.xi = d_x_i64_bf16;
+  a.w = d_w;
+  a.s = d_s;
+  a.base_f = d_base_f32;
+  a.base_i = d_base_i64;
+  a.out_f = d_out_f32;
+  a.out_if = d_out_i64f;
+  a.n8 = n_f32 / 8;
+  a.n_f32 = n_f32;
+  a.n_i64 = n_i64;
+  a.K = K;
+  const uint64_t nb_vec = (a.n8 + 255) / 256;
+  const uint64_t n_scalar = (n_f32 - 8 * a.n8) + n_i64;
+  const uint64_t nb_scalar = (n_scalar + 255) / 256;
+  if (nb_vec + nb_scalar > 0x7fffffffull || a.n8 * 32ull > 0xffffffffull)
+    return fail(PLATO_AGG_EINVAL, "fp32 arena must be < 4 GiB per launch (split it into buckets)");
+  a.nb_vec = uint32_t(nb_vec);
+  a.nb_vec_full = uint32_t(a.n8 / 256);
+  dim3 grid(uint32_t(nb_vec + nb_scalar));
+  if (d_s) {
+    hipLaunchKernelGGL(fedavg_bf16_kernel<true>, grid, dim3(256), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(fedavg_bf16_kernel<false>, grid, dim3(256), 0, stream, a);
+  }
+  return check_launch("fedavg_bf16 kernel launch");
 }
 
 int plato_agg_tune_num_variants(void) { return kNumVariants; }

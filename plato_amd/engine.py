@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .arena import F32, I64, ArenaLayout
+from .arena import CODECS, F32, I64, ArenaLayout, payload_codec
 
 
 def fp32_weights(values: Sequence[float]) -> np.ndarray:
@@ -82,19 +82,25 @@ class DeviceArena:
 
 
 class ClientSlab:
-    """K client arenas in HBM as two row-major slabs ``[cap, row]``."""
+    """K client arenas in HBM as two row-major slabs ``[cap, row]``.
 
-    def __init__(self, layout: ArenaLayout, capacity: int, device: torch.device):
+    ``codec`` selects the element types the payloads arrive in (arena.CODECS):
+    bf16 payloads stay bf16 in HBM (half the bytes) and are widened by the kernel.
+    """
+
+    def __init__(self, layout: ArenaLayout, capacity: int, device: torch.device, codec: str = "native"):
         self.layout = layout
         self.capacity = capacity
-        self.f32 = torch.empty((capacity, layout.row_f32), dtype=torch.float32, device=device)
-        self.i64 = torch.empty((capacity, layout.row_i64), dtype=torch.int64, device=device)
+        self.codec = codec
+        dt_f, dt_i = CODECS[codec]
+        self.f32 = torch.empty((capacity, layout.row_f32), dtype=dt_f, device=device)
+        self.i64 = torch.empty((capacity, layout.row_i64), dtype=dt_i, device=device)
 
     def row_pointers(self, rows: Sequence[int]) -> tuple[np.ndarray, np.ndarray]:
         base_f = self.f32.data_ptr()
         base_i = self.i64.data_ptr()
-        sf = self.layout.row_f32 * 4
-        si = self.layout.row_i64 * 8
+        sf = self.f32.stride(0) * self.f32.element_size()
+        si = self.i64.stride(0) * self.i64.element_size()
         rows = np.asarray(rows, dtype=np.int64)
         return (base_f + rows * sf).astype(np.int64), (base_i + rows * si).astype(np.int64)
 
@@ -106,13 +112,16 @@ class _Stager:
     H2D copy of client j on a dedicated copy stream.
     """
 
-    def __init__(self, layout: ArenaLayout, device: torch.device, depth: int = 3):
+    def __init__(self, layout: ArenaLayout, device: torch.device, depth: int = 3, codec: str = "native",
+                 stream: torch.cuda.Stream | None = None):
         self.layout = layout
-        self.stream = torch.cuda.Stream(device)
+        self.codec = codec
+        self.stream = stream or torch.cuda.Stream(device)
+        dt_f, dt_i = CODECS[codec]
         self.bufs = [
             (
-                torch.empty(layout.row_f32, dtype=torch.float32, pin_memory=True),
-                torch.empty(layout.row_i64, dtype=torch.int64, pin_memory=True),
+                torch.empty(layout.row_f32, dtype=dt_f, pin_memory=True),
+                torch.empty(layout.row_i64, dtype=dt_i, pin_memory=True),
             )
             for _ in range(depth)
         ]
@@ -123,7 +132,8 @@ class _Stager:
             dst_i64: torch.Tensor) -> None:
         n_f, n_i = self.layout.n_f32, self.layout.n_i64
         arena_f = getattr(state_dict, "arena_f32", None)
-        if arena_f is not None and getattr(state_dict, "layout_signature", None) == self.layout.signature:
+        if (arena_f is not None and getattr(state_dict, "layout_signature", None) == self.layout.signature
+                and arena_f.dtype == self.bufs[0][0].dtype):
             # Already laid out as the arena (plato_amd.ingest.loads): copy it as is.
             arena_i = state_dict.arena_i64
             with torch.cuda.stream(self.stream):
@@ -160,26 +170,38 @@ class FedAvgEngine:
         self.lib = _lib.lib()
         self.variant = variant
         self._layout: ArenaLayout | None = None
-        self._slab: ClientSlab | None = None
+        self._slabs: dict[str, ClientSlab] = {}
+        self._stagers: dict[str, _Stager] = {}
         self._base: DeviceArena | None = None
-        self._stager: _Stager | None = None
+        self._copy_stream: torch.cuda.Stream | None = None
+        self._slab: ClientSlab | None = None      # slab of the current round's codec
+        self._stager: _Stager | None = None       # native-dtype stager (baselines)
 
     # ----------------------------------------------------------- allocation
-    def _prepare(self, template: Mapping[str, torch.Tensor], k: int) -> ArenaLayout:
+    def _prepare(self, template: Mapping[str, torch.Tensor], k: int, codec: str = "native") -> ArenaLayout:
+        if codec not in CODECS:
+            raise ValueError(f"unknown payload codec {codec!r}")
         layout = ArenaLayout.from_state_dict(template)
         if self._layout is None or self._layout.signature != layout.signature:
             self._layout = layout
-            self._slab = None
+            self._slabs = {}
+            self._stagers = {}
             self._base = None
-            self._stager = None
         layout = self._layout
-        if self._slab is None or self._slab.capacity < k:
-            self._slab = None
-            self._slab = ClientSlab(layout, k, self.device)
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(self.device)
+        slab = self._slabs.get(codec)
+        if slab is None or slab.capacity < k:
+            self._slabs.pop(codec, None)
+            slab = ClientSlab(layout, k, self.device, codec)
+            self._slabs[codec] = slab
+        for c in {"native", codec}:
+            if c not in self._stagers:
+                self._stagers[c] = _Stager(layout, self.device, codec=c, stream=self._copy_stream)
         if self._base is None:
             self._base = DeviceArena(layout, self.device)
-        if self._stager is None:
-            self._stager = _Stager(layout, self.device)
+        self._slab = slab
+        self._stager = self._stagers["native"]
         return layout
 
     def _upload_weights(self, weights: Sequence[float], scales: Sequence[float] | None):
@@ -227,15 +249,20 @@ class FedAvgEngine:
                       _ptr(out_i64f) if n_i else None, *args_tail)
 
     # ------------------------------------------------------ host-facing API
-    def begin(self, template: Mapping[str, torch.Tensor], capacity: int) -> "AggregationRound":
-        """Start a round: device arenas for up to ``capacity`` client payloads."""
+    def begin(self, template: Mapping[str, torch.Tensor], capacity: int,
+              codec: str = "native") -> "AggregationRound":
+        """Start a round: device arenas for up to ``capacity`` client payloads.
+
+        ``template`` is the baseline (its keys, shapes, dtypes define the arena);
+        ``codec`` is how the client payloads arrive ("native" or "bf16").
+        """
         if capacity <= 0:
             raise ValueError("no client payloads to aggregate")
-        layout = self._prepare(template, capacity)
+        layout = self._prepare(template, capacity, codec)
         # The previous round's kernel may still read the slab / baseline arena:
         # order this round's H2D copies (copy stream) after it.
-        self._stager.stream.wait_stream(torch.cuda.current_stream(self.device))
-        return AggregationRound(self, layout, capacity)
+        self._copy_stream.wait_stream(torch.cuda.current_stream(self.device))
+        return AggregationRound(self, layout, capacity, codec)
 
     def stage_clients(self, payloads: Sequence[Mapping[str, torch.Tensor]], template=None,
                       what: str = "weights_received") -> ArenaLayout:
@@ -262,7 +289,7 @@ class FedAvgEngine:
             raise ValueError("no client payloads to aggregate")
         if len(weights) != k:
             raise ValueError("weights must have one entry per client")
-        rnd = self.begin(baseline, k)
+        rnd = self.begin(baseline, k, payload_codec(weights_received[0]))
         rnd.put_baseline(baseline)
         for i, sd in enumerate(weights_received):
             rnd.put_client(i, sd)
@@ -359,10 +386,13 @@ class AggregationRound:
     reference regardless of the order payloads arrived in.
     """
 
-    def __init__(self, engine: FedAvgEngine, layout: ArenaLayout, capacity: int):
+    def __init__(self, engine: FedAvgEngine, layout: ArenaLayout, capacity: int, codec: str = "native"):
         self.engine = engine
         self.layout = layout
         self.capacity = capacity
+        self.codec = codec
+        self.slab = engine._slabs[codec]
+        self.stager = engine._stagers[codec]
         self.staged = [False] * capacity
         self.has_baseline = False
         self.event: torch.cuda.Event | None = None
@@ -378,9 +408,8 @@ class AggregationRound:
                    what: str = "weights_received") -> None:
         if not 0 <= slot < self.capacity:
             raise IndexError(f"slot {slot} outside [0, {self.capacity})")
-        self.layout.check_compatible(payload, f"{what}[{slot}]")
-        eng = self.engine
-        eng._stager.put(payload, eng._slab.f32[slot], eng._slab.i64[slot])
+        self.layout.check_compatible(payload, f"{what}[{slot}]", self.codec)
+        self.stager.put(payload, self.slab.f32[slot], self.slab.i64[slot])
         self.staged[slot] = True
 
     def launch(self, weights: Sequence[float], scales: Sequence[float] | None = None,
@@ -394,17 +423,25 @@ class AggregationRound:
                 raise ValueError(f"client slot {slot} was not staged")
         if not deltas and not self.has_baseline:
             raise ValueError("baseline not staged")
+        if deltas and self.codec != "native":
+            raise ValueError("deltas are fp32 (x - b promotes bf16 payloads); use the native codec")
         eng = self.engine
         lay = self.layout
         w, s = eng._upload_weights(weights, scales)
-        pf, pi = eng._slab.row_pointers(order)
+        pf, pi = self.slab.row_pointers(order)
         tf, ti = eng._pointer_tables(pf, pi)
         stream = torch.cuda.current_stream(eng.device)
-        eng._stager.fence(stream)
+        self.stager.fence(stream)
         out_f = torch.empty(lay.row_f32, dtype=torch.float32, device=eng.device)
         out_i = torch.empty(lay.row_i64, dtype=torch.float32, device=eng.device)
-        eng.launch_fedavg(lay, tf, ti, w, s, len(order), None if deltas else eng._base.f32,
-                          None if deltas else eng._base.i64, out_f, out_i, stream)
+        if self.codec == "bf16":
+            n_i = lay.n_i64
+            _lib.call("plato_agg_fedavg_weights_bf16", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w), _ptr(s),
+                      len(order), _ptr(eng._base.f32), _ptr(eng._base.i64) if n_i else None, _ptr(out_f),
+                      _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
+        else:
+            eng.launch_fedavg(lay, tf, ti, w, s, len(order), None if deltas else eng._base.f32,
+                              None if deltas else eng._base.i64, out_f, out_i, stream)
         # D2H into fresh pinned buffers, still stream-ordered; result() only waits.
         host_f = torch.empty(lay.n_f32, dtype=torch.float32, pin_memory=True)
         host_i = torch.empty(lay.n_i64, dtype=torch.float32, pin_memory=True)
@@ -433,6 +470,8 @@ class AggregationRound:
                 raise ValueError(f"client slot {slot} was not staged")
         if not slots:
             return []
+        if self.codec != "native":
+            raise NotImplementedError("similarities of bf16-coded payloads are not on the device path yet")
         eng = self.engine
         lay = self.layout
         lay.check_compatible(reference, "reference model")
@@ -444,7 +483,7 @@ class AggregationRound:
         h = _stream_handle(stream)
         _lib.call("plato_agg_compute_deltas", _ptr(eng._base.f32), _ptr(eng._base.i64), _ptr(prev.f32),
                   _ptr(prev.i64), _ptr(v.f32), _ptr(v.i64), lay.n_f32, lay.n_i64, h)
-        pf, pi = eng._slab.row_pointers(slots)
+        pf, pi = self.slab.row_pointers(slots)
         tf, ti = eng._pointer_tables(pf, pi)
         k = len(slots)
         ws_bytes = self.engine.lib.plato_agg_client_dots_workspace(k, lay.n_f32)

@@ -19,7 +19,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
-from .arena import F32, I64, ArenaLayout
+from .arena import CODECS, F32, ArenaLayout
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libplato_ingest.so")
@@ -131,7 +131,8 @@ def _gather(keep, addr, n, infos, offsets, dst: torch.Tensor, threads: int):
         raise IngestError(f"gather failed ({rc}): {lib().plato_ingest_last_error().decode()}")
 
 
-def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: int = 0) -> OrderedDict:
+def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: int = 0,
+          codec: str | None = None) -> OrderedDict:
     """``pickle.loads`` for a pickled ``state_dict`` of CPU tensors, natively.
 
     Without ``layout``: an ``OrderedDict`` of fresh contiguous tensors (one
@@ -160,24 +161,27 @@ def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: i
 
     if len(keys) != len(layout.entries):
         raise KeyError(f"payload has {len(keys)} entries, the layout has {len(layout.entries)}")
-    f32 = torch.empty(layout.row_f32, dtype=torch.float32, pin_memory=pin)
-    i64 = torch.empty(layout.row_i64, dtype=torch.int64, pin_memory=pin)
+    if codec is None:  # bf16 payloads (model_quantize) keep their dtype in the arena
+        codec = "bf16" if infos and DTYPES[infos[0].dtype] == torch.bfloat16 else "native"
+    dt_f, dt_i = CODECS[codec]
+    f32 = torch.empty(layout.row_f32, dtype=dt_f, pin_memory=pin)
+    i64 = torch.empty(layout.row_i64, dtype=dt_i, pin_memory=pin)
+    es_f, es_i = f32.element_size(), i64.element_size()
     f_infos, f_offs, i_infos, i_offs = [], [], [], []
     for key, t in zip(keys, infos):
         if key not in layout._by_name:
             raise KeyError(f"payload entry {key!r} is not in the layout")
         e = layout[key]
-        want = 0 if e.region == F32 else 1
+        want = dt_f if e.region == F32 else dt_i
         shape = tuple(t.shape[: t.ndim])
-        if t.dtype != want or shape != e.shape:
-            raise ValueError(f"payload[{key!r}] is {DTYPES[t.dtype]}{shape}, expected "
-                             f"{'torch.float32' if want == 0 else 'torch.int64'}{e.shape}")
+        if DTYPES[t.dtype] != want or shape != e.shape:
+            raise ValueError(f"payload[{key!r}] is {DTYPES[t.dtype]}{shape}, expected {want}{e.shape}")
         if e.region == F32:
             f_infos.append(t)
-            f_offs.append(e.offset * 4)
+            f_offs.append(e.offset * es_f)
         else:
             i_infos.append(t)
-            i_offs.append(e.offset * 8)
+            i_offs.append(e.offset * es_i)
     if f_infos:
         _gather(keep, addr, n, f_infos, f_offs, f32, threads)
     if i_infos:

@@ -24,6 +24,7 @@ from __future__ import annotations
 import asyncio
 
 from .. import weights as W
+from ..arena import payload_codec
 from ..engine import FedAvgEngine
 
 
@@ -57,7 +58,8 @@ class FusedAggregationMixin(_EngineHolder):
 
     async def aggregate_weights(self, updates, baseline_weights, weights_received):
         engine = self.aggregation_engine()
-        rnd = engine.begin(baseline_weights, len(weights_received))
+        # bf16 payloads (model_quantize on the clients) stay bf16 on the device
+        rnd = engine.begin(baseline_weights, len(weights_received), payload_codec(weights_received[0]))
         rnd.put_baseline(baseline_weights)
         for slot, payload in enumerate(weights_received):
             rnd.put_client(slot, payload)

@@ -257,6 +257,13 @@ def run_case(case):
     baseline = unpack(entries, torch.from_numpy(bf), torch.from_numpy(bi))
     payloads = [unpack(entries, torch.from_numpy(xs_f[c]), torch.from_numpy(xs_i[c]))
                 for c in range(k)]
+    if case.get("codec") == "bf16":
+        # the reference's own codec pair: client model_quantize, server model_dequantize
+        from plato.processors import model_dequantize, model_quantize
+
+        q = model_quantize.Processor(client_id=1)
+        dq = model_dequantize.Processor(server_id=0)
+        payloads = [dq.process(q.process(p)) for p in payloads]
     order = case.get("order", list(range(k)))
     staleness = case.get("staleness", [0] * k)
     mode = case.get("mode", "fedavg")
@@ -406,6 +413,10 @@ def cases():
         dict(name="port_similarity_resnet18_k4", model="resnet18", k=4, seed=15, mode="port",
              num_samples=synth.num_samples(4, 15), staleness=[3, 0, 2, 7],
              current_round=9, previous={"stream": 998, "scale": -25}),
+        dict(name="bf16_codec_resnet18_k16", model="resnet18", k=16, seed=16, codec="bf16",
+             num_samples=synth.num_samples(16, 16)),
+        dict(name="bf16_codec_lenet5_k9", model="lenet5", k=9, seed=17, codec="bf16",
+             num_samples=synth.num_samples(9, 17), full=True),
         dict(name="C4_port_resnet18_k256", model="resnet18", k=256, seed=13, mode="port",
              num_samples=synth.num_samples(256, 13), staleness=[(7 * i) % 11 for i in range(256)]),
     ]

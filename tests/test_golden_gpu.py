@@ -67,7 +67,9 @@ def _launch(engine, layout, base, slab, order, weights, scales, deltas=False):
     return out_f, out_i
 
 
-NON_ASYNC = [c for c in CASES if c["recipe"].get("mode", "fedavg") != "fedasync"]
+NON_ASYNC = [c for c in CASES if c["recipe"].get("mode", "fedavg") != "fedasync"
+             and c["recipe"].get("codec") is None]
+BF16 = [c for c in CASES if c["recipe"].get("codec") == "bf16"]
 
 
 @pytest.mark.parametrize("case", NON_ASYNC, ids=[c["recipe"]["name"] for c in NON_ASYNC])
@@ -113,7 +115,7 @@ def test_full_arrays_small_cases(engine):
     full = G.load_full()
     for case in CASES:
         recipe = case["recipe"]
-        if not recipe.get("full"):
+        if not recipe.get("full") or recipe.get("codec"):
             continue
         layout, base, slab = _device_inputs(recipe)
         weights, scales = G.weights_for(recipe, W, G.reference_similarities(case))
@@ -283,3 +285,58 @@ def test_wire_ingested_payloads_match_reference(engine):
     updated = engine.aggregate_weights(baseline, received, weights)
     assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
     assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+
+
+def _bf16_payloads(recipe):
+    layout, baseline, payloads = _host_payloads(recipe)
+    # client side: Plato's model_quantize (.to(bfloat16)) of every entry
+    return layout, baseline, [type(p)((n, t.to(torch.bfloat16)) for n, t in p.items()) for p in payloads]
+
+
+@pytest.mark.parametrize("case", BF16, ids=[c["recipe"]["name"] for c in BF16])
+def test_bf16_codec_device_resident_matches_reference(engine, case):
+    """bf16 payloads kept bf16 in HBM, widened in registers == reference dequantize + FedAvg."""
+    from plato_amd import _lib
+
+    recipe, exp = case["recipe"], case["expected"]
+    layout, base, slab32 = _device_inputs(recipe)
+    slab = ClientSlab(layout, recipe["k"], torch.device(DEV), codec="bf16")
+    slab.f32.copy_(slab32.f32.to(torch.bfloat16))          # model_quantize, on the device
+    slab.i64.copy_(slab32.i64.to(torch.bfloat16))
+    del slab32
+    order = G.order_of(recipe)
+    pf, pi = slab.row_pointers(order)
+    tf, ti = torch.from_numpy(pf).to(DEV), torch.from_numpy(pi).to(DEV)
+    weights, _ = G.weights_for(recipe, W)
+    w = torch.from_numpy(fp32_weights(weights)).to(DEV)
+    out_f = torch.empty(layout.row_f32, device=DEV)
+    out_i = torch.empty(layout.row_i64, device=DEV)
+    n_i = layout.n_i64
+    _lib.call("plato_agg_fedavg_weights_bf16", tf.data_ptr(), ti.data_ptr() if n_i else None, w.data_ptr(), None,
+              len(order), base.f32.data_ptr(), base.i64.data_ptr() if n_i else None, out_f.data_ptr(),
+              out_i.data_ptr() if n_i else None, layout.n_f32, n_i, torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    assert G.sha(G.canon(out_f[: layout.n_f32].cpu().numpy())) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(out_i[: layout.n_i64].cpu().numpy())) == exp["updated_i64f_sha256"]
+
+
+@pytest.mark.parametrize("case", BF16, ids=[c["recipe"]["name"] for c in BF16])
+def test_bf16_codec_host_and_wire_paths_match_reference(engine, case):
+    import pickle
+
+    from plato_amd import ingest
+
+    recipe, exp = case["recipe"], case["expected"]
+    layout, baseline, payloads = _bf16_payloads(recipe)
+    weights, _ = G.weights_for(recipe, W)
+    order = G.order_of(recipe)
+    # host state_dicts (auto-detected codec)
+    updated = engine.aggregate_weights(baseline, [payloads[c] for c in order], weights)
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+    # from the wire: pickled bf16 payloads -> native ingest -> bf16 arenas
+    wire = [pickle.dumps(type(payloads[c])((n, t.clone()) for n, t in payloads[c].items())) for c in order]
+    received = [ingest.loads(b, layout=layout, pin=True) for b in wire]
+    assert received[0].arena_f32.dtype == torch.bfloat16
+    updated = engine.aggregate_weights(baseline, received, weights)
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]

@@ -54,6 +54,9 @@ def _inputs(recipe):
     xs_f = [x[0] for x in xs]
     xs_i = [x[1] for x in xs]
     G.apply_overrides(bf, bi, xs_f, xs_i, recipe.get("overrides", []))
+    if recipe.get("codec") == "bf16":
+        xs_f = [ref.bf16_roundtrip(x) for x in xs_f]
+        xs_i = [ref.bf16_roundtrip(x) for x in xs_i]
     order = G.order_of(recipe)
     return layout, bf, bi, [xs_f[c] for c in order], [xs_i[c] for c in order]
 
@@ -116,7 +119,8 @@ def _check_case(case, inputs, weights, scales):
         # aggregate_deltas alone: deltas formed as the reference does (x - b)
         d_f = [np.subtract(x, bf, dtype=np.float32) for x in xs_f]
         with np.errstate(over="ignore"):
-            d_i = [(x - bi) for x in xs_i]
+            d_i = [(x - bi) if x.dtype != np.float32 else np.subtract(x, bi.astype(np.float32), dtype=np.float32)
+                   for x in xs_i]
         avg_f, avg_i = ref.deltas_numpy(d_f, d_i, weights, scales)
         assert G.sha(G.canon(avg_f)) == exp["avg_f32_sha256"]
         assert G.sha(G.canon(avg_i)) == exp["avg_i64f_sha256"]
