@@ -58,7 +58,7 @@ class OracleRound:
 
 
 class OracleEngine:
-    def begin(self, template, capacity):
+    def begin(self, template, capacity, codec="native"):
         return OracleRound(ArenaLayout.from_state_dict(template), capacity)
 
 
