@@ -311,6 +311,18 @@ class FedAvgEngine:
         rnd.launch(weights, scales, deltas=True)
         return rnd.result()
 
+    def weighted_sum(self, tensors: Sequence[torch.Tensor], weights: Sequence[float]) -> torch.Tensor:
+        """``avg = zeros; avg += t_i * w_i`` over same-shape fp32 CPU tensors, in order.
+
+        The plaintext half of the HE server's hybrid FedAvg
+        (plato/servers/fedavg_he.py:88-98) and any flat weighted sum; one
+        deltas-mode launch (bit-exact with the sequential fp32 loop).
+        """
+        if not tensors:
+            raise ValueError("no tensors to sum")
+        sds = [OrderedDict(v=t) for t in tensors]
+        return self.aggregate_deltas(sds, weights)["v"]
+
     def compute_weight_deltas(self, baseline: Mapping[str, torch.Tensor],
                               weights_received: Sequence[Mapping[str, torch.Tensor]]
                               ) -> list["OrderedDict[str, torch.Tensor]"]:

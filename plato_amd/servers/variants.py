@@ -134,6 +134,38 @@ class FedAsyncMixing(_EngineHolder):
                                                      self.mixing_hyperparam)
 
 
+class GanDeltasAggregationMixin(_EngineHolder):
+    """plato/servers/fedavg_gan.py:13-43: FedAvg of (generator, discriminator) delta pairs.
+
+    The two sums are independent and use the same n_i/N weights, so both
+    models go into one arena (keys prefixed per model) and one deltas-mode
+    launch; the result is split back into the reference's (gen, disc) pair.
+    """
+
+    async def aggregate_deltas(self, updates, deltas_received):
+        import asyncio
+        from collections import OrderedDict
+
+        weights, scales = self.aggregation_weights(updates)
+        combined = []
+        for gen, disc in deltas_received:
+            d = OrderedDict((f"g.{n}", t) for n, t in gen.items())
+            d.update((f"d.{n}", t) for n, t in disc.items())
+            combined.append(d)
+        engine = self.aggregation_engine()
+        rnd = engine.begin(combined[0], len(combined))
+        for slot, d in enumerate(combined):
+            rnd.put_client(slot, d, what="deltas_received")
+            await asyncio.sleep(0)
+        rnd.launch(weights, scales, deltas=True)
+        while not rnd.ready():
+            await asyncio.sleep(0)
+        avg = rnd.result()
+        gen = {n[2:]: t for n, t in avg.items() if n.startswith("g.")}
+        disc = {n[2:]: t for n, t in avg.items() if n.startswith("d.")}
+        return gen, disc
+
+
 class FedBuffServerMixin(FedBuffWeights, FusedAggregationMixin):
     pass
 

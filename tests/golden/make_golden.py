@@ -417,9 +417,41 @@ def cases():
              num_samples=synth.num_samples(16, 16)),
         dict(name="bf16_codec_lenet5_k9", model="lenet5", k=9, seed=17, codec="bf16",
              num_samples=synth.num_samples(9, 17), full=True),
+        dict(name="gan_lenet5_resnet18_k5", mode="gan", models=["lenet5", "resnet18"], k=5, seed=18,
+             num_samples=synth.num_samples(5, 18)),
         dict(name="C4_port_resnet18_k256", model="resnet18", k=256, seed=13, mode="port",
              num_samples=synth.num_samples(256, 13), staleness=[(7 * i) % 11 for i in range(256)]),
     ]
+
+
+def run_gan_case(case):
+    """fedavg_gan.Server.aggregate_deltas (servers/fedavg_gan.py:13-43) on (gen, disc) deltas."""
+    from plato.servers import fedavg_gan
+
+    k, seed = case["k"], case["seed"]
+    parts = []
+    for j, name in enumerate(case["models"]):
+        model = make_model(name)
+        entries, nf, ni = layout_of(model.state_dict())
+        bf, bi = synth.baseline_arena(nf, ni, seed + j)
+        base = unpack(entries, torch.from_numpy(bf), torch.from_numpy(bi))
+        deltas = []
+        for c in range(k):
+            xf, xi = synth.client_arena(bf, bi, seed + j, c)
+            x = unpack(entries, torch.from_numpy(xf), torch.from_numpy(xi))
+            deltas.append(OrderedDict((n, x[n] - base[n]) for n in x))  # algorithm: current - baseline
+        parts.append((entries, deltas))
+    server = fedavg_gan.Server(model=lambda: make_model(case["models"][0]))
+    server.init_trainer()
+    updates = make_updates(case["num_samples"], [None] * k, list(range(k)), [0] * k)
+    pairs = [(parts[0][1][c], parts[1][1][c]) for c in range(k)]
+    gen, disc = asyncio.run(server.aggregate_deltas(updates, pairs))
+    out = {}
+    for tag, (entries, _), avg in (("gen", parts[0], gen), ("disc", parts[1], disc)):
+        out[f"{tag}_avg_f32_sha256"] = sha(canon(flatten(entries, avg, "f32", torch.float32)))
+        out[f"{tag}_avg_i64f_sha256"] = sha(canon(flatten(entries, avg, "i64", torch.float32)))
+    out["total_samples"] = server.total_samples
+    return out, None
 
 
 def dump_shapes(out_dir):
@@ -499,7 +531,7 @@ def main():
         if args.only and case["name"] != args.only:
             continue
         print("case", case["name"], flush=True)
-        out, _ = run_case(case)
+        out, _ = run_gan_case(case) if case.get("mode") == "gan" else run_case(case)
         arrays = out.pop("_full", None)
         if arrays:
             for key, arr in arrays.items():

@@ -67,7 +67,7 @@ def _launch(engine, layout, base, slab, order, weights, scales, deltas=False):
     return out_f, out_i
 
 
-NON_ASYNC = [c for c in CASES if c["recipe"].get("mode", "fedavg") != "fedasync"
+NON_ASYNC = [c for c in CASES if c["recipe"].get("mode", "fedavg") not in ("fedasync", "gan")
              and c["recipe"].get("codec") is None]
 BF16 = [c for c in CASES if c["recipe"].get("codec") == "bf16"]
 
@@ -340,3 +340,48 @@ def test_bf16_codec_host_and_wire_paths_match_reference(engine, case):
     assert received[0].arena_f32.dtype == torch.bfloat16
     updated = engine.aggregate_weights(baseline, received, weights)
     assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+
+
+def test_gan_deltas_match_reference():
+    """GanDeltasAggregationMixin == fedavg_gan.Server.aggregate_deltas (servers/fedavg_gan.py:13-43)."""
+    from collections import OrderedDict
+
+    from plato_amd.servers.variants import GanDeltasAggregationMixin
+
+    case = next(c for c in CASES if c["recipe"].get("mode") == "gan")
+    recipe, exp = case["recipe"], case["expected"]
+    k, seed = recipe["k"], recipe["seed"]
+    parts = []
+    for j, name in enumerate(recipe["models"]):
+        layout = ArenaLayout.from_shapes(G.model_spec(name))
+        bf, bi = synth.baseline_arena(layout.n_f32, layout.n_i64, seed + j)
+        base = layout.unpack(torch.from_numpy(bf), torch.from_numpy(bi))
+        deltas = []
+        for c in range(k):
+            xf, xi = synth.client_arena(bf, bi, seed + j, c)
+            x = layout.unpack(torch.from_numpy(xf), torch.from_numpy(xi))
+            deltas.append(OrderedDict((n, x[n] - base[n]) for n in x))
+        parts.append((layout, deltas))
+
+    class Server(GanDeltasAggregationMixin):
+        aggregation_device = DEV
+
+    server = Server()
+    updates = [types.SimpleNamespace(report=types.SimpleNamespace(num_samples=n)) for n in recipe["num_samples"]]
+    gen, disc = asyncio.run(server.aggregate_deltas(updates, [(parts[0][1][c], parts[1][1][c]) for c in range(k)]))
+    for tag, (layout, _), avg in (("gen", parts[0], gen), ("disc", parts[1], disc)):
+        assert G.sha(G.canon(_flat(layout, avg, "f32"))) == exp[f"{tag}_avg_f32_sha256"]
+        assert G.sha(G.canon(_flat(layout, avg, "i64"))) == exp[f"{tag}_avg_i64f_sha256"]
+    assert server.total_samples == exp["total_samples"]
+
+
+def test_weighted_sum_matches_sequential_loop(engine):
+    """HE hybrid plaintext part (fedavg_he.py:88-98): avg += w_i * n_i/N, flat vectors."""
+    from oracle import fedavg_oracle as ref
+
+    rng = np.random.default_rng(3)
+    vecs = [rng.standard_normal(100_003).astype(np.float32) for _ in range(7)]
+    ns = [5, 100, 33, 2, 77, 9, 41]
+    got = engine.weighted_sum([torch.from_numpy(v) for v in vecs], W.fedavg(ns)).numpy()
+    exp, _ = ref.deltas_numpy(vecs, [np.zeros(0, np.int64)] * 7, ref.fedavg_weights(ns))
+    assert got.tobytes() == exp.tobytes()
