@@ -217,7 +217,8 @@ def main():
 
     def step(variant=None):
         if args.codec == "bf16":
-            _lib.call("plato_agg_fedavg_weights_bf16", tf.data_ptr(), ti.data_ptr(), w.data_ptr(), None, k,
+            v = (args.variant or 0) if variant is None else variant
+            _lib.call("plato_agg_tune_fedavg_bf16", v, tf.data_ptr(), ti.data_ptr(), w.data_ptr(), None, k,
                       base.f32.data_ptr(), base.i64.data_ptr(), out_f.data_ptr(), out_i.data_ptr(),
                       layout.n_f32, layout.n_i64, stream.cuda_stream)
             return
@@ -228,6 +229,29 @@ def main():
     if args.codec == "bf16":  # K bf16 client arenas + fp32 baseline and result
         alg_bytes = k * 2 * (layout.n_f32 + layout.n_i64) + 2 * (layout.n_f32 * 4 + layout.n_i64 * 8)
         job_bytes = alg_bytes * (world if scaling == "weak" else 1)
+
+    if args.sweep and args.codec == "bf16":
+        nv = _lib.lib().plato_agg_tune_num_bf16_variants()
+        times = {v: [] for v in range(nv)}
+        for v in range(nv):
+            step(v)
+        torch.cuda.synchronize(dev)
+        for _ in range(5):
+            for v in range(nv):
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(stream)
+                for _ in range(args.steps):
+                    step(v)
+                e1.record(stream)
+                e1.synchronize()
+                times[v].append(e0.elapsed_time(e1) / args.steps)
+        if rank == 0:
+            for v in range(nv):
+                med = statistics.median(times[v])
+                print(json.dumps({"bf16_variant": v, "ms_median": med,
+                                  "GBps": alg_bytes / (med * 1e-3) / 1e9}), flush=True)
+        return
 
     if args.sweep:
         nv = _lib.lib().plato_agg_tune_num_variants()

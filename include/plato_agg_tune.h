@@ -35,6 +35,15 @@ int plato_agg_tune_fedavg(int variant, int has_base,
                           float* d_out_f32, float* d_out_i64f,
                           size_t n_f32, size_t n_i64, hipStream_t stream);
 
+/* bf16-payload kernel variants (plato_agg_fedavg_weights_bf16 uses 0). */
+int plato_agg_tune_num_bf16_variants(void);
+int plato_agg_tune_fedavg_bf16(int variant, const uint16_t* const* d_x_bf16,
+                               const uint16_t* const* d_x_i64_bf16,
+                               const float* d_w, const float* d_s, int K,
+                               const float* d_base_f32, const int64_t* d_base_i64,
+                               float* d_out_f32, float* d_out_i64f,
+                               size_t n_f32, size_t n_i64, hipStream_t stream);
+
 /* Ceiling probes: mode 0 = non-temporal copy src -> dst, mode 1 = non-temporal
  * read of src only; n fp32 elements (n % 4 == 0), `blocks` workgroups of 256
  * grid-striding (<= 0: 2048).  bench.py --sweep reports them as the measured

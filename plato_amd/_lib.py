@@ -80,6 +80,12 @@ SIGNATURES = {
         [_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),
          ctypes.POINTER(_c_int)],
     ),
+    "plato_agg_tune_num_bf16_variants": (_c_int, []),
+    "plato_agg_tune_fedavg_bf16": (
+        _c_int,
+        [_c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p,
+         _c_void_p, _c_void_p, _c_size_t, _c_size_t, _c_void_p],
+    ),
     "plato_agg_tune_stream": (_c_int, [_c_int, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_void_p]),
     "plato_agg_tune_fedavg": (
         _c_int,

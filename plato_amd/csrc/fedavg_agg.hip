@@ -517,6 +517,51 @@ __device__ __forceinline__ void bf16_body(const Bf16Args& a, uint32_t blk) {
   }
 }
 
+// 4 elements per lane: one 8-byte bf16 load per client, one float4 for the
+// baseline and the result (the fp32 kernel's lane mapping: 1 KiB per wave
+// instruction on the fp32 side, twice the workgroups of the 8-per-lane body).
+typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const u2 gu2;
+
+template <bool TWO, bool CHECK, int U>
+__device__ __forceinline__ void bf16_body4(const Bf16Args& a, uint32_t blk) {
+  const uint64_t n4 = a.n8 * 2;  // groups of 4 (n8 counts groups of 8 in this mode: see launcher)
+  const uint64_t e4 = uint64_t(blk) * 256 + threadIdx.x;
+  const bool live = !CHECK || e4 < n4;
+  const uint64_t g = CHECK ? (e4 < n4 ? e4 : n4 - 1) : e4;
+  const uint32_t xoff = uint32_t(g * 8u);
+  const uint32_t foff = uint32_t(g * 16u);
+  const f4 b = ld4_off<false>(a.base_f, foff);
+  f4 acc = f4_zero();
+  const int K = a.K;
+  int i = 0;
+  for (; i + U <= K; i += U) {
+    u2 q[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const uint16_t* p = sld(a.xf, i + u);
+      q[u] = __builtin_nontemporal_load((gu2*)((__attribute__((address_space(1))) const char*)p + xoff));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float wu = sld(a.w, i + u);
+      const f4 x = f4{bf16_lo(q[u].x), bf16_hi(q[u].x), bf16_lo(q[u].y), bf16_hi(q[u].y)};
+      f4 t = f4_scale(x - b, wu);
+      if constexpr (TWO) t = f4_scale(t, sld(a.s, i + u));
+      acc = acc + t;
+    }
+  }
+  for (; i < K; ++i) {
+    const uint16_t* p = sld(a.xf, i);
+    const u2 q = __builtin_nontemporal_load((gu2*)((__attribute__((address_space(1))) const char*)p + xoff));
+    const f4 x = f4{bf16_lo(q.x), bf16_hi(q.x), bf16_lo(q.y), bf16_hi(q.y)};
+    f4 t = f4_scale(x - b, sld(a.w, i));
+    if constexpr (TWO) t = f4_scale(t, sld(a.s, i));
+    acc = acc + t;
+  }
+  if (live) st4_off<true>(a.out_f, foff, b + acc);
+}
+
 template <bool TWO>
 __device__ __forceinline__ void bf16_scalar(const Bf16Args& a, uint64_t j) {
   const uint64_t tail = a.n_f32 - 8 * a.n8;
@@ -545,17 +590,35 @@ __device__ __forceinline__ void bf16_scalar(const Bf16Args& a, uint64_t j) {
   a.out_if[e] = b + acc;
 }
 
-template <bool TWO>
+template <bool TWO, int LANE, int U>
 __global__ __launch_bounds__(256) void fedavg_bf16_kernel(Bf16Args a) {
   const uint32_t blk = blockIdx.x;
   if (blk < a.nb_vec_full) {
-    bf16_body<TWO, false, 8>(a, blk);
+    if constexpr (LANE == 8) bf16_body<TWO, false, U>(a, blk); else bf16_body4<TWO, false, U>(a, blk);
   } else if (blk < a.nb_vec) {
-    bf16_body<TWO, true, 8>(a, blk);
+    if constexpr (LANE == 8) bf16_body<TWO, true, U>(a, blk); else bf16_body4<TWO, true, U>(a, blk);
   } else {
     bf16_scalar<TWO>(a, uint64_t(blk - a.nb_vec) * 256 + threadIdx.x);
   }
 }
+
+using Bf16Fn = void (*)(const Bf16Args&, dim3, hipStream_t);
+template <bool TWO, int LANE, int U>
+void launch_bf16(const Bf16Args& a, dim3 g, hipStream_t st) {
+  hipLaunchKernelGGL((fedavg_bf16_kernel<TWO, LANE, U>), g, dim3(256), 0, st, a);
+}
+struct Bf16Variant {
+  int lane, u;
+  Bf16Fn fn[2];
+};
+// variant 0 is the default of plato_agg_fedavg_weights_bf16
+const Bf16Variant kBf16Variants[] = {
+    {4, 8, {&launch_bf16<false, 4, 8>, &launch_bf16<true, 4, 8>}},
+    {8, 8, {&launch_bf16<false, 8, 8>, &launch_bf16<true, 8, 8>}},
+    {4, 16, {&launch_bf16<false, 4, 16>, &launch_bf16<true, 4, 16>}},
+    {8, 4, {&launch_bf16<false, 8, 4>, &launch_bf16<true, 8, 4>}},
+};
+constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
 
 // ---------------------------------------------------------------------------
 // Ceiling probes (tuning only): how fast this chip streams the same bytes with
@@ -741,10 +804,11 @@ int plato_agg_fedavg_deltas(const float* const* d_d_f32, const int64_t* const* d
                  stream);
 }
 
-int plato_agg_fedavg_weights_bf16(const uint16_t* const* d_x_bf16, const uint16_t* const* d_x_i64_bf16,
-                                  const float* d_w, const float* d_s, int K, const float* d_base_f32,
-                                  const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
-                                  size_t n_i64, hipStream_t stream) {
+namespace {
+int run_bf16(int variant, const uint16_t* const* d_x_bf16, const uint16_t* const* d_x_i64_bf16, const float* d_w,
+             const float* d_s, int K, const float* d_base_f32, const int64_t* d_base_i64, float* d_out_f32,
+             float* d_out_i64f, size_t n_f32, size_t n_i64, hipStream_t stream) {
+  if (variant < 0 || variant >= kNumBf16Variants) return fail(PLATO_AGG_EINVAL, "bad bf16 variant");
   if (K <= 0) return fail(PLATO_AGG_EINVAL, "K must be >= 1");
   if (!d_w) return fail(PLATO_AGG_EINVAL, "null weight array");
   if (n_f32 && (!d_x_bf16 || !d_base_f32 || !d_out_f32)) return fail(PLATO_AGG_EINVAL, "null fp32 pointer");
@@ -752,6 +816,7 @@ int plato_agg_fedavg_weights_bf16(const uint16_t* const* d_x_bf16, const uint16_
   if (n_f32 && (!aligned16(d_base_f32) || !aligned16(d_out_f32)))
     return fail(PLATO_AGG_EINVAL, "fp32 baseline/output must be 16-byte aligned");
   if (n_f32 + n_i64 == 0) return plato_agg_internal::clear_error();
+  const Bf16Variant& vr = kBf16Variants[variant];
   Bf16Args a{};
   a.xf = d_x_bf16;
   a.xi = d_x_i64_bf16;
@@ -761,24 +826,39 @@ int plato_agg_fedavg_weights_bf16(const uint16_t* const* d_x_bf16, const uint16_
   a.base_i = d_base_i64;
   a.out_f = d_out_f32;
   a.out_if = d_out_i64f;
-  a.n8 = n_f32 / 8;
+  a.n8 = n_f32 / 8;  // the vector bodies cover 8 * n8 elements (LANE 4: 2 * n8 groups of 4)
   a.n_f32 = n_f32;
   a.n_i64 = n_i64;
   a.K = K;
-  const uint64_t nb_vec = (a.n8 + 255) / 256;
+  const uint64_t groups = vr.lane == 8 ? a.n8 : 2 * a.n8;
+  const uint64_t nb_vec = (groups + 255) / 256;
   const uint64_t n_scalar = (n_f32 - 8 * a.n8) + n_i64;
   const uint64_t nb_scalar = (n_scalar + 255) / 256;
   if (nb_vec + nb_scalar > 0x7fffffffull || a.n8 * 32ull > 0xffffffffull)
     return fail(PLATO_AGG_EINVAL, "fp32 arena must be < 4 GiB per launch (split it into buckets)");
   a.nb_vec = uint32_t(nb_vec);
-  a.nb_vec_full = uint32_t(a.n8 / 256);
-  dim3 grid(uint32_t(nb_vec + nb_scalar));
-  if (d_s) {
-    hipLaunchKernelGGL(fedavg_bf16_kernel<true>, grid, dim3(256), 0, stream, a);
-  } else {
-    hipLaunchKernelGGL(fedavg_bf16_kernel<false>, grid, dim3(256), 0, stream, a);
-  }
+  a.nb_vec_full = uint32_t(groups / 256);
+  vr.fn[d_s ? 1 : 0](a, dim3(uint32_t(nb_vec + nb_scalar)), stream);
   return check_launch("fedavg_bf16 kernel launch");
+}
+}  // namespace
+
+int plato_agg_fedavg_weights_bf16(const uint16_t* const* d_x_bf16, const uint16_t* const* d_x_i64_bf16,
+                                  const float* d_w, const float* d_s, int K, const float* d_base_f32,
+                                  const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
+                                  size_t n_i64, hipStream_t stream) {
+  return run_bf16(0, d_x_bf16, d_x_i64_bf16, d_w, d_s, K, d_base_f32, d_base_i64, d_out_f32, d_out_i64f, n_f32,
+                  n_i64, stream);
+}
+
+int plato_agg_tune_num_bf16_variants(void) { return kNumBf16Variants; }
+
+int plato_agg_tune_fedavg_bf16(int variant, const uint16_t* const* d_x_bf16, const uint16_t* const* d_x_i64_bf16,
+                               const float* d_w, const float* d_s, int K, const float* d_base_f32,
+                               const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
+                               size_t n_i64, hipStream_t stream) {
+  return run_bf16(variant, d_x_bf16, d_x_i64_bf16, d_w, d_s, K, d_base_f32, d_base_i64, d_out_f32, d_out_i64f,
+                  n_f32, n_i64, stream);
 }
 
 int plato_agg_tune_num_variants(void) { return kNumVariants; }
