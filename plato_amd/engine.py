@@ -176,6 +176,9 @@ class FedAvgEngine:
         self._copy_stream: torch.cuda.Stream | None = None
         self._slab: ClientSlab | None = None      # slab of the current round's codec
         self._stager: _Stager | None = None       # native-dtype stager (baselines)
+        self._arrivals: dict = {}                 # id(payload) -> staged arrival row
+        self._arrival_free: dict = {}
+        self._arrival_slabs: dict = {}
 
     # ----------------------------------------------------------- allocation
     def _prepare(self, template: Mapping[str, torch.Tensor], k: int, codec: str = "native") -> ArenaLayout:
@@ -187,6 +190,7 @@ class FedAvgEngine:
             self._slabs = {}
             self._stagers = {}
             self._base = None
+            self._arrivals, self._arrival_free, self._arrival_slabs = {}, {}, {}
         layout = self._layout
         if self._copy_stream is None:
             self._copy_stream = torch.cuda.Stream(self.device)
@@ -217,6 +221,54 @@ class FedAvgEngine:
         tf = torch.from_numpy(pf).to(self.device)
         ti = torch.from_numpy(pi).to(self.device)
         return tf, ti
+
+    # ---------------------------------------------------- arrival staging
+    ARRIVAL_CHUNK = 16  # rows per arrival slab; rows never move once staged
+
+    def prestage(self, payload: Mapping[str, torch.Tensor], baseline_layout: ArenaLayout) -> bool:
+        """Copy one arriving payload to HBM now (H2D overlaps the other clients' arrival).
+
+        The next aggregation round adopts it by identity (``AggregationRound.adopt``);
+        the payload must not be modified after arrival.  Returns False if the
+        payload does not fit the layout (it is then staged at aggregation time).
+        """
+        codec = payload_codec(payload)
+        try:
+            baseline_layout.check_compatible(payload, "arriving payload", codec)
+        except (KeyError, ValueError):
+            return False
+        if self._layout is None or self._layout.signature != baseline_layout.signature:
+            self._layout = baseline_layout
+            self._slabs, self._stagers, self._base = {}, {}, None
+            self._arrivals, self._arrival_free, self._arrival_slabs = {}, {}, {}
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(self.device)
+        if codec not in self._stagers:
+            self._stagers[codec] = _Stager(self._layout, self.device, codec=codec, stream=self._copy_stream)
+        free = self._arrival_free.setdefault(codec, [])
+        if not free:
+            slabs = self._arrival_slabs.setdefault(codec, [])
+            slab = ClientSlab(self._layout, self.ARRIVAL_CHUNK, self.device, codec)
+            slabs.append(slab)
+            free.extend((slab, r) for r in range(self.ARRIVAL_CHUNK))
+        slab, row = free.pop()
+        self._stagers[codec].put(payload, slab.f32[row], slab.i64[row])
+        pf, pi = slab.row_pointers([row])
+        # keep the dict alive: its id() is the key
+        self._arrivals[id(payload)] = (payload, codec, self._layout.signature, int(pf[0]), int(pi[0]), slab, row)
+        return True
+
+    def _arrival_rows(self, payload, layout: ArenaLayout, codec: str):
+        hit = self._arrivals.get(id(payload))
+        if hit is None or hit[0] is not payload or hit[1] != codec or hit[2] != layout.signature:
+            return None
+        return hit[3], hit[4]
+
+    def release_arrivals(self) -> None:
+        """Return every arrival slot (after the round that used them has completed)."""
+        for payload, codec, _, _, _, slab, row in self._arrivals.values():
+            self._arrival_free.setdefault(codec, []).append((slab, row))
+        self._arrivals = {}
 
     # ------------------------------------------------------ raw device call
     def launch_fedavg(self, layout: ArenaLayout, ptr_f32: torch.Tensor, ptr_i64: torch.Tensor | None,
@@ -406,6 +458,9 @@ class AggregationRound:
         self.slab = engine._slabs[codec]
         self.stager = engine._stagers[codec]
         self.staged = [False] * capacity
+        # per slot: device pointers of its fp32 / int64 rows (round slab or an arrival slot)
+        self._pf = [0] * capacity
+        self._pi = [0] * capacity
         self.has_baseline = False
         self.event: torch.cuda.Event | None = None
         self._out = None
@@ -422,7 +477,24 @@ class AggregationRound:
             raise IndexError(f"slot {slot} outside [0, {self.capacity})")
         self.layout.check_compatible(payload, f"{what}[{slot}]", self.codec)
         self.stager.put(payload, self.slab.f32[slot], self.slab.i64[slot])
+        pf, pi = self.slab.row_pointers([slot])
+        self._pf[slot], self._pi[slot] = int(pf[0]), int(pi[0])
         self.staged[slot] = True
+
+    def adopt(self, slot: int, payload: Mapping[str, torch.Tensor]) -> bool:
+        """Use ``payload``'s copy already staged at arrival (``FedAvgEngine.prestage``), if any.
+
+        Returns False (nothing done) when the payload was not prestaged for
+        this round's layout and codec; the caller then stages it with put_client.
+        """
+        if not 0 <= slot < self.capacity:
+            raise IndexError(f"slot {slot} outside [0, {self.capacity})")
+        hit = self.engine._arrival_rows(payload, self.layout, self.codec)
+        if hit is None:
+            return False
+        self._pf[slot], self._pi[slot] = hit
+        self.staged[slot] = True
+        return True
 
     def launch(self, weights: Sequence[float], scales: Sequence[float] | None = None,
                order: Sequence[int] | None = None, deltas: bool = False) -> None:
@@ -440,7 +512,8 @@ class AggregationRound:
         eng = self.engine
         lay = self.layout
         w, s = eng._upload_weights(weights, scales)
-        pf, pi = self.slab.row_pointers(order)
+        pf = np.asarray([self._pf[i] for i in order], dtype=np.int64)
+        pi = np.asarray([self._pi[i] for i in order], dtype=np.int64)
         tf, ti = eng._pointer_tables(pf, pi)
         stream = torch.cuda.current_stream(eng.device)
         self.stager.fence(stream)

@@ -62,7 +62,9 @@ class FusedAggregationMixin(_EngineHolder):
         rnd = engine.begin(baseline_weights, len(weights_received), payload_codec(weights_received[0]))
         rnd.put_baseline(baseline_weights)
         for slot, payload in enumerate(weights_received):
-            rnd.put_client(slot, payload)
+            # payloads staged at arrival (WireIngestMixin.stage_on_arrival) are adopted in place
+            if not rnd.adopt(slot, payload):
+                rnd.put_client(slot, payload)
             # Yield to other tasks in the server between clients, as the
             # reference does per client (servers/fedavg.py:157).
             await asyncio.sleep(0)
@@ -75,7 +77,9 @@ class FusedAggregationMixin(_EngineHolder):
         rnd.launch(weights, scales)
         while not rnd.ready():
             await asyncio.sleep(0)
-        return rnd.result()
+        result = rnd.result()
+        engine.release_arrivals()
+        return result
 
 
 class DeltasAggregationMixin(_EngineHolder):

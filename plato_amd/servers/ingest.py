@@ -24,6 +24,9 @@ from ..arena import ArenaLayout
 class WireIngestMixin:
     #: pin the per-payload arenas (async H2D); False keeps them pageable
     ingest_pinned = True
+    #: copy each payload to HBM as soon as it arrives (the aggregation hook then
+    #: adopts it); payloads must not be modified in place after arrival
+    stage_on_arrival = False
 
     def _ingest_layout(self):
         try:
@@ -51,6 +54,10 @@ class WireIngestMixin:
         payload = b"".join(self.client_chunks[sid])
         _data = self.ingest_payload(payload)
         self.client_chunks[sid] = []
+        if self.stage_on_arrival and isinstance(_data, ingest.ArenaStateDict):
+            layout = self._ingest_layout()
+            if layout is not None:
+                self.aggregation_engine().prestage(_data, layout)
 
         if self.client_payload[sid] is None:
             self.client_payload[sid] = _data

@@ -41,6 +41,9 @@ class OracleRound:
     def put_client(self, slot, sd, what=None):
         self.slots[slot] = sd
 
+    def adopt(self, slot, sd):
+        return False
+
     def launch(self, weights, scales=None, order=None, deltas=False):
         flat = lambda sd, r: torch.cat([sd[e.name].reshape(-1) for e in self.layout.entries if e.region == r])  # noqa
         xs = [self.slots[i] for i in range(len(weights))]
@@ -60,6 +63,9 @@ class OracleRound:
 class OracleEngine:
     def begin(self, template, capacity, codec="native"):
         return OracleRound(ArenaLayout.from_state_dict(template), capacity)
+
+    def release_arrivals(self):
+        pass
 
 
 def main():

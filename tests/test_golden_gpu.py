@@ -387,3 +387,44 @@ def test_weighted_sum_matches_sequential_loop(engine):
     got = engine.weighted_sum([torch.from_numpy(v) for v in vecs], W.fedavg(ns)).numpy()
     exp, _ = ref.deltas_numpy(vecs, [np.zeros(0, np.int64)] * 7, ref.fedavg_weights(ns))
     assert got.tobytes() == exp.tobytes()
+
+
+def test_stage_on_arrival_then_adopt_matches_reference():
+    """Payloads staged to HBM as they arrive (any arrival order), summed in updates order."""
+    import pickle
+
+    from plato_amd import ingest
+    from plato_amd.servers import FusedAggregationMixin, WireIngestMixin
+
+    case = next(c for c in CASES if c["recipe"]["name"] == "resnet18_k16_permuted")
+    recipe, exp = case["recipe"], case["expected"]
+    layout, baseline, payloads = _host_payloads(recipe)
+
+    class Algo:
+        def extract_weights(self):
+            return baseline
+
+    class Server(WireIngestMixin, FusedAggregationMixin):
+        aggregation_device = DEV
+        stage_on_arrival = True
+
+        def __init__(self):
+            self.algorithm = Algo()
+            self.client_chunks, self.client_payload, self.training_clients = {}, {}, {}
+
+    server = Server()
+    arrived = {}
+    for c in reversed(range(recipe["k"])):  # arrival order differs from the update order
+        sid = f"s{c}"
+        server.client_chunks[sid] = [pickle.dumps(type(payloads[c])((n, t.clone()) for n, t in payloads[c].items()))]
+        server.client_payload[sid] = None
+        server.training_clients[c + 1] = True
+        asyncio.run(server._client_payload_arrived(sid, c + 1))
+        arrived[c] = server.client_payload[sid]
+    eng = server.aggregation_engine()
+    assert len(eng._arrivals) == recipe["k"]
+    updates = _updates(recipe, [arrived[c] for c in range(recipe["k"])])
+    updated = asyncio.run(server.aggregate_weights(updates, baseline, [u.payload for u in updates]))
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+    assert len(eng._arrivals) == 0  # released after the round
