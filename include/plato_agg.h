@@ -46,8 +46,21 @@
  *   plato_agg_client_dots      <- the model-wide reductions of Port's
  *                                 cosine_similarity (examples/async/port/
  *                                 port_server.py:24-52, F.cosine_similarity over
- *                                 the flattened models) and of the norm-based
- *                                 variants (Polaris, FedAdp, FedAtt)
+ *                                 the flattened models)
+ *   plato_agg_entry_stats      <- the per-tensor reductions of the norm- and
+ *                                 angle-based variants: FedAtt's per-layer
+ *                                 torch.linalg.norm (examples/server_aggregation/
+ *                                 fedatt/fedatt_algorithm.py:34-39), FedAdp's
+ *                                 np.inner / np.linalg.norm of flattened deltas
+ *                                 (examples/server_aggregation/fedadp/
+ *                                 fedadp_server.py:95-99), Polaris' per-client
+ *                                 conv-layer squared deltas (examples/
+ *                                 client_selection/polaris/polaris_server.py:76-89)
+ *   plato_agg_fedavg_entrywise <- weighted sums whose weight depends on the
+ *                                 tensor as well as the client: FedAtt's
+ *                                 attentive aggregation (fedatt_algorithm.py:44-69)
+ *                                 and FedAdp's global-gradient pass
+ *                                 (fedadp_server.py:43-50)
  */
 #ifndef PLATO_AGG_H
 #define PLATO_AGG_H
@@ -171,6 +184,79 @@ int plato_agg_client_dots(const float* const* d_x, const int64_t* const* d_x_i64
                           const float* d_v, const int64_t* d_v_i64,
                           size_t n_f32, size_t n_i64, double* d_workspace,
                           double* d_out, hipStream_t stream);
+
+/*
+ * Per-entry work: a state_dict entry ("tensor") is a contiguous element range
+ * of the fp32 or the int64 arena.  Kernels that need the entry of an element
+ * read a chunk table: each chunk is a piece of ONE entry, [begin, end) in
+ * elements of its region, numbered with the entry's index `entry` in the
+ * layout (0 <= entry < n_entries, across both regions).  Chunks of the same
+ * entry are contiguous and the tables are sorted by entry (host-built once
+ * per layout: plato_amd/arena.py ArenaLayout.chunk_tables).  Chunk length
+ * sets the work per workgroup; any length is correct.
+ */
+typedef struct plato_agg_chunk {
+  uint32_t entry;
+  uint32_t begin;
+  uint32_t end;
+  uint32_t reserved;
+} plato_agg_chunk;
+
+/*
+ * Per (client, entry) reductions, accumulated in fp64 in a fixed order:
+ *   d_i = x_i - base (fp32; int64 entries: fp32(int64 x - b)), or x_i if d_base is NULL
+ *   d_out[i * E + e]           = sum_{elements of e} d_i * v     (0 <= i < K; 0 if d_v is NULL)
+ *   d_out[(K + i) * E + e]     = sum d_i^2
+ *   d_out[2K * E + e]          = sum v^2                         (0 if d_v is NULL)
+ * v is an fp32 arena (its int64 entries given as fp32 in d_v_i64f).
+ * d_workspace must hold plato_agg_entry_stats_workspace(K, n_chunks_f32 + n_chunks_i64) bytes.
+ */
+size_t plato_agg_entry_stats_workspace(int K, uint32_t n_chunks);
+int plato_agg_entry_stats(const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+                          const float* d_base_f32, const int64_t* d_base_i64,
+                          const float* d_v_f32, const float* d_v_i64f,
+                          const plato_agg_chunk* d_chunks_f32, uint32_t n_chunks_f32,
+                          const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64,
+                          int n_entries, size_t n_f32, size_t n_i64,
+                          double* d_workspace, double* d_out, hipStream_t stream);
+
+/*
+ * Weighted sum with a weight per (entry, client), bit-exact with torch's fp32
+ * CPU ops:
+ *   d_i = x_i - b (as above), or x_i if d_base is NULL
+ *   acc = +0; for i in order: acc = acc + fp32(d_i * W[e * K + i])
+ *   u   = fp32(acc * scale); if d_noise: u = fp32(u + fp32(noise * noise_scale))
+ *   out = (flags & PLATO_AGG_ADD_BASE) ? fp32(b + u) : u      (int64 b: fp32(b) + u)
+ * FedAtt: W = -softmax(norms), scale = -epsilon, noise = torch.randn draws,
+ * noise_scale = magnitude, ADD_BASE (update_weights).  d_base is required
+ * with ADD_BASE.  Alignment: base/out/noise fp32 arrays 16-byte aligned.
+ */
+#define PLATO_AGG_ADD_BASE 1
+int plato_agg_fedavg_entrywise(const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+                               const float* d_w, int n_entries,
+                               const plato_agg_chunk* d_chunks_f32, uint32_t n_chunks_f32,
+                               const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64,
+                               const float* d_base_f32, const int64_t* d_base_i64,
+                               const float* d_noise_f32, const float* d_noise_i64f,
+                               float scale, float noise_scale, int flags,
+                               float* d_out_f32, float* d_out_i64f,
+                               size_t n_f32, size_t n_i64, hipStream_t stream);
+
+/*
+ * torch.linalg.norm of every (client, entry) delta, in x86-64 PyTorch's CPU
+ * order (ATen's vectorised 2-norm: 8 fp32 lanes of fma(v, v, acc) over the
+ * first n - n%8 elements, lanes added in order, tail fma'd, fp32 sqrt), so
+ * the fp32 result equals the reference's bit for bit:
+ *   d_out[i * n_entries + entry] = norm(d_i restricted to entry)
+ * d_entries_* hold ONE piece per entry (ArenaLayout.chunk_tables(2**32)).
+ * FedAtt: examples/server_aggregation/fedatt/fedatt_algorithm.py:34-39.
+ */
+int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+                              const float* d_base_f32, const int64_t* d_base_i64,
+                              const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
+                              const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64,
+                              int n_entries, size_t n_f32, size_t n_i64, float* d_out,
+                              hipStream_t stream);
 
 /*
  * Deterministic synthetic payloads for tests and benchmarks (a counter-based

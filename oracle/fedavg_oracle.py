@@ -220,3 +220,168 @@ def load_into(model_state: Mapping, updated: Mapping) -> None:
     """load_state_dict's per-key copy_ (fp32 -> int64 truncation included)."""
     for name, dst in model_state.items():
         dst.copy_(updated[name])
+
+
+# --------------------------------------------------------------------------
+# 3. per-entry variants (FedAtt, FedAdp, Polaris)
+# --------------------------------------------------------------------------
+def _region_deltas(entries, region, base, x):
+    """Flat region delta as compute_weight_deltas forms it (int64: wrap, then fp32)."""
+    if region == "f32":
+        return np.subtract(x, base, dtype=np.float32)
+    with np.errstate(over="ignore"):
+        return (x.astype(np.int64) - base.astype(np.int64)).astype(np.float32)
+
+
+def entry_index(entries, region: str, n: int) -> np.ndarray:
+    """Element -> entry index (position in ``entries``) for one region; -1 = padding."""
+    idx = np.full(n, -1, dtype=np.int64)
+    for e_i, e in enumerate(entries):
+        if e.region == region:
+            idx[e.offset:e.offset + e.numel] = e_i
+    return idx
+
+
+def entry_stats_fp64(entries, bf, bi, xs_f, xs_i, vf=None, vi=None):
+    """Per (client, entry) fp64 sums d.v and d.d, per entry v.v (plato_agg_entry_stats).
+
+    The deltas are fp32 as the reference forms them; the sums are exact-ish
+    fp64 (np.add.reduceat), a restatement of the device kernel's contract
+    rather than of a reference line.
+    """
+    n_e = len(entries)
+    k = len(xs_f)
+    dd = np.zeros((k, n_e))
+    dv = np.zeros((k, n_e))
+    vv = np.zeros(n_e)
+    for region, base, xs, v in (("f32", bf, xs_f, vf), ("i64", bi, xs_i, vi)):
+        ents = [(e_i, e) for e_i, e in enumerate(entries) if e.region == region and e.numel]
+        if not ents:
+            continue
+        for i in range(k):
+            d = _region_deltas(entries, region, base, xs[i]).astype(np.float64)
+            for e_i, e in ents:
+                seg = d[e.offset:e.offset + e.numel]
+                dd[i, e_i] = np.dot(seg, seg)
+                if v is not None:
+                    dv[i, e_i] = np.dot(seg, np.asarray(v[e.offset:e.offset + e.numel], dtype=np.float64))
+        if v is not None:
+            for e_i, e in ents:
+                seg = np.asarray(v[e.offset:e.offset + e.numel], dtype=np.float64)
+                vv[e_i] = np.dot(seg, seg)
+    return dv, dd, vv
+
+
+def entrywise_numpy(entries, bf, bi, xs_f, xs_i, w_ek, scale=1.0, noise_f=None, noise_i=None,
+                    noise_scale=0.0, add_base=True):
+    """plato_agg_fedavg_entrywise on flat arenas, one rounding per op:
+
+        acc = +0; for i: acc = fp32(acc + fp32(fp32(x_i - b) * W[entry, i]))
+        u = fp32(acc * scale) [+ fp32(noise * noise_scale)];  out = fp32(b + u) if add_base
+
+    With W = -softmax(norms), scale = -epsilon, noise_scale = magnitude this is
+    examples/server_aggregation/fedatt/fedatt_algorithm.py:44-69 + update_weights.
+    """
+    w = np.asarray(w_ek, dtype=np.float64).astype(np.float32)
+    outs = []
+    for region, base, xs, nz in (("f32", bf, xs_f, noise_f), ("i64", bi, xs_i, noise_i)):
+        idx = entry_index(entries, region, base.size)
+        acc = np.zeros(base.size, dtype=np.float32)
+        for i in range(len(xs)):
+            d = _region_deltas(entries, region, base, xs[i])
+            wi = np.where(idx >= 0, w[np.maximum(idx, 0), i], np.float32(0)).astype(np.float32)
+            acc = np.add(acc, np.multiply(d, wi, dtype=np.float32), dtype=np.float32)
+        u = np.multiply(acc, np.float32(scale), dtype=np.float32)
+        if nz is not None:
+            u = np.add(u, np.multiply(nz, np.float32(noise_scale), dtype=np.float32), dtype=np.float32)
+        if add_base:
+            u = np.add(base.astype(np.float32), u, dtype=np.float32)
+        outs.append(u)
+    return outs[0], outs[1]
+
+
+def fedatt_torch(baseline: Mapping, weights_received: Sequence[Mapping], epsilon=1.2, magnitude=0.001):
+    """FedAtt's aggregation as torch CPU ops (fedatt_algorithm.py:23-69 + algorithms/fedavg.py:13-37).
+
+    The caller seeds torch's CPU generator; the noise is one ``torch.randn``
+    per key in baseline order, drawn after all attention weights.  Returns
+    (updated dict, norms [E][K] fp32, atts [E][K] fp32).
+    """
+    import torch
+    import torch.nn.functional as F
+
+    names = list(baseline.keys())
+    deltas = [OrderedDict((n, x[n] - baseline[n]) for n in x) for x in weights_received]
+    norms = np.zeros((len(names), len(deltas)), dtype=np.float32)
+    atts = {}
+    for e, name in enumerate(names):
+        col = torch.zeros(len(deltas))
+        for i, d in enumerate(deltas):
+            col[i] = torch.linalg.norm(-(d[name].to(torch.float32)))
+        norms[e] = col.numpy()
+        atts[name] = F.softmax(col, dim=0)
+    updated = OrderedDict()
+    for name, weight in baseline.items():
+        acc = torch.zeros(weight.shape)
+        for i, d in enumerate(deltas):
+            acc += torch.mul(-(d[name].float()), atts[name][i])
+        step = -torch.mul(acc, epsilon) + torch.mul(torch.randn(weight.shape), magnitude)
+        updated[name] = weight + step
+    return updated, norms, np.stack([atts[n].numpy() for n in names])
+
+
+def torch_cpu_norm_f32(rows: np.ndarray) -> np.ndarray:
+    """``torch.linalg.norm`` of each row of an fp32 ``[K, n]`` matrix, in x86-64
+    PyTorch's CPU order (ATen's vectorised last-dim 2-norm, as measured for
+    torch 2.10 here): 8 lanes of fp32 fma(v, v, acc) over the first n - n%8
+    elements, lanes summed in order, the tail fma'd, fp32 sqrt."""
+    rows = np.asarray(rows, dtype=np.float32)
+    k, n = rows.shape
+    m = n - n % 8
+    acc = np.zeros((k, 8), dtype=np.float32)
+    blocks = rows[:, :m].reshape(k, -1, 8).astype(np.float64)
+    for t in range(blocks.shape[1]):  # fma: exact product + one rounding
+        acc = (acc + blocks[:, t] * blocks[:, t]).astype(np.float32)
+    s = acc[:, 0].copy()
+    for j in range(1, 8):
+        s = np.add(s, acc[:, j], dtype=np.float32)
+    for e in range(m, n):
+        v = rows[:, e].astype(np.float64)
+        s = (s + v * v).astype(np.float32)
+    return np.sqrt(s, dtype=np.float32)
+
+
+def fedadp_flatten(named: Mapping, lr: float) -> np.ndarray:
+    """FedAdp's process_grad (fedadp_server.py:122-133): entries sorted by name.lower(),
+    the first as is, every other as fp32 ``-x / lr``, concatenated."""
+    import torch
+
+    items = sorted(named.items(), key=lambda kv: kv[0].lower())
+    parts = [np.asarray(items[0][1]).reshape(-1)]
+    for _, t in items[1:]:
+        parts.append(np.asarray(-t / lr).reshape(-1))
+    return np.concatenate(parts)
+
+
+def fedadp_angles_numpy(global_grads: Mapping, deltas: Sequence[Mapping], lr: float) -> list:
+    """fedadp_server.py:91-99: float32 np.inner / np.linalg.norm / arccos of the flattened vectors."""
+    g = fedadp_flatten(global_grads, lr)
+    angles = []
+    for d in deltas:
+        loc = fedadp_flatten(d, lr)
+        inner = np.inner(g, loc)
+        norms = np.linalg.norm(g) * np.linalg.norm(loc)
+        angles.append(np.arccos(np.clip(inner / norms, -1.0, 1.0)))
+    return angles
+
+
+def polaris_norms_numpy(deltas: Sequence[Mapping]) -> list:
+    """polaris_server.py:76-89: sqrt of the float32 sum over 'conv' layers of np.sum(np.square(delta))."""
+    out = []
+    for d in deltas:
+        squared = 0
+        for layer, value in d.items():
+            if "conv" in layer:
+                squared += np.sum(np.square(np.asarray(value)))
+        out.append(np.sqrt(squared))
+    return out

@@ -18,6 +18,7 @@ ABI_VERSION = 1
 PLATO_AGG_OK = 0
 PLATO_AGG_EINVAL = -1
 PLATO_AGG_EHIP = -2
+PLATO_AGG_ADD_BASE = 1
 
 _c_void_p = ctypes.c_void_p
 _c_size_t = ctypes.c_size_t
@@ -72,6 +73,24 @@ SIGNATURES = {
         _c_int,
         [_c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_size_t,
          _c_void_p, _c_void_p, _c_void_p],
+    ),
+    "plato_agg_entry_stats_workspace": (_c_size_t, [_c_int, ctypes.c_uint32]),
+    "plato_agg_entry_stats": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+         _c_void_p, ctypes.c_uint32, _c_void_p, ctypes.c_uint32, _c_int, _c_size_t, _c_size_t,
+         _c_void_p, _c_void_p, _c_void_p],
+    ),
+    "plato_agg_fedavg_entrywise": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_int, _c_void_p, _c_int, _c_void_p, ctypes.c_uint32, _c_void_p,
+         ctypes.c_uint32, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_float, _c_float, _c_int,
+         _c_void_p, _c_void_p, _c_size_t, _c_size_t, _c_void_p],
+    ),
+    "plato_agg_entry_norms_f32": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_void_p,
+         ctypes.c_uint32, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p],
     ),
     # tuning / benchmarking (include/plato_agg_tune.h)
     "plato_agg_tune_num_variants": (_c_int, []),

@@ -18,6 +18,8 @@ so checkpointing and client-side use are unchanged.  Compose as
 
 from __future__ import annotations
 
+import numpy as np
+
 from ..engine import FedAvgEngine
 
 
@@ -44,3 +46,67 @@ class FedAvgAlgorithmMixin(_AlgorithmEngine):
 class FedAsyncAlgorithmMixin(FedAvgAlgorithmMixin):
     async def aggregate_weights(self, baseline_weights, weights_received, mixing=0.9, **kwargs):
         return self.aggregation_engine().mix_weights(baseline_weights, weights_received[0], mixing)
+
+
+class FedAttAlgorithmMixin(_AlgorithmEngine):
+    """FedAtt's attentive aggregation on the GPU.
+
+    examples/server_aggregation/fedatt/fedatt_algorithm.py:23-69:
+    ``att[name] = softmax_i(|delta_i[name]|)`` per entry, then
+    ``new = b + (-(sum_i -delta_i * att_i) * epsilon + randn * magnitude)``.
+
+    * per-(client, entry) norms: ``plato_agg_entry_norms_f32``, which follows
+      torch's CPU reduction order, so they equal the reference's fp32 values;
+    * softmax with the same torch op (weights.fedatt_attention);
+    * the noise is drawn on the host with ``torch.randn(shape)`` per key in
+      baseline order — the reference's own RNG stream, so a seeded run gives
+      the reference's bits;
+    * ``plato_agg_fedavg_entrywise`` with ``W = -att``, ``scale = -epsilon``,
+      ``noise_scale = magnitude``, plus the baseline (``update_weights``).
+
+    ``epsilon`` / ``magnitude`` come from ``Config().algorithm`` like the
+    reference (defaults 1.2 / 0.001) unless set on the class.
+    """
+
+    fedatt_epsilon = None
+    fedatt_magnitude = None
+
+    def _fedatt_param(self, name, default):
+        value = getattr(self, f"fedatt_{name}")
+        if value is not None:
+            return value
+        try:
+            from plato.config import Config
+
+            alg = Config().algorithm
+            return getattr(alg, name) if hasattr(alg, name) else default
+        except Exception:  # Plato not importable / not configured
+            return default
+
+    async def aggregate_weights(self, baseline_weights, weights_received, **kwargs):
+        import asyncio
+        from collections import OrderedDict
+
+        import torch
+
+        from .. import weights as W
+
+        engine = self.aggregation_engine()
+        rnd = engine.begin(baseline_weights, len(weights_received))
+        rnd.put_baseline(baseline_weights)
+        for slot, payload in enumerate(weights_received):
+            if not rnd.adopt(slot, payload):
+                rnd.put_client(slot, payload)
+            await asyncio.sleep(0)
+        # the reference's fp32 norms bit for bit (torch's CPU reduction order), then its softmax
+        atts = W.fedatt_attention(rnd.entry_norms(range(len(weights_received))))
+        epsilon = self._fedatt_param("epsilon", 1.2)
+        magnitude = self._fedatt_param("magnitude", 0.001)
+        noise = OrderedDict((name, torch.randn(weight.shape)) for name, weight in baseline_weights.items())
+        rnd.launch_entrywise(-atts.astype(np.float64), scale=-epsilon, noise=noise,
+                             noise_scale=magnitude, add_base=True)
+        while not rnd.ready():
+            await asyncio.sleep(0)
+        result = rnd.result()
+        engine.release_arrivals()
+        return result

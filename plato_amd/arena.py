@@ -22,6 +22,7 @@ from collections import OrderedDict
 from dataclasses import dataclass
 from typing import Mapping
 
+import numpy as np
 import torch
 
 F32 = "f32"
@@ -35,7 +36,9 @@ ROW_ALIGN = 64
 # sends them.  "native": the model's own dtypes.  "bf16": Plato's
 # model_quantize outbound processor (plato/processors/model_quantize.py:15)
 # casts every entry to bfloat16.
-CODECS = {"native": (torch.float32, torch.int64), "bf16": (torch.bfloat16, torch.bfloat16)}
+CODECS = {"native": (torch.float32, torch.int64), "bf16": (torch.bfloat16, torch.bfloat16),
+          # all-fp32 arrays over the model's keys (FedAtt's noise draws)
+          "f32": (torch.float32, torch.float32)}
 
 
 def payload_codec(state_dict) -> str:
@@ -65,6 +68,7 @@ class ArenaLayout:
         self.row_i64 = max(n_i64, 1)
         self._by_name = {e.name: e for e in entries}
         self.signature = tuple((e.name, e.region, e.shape) for e in entries)
+        self._cache: dict = {}
 
     # ------------------------------------------------------------------ build
     @classmethod
@@ -136,6 +140,37 @@ class ArenaLayout:
                     f"{what}[{entry.name!r}] is {tensor.dtype}{tuple(tensor.shape)}, "
                     f"expected {want}{entry.shape}"
                 )
+
+    def chunk_tables(self, cap: int):
+        """Per-entry work pieces for the chunked kernels (``plato_agg_chunk`` rows).
+
+        Returns two ``uint32 [n, 4]`` arrays, (entry index, begin, end, 0), for
+        the fp32 and the int64 region, sorted by entry.  fp32 entries are cut
+        at multiples of ``cap`` elements of the arena (``cap`` % 4 == 0), so
+        only the first and last piece of an entry start or end inside a
+        float4 group; each int64 entry is one piece.  Empty entries get none.
+        """
+        if cap <= 0 or cap % 4:
+            raise ValueError("chunk capacity must be a positive multiple of 4")
+        key = ("chunks", cap)
+        cached = self._cache.get(key)
+        if cached is not None:
+            return cached
+        f32, i64 = [], []
+        for idx, e in enumerate(self.entries):
+            if e.numel == 0:
+                continue
+            if e.region == I64:
+                i64.append((idx, e.offset, e.offset + e.numel, 0))
+                continue
+            lo, end = e.offset, e.offset + e.numel
+            while lo < end:
+                hi = min(end, (lo // cap + 1) * cap)
+                f32.append((idx, lo, hi, 0))
+                lo = hi
+        out = (np.asarray(f32, dtype=np.uint32).reshape(-1, 4), np.asarray(i64, dtype=np.uint32).reshape(-1, 4))
+        self._cache[key] = out
+        return out
 
     # ---------------------------------------------------------- pack / unpack
     def pack(self, state_dict: Mapping[str, torch.Tensor], out_f32: torch.Tensor,

@@ -1,0 +1,673 @@
+// entrywise.hip — per-entry (per state_dict tensor) kernels for the FedAvg
+// variants whose numbers depend on the tensor as well as the client
+// (SURVEY.md §8(f) rank 2):
+//   * entry_stats: per (client, entry) sums of d^2 and d*v in fp64 — FedAtt's
+//     per-layer norms, FedAdp's inner products / norms, Polaris' conv norms;
+//   * fedavg_entrywise: acc += fp32(d * W[entry][client]) with an fp32 post-op
+//     (scale, additive noise, + baseline) — FedAtt's attentive aggregation and
+//     FedAdp's global-gradient pass.
+//
+// Both walk a host-built chunk table (include/plato_agg.h plato_agg_chunk):
+// one workgroup per chunk, so the entry — and with it every weight — is
+// workgroup-uniform and read through the scalar cache, exactly like the
+// client pointers.  Entries are packed back to back in the arena (not
+// 4-aligned), so the first and last float4 group of a chunk are partial:
+// elements outside [begin, end) are masked (no contribution, no store); the
+// neighbouring chunk owns them.  Interior groups take the dwordx4 path.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "common.h"
+#include "plato_agg.h"
+
+namespace {
+
+using plato_agg_internal::clear_error;
+using plato_agg_internal::set_error;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const f4 gf4;
+typedef __attribute__((address_space(1))) f4 gf4w;
+
+constexpr int kBlock = 256;
+constexpr int kWaves = kBlock / 64;
+
+template <class T>
+__device__ __forceinline__ T sld(const T* p, uint64_t i) {
+  return ((__attribute__((address_space(4))) const T*)p)[i];
+}
+
+__device__ __forceinline__ f4 ld_nt(const float* p, uint64_t g) { return __builtin_nontemporal_load((gf4*)p + g); }
+__device__ __forceinline__ f4 ld_c(const float* p, uint64_t g) { return *((gf4*)p + g); }
+__device__ __forceinline__ void st_nt(float* p, uint64_t g, f4 v) { __builtin_nontemporal_store(v, (gf4w*)p + g); }
+
+__device__ __forceinline__ double wave_sum(double x) {
+#pragma unroll
+  for (int off = 32; off >= 1; off >>= 1) x += __shfl_xor(x, off, 64);
+  return x;
+}
+
+struct Chunk {
+  uint32_t entry, begin, end;
+};
+
+__device__ __forceinline__ Chunk load_chunk(const plato_agg_chunk* t, uint32_t c, uint64_t n) {
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(t + c);
+  Chunk ch{sld(p, 0), sld(p, 1), sld(p, 2)};
+  // never trust the table past the arena (a bad table gives wrong sums, not a fault)
+  if (ch.end > n) ch.end = uint32_t(n);
+  if (ch.begin > ch.end) ch.begin = ch.end;
+  return ch;
+}
+
+__device__ __forceinline__ float i64_delta(const int64_t* x, const int64_t* b, uint64_t e) {
+  const int64_t xv = x[e];
+  // torch's int64 subtraction wraps; the promotion to fp32 happens after
+  const int64_t d = b ? (int64_t)((uint64_t)xv - (uint64_t)b[e]) : xv;
+  return (float)d;
+}
+
+// ---------------------------------------------------------------------------
+// entry_stats
+// ---------------------------------------------------------------------------
+// Workspace rows (each n_chunks doubles): [0, K) d.v, [K, 2K) d.d, 2K v.v.
+constexpr int kSV = 4;  // float4 groups per lane per pass (chunk pass = 4096 floats)
+constexpr int kSU = 4;  // clients per batch
+
+struct StatArgs {
+  const float* const* xf;
+  const int64_t* const* xi;
+  const float* base_f;
+  const int64_t* base_i;
+  const float* v_f;
+  const float* v_if;
+  const plato_agg_chunk* cf;
+  const plato_agg_chunk* ci;
+  double* ws;
+  uint64_t n_f32, n_i64;
+  uint32_t ncf, nci, nc;
+  int K;
+};
+
+// Block-wide sum of NV per-lane values; thread 0..NV-1 get the totals in out.
+template <int NV>
+__device__ __forceinline__ void block_sums(double (&v)[NV], double (*red)[2 * kSU + 1], double* out) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int j = 0; j < NV; ++j) v[j] = wave_sum(v[j]);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < NV; ++j) red[wave][j] = v[j];
+  }
+  __syncthreads();
+  if (threadIdx.x < NV) {
+    double t = 0.0;
+    for (int w = 0; w < kWaves; ++w) t += red[w][threadIdx.x];
+    out[threadIdx.x] = t;
+  }
+  __syncthreads();
+}
+
+// Accumulate into ws[row * nc + c]; the pass index makes the first write a store.
+__device__ __forceinline__ void ws_acc(const StatArgs& a, uint64_t row, uint32_t c, double t, bool first) {
+  double* p = a.ws + row * a.nc + c;
+  *p = first ? t : *p + t;
+}
+
+__device__ __forceinline__ double masked_dot(f4 p, f4 q, const bool (&m)[4]) {
+  double s = 0.0;
+  if (m[0]) s += (double)p.x * q.x;
+  if (m[1]) s += (double)p.y * q.y;
+  if (m[2]) s += (double)p.z * q.z;
+  if (m[3]) s += (double)p.w * q.w;
+  return s;
+}
+
+template <bool HAS_BASE, bool HAS_V>
+__device__ void stats_f32_chunk(const StatArgs& a, uint32_t c) {
+  __shared__ double red[kWaves][2 * kSU + 1];
+  __shared__ double tot[2 * kSU + 1];
+  const Chunk ch = load_chunk(a.cf, c, a.n_f32);
+  const uint64_t n4 = a.n_f32 / 4;  // groups with 4 in-range elements
+  const uint64_t g0 = ch.begin / 4, g1 = (uint64_t(ch.end) + 3) / 4;
+  const int K = a.K;
+  constexpr uint64_t kPass = uint64_t(kBlock) * kSV;
+  uint64_t gp = g0;
+  bool first = true;
+  do {
+    // this lane's groups of the pass; clamp the address, mask the elements
+    uint64_t g[kSV];
+    bool m[kSV][4];
+    bool vec[kSV];
+    f4 b[kSV], v[kSV];
+#pragma unroll
+    for (int j = 0; j < kSV; ++j) {
+      const uint64_t gg = gp + threadIdx.x + uint64_t(j) * kBlock;
+      const bool in = gg < g1;
+      g[j] = in ? gg : (g1 > g0 ? g1 - 1 : g0);
+      vec[j] = g[j] < n4;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t e = 4 * gg + q;
+        m[j][q] = in && e >= ch.begin && e < ch.end;
+      }
+      b[j] = f4{0.f, 0.f, 0.f, 0.f};
+      v[j] = f4{0.f, 0.f, 0.f, 0.f};
+      if (vec[j]) {
+        if (HAS_BASE) b[j] = ld_c(a.base_f, g[j]);
+        if (HAS_V) v[j] = ld_c(a.v_f, g[j]);
+      } else {
+        // the arena's last, partial group: scalar loads of the in-range elements
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const uint64_t e = 4 * g[j] + q;
+          if (e < a.n_f32) {
+            if (HAS_BASE) b[j][q] = a.base_f[e];
+            if (HAS_V) v[j][q] = a.v_f[e];
+          }
+        }
+      }
+    }
+    if (HAS_V) {
+      double s[1] = {0.0};
+#pragma unroll
+      for (int j = 0; j < kSV; ++j) s[0] += masked_dot(v[j], v[j], m[j]);
+      block_sums<1>(s, red, tot);
+      if (threadIdx.x == 0) ws_acc(a, uint64_t(2 * K), c, tot[0], first);
+    }
+    for (int i0 = 0; i0 < K; i0 += kSU) {
+      f4 x[kSU][kSV];
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) {
+        const int i = i0 + u < K ? i0 + u : K - 1;
+        const float* p = sld(a.xf, i);
+#pragma unroll
+        for (int j = 0; j < kSV; ++j) {
+          if (vec[j]) {
+            x[u][j] = ld_nt(p, g[j]);
+          } else {
+            x[u][j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              const uint64_t e = 4 * g[j] + q;
+              if (e < a.n_f32) x[u][j][q] = p[e];
+            }
+          }
+        }
+      }
+      double acc[2 * kSU];
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) {
+        double dv = 0.0, dd = 0.0;
+#pragma unroll
+        for (int j = 0; j < kSV; ++j) {
+          // the delta is formed in fp32, as compute_weight_deltas does
+          const f4 d = HAS_BASE ? x[u][j] - b[j] : x[u][j];
+          if (HAS_V) dv += masked_dot(d, v[j], m[j]);
+          dd += masked_dot(d, d, m[j]);
+        }
+        acc[u] = dv;
+        acc[kSU + u] = dd;
+      }
+      block_sums<2 * kSU>(acc, red, tot);
+      if (threadIdx.x < 2 * kSU) {
+        const int u = threadIdx.x % kSU;
+        if (i0 + u < K) {
+          const bool is_dd = threadIdx.x >= kSU;
+          if (is_dd || HAS_V) ws_acc(a, uint64_t(is_dd ? K + i0 + u : i0 + u), c, tot[threadIdx.x], first);
+        }
+      }
+    }
+    gp += kPass;
+    first = false;
+  } while (gp < g1);
+}
+
+template <bool HAS_BASE, bool HAS_V>
+__device__ void stats_i64_chunk(const StatArgs& a, uint32_t cc) {
+  __shared__ double red[kWaves][2 * kSU + 1];
+  __shared__ double tot[2 * kSU + 1];
+  const Chunk ch = load_chunk(a.ci, cc, a.n_i64);
+  const uint32_t c = a.ncf + cc;
+  const int K = a.K;
+  if (HAS_V) {
+    double s[1] = {0.0};
+    for (uint64_t e = ch.begin + threadIdx.x; e < ch.end; e += kBlock) s[0] += (double)a.v_if[e] * a.v_if[e];
+    block_sums<1>(s, red, tot);
+    if (threadIdx.x == 0) ws_acc(a, uint64_t(2 * K), c, tot[0], true);
+  }
+  for (int i0 = 0; i0 < K; i0 += kSU) {
+    double acc[2 * kSU];
+#pragma unroll
+    for (int u = 0; u < 2 * kSU; ++u) acc[u] = 0.0;
+    for (uint64_t e = ch.begin + threadIdx.x; e < ch.end; e += kBlock) {
+      const double vv = HAS_V ? (double)a.v_if[e] : 0.0;
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) {
+        if (i0 + u < K) {
+          const float d = i64_delta(sld(a.xi, i0 + u), HAS_BASE ? a.base_i : nullptr, e);
+          acc[u] += (double)d * vv;
+          acc[kSU + u] += (double)d * d;
+        }
+      }
+    }
+    block_sums<2 * kSU>(acc, red, tot);
+    if (threadIdx.x < 2 * kSU) {
+      const int u = threadIdx.x % kSU;
+      if (i0 + u < K) {
+        const bool is_dd = threadIdx.x >= kSU;
+        if (is_dd || HAS_V) ws_acc(a, uint64_t(is_dd ? K + i0 + u : i0 + u), c, tot[threadIdx.x], true);
+      }
+    }
+  }
+}
+
+template <bool HAS_BASE, bool HAS_V>
+__global__ __launch_bounds__(kBlock) void entry_stats_partial(StatArgs a) {
+  const uint32_t c = blockIdx.x;
+  if (c < a.ncf) {
+    stats_f32_chunk<HAS_BASE, HAS_V>(a, c);
+  } else {
+    stats_i64_chunk<HAS_BASE, HAS_V>(a, c - a.ncf);
+  }
+}
+
+// first chunk of `entry` in a table sorted by entry (n if none)
+__device__ uint32_t lower_bound(const plato_agg_chunk* t, uint32_t n, uint32_t entry) {
+  uint32_t lo = 0, hi = n;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (t[mid].entry < entry) {
+      lo = mid + 1;
+    } else {
+      hi = mid;
+    }
+  }
+  return lo;
+}
+
+// One thread per (row, entry): sum that entry's chunk partials in table order.
+__global__ __launch_bounds__(kBlock) void entry_stats_final(const double* ws, uint32_t nc,
+                                                           const plato_agg_chunk* cf, uint32_t ncf,
+                                                           const plato_agg_chunk* ci, uint32_t nci,
+                                                           uint32_t n_entries, uint64_t rows, bool has_v,
+                                                           int K, double* out) {
+  const uint64_t idx = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  if (idx >= rows * n_entries) return;
+  const uint64_t row = idx / n_entries;
+  const uint32_t e = uint32_t(idx % n_entries);
+  double s = 0.0;
+  const bool computed = has_v || (row >= uint64_t(K) && row < uint64_t(2 * K));
+  if (computed) {
+    const double* w = ws + row * nc;
+    for (uint32_t c = lower_bound(cf, ncf, e); c < ncf && cf[c].entry == e; ++c) s += w[c];
+    for (uint32_t c = lower_bound(ci, nci, e); c < nci && ci[c].entry == e; ++c) s += w[ncf + c];
+  }
+  out[idx] = s;
+}
+
+// ---------------------------------------------------------------------------
+// fedavg_entrywise
+// ---------------------------------------------------------------------------
+constexpr int kEU = 8;  // clients per batch (independent dwordx4 loads per lane)
+
+struct EwArgs {
+  const float* const* xf;
+  const int64_t* const* xi;
+  const float* w;  // [n_entries][K]
+  const float* base_f;
+  const int64_t* base_i;
+  const float* noise_f;
+  const float* noise_if;
+  float* out_f;
+  float* out_if;
+  const plato_agg_chunk* cf;
+  const plato_agg_chunk* ci;
+  uint64_t n_f32, n_i64;
+  uint32_t ncf, nci;
+  float scale, noise_scale;
+  int K, flags;
+};
+
+template <bool HAS_BASE>
+__device__ __forceinline__ f4 ew_post(const EwArgs& a, f4 acc, f4 b, f4 noise, bool has_noise) {
+  f4 u = acc * a.scale;
+  if (has_noise) u = u + noise * a.noise_scale;
+  if (HAS_BASE && (a.flags & PLATO_AGG_ADD_BASE)) u = b + u;
+  return u;
+}
+
+template <bool HAS_BASE>
+__device__ void ew_f32_chunk(const EwArgs& a, uint32_t c) {
+  const Chunk ch = load_chunk(a.cf, c, a.n_f32);
+  const uint64_t n4 = a.n_f32 / 4;
+  const uint64_t g0 = ch.begin / 4, g1 = (uint64_t(ch.end) + 3) / 4;
+  const float* wrow = a.w + uint64_t(ch.entry) * a.K;
+  const int K = a.K;
+  const bool has_noise = a.noise_f != nullptr;
+  for (uint64_t g = g0 + threadIdx.x; g < g1; g += kBlock) {
+    const uint64_t e0 = 4 * g;
+    const bool full = e0 >= ch.begin && e0 + 4 <= ch.end;  // all 4 elements in the chunk (=> in range)
+    if (full && g < n4) {
+      const f4 b = HAS_BASE ? ld_c(a.base_f, g) : f4{0.f, 0.f, 0.f, 0.f};
+      f4 acc = f4{0.f, 0.f, 0.f, 0.f};
+      int i = 0;
+      for (; i + kEU <= K; i += kEU) {
+        f4 x[kEU];
+#pragma unroll
+        for (int u = 0; u < kEU; ++u) x[u] = ld_nt(sld(a.xf, i + u), g);
+#pragma unroll
+        for (int u = 0; u < kEU; ++u) {
+          const f4 d = HAS_BASE ? x[u] - b : x[u];
+          acc = acc + d * sld(wrow, i + u);
+        }
+      }
+      for (; i < K; ++i) {
+        const f4 x = ld_nt(sld(a.xf, i), g);
+        const f4 d = HAS_BASE ? x - b : x;
+        acc = acc + d * sld(wrow, i);
+      }
+      const f4 noise = has_noise ? ld_c(a.noise_f, g) : f4{0.f, 0.f, 0.f, 0.f};
+      st_nt(a.out_f, g, ew_post<HAS_BASE>(a, acc, b, noise, has_noise));
+    } else {
+      // boundary group: the chunk's own elements one by one
+      for (int q = 0; q < 4; ++q) {
+        const uint64_t e = e0 + q;
+        if (e < ch.begin || e >= ch.end) continue;
+        const float b = HAS_BASE ? a.base_f[e] : 0.f;
+        float acc = 0.f;
+        for (int i = 0; i < K; ++i) {
+          const float x = sld(a.xf, i)[e];
+          const float d = HAS_BASE ? x - b : x;
+          acc = acc + d * sld(wrow, i);
+        }
+        float u = acc * a.scale;
+        if (has_noise) u = u + a.noise_f[e] * a.noise_scale;
+        if (HAS_BASE && (a.flags & PLATO_AGG_ADD_BASE)) u = b + u;
+        a.out_f[e] = u;
+      }
+    }
+  }
+}
+
+template <bool HAS_BASE>
+__device__ void ew_i64_chunk(const EwArgs& a, uint32_t cc) {
+  const Chunk ch = load_chunk(a.ci, cc, a.n_i64);
+  const float* wrow = a.w + uint64_t(ch.entry) * a.K;
+  for (uint64_t e = ch.begin + threadIdx.x; e < ch.end; e += kBlock) {
+    float acc = 0.f;
+    for (int i = 0; i < a.K; ++i) {
+      const float d = i64_delta(sld(a.xi, i), HAS_BASE ? a.base_i : nullptr, e);
+      acc = acc + d * sld(wrow, i);
+    }
+    float u = acc * a.scale;
+    if (a.noise_if) u = u + a.noise_if[e] * a.noise_scale;
+    // update_weights: int64 weight + fp32 delta -> fp32(b) + u
+    if (HAS_BASE && (a.flags & PLATO_AGG_ADD_BASE)) u = (float)a.base_i[e] + u;
+    a.out_if[e] = u;
+  }
+}
+
+template <bool HAS_BASE>
+__global__ __launch_bounds__(kBlock) void fedavg_entrywise_kernel(EwArgs a) {
+  const uint32_t c = blockIdx.x;
+  if (c < a.ncf) {
+    ew_f32_chunk<HAS_BASE>(a, c);
+  } else {
+    ew_i64_chunk<HAS_BASE>(a, c - a.ncf);
+  }
+}
+
+
+// ---------------------------------------------------------------------------
+// entry_norms_f32: torch.linalg.norm(fp32 tensor) exactly as x86-64 PyTorch
+// computes it on the CPU (ATen's vectorised last-dim 2-norm reduction, the
+// path a contiguous whole-tensor norm takes): 8 fp32 lanes, lane j
+// accumulating fma(v, v, acc_j) over elements j, j+8, ... of the first
+// n - n%8 elements; then acc_0 + acc_1 + ... + acc_7 in order, the tail
+// elements fma'd onto that, and an fp32 sqrt.  Reproducing the order makes
+// FedAtt's attention (fedatt_algorithm.py:39) bit-exact; it is a serial
+// chain of n/8 fmas per lane, so one thread per (client, entry, lane), eight
+// clients of one entry per wavefront.
+// ---------------------------------------------------------------------------
+constexpr int kNormLanes = 8;
+
+struct NormArgs {
+  const float* const* xf;
+  const int64_t* const* xi;
+  const float* base_f;
+  const int64_t* base_i;
+  const plato_agg_chunk* ef;  // one piece per fp32 entry
+  const plato_agg_chunk* ei;  // one piece per int64 entry
+  float* out;                 // [K][n_entries]
+  uint64_t n_f32, n_i64;
+  uint32_t nef, nei, n_entries;
+  int K;
+};
+
+template <bool HAS_BASE>
+__global__ __launch_bounds__(kBlock) void entry_norms_kernel(NormArgs a) {
+  const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
+  const int j = int(t % kNormLanes);
+  const uint64_t pair = t / kNormLanes;  // entry-major: 8 clients of one entry per wave
+  const uint64_t n_pairs = uint64_t(a.nef + a.nei) * a.K;
+  const bool live = pair < n_pairs;
+  const uint32_t ent = live ? uint32_t(pair / a.K) : 0;
+  const int i = live ? int(pair % a.K) : 0;
+  float acc = 0.f;
+  uint32_t entry = 0;
+  if (live && ent < a.nef) {
+    const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
+    entry = ch.entry;
+    const float* x = a.xf[i];
+    const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+    const uint64_t p0 = uint64_t(ch.begin) + j;
+    uint64_t r = 0;
+    constexpr int kUnroll = 8;
+    for (; r + kUnroll * kNormLanes <= m; r += kUnroll * kNormLanes) {
+      float v[kUnroll];
+#pragma unroll
+      for (int q = 0; q < kUnroll; ++q) {
+        const uint64_t e = p0 + r + uint64_t(q) * kNormLanes;
+        v[q] = HAS_BASE ? x[e] - a.base_f[e] : x[e];
+      }
+#pragma unroll
+      for (int q = 0; q < kUnroll; ++q) acc = __builtin_fmaf(v[q], v[q], acc);
+    }
+    for (; r < m; r += kNormLanes) {
+      const uint64_t e = p0 + r;
+      const float v = HAS_BASE ? x[e] - a.base_f[e] : x[e];
+      acc = __builtin_fmaf(v, v, acc);
+    }
+  } else if (live) {
+    const Chunk ch = load_chunk(a.ei, ent - a.nef, a.n_i64);
+    entry = ch.entry;
+    const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+    for (uint64_t r = 0; r < m; r += kNormLanes) {
+      const float v = i64_delta(a.xi[i], HAS_BASE ? a.base_i : nullptr, ch.begin + r + j);
+      acc = __builtin_fmaf(v, v, acc);
+    }
+  }
+  // combine the 8 lanes of this (client, entry) in lane order, then the tail
+  // (lane 0, sequentially, as ATen does after its vector loop)
+  float s = __shfl(acc, (threadIdx.x & ~(kNormLanes - 1)), 64);
+  for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, (threadIdx.x & ~(kNormLanes - 1)) + l, 64);
+  if (!live || j != 0) return;
+  if (ent < a.nef) {
+    const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
+    const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+    const float* x = a.xf[i];
+    for (uint64_t e = ch.begin + m; e < ch.end; ++e) {
+      const float v = HAS_BASE ? x[e] - a.base_f[e] : x[e];
+      s = __builtin_fmaf(v, v, s);
+    }
+  } else {
+    const Chunk ch = load_chunk(a.ei, ent - a.nef, a.n_i64);
+    const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+    for (uint64_t e = ch.begin + m; e < ch.end; ++e) {
+      const float v = i64_delta(a.xi[i], HAS_BASE ? a.base_i : nullptr, e);
+      s = __builtin_fmaf(v, v, s);
+    }
+  }
+  if (entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + entry] = sqrtf(s);
+}
+
+bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
+
+int launch_error(const char* what) {
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(PLATO_AGG_EHIP, std::string(what) + ": " + hipGetErrorString(err));
+  return clear_error();
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t plato_agg_entry_stats_workspace(int K, uint32_t n_chunks) {
+  return size_t((2 * uint64_t(K > 0 ? K : 0) + 1) * (n_chunks ? n_chunks : 1) * sizeof(double));
+}
+
+int plato_agg_entry_stats(const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+                          const float* d_base_f32, const int64_t* d_base_i64, const float* d_v_f32,
+                          const float* d_v_i64f, const plato_agg_chunk* d_chunks_f32, uint32_t n_chunks_f32,
+                          const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64, int n_entries,
+                          size_t n_f32, size_t n_i64, double* d_workspace, double* d_out, hipStream_t stream) {
+  if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
+  if (n_entries <= 0) return set_error(PLATO_AGG_EINVAL, "n_entries must be >= 1");
+  if (!d_workspace || !d_out) return set_error(PLATO_AGG_EINVAL, "null workspace/output pointer");
+  if (n_chunks_f32 && (!d_x_f32 || !d_chunks_f32)) return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
+  if (n_chunks_i64 && (!d_x_i64 || !d_chunks_i64 || (d_base_f32 && !d_base_i64) || (d_v_f32 && !d_v_i64f)))
+    return set_error(PLATO_AGG_EINVAL, "null int64 pointer");
+  if (misaligned(d_base_f32) || misaligned(d_v_f32))
+    return set_error(PLATO_AGG_EINVAL, "fp32 baseline / v must be 16-byte aligned");
+  if (n_f32 > 0xffffffffull || n_i64 > 0xffffffffull)
+    return set_error(PLATO_AGG_EINVAL, "arena too large for 32-bit chunk offsets");
+  const uint64_t nc = uint64_t(n_chunks_f32) + n_chunks_i64;
+  if (nc == 0 || nc > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "bad chunk count");
+  StatArgs a{};
+  a.xf = d_x_f32;
+  a.xi = d_x_i64;
+  a.base_f = d_base_f32;
+  a.base_i = d_base_i64;
+  a.v_f = d_v_f32;
+  a.v_if = d_v_i64f;
+  a.cf = d_chunks_f32;
+  a.ci = d_chunks_i64;
+  a.ws = d_workspace;
+  a.n_f32 = n_f32;
+  a.n_i64 = n_i64;
+  a.ncf = n_chunks_f32;
+  a.nci = n_chunks_i64;
+  a.nc = uint32_t(nc);
+  a.K = K;
+  const dim3 grid{uint32_t(nc)}, block{kBlock};
+  const bool hb = d_base_f32 != nullptr, hv = d_v_f32 != nullptr;
+  if (hb && hv) {
+    hipLaunchKernelGGL((entry_stats_partial<true, true>), grid, block, 0, stream, a);
+  } else if (hb) {
+    hipLaunchKernelGGL((entry_stats_partial<true, false>), grid, block, 0, stream, a);
+  } else if (hv) {
+    hipLaunchKernelGGL((entry_stats_partial<false, true>), grid, block, 0, stream, a);
+  } else {
+    hipLaunchKernelGGL((entry_stats_partial<false, false>), grid, block, 0, stream, a);
+  }
+  const uint64_t rows = 2 * uint64_t(K) + 1;
+  const uint64_t total = rows * uint64_t(n_entries);
+  hipLaunchKernelGGL(entry_stats_final, dim3(uint32_t((total + kBlock - 1) / kBlock)), block, 0, stream,
+                     d_workspace, a.nc, d_chunks_f32, n_chunks_f32, d_chunks_i64, n_chunks_i64,
+                     uint32_t(n_entries), rows, hv, K, d_out);
+  return launch_error("entry_stats launch");
+}
+
+int plato_agg_fedavg_entrywise(const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+                               const float* d_w, int n_entries, const plato_agg_chunk* d_chunks_f32,
+                               uint32_t n_chunks_f32, const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64,
+                               const float* d_base_f32, const int64_t* d_base_i64, const float* d_noise_f32,
+                               const float* d_noise_i64f, float scale, float noise_scale, int flags,
+                               float* d_out_f32, float* d_out_i64f, size_t n_f32, size_t n_i64,
+                               hipStream_t stream) {
+  if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
+  if (n_entries <= 0 || !d_w) return set_error(PLATO_AGG_EINVAL, "null weight table");
+  if ((flags & PLATO_AGG_ADD_BASE) && !d_base_f32) return set_error(PLATO_AGG_EINVAL, "ADD_BASE needs a baseline");
+  if (n_chunks_f32 && (!d_x_f32 || !d_chunks_f32 || !d_out_f32))
+    return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
+  if (n_chunks_i64 && (!d_x_i64 || !d_chunks_i64 || !d_out_i64f || (d_base_f32 && !d_base_i64) ||
+                       (d_noise_f32 && !d_noise_i64f)))
+    return set_error(PLATO_AGG_EINVAL, "null int64 pointer");
+  if (misaligned(d_base_f32) || misaligned(d_noise_f32) || misaligned(d_out_f32))
+    return set_error(PLATO_AGG_EINVAL, "fp32 baseline / noise / output must be 16-byte aligned");
+  if (n_f32 > 0xffffffffull || n_i64 > 0xffffffffull)
+    return set_error(PLATO_AGG_EINVAL, "arena too large for 32-bit chunk offsets");
+  const uint64_t nc = uint64_t(n_chunks_f32) + n_chunks_i64;
+  if (nc == 0) return clear_error();
+  if (nc > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "bad chunk count");
+  EwArgs a{};
+  a.xf = d_x_f32;
+  a.xi = d_x_i64;
+  a.w = d_w;
+  a.base_f = d_base_f32;
+  a.base_i = d_base_i64;
+  a.noise_f = d_noise_f32;
+  a.noise_if = d_noise_i64f;
+  a.out_f = d_out_f32;
+  a.out_if = d_out_i64f;
+  a.cf = d_chunks_f32;
+  a.ci = d_chunks_i64;
+  a.n_f32 = n_f32;
+  a.n_i64 = n_i64;
+  a.ncf = n_chunks_f32;
+  a.nci = n_chunks_i64;
+  a.scale = scale;
+  a.noise_scale = noise_scale;
+  a.K = K;
+  a.flags = flags;
+  if (d_base_f32) {
+    hipLaunchKernelGGL(fedavg_entrywise_kernel<true>, dim3(uint32_t(nc)), dim3(kBlock), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(fedavg_entrywise_kernel<false>, dim3(uint32_t(nc)), dim3(kBlock), 0, stream, a);
+  }
+  return launch_error("fedavg_entrywise launch");
+}
+
+int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+                              const float* d_base_f32, const int64_t* d_base_i64,
+                              const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
+                              const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
+                              size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
+  if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
+  if (n_entries <= 0 || !d_out) return set_error(PLATO_AGG_EINVAL, "null output / no entries");
+  if (n_entries_f32 && (!d_x_f32 || !d_entries_f32)) return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
+  if (n_entries_i64 && (!d_x_i64 || !d_entries_i64 || (d_base_f32 && !d_base_i64)))
+    return set_error(PLATO_AGG_EINVAL, "null int64 pointer");
+  if (n_f32 > 0xffffffffull || n_i64 > 0xffffffffull)
+    return set_error(PLATO_AGG_EINVAL, "arena too large for 32-bit chunk offsets");
+  const uint64_t threads = (uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K) * kNormLanes;
+  if (threads == 0) return clear_error();
+  if (threads / kBlock + 1 > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "too many (client, entry) pairs");
+  NormArgs a{};
+  a.xf = d_x_f32;
+  a.xi = d_x_i64;
+  a.base_f = d_base_f32;
+  a.base_i = d_base_i64;
+  a.ef = d_entries_f32;
+  a.ei = d_entries_i64;
+  a.out = d_out;
+  a.n_f32 = n_f32;
+  a.n_i64 = n_i64;
+  a.nef = n_entries_f32;
+  a.nei = n_entries_i64;
+  a.n_entries = uint32_t(n_entries);
+  a.K = K;
+  const dim3 grid{uint32_t((threads + kBlock - 1) / kBlock)};
+  if (d_base_f32) {
+    hipLaunchKernelGGL(entry_norms_kernel<true>, grid, dim3(kBlock), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(entry_norms_kernel<false>, grid, dim3(kBlock), 0, stream, a);
+  }
+  return launch_error("entry_norms launch");
+}
+
+}  // extern "C"

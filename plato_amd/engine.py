@@ -75,10 +75,10 @@ def _stream_handle(stream: torch.cuda.Stream) -> int:
 class DeviceArena:
     """One model arena in HBM: fp32 region + int64 region (+ fp32 view of int64 results)."""
 
-    def __init__(self, layout: ArenaLayout, device: torch.device):
+    def __init__(self, layout: ArenaLayout, device: torch.device, i64_dtype: torch.dtype = torch.int64):
         self.layout = layout
         self.f32 = torch.empty(layout.row_f32, dtype=torch.float32, device=device)
-        self.i64 = torch.empty(layout.row_i64, dtype=torch.int64, device=device)
+        self.i64 = torch.empty(layout.row_i64, dtype=i64_dtype, device=device)
 
 
 class ClientSlab:
@@ -221,6 +221,28 @@ class FedAvgEngine:
         tf = torch.from_numpy(pf).to(self.device)
         ti = torch.from_numpy(pi).to(self.device)
         return tf, ti
+
+    # per-entry kernels: chunk capacity (elements) per workgroup
+    STATS_CHUNK = 4096      # entry_stats: 256 lanes x 4 float4 groups
+    ENTRYWISE_CHUNK = 1024  # fedavg_entrywise: 256 lanes x 1 float4 group
+
+    def _chunks(self, layout: ArenaLayout, cap: int):
+        """Device copies of ``layout.chunk_tables(cap)`` (cached per layout)."""
+        key = ("dev_chunks", cap, str(self.device))
+        hit = layout._cache.get(key)
+        if hit is None:
+            cf, ci = layout.chunk_tables(cap)
+            hit = (torch.from_numpy(cf.view(np.int32).copy()).to(self.device),
+                   torch.from_numpy(ci.view(np.int32).copy()).to(self.device))
+            layout._cache[key] = hit
+        return hit
+
+    def _f32_stager(self) -> "_Stager":
+        st = self._stagers.get("f32")
+        if st is None:
+            st = _Stager(self._layout, self.device, codec="f32", stream=self._copy_stream)
+            self._stagers["f32"] = st
+        return st
 
     # ---------------------------------------------------- arrival staging
     ARRIVAL_CHUNK = 16  # rows per arrival slab; rows never move once staged
@@ -527,7 +549,11 @@ class AggregationRound:
         else:
             eng.launch_fedavg(lay, tf, ti, w, s, len(order), None if deltas else eng._base.f32,
                               None if deltas else eng._base.i64, out_f, out_i, stream)
-        # D2H into fresh pinned buffers, still stream-ordered; result() only waits.
+        self._fetch(stream, out_f, out_i, (tf, ti, w, s))
+
+    def _fetch(self, stream, out_f: torch.Tensor, out_i: torch.Tensor, keep=()) -> None:
+        """D2H into fresh pinned buffers, stream-ordered; result() only waits."""
+        lay = self.layout
         host_f = torch.empty(lay.n_f32, dtype=torch.float32, pin_memory=True)
         host_i = torch.empty(lay.n_i64, dtype=torch.float32, pin_memory=True)
         host_f.copy_(out_f[: lay.n_f32], non_blocking=True)
@@ -535,7 +561,133 @@ class AggregationRound:
         self.event = torch.cuda.Event()
         self.event.record(stream)
         # keep device buffers alive until the copies finish
-        self._out = (host_f, host_i, out_f, out_i, tf, ti, w, s)
+        self._out = (host_f, host_i, out_f, out_i, keep)
+
+    def _check_slots(self, slots: Sequence[int]) -> list[int]:
+        slots = list(slots)
+        for slot in slots:
+            if not (0 <= slot < self.capacity and self.staged[slot]):
+                raise ValueError(f"client slot {slot} was not staged")
+        if not slots:
+            raise ValueError("no client slots")
+        if self.codec != "native":
+            raise NotImplementedError("per-entry kernels take native (fp32/int64) payloads")
+        return slots
+
+    def entry_stats(self, slots: Sequence[int], v: tuple | None = None, deltas: bool = False):
+        """Per (client, entry) fp64 sums over the staged slots (``plato_agg_entry_stats``).
+
+        ``d_i = x_i - baseline`` (``deltas=False``) or ``x_i``.  ``v`` is an
+        optional device vector ``(fp32 arena, fp32 values of the int64
+        entries)``, e.g. :meth:`launch_entrywise`'s ``device=True`` output.
+        Returns ``(dv [K, E] | None, dd [K, E], vv [E] | None)`` as float64
+        numpy arrays, entries in layout order.
+        """
+        slots = self._check_slots(slots)
+        if not deltas and not self.has_baseline:
+            raise ValueError("baseline not staged")
+        eng, lay = self.engine, self.layout
+        k, n_e = len(slots), len(lay.entries)
+        cf, ci = eng._chunks(lay, eng.STATS_CHUNK)
+        pf = np.asarray([self._pf[i] for i in slots], dtype=np.int64)
+        pi = np.asarray([self._pi[i] for i in slots], dtype=np.int64)
+        tf, ti = eng._pointer_tables(pf, pi)
+        stream = torch.cuda.current_stream(eng.device)
+        self.stager.fence(stream)
+        ncf, nci = int(cf.shape[0]), int(ci.shape[0])
+        ws = torch.empty((eng.lib.plato_agg_entry_stats_workspace(k, ncf + nci) + 7) // 8,
+                         dtype=torch.float64, device=eng.device)
+        out = torch.empty((2 * k + 1) * n_e, dtype=torch.float64, device=eng.device)
+        vf, vi = (None, None) if v is None else v
+        n_i = lay.n_i64
+        _lib.call("plato_agg_entry_stats", _ptr(tf), _ptr(ti) if n_i else None, k,
+                  None if deltas else _ptr(eng._base.f32), None if (deltas or not n_i) else _ptr(eng._base.i64),
+                  _ptr(vf), _ptr(vi) if (vf is not None and n_i) else None,
+                  _ptr(cf), ncf, _ptr(ci) if nci else None, nci, n_e, lay.n_f32, n_i, _ptr(ws), _ptr(out),
+                  _stream_handle(stream))
+        res = out.cpu().numpy().reshape(2 * k + 1, n_e)
+        if v is None:
+            return None, res[k:2 * k].copy(), None
+        return res[:k].copy(), res[k:2 * k].copy(), res[2 * k].copy()
+
+    def entry_norms(self, slots: Sequence[int]) -> np.ndarray:
+        """fp32 ``torch.linalg.norm`` of each (client, entry) delta in torch's CPU order.
+
+        ``plato_agg_entry_norms_f32``: bit-equal to the reference's
+        ``torch.linalg.norm(-delta)`` (fedatt_algorithm.py:39).  Returns
+        ``[E, K]`` float32 (entries in layout order, clients in ``slots`` order).
+        """
+        slots = self._check_slots(slots)
+        if not self.has_baseline:
+            raise ValueError("baseline not staged")
+        eng, lay = self.engine, self.layout
+        k, n_e = len(slots), len(lay.entries)
+        ef, ei = eng._chunks(lay, 1 << 32)  # one piece per entry
+        pf = np.asarray([self._pf[i] for i in slots], dtype=np.int64)
+        pi = np.asarray([self._pi[i] for i in slots], dtype=np.int64)
+        tf, ti = eng._pointer_tables(pf, pi)
+        stream = torch.cuda.current_stream(eng.device)
+        self.stager.fence(stream)
+        out = torch.zeros(k * n_e, dtype=torch.float32, device=eng.device)
+        n_i = lay.n_i64
+        nef, nei = int(ef.shape[0]), int(ei.shape[0])
+        _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti) if n_i else None, k, _ptr(eng._base.f32),
+                  _ptr(eng._base.i64) if n_i else None, _ptr(ef), nef, _ptr(ei) if nei else None, nei, n_e,
+                  lay.n_f32, n_i, _ptr(out), _stream_handle(stream))
+        return np.ascontiguousarray(out.cpu().numpy().reshape(k, n_e).T)
+
+    def launch_entrywise(self, weights: np.ndarray, order: Sequence[int] | None = None, scale: float = 1.0,
+                         noise: Mapping[str, torch.Tensor] | None = None, noise_scale: float = 0.0,
+                         add_base: bool = True, deltas: bool = False, device: bool = False):
+        """Weighted sum with a weight per (entry, client) (``plato_agg_fedavg_entrywise``).
+
+        ``weights`` is ``[E, K]`` (entries in layout order, clients in
+        ``order``), rounded to fp32 like torch's scalar multiply.  ``noise``
+        is a state_dict of fp32 tensors added as ``noise * noise_scale``.
+        ``device=True`` returns the device result ``(fp32 arena, int64
+        entries as fp32)`` instead of scheduling the D2H for :meth:`result`.
+        """
+        order = list(range(np.shape(weights)[1])) if order is None else list(order)
+        slots = self._check_slots(order)
+        if not deltas and not self.has_baseline:
+            raise ValueError("baseline not staged")
+        if deltas and add_base:
+            raise ValueError("add_base needs the baseline (deltas=False)")
+        eng, lay = self.engine, self.layout
+        k, n_e = len(slots), len(lay.entries)
+        w = np.ascontiguousarray(np.asarray(weights, dtype=np.float64).astype(np.float32))
+        if w.shape != (n_e, k):
+            raise ValueError(f"weights must be [entries={n_e}, clients={k}], got {w.shape}")
+        cf, ci = eng._chunks(lay, eng.ENTRYWISE_CHUNK)
+        pf = np.asarray([self._pf[i] for i in slots], dtype=np.int64)
+        pi = np.asarray([self._pi[i] for i in slots], dtype=np.int64)
+        tf, ti = eng._pointer_tables(pf, pi)
+        dw = torch.from_numpy(w).to(eng.device)
+        nz = None
+        if noise is not None:
+            nz = DeviceArena(lay, eng.device, i64_dtype=torch.float32)
+            lay.check_compatible(noise, "noise", "f32")
+            eng._f32_stager().put(noise, nz.f32, nz.i64)
+        stream = torch.cuda.current_stream(eng.device)
+        self.stager.fence(stream)
+        if nz is not None:
+            eng._f32_stager().fence(stream)
+        out_f = torch.empty(lay.row_f32, dtype=torch.float32, device=eng.device)
+        out_i = torch.empty(lay.row_i64, dtype=torch.float32, device=eng.device)
+        n_i = lay.n_i64
+        ncf, nci = int(cf.shape[0]), int(ci.shape[0])
+        _lib.call("plato_agg_fedavg_entrywise", _ptr(tf), _ptr(ti) if n_i else None, k, _ptr(dw), n_e,
+                  _ptr(cf), ncf, _ptr(ci) if nci else None, nci,
+                  None if deltas else _ptr(eng._base.f32), None if (deltas or not n_i) else _ptr(eng._base.i64),
+                  None if nz is None else _ptr(nz.f32), None if (nz is None or not n_i) else _ptr(nz.i64),
+                  float(scale), float(noise_scale), _lib.PLATO_AGG_ADD_BASE if add_base else 0,
+                  _ptr(out_f), _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
+        if device:
+            # inputs stay referenced by the caller's stream order; nothing to fetch
+            self._keep = (tf, ti, dw, nz)
+            return out_f, out_i
+        self._fetch(stream, out_f, out_i, (tf, ti, dw, nz))
+        return None
 
     def model_similarities(self, reference: Mapping[str, torch.Tensor], slots: Sequence[int],
                            eps: float = 1e-8) -> list[np.float32]:

@@ -11,6 +11,8 @@ from __future__ import annotations
 
 import os
 
+import numpy as np
+
 from .. import weights as W
 from .fedavg import FusedAggregationMixin, _EngineHolder
 
@@ -166,6 +168,106 @@ class GanDeltasAggregationMixin(_EngineHolder):
         return gen, disc
 
 
+def _staged_round(server, who):
+    rnd = getattr(server, "_plato_amd_round", None)
+    if rnd is None:
+        raise RuntimeError(f"{who} needs the staged round (use the fused aggregate_weights hook)")
+    return rnd
+
+
+def _config_attr(section, name, default):
+    try:
+        from plato.config import Config
+
+        sec = getattr(Config(), section)
+        return getattr(sec, name) if hasattr(sec, name) else default
+    except Exception:  # Plato not importable / not configured
+        return default
+
+
+class FedAdpWeights(_EngineHolder):
+    """examples/server_aggregation/fedadp/fedadp_server.py:38-133 on the staged round.
+
+    The reference computes ``global_grads = sum_i delta_i * n_i/N`` (``:43-50``),
+    the angle of every client's flattened delta with it (``:86-99``), smoothed
+    per client into a contribution (``:101-120``), and averages the deltas
+    with ``n_i exp(c_i) / sum`` (``:53-68``).  Here:
+
+    1. ``global_grads`` = one ``fedavg_entrywise`` pass (no baseline added),
+       left in HBM, bit-exact with the reference's;
+    2. ``plato_agg_entry_stats`` gives per (client, entry) ``d.g`` and ``d.d``
+       plus per-entry ``g.g``; ``process_grad``'s ``-x/lr`` scaling folds into
+       per-entry factors (weights.fedadp_process_scales);
+    3. the host runs the reference's scalar code (weights.fedadp_*), and the
+       fused kernel does the final ``b + sum_i delta_i * w_i``.
+
+    ``self.local_angles`` and ``self.adaptive_weighting`` are kept as the
+    reference keeps them; ``self.selected_clients`` / ``self.current_round``
+    come from the server.
+    """
+
+    #: FedAdp's alpha; None = Config().algorithm.alpha, else 5 (fedadp_server.py:112-114)
+    fedadp_alpha = None
+    #: learning rate of process_grad; None = Config().parameters.optimizer.lr
+    fedadp_lr = None
+
+    def aggregation_weights(self, updates):
+        rnd = _staged_round(self, "FedAdp")
+        if getattr(self, "local_angles", None) is None:
+            self.local_angles = {}
+        num_samples = [u.report.num_samples for u in updates]
+        k = len(updates)
+        lay = rnd.layout
+        names = lay.keys()
+        w1 = np.tile(np.asarray(W.fedavg(num_samples), dtype=np.float64), (len(names), 1))
+        grads = rnd.launch_entrywise(w1, add_base=False, device=True)
+        dv, dd, vv = rnd.entry_stats(range(k), v=grads)
+        lr = self.fedadp_lr
+        if lr is None:
+            lr = _config_attr("parameters", "optimizer", None)
+            lr = getattr(lr, "lr", None) if lr is not None else None
+            if lr is None:
+                raise ValueError("FedAdp needs parameters.optimizer.lr (or set fedadp_lr)")
+        alpha = self.fedadp_alpha if self.fedadp_alpha is not None else _config_attr("algorithm", "alpha", 5)
+        angles = W.fedadp_angles(dv, dd, vv, W.fedadp_process_scales(names, lr))
+        contribs = W.fedadp_contributions(angles, self.selected_clients, self.local_angles,
+                                          self.current_round, alpha)
+        self.adaptive_weighting = W.fedadp_weighting(contribs, num_samples)
+        return self.adaptive_weighting, None
+
+
+class PolarisWeights(_EngineHolder):
+    """examples/client_selection/polaris/polaris_server.py:68-100 on the staged round.
+
+    FedAvg weights, plus the per-client norm of the conv-layer deltas the
+    reference records for its client-selection solver
+    (``self.squared_deltas_current_round``, ``self.unexplored_clients``),
+    from one ``plato_agg_entry_stats`` pass over the staged payloads.  The
+    solver itself (cvxopt/mosek, ``:129-186``) stays the reference's.
+    """
+
+    def aggregation_weights(self, updates):
+        weights, scales = super().aggregation_weights(updates)  # FedAvg n_i/N, sets total_samples
+        rnd = _staged_round(self, "Polaris")
+        _, dd, _ = rnd.entry_stats(range(len(updates)))
+        norms = W.polaris_delta_norms(dd, rnd.layout.keys())
+        self.squared_deltas_current_round = np.zeros(self.number_of_client)
+        sum_deltas_current_round = 0
+        deltas_counter = 0
+        for update, norm in zip(updates, norms):
+            self.squared_deltas_current_round[update.client_id - 1] = norm
+            if (update.client_id - 1) in self.unexplored_clients:
+                self.unexplored_clients.remove(update.client_id - 1)
+            sum_deltas_current_round += norm
+            deltas_counter += 1
+        avg_deltas_current_round = sum_deltas_current_round / deltas_counter
+        expect_deltas = self.alpha * avg_deltas_current_round
+        for client_counter in range(200):  # the reference's literal bound (polaris_server.py:96)
+            if client_counter in self.unexplored_clients:
+                self.squared_deltas_current_round[client_counter] = expect_deltas
+        return weights, scales
+
+
 class FedBuffServerMixin(FedBuffWeights, FusedAggregationMixin):
     pass
 
@@ -175,4 +277,12 @@ class PortServerMixin(PortWeights, FusedAggregationMixin):
 
 
 class PiscesServerMixin(PiscesWeights, FusedAggregationMixin):
+    pass
+
+
+class FedAdpServerMixin(FedAdpWeights, FusedAggregationMixin):
+    pass
+
+
+class PolarisServerMixin(PolarisWeights, FusedAggregationMixin):
     pass

@@ -124,3 +124,98 @@ def fedasync_mixing(mixing: float, staleness: int, func: str = "constant", a: fl
     else:
         raise ValueError(f"unknown staleness weighting function {func!r}")
     return mixing * factor
+
+
+# --------------------------------------------------------------------------
+# Per-entry variants: the numbers depend on reductions over the deltas, which
+# the device computes (plato_agg_entry_stats, fp64, fixed order); the host
+# finishes them with the reference's own scalar expressions.
+# --------------------------------------------------------------------------
+def fedatt_attention(norms: np.ndarray) -> np.ndarray:
+    """FedAtt attention ``[entry, client]`` from the fp32 norms ``[entry, client]``.
+
+    examples/server_aggregation/fedatt/fedatt_algorithm.py:32-42:
+    ``atts[name][i] = torch.linalg.norm(-delta)`` into an fp32 tensor, then
+    ``F.softmax(atts[name], dim=0)`` per entry — the same torch op here, one
+    softmax over the clients of each entry.
+    """
+    import torch
+
+    t = torch.from_numpy(np.ascontiguousarray(norms, dtype=np.float32))
+    return torch.softmax(t, dim=1).numpy()
+
+
+def fedadp_process_scales(names: Sequence[str], lr: float) -> np.ndarray:
+    """Per-entry factor of FedAdp's flattening on products of two flattened vectors.
+
+    ``process_grad`` (examples/server_aggregation/fedadp/fedadp_server.py:122-133)
+    sorts the entries by ``name.lower()``, keeps the first as is and divides
+    every other by ``-lr``; a product of two such vectors therefore weighs
+    entry e by 1 (first) or 1/lr^2.
+    """
+    order = sorted(range(len(names)), key=lambda i: names[i].lower())
+    scales = np.full(len(names), 1.0 / (lr * lr))
+    if order:
+        scales[order[0]] = 1.0
+    return scales
+
+
+def fedadp_angles(dv: np.ndarray, dd: np.ndarray, vv: np.ndarray, scales: np.ndarray) -> list:
+    """Angles between each client's flattened delta and the global one (fedadp_server.py:94-99).
+
+    The reference forms ``np.inner`` and ``np.linalg.norm`` of float32 arrays
+    (float32 results), then ``np.arccos(np.clip(inner / norms, -1.0, 1.0))``
+    in float32; here the sums come from the device in fp64 and are rounded to
+    float32 where the reference holds float32 values.
+    """
+    g_norm = np.float32(np.sqrt(float(np.dot(vv, scales))))
+    angles = []
+    for k in range(dv.shape[0]):
+        inner = np.float32(float(np.dot(dv[k], scales)))
+        l_norm = np.float32(np.sqrt(float(np.dot(dd[k], scales))))
+        norms = g_norm * l_norm
+        angles.append(np.arccos(np.clip(inner / norms, -1.0, 1.0)))
+    return angles
+
+
+def fedadp_contributions(angles, selected_clients, local_angles: dict, current_round: int,
+                         alpha: float = 5) -> list:
+    """fedadp_server.py:101-120: smoothed angles (updated in ``local_angles``) -> contributions."""
+    import math
+
+    contribs = [None] * len(angles)
+    for i, angle in enumerate(angles):
+        client_id = selected_clients[i]
+        if client_id not in local_angles:
+            local_angles[client_id] = angle
+        local_angles[client_id] = ((current_round - 1) / current_round) * local_angles[client_id] + (
+            1 / current_round) * angle
+        contribs[i] = alpha * (1 - math.exp(-math.exp(-alpha * (local_angles[client_id] - 1))))
+    return contribs
+
+
+def fedadp_weighting(contribs, num_samples) -> list:
+    """fedadp_server.py:70-84: ``n_i * exp(c_i) / sum_j n_j * exp(c_j)``."""
+    import math
+
+    total_weight = 0.0
+    for i, contrib in enumerate(contribs):
+        total_weight += num_samples[i] * math.exp(contrib)
+    return [(num_samples[i] * math.exp(contrib)) / total_weight for i, contrib in enumerate(contribs)]
+
+
+def polaris_delta_norms(dd: np.ndarray, names: Sequence[str]) -> list:
+    """Per client ``sqrt(sum over 'conv' layers of np.sum(np.square(delta)))``.
+
+    examples/client_selection/polaris/polaris_server.py:76-89: each layer's
+    ``np.sum`` is a float32 scalar and they are added in float32
+    (``0 + np.float32``), then ``np.sqrt`` in float32.
+    """
+    conv = [e for e, name in enumerate(names) if "conv" in name]
+    out = []
+    for k in range(dd.shape[0]):
+        squared = 0
+        for e in conv:
+            squared += np.float32(dd[k, e])
+        out.append(np.sqrt(squared))
+    return out

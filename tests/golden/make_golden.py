@@ -56,6 +56,8 @@ STUBBED = [
     "socketio", "torchvision", "zstd", "lightly", "opacus", "torch_optimizer", "gym", "boto3",
     "botocore", "evaluate", "tenseal", "cv2", "pycocotools", "skimage", "ultralytics", "h5py",
     "timm", "mmcv", "wandb", "torchmetrics",
+    # polaris_server.py imports these at module level (client selection solver, unused here)
+    "cvxopt", "mosek", "turtle",
 ]
 
 CANON_NAN = np.uint32(0x7FC00000)
@@ -137,7 +139,8 @@ def boot_reference(ref_root: str, workdir: str):
     sys.argv = ["make_golden", "-b", workdir]
     sys.path.insert(0, ref_root)
     for sub in ("examples/async/fedbuff", "examples/async/port", "examples/async/fedasync",
-                "examples/client_selection/pisces"):
+                "examples/client_selection/pisces", "examples/server_aggregation/fedatt",
+                "examples/server_aggregation/fedadp", "examples/client_selection/polaris"):
         sys.path.insert(0, os.path.join(ref_root, sub))
     from plato.config import Config
 
@@ -241,6 +244,15 @@ def server_class(mode):
     if mode == "fedasync":
         import fedasync_server
         return fedasync_server.Server
+    if mode == "fedatt":
+        import fedatt_server
+        return fedatt_server.Server
+    if mode == "fedadp":
+        import fedadp_server
+        return fedadp_server.Server
+    if mode == "polaris":
+        import polaris_server
+        return polaris_server.Server
     raise ValueError(mode)
 
 
@@ -277,9 +289,25 @@ def run_case(case):
         # what FedAsync's configure() reads from the config (fedasync_server.py:37-65)
         server.mixing_hyperparam = 0.9
         server.adaptive_mixing = True
+    elif mode == "fedatt":
+        import fedatt_algorithm
+
+        server = cls(model=lambda: model, algorithm=fedatt_algorithm.Algorithm)
+        server.init_trainer()
     else:
         server = cls(model=lambda: model)
         server.init_trainer()
+    if mode == "polaris":
+        # what Polaris' configure() sets (polaris_server.py:43-51)
+        server.number_of_client = case.get("total_clients", 1024)
+        server.local_gradient_bounds = 0.5 * np.ones(server.number_of_client)
+        server.local_stalenesses = 0.01 * np.ones(server.number_of_client)
+        server.aggregation_weights = np.ones(server.number_of_client) * (1.0 / server.number_of_client)
+        server.unexplored_clients = list(range(server.number_of_client))
+        server.alpha = 10
+    if mode == "fedadp":
+        server.selected_clients = [c + 1 for c in order]
+        server.local_angles = {int(c): np.float32(float.fromhex(a)) for c, a in case.get("local_angles", {}).items()}
     if mode == "pisces":
         server.client_staleness = {c + 1: [] for c in range(k)}
     server.algorithm.load_weights(copy.deepcopy(baseline))
@@ -314,6 +342,27 @@ def run_case(case):
                 f32hex(sim.item()) if isinstance(sim, torch.Tensor) else float(sim))
             return sim
         server.cosine_similarity = spy_cs
+    if mode == "fedatt":
+        import fedatt_algorithm
+
+        real_softmax = fedatt_algorithm.F.softmax
+
+        def spy_softmax(t, dim=0):
+            out = real_softmax(t, dim=dim)
+            captured.setdefault("norms", []).append([f32hex(v) for v in t.numpy()])
+            captured.setdefault("atts", []).append([f32hex(v) for v in out.numpy()])
+            return out
+        fedatt_algorithm.F = types.SimpleNamespace(softmax=spy_softmax)
+        torch.manual_seed(case["noise_seed"])
+    if mode == "fedadp":
+        orig_w = server.calc_adaptive_weighting
+
+        def spy_w(deltas, num_samples):
+            captured["global_grads"] = {n: t.clone() for n, t in server.global_grads.items()}
+            res = orig_w(deltas, num_samples)
+            captured["adaptive"] = [float(x).hex() for x in res]
+            return res
+        server.calc_adaptive_weighting = spy_w
     orig_load = server.algorithm.load_weights
 
     def spy_load(weights):
@@ -321,7 +370,7 @@ def run_case(case):
         return orig_load(weights)
     server.algorithm.load_weights = spy_load
 
-    if mode in ("fedavg", "fedbuff", "port", "fedasync"):
+    if mode in ("fedavg", "fedbuff", "port", "fedasync", "fedatt", "fedadp", "polaris"):
         asyncio.run(server._process_reports())
     else:  # pisces: drive the hot path directly (its weights_aggregated needs client selection state)
         weights_received = [u.payload for u in server.updates]
@@ -348,6 +397,19 @@ def run_case(case):
     out["samples_loaded_i64"] = [[int(i), int(li[i])] for i in range(min(ni, 64))]
     if "sims" in captured:
         out["port_similarities"] = captured["sims"]
+    if mode == "fedatt":
+        out["fedatt_norms"] = captured["norms"]   # [entry][client], baseline key order
+        out["fedatt_atts"] = captured["atts"]
+    if mode == "fedadp":
+        gg = captured["global_grads"]
+        out["global_grads_f32_sha256"] = sha(canon(flatten(entries, gg, "f32", torch.float32)))
+        out["global_grads_i64f_sha256"] = sha(canon(flatten(entries, gg, "i64", torch.float32)))
+        out["adaptive_weighting"] = captured["adaptive"]
+        out["local_angles"] = {str(c): f32hex(a) for c, a in server.local_angles.items()}
+    if mode == "polaris":
+        sq = server.squared_deltas_current_round
+        out["squared_deltas"] = {str(i): float(sq[i]).hex() for i in range(len(sq)) if sq[i] != 0}
+        out["total_samples"] = server.total_samples
     if "avg" in captured:
         out["avg_f32_sha256"] = sha(canon(flatten(entries, captured["avg"], "f32", torch.float32)))
         out["avg_i64f_sha256"] = sha(canon(flatten(entries, captured["avg"], "i64", torch.float32)))
@@ -419,6 +481,16 @@ def cases():
              num_samples=synth.num_samples(9, 17), full=True),
         dict(name="gan_lenet5_resnet18_k5", mode="gan", models=["lenet5", "resnet18"], k=5, seed=18,
              num_samples=synth.num_samples(5, 18)),
+        dict(name="fedatt_lenet5_k6", model="lenet5", k=6, seed=19, mode="fedatt", noise_seed=7,
+             num_samples=synth.num_samples(6, 19), full=True),
+        dict(name="fedatt_resnet18_k8", model="resnet18", k=8, seed=20, mode="fedatt", noise_seed=11,
+             num_samples=synth.num_samples(8, 20)),
+        dict(name="fedadp_lenet5_k6", model="lenet5", k=6, seed=21, mode="fedadp", current_round=3,
+             num_samples=synth.num_samples(6, 21), local_angles={"2": "0x1.8p+0", "5": "0x1.2p-1"}, full=True),
+        dict(name="fedadp_resnet18_k8", model="resnet18", k=8, seed=22, mode="fedadp", current_round=1,
+             num_samples=synth.num_samples(8, 22), order=[3, 0, 7, 1, 2, 6, 4, 5]),
+        dict(name="polaris_resnet18_k8", model="resnet18", k=8, seed=23, mode="polaris",
+             num_samples=synth.num_samples(8, 23), order=[2, 0, 5, 7, 1, 3, 6, 4]),
         dict(name="C4_port_resnet18_k256", model="resnet18", k=256, seed=13, mode="port",
              num_samples=synth.num_samples(256, 13), staleness=[(7 * i) % 11 for i in range(256)]),
     ]

@@ -67,7 +67,8 @@ def _launch(engine, layout, base, slab, order, weights, scales, deltas=False):
     return out_f, out_i
 
 
-NON_ASYNC = [c for c in CASES if c["recipe"].get("mode", "fedavg") not in ("fedasync", "gan")
+NON_ASYNC = [c for c in CASES
+             if c["recipe"].get("mode", "fedavg") not in ("fedasync", "gan") + G.PER_ENTRY_MODES
              and c["recipe"].get("codec") is None]
 BF16 = [c for c in CASES if c["recipe"].get("codec") == "bf16"]
 

@@ -90,7 +90,8 @@ def test_known_answer_reference_fedavg_tests():
     assert ka["aggregated"]["head.weight"] == ["3f599999"]  # 0.84999996, not 0.85
 
 
-NON_ASYNC = [c for c in CASES if c["recipe"].get("mode", "fedavg") not in ("fedasync", "gan")]
+NON_ASYNC = [c for c in CASES
+             if c["recipe"].get("mode", "fedavg") not in ("fedasync", "gan") + G.PER_ENTRY_MODES]
 
 
 @pytest.mark.parametrize("case", NON_ASYNC, ids=_ids(NON_ASYNC))

@@ -1,0 +1,226 @@
+"""GPU parity of the per-entry kernels and the FedAtt / FedAdp / Polaris hooks.
+
+* plato_agg_fedavg_entrywise vs oracle.entrywise_numpy: bit-exact, on a layout
+  of awkward entry sizes and with chunk capacities small enough that entries
+  span many chunks and chunks start/end inside float4 groups;
+* plato_agg_entry_stats vs oracle.entry_stats_fp64: 1e-12 relative (both fp64,
+  different summation order);
+* plato_agg_entry_norms_f32 vs oracle.torch_cpu_norm_f32: bit-exact;
+* the product hooks vs the reference fixtures: FedAtt bit-exact end to end,
+  FedAdp's global gradient bit-exact and its model within the tolerance of the
+  reference's own float32 BLAS reductions (see tests/test_per_entry.py),
+  Polaris' model bit-exact and its norms within 1e-5.
+"""
+
+import asyncio
+import types
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import fedavg_oracle as ref
+from plato_amd.arena import ArenaLayout
+from plato_amd.engine import FedAvgEngine
+from tests import golden_cases as G
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+CASES = {c["recipe"]["name"]: c for c in G.load_cases()}
+
+SPEC = [("a", (3,), "f32"), ("n0", (), "i64"), ("b", (1,), "f32"), ("c", (5, 7), "f32"), ("d", (64,), "f32"),
+        ("n1", (4,), "i64"), ("e", (1000,), "f32"), ("f", (0,), "f32"), ("g", (4099,), "f32"), ("h", (2,), "f32"),
+        ("n2", (), "i64"), ("big", (3, 4097), "f32")]
+
+
+@pytest.fixture(scope="module")
+def engine():
+    return FedAvgEngine(DEV)
+
+
+def _random_round(engine, k, seed):
+    layout = ArenaLayout.from_shapes(SPEC)
+    rng = np.random.default_rng(seed)
+    bf = rng.standard_normal(layout.n_f32).astype(np.float32)
+    bi = rng.integers(-1000, 1000, layout.n_i64)
+    xs_f = [(bf + 0.01 * rng.standard_normal(layout.n_f32)).astype(np.float32) for _ in range(k)]
+    xs_i = [bi + rng.integers(0, 9, layout.n_i64) for _ in range(k)]
+    base = layout.unpack(torch.from_numpy(bf), torch.from_numpy(bi))
+    pays = [layout.unpack(torch.from_numpy(xs_f[i]), torch.from_numpy(xs_i[i])) for i in range(k)]
+    rnd = engine.begin(base, k)
+    rnd.put_baseline(base)
+    for i in range(k):
+        rnd.put_client(i, pays[i])
+    return layout, rnd, bf, bi, xs_f, xs_i, rng
+
+
+@pytest.mark.parametrize("cap", [8, 20, 1024])
+@pytest.mark.parametrize("noise,add_base", [(False, True), (True, True), (False, False)])
+def test_entrywise_matches_oracle(engine, monkeypatch, cap, noise, add_base):
+    monkeypatch.setattr(FedAvgEngine, "ENTRYWISE_CHUNK", cap)
+    k = 5
+    layout, rnd, bf, bi, xs_f, xs_i, rng = _random_round(engine, k, 10 + cap)
+    w = rng.standard_normal((len(layout.entries), k))
+    nz = nf = ni = None
+    if noise:
+        nf = rng.standard_normal(layout.n_f32).astype(np.float32)
+        ni = rng.standard_normal(layout.n_i64).astype(np.float32)
+        nz = layout.unpack(torch.from_numpy(nf), torch.from_numpy(ni))
+    order = [3, 0, 4, 1, 2]
+    rnd.launch_entrywise(w, order=order, scale=-1.2, noise=nz, noise_scale=0.001, add_base=add_base)
+    got = rnd.result()
+    exp_f, exp_i = ref.entrywise_numpy(layout.entries, bf, bi, [xs_f[i] for i in order], [xs_i[i] for i in order],
+                                       w, -1.2, nf, ni, 0.001, add_base)
+    got_f = torch.cat([got[e.name].reshape(-1) for e in layout.entries if e.region == "f32"]).numpy()
+    got_i = torch.cat([got[e.name].reshape(-1) for e in layout.entries if e.region == "i64"]).numpy()
+    assert got_f.tobytes() == exp_f.tobytes()
+    assert got_i.tobytes() == exp_i.tobytes()
+
+
+@pytest.mark.parametrize("cap", [4, 36, 4096])
+def test_entry_stats_match_oracle(engine, monkeypatch, cap):
+    monkeypatch.setattr(FedAvgEngine, "STATS_CHUNK", cap)
+    k = 6
+    layout, rnd, bf, bi, xs_f, xs_i, rng = _random_round(engine, k, 20 + cap)
+    vf = rng.standard_normal(layout.row_f32).astype(np.float32)
+    vi = rng.standard_normal(layout.row_i64).astype(np.float32)
+    v = (torch.from_numpy(vf).to(DEV), torch.from_numpy(vi).to(DEV))
+    dv, dd, vv = rnd.entry_stats(range(k), v=v)
+    e_dv, e_dd, e_vv = ref.entry_stats_fp64(layout.entries, bf, bi, xs_f, xs_i, vf, vi)
+    np.testing.assert_allclose(dd, e_dd, rtol=1e-12, atol=1e-300)
+    np.testing.assert_allclose(dv, e_dv, rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(vv, e_vv, rtol=1e-12, atol=1e-300)
+    assert dd[:, [i for i, e in enumerate(layout.entries) if e.numel == 0]].sum() == 0
+    # without v: the d.d rows only, and the same values
+    none_dv, dd2, none_vv = rnd.entry_stats(range(k))
+    assert none_dv is None and none_vv is None and dd2.tobytes() == dd.tobytes()
+
+
+def test_entry_norms_follow_torch_cpu_order(engine):
+    k = 7
+    layout, rnd, bf, bi, xs_f, xs_i, _ = _random_round(engine, k, 5)
+    got = rnd.entry_norms(range(k))
+    for e_i, e in enumerate(layout.entries):
+        if e.region == "f32":
+            rows = np.stack([np.subtract(x[e.offset:e.offset + e.numel], bf[e.offset:e.offset + e.numel],
+                                         dtype=np.float32) for x in xs_f])
+        else:
+            rows = np.stack([(x[e.offset:e.offset + e.numel] - bi[e.offset:e.offset + e.numel]).astype(np.float32)
+                             for x in xs_i])
+        exp = ref.torch_cpu_norm_f32(rows) if e.numel else np.zeros(k, np.float32)
+        assert got[e_i].tobytes() == exp.tobytes(), e.name
+        if e.numel:  # and the torch op itself, on this host
+            t = torch.from_numpy(rows)
+            assert got[e_i].tolist() == [torch.linalg.norm(-t[i]).item() for i in range(k)], e.name
+
+
+# ------------------------------------------------------------------ hooks vs reference
+def _host(recipe):
+    layout, base, pays, arenas = G.host_state_dicts(recipe)
+    st = recipe.get("staleness", [0] * recipe["k"])
+    updates = [types.SimpleNamespace(client_id=c + 1, report=types.SimpleNamespace(num_samples=recipe["num_samples"][c]),
+                                     payload=p, staleness=st[c]) for c, p in zip(G.order_of(recipe), pays)]
+    return layout, base, pays, arenas, updates
+
+
+def _flat(layout, sd, region):
+    parts = [sd[e.name].reshape(-1).float() for e in layout.entries if e.region == region]
+    return torch.cat(parts).numpy() if parts else np.zeros(0, np.float32)
+
+
+def _hex_matrix(rows):
+    return np.array([[G.hexf(h) for h in row] for row in rows], dtype=np.float32)
+
+
+@pytest.mark.parametrize("name", ["fedatt_lenet5_k6", "fedatt_resnet18_k8"])
+def test_fedatt_algorithm_is_bit_exact(engine, name):
+    from plato_amd.algorithms.fedavg import FedAttAlgorithmMixin
+
+    recipe, exp = CASES[name]["recipe"], CASES[name]["expected"]
+    layout, base, pays, _, _ = _host(recipe)
+
+    class Algorithm(FedAttAlgorithmMixin):
+        aggregation_device = DEV
+
+    alg = Algorithm()
+    alg._plato_amd_engine = engine
+    # the device norms equal the reference's fp32 values
+    rnd = engine.begin(base, recipe["k"])
+    rnd.put_baseline(base)
+    for i, p in enumerate(pays):
+        rnd.put_client(i, p)
+    norms = rnd.entry_norms(range(recipe["k"]))
+    assert norms.view(np.uint32).tolist() == _hex_matrix(exp["fedatt_norms"]).view(np.uint32).tolist()
+    torch.manual_seed(recipe["noise_seed"])
+    updated = asyncio.run(alg.aggregate_weights(base, pays))
+    assert list(updated) == layout.keys()
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+    assert G.sha(ref.trunc_to_int64(_flat(layout, updated, "i64"))) == exp["loaded_i64_sha256"]
+
+
+@pytest.mark.parametrize("name", ["fedadp_lenet5_k6", "fedadp_resnet18_k8"])
+def test_fedadp_server_matches_reference(engine, name):
+    from plato_amd.servers.variants import FedAdpServerMixin
+
+    recipe, exp = CASES[name]["recipe"], CASES[name]["expected"]
+    layout, base, pays, (bf, bi, xs_f, xs_i), updates = _host(recipe)
+
+    class Server(FedAdpServerMixin):
+        aggregation_device = DEV
+        fedadp_lr = 0.01
+
+    server = Server()
+    server._plato_amd_engine = engine
+    server.current_round = recipe["current_round"]
+    server.selected_clients = [c + 1 for c in G.order_of(recipe)]
+    server.local_angles = {int(c): np.float32(float.fromhex(a)) for c, a in recipe.get("local_angles", {}).items()}
+    updated = asyncio.run(server.aggregate_weights(updates, base, pays))
+    # the weights: within the reference's own float32-BLAS error (tests/test_per_entry.py)
+    np.testing.assert_allclose(server.adaptive_weighting, [float.fromhex(h) for h in exp["adaptive_weighting"]],
+                               rtol=2e-3)
+    # the model they give: normwise against the oracle with the reference's weights
+    ref_w = [float.fromhex(h) for h in exp["adaptive_weighting"]]
+    ref_f, _ = ref.fedavg_numpy(bf, bi, xs_f, xs_i, ref_w)
+    got = _flat(layout, updated, "f32").astype(np.float64)
+    assert np.max(np.abs(got - ref_f)) / np.max(np.abs(ref_f)) <= 1e-5
+
+    # global gradient (deltas pass, no baseline) bit-exact; model bit-exact given the reference's weights
+    rnd = engine.begin(base, recipe["k"])
+    rnd.put_baseline(base)
+    for i, p in enumerate(pays):
+        rnd.put_client(i, p)
+    w1 = np.tile(np.asarray([u.report.num_samples for u in updates], dtype=np.float64)
+                 / sum(u.report.num_samples for u in updates), (len(layout.entries), 1))
+    g_f, g_i = rnd.launch_entrywise(w1, add_base=False, device=True)
+    assert G.sha(G.canon(g_f[: layout.n_f32].cpu().numpy())) == exp["global_grads_f32_sha256"]
+    assert G.sha(G.canon(g_i[: layout.n_i64].cpu().numpy())) == exp["global_grads_i64f_sha256"]
+    rnd.launch(ref_w)
+    again = rnd.result()
+    assert G.sha(G.canon(_flat(layout, again, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(ref.trunc_to_int64(_flat(layout, again, "i64"))) == exp["loaded_i64_sha256"]
+
+
+def test_polaris_server_matches_reference(engine):
+    from plato_amd.servers.variants import PolarisServerMixin
+
+    recipe, exp = CASES["polaris_resnet18_k8"]["recipe"], CASES["polaris_resnet18_k8"]["expected"]
+    layout, base, pays, _, updates = _host(recipe)
+
+    class Server(PolarisServerMixin):
+        aggregation_device = DEV
+
+    server = Server()
+    server._plato_amd_engine = engine
+    server.number_of_client = 1024
+    server.unexplored_clients = list(range(1024))
+    server.alpha = 10
+    updated = asyncio.run(server.aggregate_weights(updates, base, pays))
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(ref.trunc_to_int64(_flat(layout, updated, "i64"))) == exp["loaded_i64_sha256"]
+    assert server.total_samples == exp["total_samples"]
+    want = {int(c): float.fromhex(v) for c, v in exp["squared_deltas"].items()}
+    got = {i: float(v) for i, v in enumerate(server.squared_deltas_current_round) if v != 0}
+    assert set(got) == set(want)
+    np.testing.assert_allclose([got[c] for c in sorted(want)], [want[c] for c in sorted(want)], rtol=1e-5)
+    assert sorted(set(range(1024)) - set(server.unexplored_clients)) == sorted(c for c in G.order_of(recipe))
