@@ -179,11 +179,14 @@ def test_fedadp_server_matches_reference(engine, name):
     # the weights: within the reference's own float32-BLAS error (tests/test_per_entry.py)
     np.testing.assert_allclose(server.adaptive_weighting, [float.fromhex(h) for h in exp["adaptive_weighting"]],
                                rtol=2e-3)
-    # the model they give: normwise against the oracle with the reference's weights
+    # the model: bit-exact FedAvg with those weights ...
+    got = _flat(layout, updated, "f32")
+    own_f, _ = ref.fedavg_numpy(bf, bi, xs_f, xs_i, server.adaptive_weighting)
+    assert got.tobytes() == own_f.tobytes()
+    # ... and within 1e-4 normwise of the reference's model (weights 2e-3 apart times deltas ~1e-2)
     ref_w = [float.fromhex(h) for h in exp["adaptive_weighting"]]
     ref_f, _ = ref.fedavg_numpy(bf, bi, xs_f, xs_i, ref_w)
-    got = _flat(layout, updated, "f32").astype(np.float64)
-    assert np.max(np.abs(got - ref_f)) / np.max(np.abs(ref_f)) <= 1e-5
+    assert np.max(np.abs(got.astype(np.float64) - ref_f)) / np.max(np.abs(ref_f)) <= 1e-4
 
     # global gradient (deltas pass, no baseline) bit-exact; model bit-exact given the reference's weights
     rnd = engine.begin(base, recipe["k"])
