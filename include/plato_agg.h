@@ -56,6 +56,9 @@
  *                                 fedadp_server.py:95-99), Polaris' per-client
  *                                 conv-layer squared deltas (examples/
  *                                 client_selection/polaris/polaris_server.py:76-89)
+ *   plato_agg_fedavg_qsgd      <- the model_dequantize_qsgd inbound processor
+ *                                 (plato/processors/model_dequantize_qsgd.py:34-60)
+ *                                 followed by the FedAvg chain, on QSGD payloads
  *   plato_agg_fedavg_entrywise <- weighted sums whose weight depends on the
  *                                 tensor as well as the client: FedAtt's
  *                                 attentive aggregation (fedatt_algorithm.py:44-69)
@@ -257,6 +260,26 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
                               const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64,
                               int n_entries, size_t n_f32, size_t n_i64, float* d_out,
                               hipStream_t stream);
+
+/*
+ * FedAvg over QSGD-coded payloads (one byte per element: bit 7 sign, bits
+ * 0-6 |zeta|; one max_v per (entry, client)), decoded exactly as
+ * model_dequantize_qsgd.py:51-58 does before the FedAvg chain:
+ *   x   = fp32(fp32(fp32(zeta) * max_v[entry * K + i]) / divisor)   (divisor = level - 1)
+ *   d   = x - b   (int64 entries: x - fp32(b)),  t = fp32(d * w_i) [* s_i],  acc += t
+ *   out = fp32(b + acc)     (int64 entries: fp32(b) + acc)
+ * d_codes_* are K device pointers to byte arenas laid out like the fp32 /
+ * int64 regions (element e <-> byte e), 16-byte aligned.  Chunk tables as
+ * for plato_agg_fedavg_entrywise (pieces of <= 4096 elements run one pass).
+ */
+int plato_agg_fedavg_qsgd(const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64, int K,
+                          const float* d_max_v, int n_entries, float divisor,
+                          const float* d_w, const float* d_s,
+                          const plato_agg_chunk* d_chunks_f32, uint32_t n_chunks_f32,
+                          const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64,
+                          const float* d_base_f32, const int64_t* d_base_i64,
+                          float* d_out_f32, float* d_out_i64f, size_t n_f32, size_t n_i64,
+                          hipStream_t stream);
 
 /*
  * Deterministic synthetic payloads for tests and benchmarks (a counter-based

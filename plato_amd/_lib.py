@@ -92,6 +92,12 @@ SIGNATURES = {
         [_c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_void_p,
          ctypes.c_uint32, _c_int, _c_size_t, _c_size_t, _c_void_p, _c_void_p],
     ),
+    "plato_agg_fedavg_qsgd": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_int, _c_void_p, _c_int, _c_float, _c_void_p, _c_void_p, _c_void_p,
+         ctypes.c_uint32, _c_void_p, ctypes.c_uint32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+         _c_size_t, _c_size_t, _c_void_p],
+    ),
     # tuning / benchmarking (include/plato_agg_tune.h)
     "plato_agg_tune_num_variants": (_c_int, []),
     "plato_agg_tune_describe": (

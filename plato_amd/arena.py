@@ -38,11 +38,16 @@ ROW_ALIGN = 64
 # casts every entry to bfloat16.
 CODECS = {"native": (torch.float32, torch.int64), "bf16": (torch.bfloat16, torch.bfloat16),
           # all-fp32 arrays over the model's keys (FedAtt's noise draws)
-          "f32": (torch.float32, torch.float32)}
+          "f32": (torch.float32, torch.float32),
+          # QSGD code bytes (plato_amd.processors.qsgd.QsgdPayload)
+          "qsgd": (torch.uint8, torch.uint8)}
 
 
 def payload_codec(state_dict) -> str:
-    """The codec a payload arrives in (all-bf16 entries -> "bf16")."""
+    """The codec a payload arrives in (all-bf16 entries -> "bf16"; QSGD payloads say so)."""
+    codec = getattr(state_dict, "plato_codec", None)
+    if codec is not None:
+        return codec
     for tensor in state_dict.values():
         return "bf16" if isinstance(tensor, torch.Tensor) and tensor.dtype == torch.bfloat16 else "native"
     return "native"
@@ -135,7 +140,9 @@ class ArenaLayout:
                 raise KeyError(f"{what} is missing {entry.name!r}")
             tensor = state_dict[entry.name]
             want = CODECS[codec][0] if entry.region == F32 else CODECS[codec][1]
-            if tensor.dtype != want or tuple(tensor.shape) != entry.shape:
+            # coded payloads keep flat code bytes and carry the tensor shapes separately
+            shape = tuple(getattr(state_dict, "shapes", {}).get(entry.name, tensor.shape))
+            if tensor.dtype != want or shape != entry.shape or tensor.numel() != entry.numel:
                 raise ValueError(
                     f"{what}[{entry.name!r}] is {tensor.dtype}{tuple(tensor.shape)}, "
                     f"expected {want}{entry.shape}"

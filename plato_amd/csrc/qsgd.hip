@@ -1,0 +1,258 @@
+// qsgd.hip — FedAvg over QSGD-coded client payloads, dequantized in registers
+// (server inbound codecs on the device).
+//
+// Plato's QSGD pair (plato/processors/model_quantize_qsgd.py:95-139,
+// model_dequantize_qsgd.py:34-60) sends one byte per element (bit 7 sign,
+// bits 0-6 |zeta|) plus one fp32 max_v per entry, and the server decodes
+//     x = fp32(fp32(fp32(zeta) * max_v) / (level - 1))
+// before FedAvg.  Here the payload stays one byte per element through PCIe
+// and HBM (client traffic / 4 vs fp32), and each workgroup — one chunk of one
+// entry, so max_v is workgroup-uniform — builds a 256-entry decode table per
+// client in LDS with the exact (IEEE) division, then every element-client is
+// one LDS lookup: the division is paid 256 times per (client, chunk) instead
+// of once per element.  The FedAvg arithmetic after decoding is the same
+// separately rounded chain as fedavg_agg.hip (int64 entries: the decoded fp32
+// value minus fp32(b), as torch promotes fp32 - int64).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "common.h"
+#include "plato_agg.h"
+
+namespace {
+
+using plato_agg_internal::clear_error;
+using plato_agg_internal::set_error;
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const f4 gf4;
+typedef __attribute__((address_space(1))) f4 gf4w;
+typedef __attribute__((address_space(1))) const u4 gu4;
+
+constexpr int kBlock = 256;
+constexpr int kU = 8;       // clients per LDS table batch
+constexpr int kG = 16;      // elements per lane group (one 16-byte code load)
+
+template <class T>
+__device__ __forceinline__ T sld(const T* p, uint64_t i) {
+  return ((__attribute__((address_space(4))) const T*)p)[i];
+}
+
+struct QArgs {
+  const uint8_t* const* cf;   // K code arenas (fp32 region, one byte per element)
+  const uint8_t* const* ci;   // K code arenas (int64 region)
+  const float* mv;            // [n_entries][K] max_v
+  const float* w;             // [K]
+  const float* s;             // [K] or null
+  const plato_agg_chunk* tf;
+  const plato_agg_chunk* ti;
+  const float* base_f;
+  const int64_t* base_i;
+  float* out_f;
+  float* out_if;
+  uint64_t n_f32, n_i64;
+  uint32_t ncf, nci;
+  float divisor;
+  int K;
+};
+
+struct Chunk {
+  uint32_t entry, begin, end;
+};
+
+__device__ __forceinline__ Chunk load_chunk(const plato_agg_chunk* t, uint32_t c, uint64_t n) {
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(t + c);
+  Chunk ch{sld(p, 0), sld(p, 1), sld(p, 2)};
+  if (ch.end > n) ch.end = uint32_t(n);
+  if (ch.begin > ch.end) ch.begin = ch.end;
+  return ch;
+}
+
+// model_dequantize_qsgd.py:51-58: byte -> zeta (sign-magnitude), then the fp32 chain
+__device__ __forceinline__ float decode(uint32_t byte, float max_v, float divisor) {
+  const int z = byte >= 128 ? -int(byte - 128) : int(byte);
+  return (float(z) * max_v) / divisor;
+}
+
+__device__ __forceinline__ float term(float x, float b, float w, float s, bool two) {
+  float t = (x - b) * w;
+  if (two) t = t * s;
+  return t;
+}
+
+template <bool TWO>
+__device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
+  const Chunk ch = load_chunk(a.tf, c, a.n_f32);
+  const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
+  const uint64_t g0 = ch.begin / kG, g1 = (uint64_t(ch.end) + kG - 1) / kG;
+  const int K = a.K;
+  for (uint64_t gp = g0; gp < g1; gp += kBlock) {  // one pass for chunks <= 4096 elements
+    const uint64_t g = gp + threadIdx.x;
+    const bool have = g < g1;
+    const uint64_t e0 = g * kG;
+    const bool full = have && e0 >= ch.begin && e0 + kG <= ch.end;
+    float b[kG], acc[kG];
+#pragma unroll
+    for (int q = 0; q < kG; ++q) {
+      acc[q] = 0.f;
+      b[q] = 0.f;
+    }
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < kG / 4; ++q) {
+        const f4 v = *((gf4*)(a.base_f + e0) + q);
+        b[4 * q] = v.x;
+        b[4 * q + 1] = v.y;
+        b[4 * q + 2] = v.z;
+        b[4 * q + 3] = v.w;
+      }
+    } else if (have) {
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const uint64_t e = e0 + q;
+        if (e >= ch.begin && e < ch.end) b[q] = a.base_f[e];
+      }
+    }
+    for (int i0 = 0; i0 < K; i0 += kU) {
+      const int nu = K - i0 < kU ? K - i0 : kU;
+      __syncthreads();  // previous batch's lookups are done
+      for (int t = threadIdx.x; t < kU * 256; t += kBlock) {
+        const int u = t >> 8;
+        if (u < nu) lut[u][t & 255] = decode(uint32_t(t & 255), sld(mrow, i0 + u), a.divisor);
+      }
+      __syncthreads();
+      if (full) {
+        u4 code[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int i = i0 + u < K ? i0 + u : K - 1;
+          code[u] = __builtin_nontemporal_load((gu4*)(sld(a.cf, i) + e0));
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          if (u < nu) {
+            const float wu = sld(a.w, i0 + u);
+            const float su = TWO ? sld(a.s, i0 + u) : 1.f;
+#pragma unroll
+            for (int q = 0; q < kG; ++q) {
+              const uint32_t word = code[u][q >> 2];
+              const float x = lut[u][(word >> (8 * (q & 3))) & 255u];
+              acc[q] = acc[q] + term(x, b[q], wu, su, TWO);
+            }
+          }
+        }
+      } else if (have) {
+        for (int u = 0; u < nu; ++u) {
+          const uint8_t* p = sld(a.cf, i0 + u);
+          const float wu = sld(a.w, i0 + u);
+          const float su = TWO ? sld(a.s, i0 + u) : 1.f;
+#pragma unroll
+          for (int q = 0; q < kG; ++q) {
+            const uint64_t e = e0 + q;
+            if (e >= ch.begin && e < ch.end) acc[q] = acc[q] + term(lut[u][p[e]], b[q], wu, su, TWO);
+          }
+        }
+      }
+    }
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < kG / 4; ++q) {
+        const f4 v = f4{b[4 * q] + acc[4 * q], b[4 * q + 1] + acc[4 * q + 1], b[4 * q + 2] + acc[4 * q + 2],
+                        b[4 * q + 3] + acc[4 * q + 3]};
+        __builtin_nontemporal_store(v, (gf4w*)(a.out_f + e0) + q);
+      }
+    } else if (have) {
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const uint64_t e = e0 + q;
+        if (e >= ch.begin && e < ch.end) a.out_f[e] = b[q] + acc[q];
+      }
+    }
+  }
+}
+
+template <bool TWO>
+__device__ void qsgd_i64_chunk(const QArgs& a, uint32_t cc) {
+  const Chunk ch = load_chunk(a.ti, cc, a.n_i64);
+  const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
+  for (uint64_t e = ch.begin + threadIdx.x; e < ch.end; e += kBlock) {
+    // fp32 payload - int64 baseline promotes the baseline to fp32 (algorithms/fedavg.py:23)
+    const float b = (float)a.base_i[e];
+    float acc = 0.f;
+    for (int i = 0; i < a.K; ++i) {
+      const float x = decode(sld(a.ci, i)[e], sld(mrow, i), a.divisor);
+      acc = acc + term(x, b, sld(a.w, i), TWO ? sld(a.s, i) : 1.f, TWO);
+    }
+    a.out_if[e] = b + acc;
+  }
+}
+
+template <bool TWO>
+__global__ __launch_bounds__(kBlock) void fedavg_qsgd_kernel(QArgs a) {
+  __shared__ float lut[kU][256];
+  const uint32_t c = blockIdx.x;
+  if (c < a.ncf) {
+    qsgd_f32_chunk<TWO>(a, c, lut);
+  } else {
+    qsgd_i64_chunk<TWO>(a, c - a.ncf);
+  }
+}
+
+bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
+
+}  // namespace
+
+extern "C" {
+
+int plato_agg_fedavg_qsgd(const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64, int K,
+                          const float* d_max_v, int n_entries, float divisor, const float* d_w, const float* d_s,
+                          const plato_agg_chunk* d_chunks_f32, uint32_t n_chunks_f32,
+                          const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64, const float* d_base_f32,
+                          const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
+                          size_t n_i64, hipStream_t stream) {
+  if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
+  if (n_entries <= 0 || !d_max_v || !d_w) return set_error(PLATO_AGG_EINVAL, "null max_v / weight table");
+  if (!(divisor != 0.f)) return set_error(PLATO_AGG_EINVAL, "divisor (quantization_level - 1) must be non-zero");
+  if (n_chunks_f32 && (!d_codes_f32 || !d_chunks_f32 || !d_base_f32 || !d_out_f32))
+    return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
+  if (n_chunks_i64 && (!d_codes_i64 || !d_chunks_i64 || !d_base_i64 || !d_out_i64f))
+    return set_error(PLATO_AGG_EINVAL, "null int64 pointer");
+  if (misaligned(d_base_f32) || misaligned(d_out_f32))
+    return set_error(PLATO_AGG_EINVAL, "fp32 baseline / output must be 16-byte aligned");
+  if (n_f32 > 0xffffffffull || n_i64 > 0xffffffffull)
+    return set_error(PLATO_AGG_EINVAL, "arena too large for 32-bit chunk offsets");
+  const uint64_t nc = uint64_t(n_chunks_f32) + n_chunks_i64;
+  if (nc == 0) return clear_error();
+  if (nc > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "bad chunk count");
+  QArgs a{};
+  a.cf = d_codes_f32;
+  a.ci = d_codes_i64;
+  a.mv = d_max_v;
+  a.w = d_w;
+  a.s = d_s;
+  a.tf = d_chunks_f32;
+  a.ti = d_chunks_i64;
+  a.base_f = d_base_f32;
+  a.base_i = d_base_i64;
+  a.out_f = d_out_f32;
+  a.out_if = d_out_i64f;
+  a.n_f32 = n_f32;
+  a.n_i64 = n_i64;
+  a.ncf = n_chunks_f32;
+  a.nci = n_chunks_i64;
+  a.divisor = divisor;
+  a.K = K;
+  if (d_s) {
+    hipLaunchKernelGGL(fedavg_qsgd_kernel<true>, dim3(uint32_t(nc)), dim3(kBlock), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(fedavg_qsgd_kernel<false>, dim3(uint32_t(nc)), dim3(kBlock), 0, stream, a);
+  }
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(PLATO_AGG_EHIP, std::string("fedavg_qsgd launch: ") + hipGetErrorString(err));
+  return clear_error();
+}
+
+}  // extern "C"

@@ -224,6 +224,7 @@ class FedAvgEngine:
 
     # per-entry kernels: chunk capacity (elements) per workgroup
     STATS_CHUNK = 4096      # entry_stats: 256 lanes x 4 float4 groups
+    QSGD_CHUNK = 4096       # fedavg_qsgd: 256 lanes x 16 one-byte codes
     ENTRYWISE_CHUNK = 1024  # fedavg_entrywise: 256 lanes x 1 float4 group
 
     def _chunks(self, layout: ArenaLayout, cap: int):
@@ -483,6 +484,9 @@ class AggregationRound:
         # per slot: device pointers of its fp32 / int64 rows (round slab or an arrival slot)
         self._pf = [0] * capacity
         self._pi = [0] * capacity
+        # QSGD codec: per slot max_v per entry (layout order) and the clients' quantization level
+        self._mv: list = [None] * capacity
+        self._level: int | None = None
         self.has_baseline = False
         self.event: torch.cuda.Event | None = None
         self._out = None
@@ -498,10 +502,20 @@ class AggregationRound:
         if not 0 <= slot < self.capacity:
             raise IndexError(f"slot {slot} outside [0, {self.capacity})")
         self.layout.check_compatible(payload, f"{what}[{slot}]", self.codec)
+        self._coded_scales(slot, payload)
         self.stager.put(payload, self.slab.f32[slot], self.slab.i64[slot])
         pf, pi = self.slab.row_pointers([slot])
         self._pf[slot], self._pi[slot] = int(pf[0]), int(pi[0])
         self.staged[slot] = True
+
+    def _coded_scales(self, slot: int, payload) -> None:
+        if self.codec != "qsgd":
+            return
+        level = int(payload.level)
+        if self._level is not None and level != self._level:
+            raise ValueError(f"QSGD payloads of one round must share quantization_level ({level} != {self._level})")
+        self._level = level
+        self._mv[slot] = payload.max_v_array(self.layout.keys())
 
     def adopt(self, slot: int, payload: Mapping[str, torch.Tensor]) -> bool:
         """Use ``payload``'s copy already staged at arrival (``FedAvgEngine.prestage``), if any.
@@ -514,6 +528,7 @@ class AggregationRound:
         hit = self.engine._arrival_rows(payload, self.layout, self.codec)
         if hit is None:
             return False
+        self._coded_scales(slot, payload)
         self._pf[slot], self._pi[slot] = hit
         self.staged[slot] = True
         return True
@@ -530,7 +545,7 @@ class AggregationRound:
         if not deltas and not self.has_baseline:
             raise ValueError("baseline not staged")
         if deltas and self.codec != "native":
-            raise ValueError("deltas are fp32 (x - b promotes bf16 payloads); use the native codec")
+            raise ValueError("deltas are fp32 (x - b promotes coded payloads); use the native codec")
         eng = self.engine
         lay = self.layout
         w, s = eng._upload_weights(weights, scales)
@@ -541,7 +556,17 @@ class AggregationRound:
         self.stager.fence(stream)
         out_f = torch.empty(lay.row_f32, dtype=torch.float32, device=eng.device)
         out_i = torch.empty(lay.row_i64, dtype=torch.float32, device=eng.device)
-        if self.codec == "bf16":
+        if self.codec == "qsgd":
+            n_i = lay.n_i64
+            mv = torch.from_numpy(np.ascontiguousarray(np.stack([self._mv[i] for i in order], axis=1))).to(eng.device)
+            cf, ci = eng._chunks(lay, eng.QSGD_CHUNK)
+            ncf, nci = int(cf.shape[0]), int(ci.shape[0])
+            _lib.call("plato_agg_fedavg_qsgd", _ptr(tf), _ptr(ti) if n_i else None, len(order), _ptr(mv),
+                      len(lay.entries), float(self._level - 1), _ptr(w), _ptr(s), _ptr(cf), ncf,
+                      _ptr(ci) if nci else None, nci, _ptr(eng._base.f32), _ptr(eng._base.i64) if n_i else None,
+                      _ptr(out_f), _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
+            w = (w, mv)
+        elif self.codec == "bf16":
             n_i = lay.n_i64
             _lib.call("plato_agg_fedavg_weights_bf16", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w), _ptr(s),
                       len(order), _ptr(eng._base.f32), _ptr(eng._base.i64) if n_i else None, _ptr(out_f),

@@ -276,6 +276,17 @@ def run_case(case):
         q = model_quantize.Processor(client_id=1)
         dq = model_dequantize.Processor(server_id=0)
         payloads = [dq.process(q.process(p)) for p in payloads]
+    if case.get("codec") == "qsgd":
+        # QSGD wire payloads (oracle/qsgd.py, the format of model_quantize_qsgd.py:130-139)
+        # decoded by the reference's own server-side processor
+        from plato.processors import model_dequantize_qsgd
+
+        from oracle import qsgd
+
+        ents = [types.SimpleNamespace(name=n, region=r, offset=o, numel=c, shape=tuple(s))
+                for n, r, o, c, s in entries]
+        dq = model_dequantize_qsgd.Processor(server_id=0)
+        payloads = [dq.process(qsgd.client_wire(ents, seed, c)[0]) for c in range(k)]
     order = case.get("order", list(range(k)))
     staleness = case.get("staleness", [0] * k)
     mode = case.get("mode", "fedavg")
@@ -491,6 +502,10 @@ def cases():
              num_samples=synth.num_samples(8, 22), order=[3, 0, 7, 1, 2, 6, 4, 5]),
         dict(name="polaris_resnet18_k8", model="resnet18", k=8, seed=23, mode="polaris",
              num_samples=synth.num_samples(8, 23), order=[2, 0, 5, 7, 1, 3, 6, 4]),
+        dict(name="qsgd_codec_lenet5_k6", model="lenet5", k=6, seed=24, codec="qsgd",
+             num_samples=synth.num_samples(6, 24), full=True),
+        dict(name="qsgd_codec_resnet18_k3", model="resnet18", k=3, seed=25, codec="qsgd",
+             num_samples=synth.num_samples(3, 25), order=[2, 0, 1]),
         dict(name="C4_port_resnet18_k256", model="resnet18", k=256, seed=13, mode="port",
              num_samples=synth.num_samples(256, 13), staleness=[(7 * i) % 11 for i in range(256)]),
     ]

@@ -57,6 +57,13 @@ def _inputs(recipe):
     if recipe.get("codec") == "bf16":
         xs_f = [ref.bf16_roundtrip(x) for x in xs_f]
         xs_i = [ref.bf16_roundtrip(x) for x in xs_i]
+    if recipe.get("codec") == "qsgd":
+        from oracle import qsgd
+
+        deq = [qsgd.dequantize_regions(layout.entries, *qsgd.client_wire(layout.entries, seed, c)[1:])
+               for c in range(k)]
+        xs_f = [d[0] for d in deq]
+        xs_i = [d[1] for d in deq]
     order = G.order_of(recipe)
     return layout, bf, bi, [xs_f[c] for c in order], [xs_i[c] for c in order]
 
