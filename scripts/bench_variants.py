@@ -1,0 +1,137 @@
+"""Timing of the variant kernels on C2-sized inputs (K ResNet-18 client updates in HBM).
+
+One JSON line per kernel: median ms over R repetitions (HIP events on the
+launch stream), algorithmic bytes, GB/s and fraction of the 8 TB/s peak.
+
+* qsgd        plato_agg_fedavg_qsgd: K x 1 B codes + fp32 baseline read + result write
+* entrywise   plato_agg_fedavg_entrywise (FedAtt's sum, noise + baseline): K x 4 B + 3 x 4 B
+* stats       plato_agg_entry_stats with v (FedAdp): K x 4 B + 2 x 4 B
+* norms       plato_agg_entry_norms_f32 (FedAtt, torch CPU order): K x 4 B + 4 B; a serial
+              fma chain per (client, entry, lane) — latency-bound by the largest entry
+* fedavg      the FedAvg kernel itself, for reference
+
+Usage: python scripts/bench_variants.py [--clients 128] [--reps 10]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+PEAK = 8000.0
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=128)
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--only", default=None)
+    args = ap.parse_args()
+
+    from plato_amd import _lib, workloads
+    from plato_amd.arena import ArenaLayout
+    from plato_amd.engine import ClientSlab, DeviceArena, FedAvgEngine, _ptr
+    from plato_amd.synthetic import fill_baseline, fill_clients
+
+    dev = torch.device("cuda", 0)
+    k = args.clients
+    layout = ArenaLayout.from_shapes(workloads.resnet(18, 10))
+    engine = FedAvgEngine(dev)
+    base = DeviceArena(layout, dev)
+    slab = ClientSlab(layout, k, dev)
+    fill_baseline(base, 0)
+    fill_clients(slab, base, 0, k)
+    stream = torch.cuda.current_stream(dev)
+    h = stream.cuda_stream
+    pf, pi = slab.row_pointers(range(k))
+    tf = torch.from_numpy(pf).to(dev)
+    ti = torch.from_numpy(pi).to(dev)
+    n_f, n_i, n_e = layout.n_f32, layout.n_i64, len(layout.entries)
+    out_f = torch.empty(layout.row_f32, device=dev)
+    out_i = torch.empty(layout.row_i64, device=dev)
+    w = torch.full((k,), 1.0 / k, device=dev)
+    w_ek = torch.full((n_e, k), -1.0 / k, device=dev)
+    noise = torch.randn(layout.row_f32, device=dev)
+    noise_i = torch.randn(layout.row_i64, device=dev)
+
+    def chunks(cap):
+        return engine._chunks(layout, cap)
+
+    # QSGD codes: random bytes (every sign / magnitude), one max_v per (entry, client)
+    qslab = ClientSlab(layout, k, dev, codec="qsgd")
+    qslab.f32.copy_(torch.randint(0, 256, qslab.f32.shape, dtype=torch.uint8, device=dev))
+    qslab.i64.copy_(torch.randint(0, 256, qslab.i64.shape, dtype=torch.uint8, device=dev))
+    qpf, qpi = qslab.row_pointers(range(k))
+    qtf = torch.from_numpy(qpf).to(dev)
+    qti = torch.from_numpy(qpi).to(dev)
+    max_v = torch.rand((n_e, k), device=dev) * 0.1 + 0.01
+    ws_stats = torch.empty((engine.lib.plato_agg_entry_stats_workspace(k, int(sum(t.shape[0] for t in chunks(4096))))
+                            + 7) // 8, dtype=torch.float64, device=dev)
+    stats_out = torch.empty((2 * k + 1) * n_e, dtype=torch.float64, device=dev)
+    norms_out = torch.empty(k * n_e, dtype=torch.float32, device=dev)
+
+    def run_qsgd():
+        cf, ci = chunks(engine.QSGD_CHUNK)
+        _lib.call("plato_agg_fedavg_qsgd", _ptr(qtf), _ptr(qti), k, _ptr(max_v), n_e, 63.0, _ptr(w), None,
+                  _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(out_f),
+                  _ptr(out_i), n_f, n_i, h)
+
+    def run_entrywise():
+        cf, ci = chunks(engine.ENTRYWISE_CHUNK)
+        _lib.call("plato_agg_fedavg_entrywise", _ptr(tf), _ptr(ti), k, _ptr(w_ek), n_e, _ptr(cf), cf.shape[0],
+                  _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(noise), _ptr(noise_i), -1.2, 0.001,
+                  _lib.PLATO_AGG_ADD_BASE, _ptr(out_f), _ptr(out_i), n_f, n_i, h)
+
+    def run_stats():
+        cf, ci = chunks(engine.STATS_CHUNK)
+        _lib.call("plato_agg_entry_stats", _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64), _ptr(out_f),
+                  _ptr(out_i), _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], n_e, n_f, n_i, _ptr(ws_stats),
+                  _ptr(stats_out), h)
+
+    def run_norms():
+        ef, ei = chunks(1 << 32)
+        _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64), _ptr(ef),
+                  ef.shape[0], _ptr(ei), ei.shape[0], n_e, n_f, n_i, _ptr(norms_out), h)
+
+    def run_fedavg():
+        engine.launch_fedavg(layout, tf, ti, w, None, k, base.f32, base.i64, out_f, out_i, stream)
+
+    kernels = {
+        "qsgd": (run_qsgd, k * (n_f + n_i) + n_f * 8 + n_i * 12),
+        "entrywise": (run_entrywise, (k + 3) * n_f * 4 + (k + 2) * n_i * 8),
+        "stats": (run_stats, (k + 2) * n_f * 4 + (k + 1) * n_i * 8),
+        "norms": (run_norms, (k + 1) * n_f * 4 + (k + 1) * n_i * 8),
+        "fedavg": (run_fedavg, layout.algorithmic_bytes(k)),
+    }
+    for name, (fn, nbytes) in kernels.items():
+        if args.only and name not in args.only.split(","):
+            continue
+        fn()
+        torch.cuda.synchronize(dev)
+        times = []
+        for _ in range(args.reps):
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            fn()
+            e1.record(stream)
+            e1.synchronize()
+            times.append(e0.elapsed_time(e1))
+        med = statistics.median(times)
+        gbs = nbytes / (med * 1e-3) / 1e9
+        print(json.dumps({"kernel": name, "clients": k, "ms_median": round(med, 4), "ms_min": round(min(times), 4),
+                          "algorithmic_bytes": int(nbytes), "GBps": round(gbs, 1),
+                          "frac_of_8TBps": round(gbs / PEAK, 4)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

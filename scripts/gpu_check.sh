@@ -26,6 +26,7 @@ for step in "$@"; do
     dist2c3) run bench_dist2_c3 600 env PLATO_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --config C3 --clients 256 --steps 5 --warmup 2 ;;
     bf16) run bench_bf16 600 python bench.py --codec bf16 --steps 20 ;;
     bf16sweep) run sweep_bf16 600 python bench.py --codec bf16 --sweep --steps 10 ;;
+    variants) run bench_variants 600 python scripts/bench_variants.py ;;
     configs) for c in C1 C3 C4 C5 C5-gpt2; do run bench_$c 600 python bench.py --config $c --steps 10 --warmup 3; done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
