@@ -125,11 +125,11 @@ __device__ __forceinline__ double masked_dot(f4 p, f4 q, const bool (&m)[4]) {
   return s;
 }
 
-template <bool HAS_BASE, bool HAS_V>
-__device__ void stats_f32_chunk(const StatArgs& a, uint32_t c) {
-  __shared__ double red[kWaves][2 * kSU + 1];
-  __shared__ double tot[2 * kSU + 1];
-  const Chunk ch = load_chunk(a.cf, c, a.n_f32);
+// TAIL: the chunk reaches the arena's last, partial float4 group (scalar loads
+// there); every other chunk loads whole groups unconditionally.
+template <bool HAS_BASE, bool HAS_V, bool TAIL>
+__device__ void stats_f32_chunk(const StatArgs& a, uint32_t c, const Chunk ch, double (*red)[2 * kSU + 1],
+                                double* tot) {
   const uint64_t n4 = a.n_f32 / 4;  // groups with 4 in-range elements
   const uint64_t g0 = ch.begin / 4, g1 = (uint64_t(ch.end) + 3) / 4;
   const int K = a.K;
@@ -147,7 +147,7 @@ __device__ void stats_f32_chunk(const StatArgs& a, uint32_t c) {
       const uint64_t gg = gp + threadIdx.x + uint64_t(j) * kBlock;
       const bool in = gg < g1;
       g[j] = in ? gg : (g1 > g0 ? g1 - 1 : g0);
-      vec[j] = g[j] < n4;
+      vec[j] = !TAIL || g[j] < n4;
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const uint64_t e = 4 * gg + q;
@@ -226,9 +226,7 @@ __device__ void stats_f32_chunk(const StatArgs& a, uint32_t c) {
 }
 
 template <bool HAS_BASE, bool HAS_V>
-__device__ void stats_i64_chunk(const StatArgs& a, uint32_t cc) {
-  __shared__ double red[kWaves][2 * kSU + 1];
-  __shared__ double tot[2 * kSU + 1];
+__device__ void stats_i64_chunk(const StatArgs& a, uint32_t cc, double (*red)[2 * kSU + 1], double* tot) {
   const Chunk ch = load_chunk(a.ci, cc, a.n_i64);
   const uint32_t c = a.ncf + cc;
   const int K = a.K;
@@ -266,11 +264,18 @@ __device__ void stats_i64_chunk(const StatArgs& a, uint32_t cc) {
 
 template <bool HAS_BASE, bool HAS_V>
 __global__ __launch_bounds__(kBlock) void entry_stats_partial(StatArgs a) {
+  __shared__ double red[kWaves][2 * kSU + 1];
+  __shared__ double tot[2 * kSU + 1];
   const uint32_t c = blockIdx.x;
   if (c < a.ncf) {
-    stats_f32_chunk<HAS_BASE, HAS_V>(a, c);
+    const Chunk ch = load_chunk(a.cf, c, a.n_f32);
+    if ((uint64_t(ch.end) + 3) / 4 > a.n_f32 / 4) {
+      stats_f32_chunk<HAS_BASE, HAS_V, true>(a, c, ch, red, tot);
+    } else {
+      stats_f32_chunk<HAS_BASE, HAS_V, false>(a, c, ch, red, tot);
+    }
   } else {
-    stats_i64_chunk<HAS_BASE, HAS_V>(a, c - a.ncf);
+    stats_i64_chunk<HAS_BASE, HAS_V>(a, c - a.ncf, red, tot);
   }
 }
 
