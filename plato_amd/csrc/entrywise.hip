@@ -431,13 +431,23 @@ __global__ __launch_bounds__(kBlock) void fedavg_entrywise_kernel(EwArgs a) {
 // computes it on the CPU (ATen's vectorised last-dim 2-norm reduction, the
 // path a contiguous whole-tensor norm takes): 8 fp32 lanes, lane j
 // accumulating fma(v, v, acc_j) over elements j, j+8, ... of the first
-// n - n%8 elements; then acc_0 + acc_1 + ... + acc_7 in order, the tail
+// m = n - n%8 elements; then acc_0 + acc_1 + ... + acc_7 in order, the tail
 // elements fma'd onto that, and an fp32 sqrt.  Reproducing the order makes
-// FedAtt's attention (fedatt_algorithm.py:39) bit-exact; it is a serial
-// chain of n/8 fmas per lane, so one thread per (client, entry, lane), eight
-// clients of one entry per wavefront.
+// FedAtt's attention (fedatt_algorithm.py:39) bit-exact.
+//
+// Each chain is serial (m/8 dependent fmas), so the kernel is built for
+// bytes in flight per chain: ONE wavefront per (entry, client).  All 64 lanes
+// load the delta coalesced, kNR elements each per tile (lane L, register r
+// holds element 64r + L), prefetching the next tile while the current one is
+// consumed; step s = 8r + q of chain j needs element 64r + 8q + j, which lane
+// 8q + j holds in register r, so it arrives by one cross-lane read
+// (ds_bpermute) per step.  Lanes j, j+8, ... run chain j redundantly; lane
+// j < 8 is the one that counts.  Elements past m are fed as +0 (acc + 0*0
+// leaves a non-negative acc unchanged).
 // ---------------------------------------------------------------------------
 constexpr int kNormLanes = 8;
+constexpr int kNR = 32;                 // elements per lane per tile
+constexpr int kNTile = 64 * kNR;        // 2048 elements per tile
 
 struct NormArgs {
   const float* const* xf;
@@ -452,71 +462,69 @@ struct NormArgs {
   int K;
 };
 
+template <bool HAS_BASE, bool I64>
+__device__ __forceinline__ float norm_delta(const NormArgs& a, int i, uint64_t e) {
+  if constexpr (I64) {
+    return i64_delta(a.xi[i], HAS_BASE ? a.base_i : nullptr, e);
+  } else {
+    const float x = __builtin_nontemporal_load(((__attribute__((address_space(1))) const float*)a.xf[i]) + e);
+    return HAS_BASE ? x - a.base_f[e] : x;
+  }
+}
+
+template <bool HAS_BASE, bool I64>
+__device__ void norm_pair(const NormArgs& a, const Chunk ch, int i, int lane) {
+  const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+  const int j = lane & (kNormLanes - 1);
+  float acc = 0.f;
+  float cur[kNR], nxt[kNR];
+  auto load_tile = [&](uint64_t t0, float (&dst)[kNR]) {
+    // clamp the address, zero the value: no branch around the loads (m > 0 here)
+#pragma unroll
+    for (int r = 0; r < kNR; ++r) {
+      const uint64_t off = t0 + uint64_t(r) * 64 + lane;
+      const float v = norm_delta<HAS_BASE, I64>(a, i, ch.begin + (off < m ? off : m - 1));
+      dst[r] = off < m ? v : 0.f;
+    }
+  };
+  if (m) load_tile(0, cur);
+  for (uint64_t t0 = 0; t0 < m; t0 += kNTile) {
+    if (t0 + kNTile < m) load_tile(t0 + kNTile, nxt);
+#pragma unroll
+    for (int r = 0; r < kNR; ++r) {
+#pragma unroll
+      for (int q = 0; q < kNormLanes; ++q) {
+        const float v = __shfl(cur[r], q * kNormLanes + j, 64);
+        acc = __builtin_fmaf(v, v, acc);
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < kNR; ++r) cur[r] = nxt[r];
+  }
+  // lanes added in order (ATen's buffer[0] + buffer[1] + ...), then the tail on top
+  float s = __shfl(acc, 0, 64);
+  for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, l, 64);
+  if (lane != 0) return;
+  for (uint64_t e = m; e < n; ++e) {
+    const float v = norm_delta<HAS_BASE, I64>(a, i, ch.begin + e);
+    s = __builtin_fmaf(v, v, s);
+  }
+  if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
+}
+
 template <bool HAS_BASE>
 __global__ __launch_bounds__(kBlock) void entry_norms_kernel(NormArgs a) {
-  const uint64_t t = uint64_t(blockIdx.x) * kBlock + threadIdx.x;
-  const int j = int(t % kNormLanes);
-  const uint64_t pair = t / kNormLanes;  // entry-major: 8 clients of one entry per wave
-  const uint64_t n_pairs = uint64_t(a.nef + a.nei) * a.K;
-  const bool live = pair < n_pairs;
-  const uint32_t ent = live ? uint32_t(pair / a.K) : 0;
-  const int i = live ? int(pair % a.K) : 0;
-  float acc = 0.f;
-  uint32_t entry = 0;
-  if (live && ent < a.nef) {
-    const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
-    entry = ch.entry;
-    const float* x = a.xf[i];
-    const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
-    const uint64_t p0 = uint64_t(ch.begin) + j;
-    uint64_t r = 0;
-    constexpr int kUnroll = 8;
-    for (; r + kUnroll * kNormLanes <= m; r += kUnroll * kNormLanes) {
-      float v[kUnroll];
-#pragma unroll
-      for (int q = 0; q < kUnroll; ++q) {
-        const uint64_t e = p0 + r + uint64_t(q) * kNormLanes;
-        v[q] = HAS_BASE ? x[e] - a.base_f[e] : x[e];
-      }
-#pragma unroll
-      for (int q = 0; q < kUnroll; ++q) acc = __builtin_fmaf(v[q], v[q], acc);
-    }
-    for (; r < m; r += kNormLanes) {
-      const uint64_t e = p0 + r;
-      const float v = HAS_BASE ? x[e] - a.base_f[e] : x[e];
-      acc = __builtin_fmaf(v, v, acc);
-    }
-  } else if (live) {
-    const Chunk ch = load_chunk(a.ei, ent - a.nef, a.n_i64);
-    entry = ch.entry;
-    const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
-    for (uint64_t r = 0; r < m; r += kNormLanes) {
-      const float v = i64_delta(a.xi[i], HAS_BASE ? a.base_i : nullptr, ch.begin + r + j);
-      acc = __builtin_fmaf(v, v, acc);
-    }
-  }
-  // combine the 8 lanes of this (client, entry) in lane order, then the tail
-  // (lane 0, sequentially, as ATen does after its vector loop)
-  float s = __shfl(acc, (threadIdx.x & ~(kNormLanes - 1)), 64);
-  for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, (threadIdx.x & ~(kNormLanes - 1)) + l, 64);
-  if (!live || j != 0) return;
+  // one wavefront per (entry, client), entry-major
+  const uint64_t pair = uint64_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (pair >= uint64_t(a.nef + a.nei) * a.K) return;  // whole wavefronts exit together
+  const uint32_t ent = uint32_t(pair / a.K);
+  const int i = int(pair % a.K);
   if (ent < a.nef) {
-    const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
-    const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
-    const float* x = a.xf[i];
-    for (uint64_t e = ch.begin + m; e < ch.end; ++e) {
-      const float v = HAS_BASE ? x[e] - a.base_f[e] : x[e];
-      s = __builtin_fmaf(v, v, s);
-    }
+    norm_pair<HAS_BASE, false>(a, load_chunk(a.ef, ent, a.n_f32), i, lane);
   } else {
-    const Chunk ch = load_chunk(a.ei, ent - a.nef, a.n_i64);
-    const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
-    for (uint64_t e = ch.begin + m; e < ch.end; ++e) {
-      const float v = i64_delta(a.xi[i], HAS_BASE ? a.base_i : nullptr, e);
-      s = __builtin_fmaf(v, v, s);
-    }
+    norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane);
   }
-  if (entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + entry] = sqrtf(s);
 }
 
 bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
@@ -649,7 +657,7 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
     return set_error(PLATO_AGG_EINVAL, "null int64 pointer");
   if (n_f32 > 0xffffffffull || n_i64 > 0xffffffffull)
     return set_error(PLATO_AGG_EINVAL, "arena too large for 32-bit chunk offsets");
-  const uint64_t threads = (uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K) * kNormLanes;
+  const uint64_t threads = (uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K) * 64;  // a wave per pair
   if (threads == 0) return clear_error();
   if (threads / kBlock + 1 > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "too many (client, entry) pairs");
   NormArgs a{};

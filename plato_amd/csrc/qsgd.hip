@@ -119,9 +119,15 @@ __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
     for (int i0 = 0; i0 < K; i0 += kU) {
       const int nu = K - i0 < kU ? K - i0 : kU;
       __syncthreads();  // previous batch's lookups are done
-      for (int t = threadIdx.x; t < kU * 256; t += kBlock) {
-        const int u = t >> 8;
-        if (u < nu) lut[u][t & 255] = decode(uint32_t(t & 255), sld(mrow, i0 + u), a.divisor);
+      // codes 128 + z decode to exactly -decode(z) (round-to-nearest is sign-symmetric),
+      // except 128 itself: zeta = -0 is the integer 0
+      for (int t = threadIdx.x; t < kU * 128; t += kBlock) {
+        const int u = t >> 7, z = t & 127;
+        if (u < nu) {
+          const float v = decode(uint32_t(z), sld(mrow, i0 + u), a.divisor);
+          lut[u][z] = v;
+          lut[u][z + 128] = z ? -v : v;
+        }
       }
       __syncthreads();
       if (full) {
