@@ -439,11 +439,10 @@ __global__ __launch_bounds__(kBlock) void fedavg_entrywise_kernel(EwArgs a) {
 // bytes in flight per chain: ONE wavefront per (entry, client).  All 64 lanes
 // load the delta coalesced, kNR elements each per tile (lane L, register r
 // holds element 64r + L), prefetching the next tile while the current one is
-// consumed; step s = 8r + q of chain j needs element 64r + 8q + j, which lane
-// 8q + j holds in register r, so it arrives by one cross-lane read
-// (ds_bpermute) per step.  Lanes j, j+8, ... run chain j redundantly; lane
-// j < 8 is the one that counts.  Elements past m are fed as +0 (acc + 0*0
-// leaves a non-negative acc unchanged).
+// consumed.  The tile is transposed through a wave-private LDS region so that
+// chain j's steps are contiguous (32 ds_write_b32 per lane per tile), and
+// lanes 0..7 walk their chain with 16-byte LDS reads, 4 fmas each.  Elements
+// past m are fed as +0 (acc + 0*0 leaves a non-negative acc unchanged).
 // ---------------------------------------------------------------------------
 constexpr int kNormLanes = 8;
 constexpr int kNR = 32;                 // elements per lane per tile
@@ -462,20 +461,27 @@ struct NormArgs {
   int K;
 };
 
+// one client's delta at element e of its region (pointers hoisted by the caller)
 template <bool HAS_BASE, bool I64>
-__device__ __forceinline__ float norm_delta(const NormArgs& a, int i, uint64_t e) {
+__device__ __forceinline__ float norm_delta(const void* x, const void* b, uint64_t e) {
   if constexpr (I64) {
-    return i64_delta(a.xi[i], HAS_BASE ? a.base_i : nullptr, e);
+    return i64_delta((const int64_t*)x, HAS_BASE ? (const int64_t*)b : nullptr, e);
   } else {
-    const float x = __builtin_nontemporal_load(((__attribute__((address_space(1))) const float*)a.xf[i]) + e);
-    return HAS_BASE ? x - a.base_f[e] : x;
+    const float xv = __builtin_nontemporal_load(((__attribute__((address_space(1))) const float*)x) + e);
+    return HAS_BASE ? xv - ((__attribute__((address_space(1))) const float*)b)[e] : xv;
   }
 }
 
+// LDS transpose region of one wavefront: chain j's 256 steps of a tile in row
+// j, rows padded by 8 floats so that both the 64-lane writes and the 8-lane
+// 16-byte reads hit distinct banks.
+constexpr int kNRow = kNTile / kNormLanes + 8;
+
 template <bool HAS_BASE, bool I64>
-__device__ void norm_pair(const NormArgs& a, const Chunk ch, int i, int lane) {
+__device__ void norm_pair(const NormArgs& a, const Chunk ch, int i, int lane, float (*rows)[kNRow]) {
   const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
-  const int j = lane & (kNormLanes - 1);
+  const void* x = I64 ? (const void*)sld(a.xi, i) : (const void*)sld(a.xf, i);
+  const void* b = I64 ? (const void*)a.base_i : (const void*)a.base_f;
   float acc = 0.f;
   float cur[kNR], nxt[kNR];
   auto load_tile = [&](uint64_t t0, float (&dst)[kNR]) {
@@ -483,21 +489,33 @@ __device__ void norm_pair(const NormArgs& a, const Chunk ch, int i, int lane) {
 #pragma unroll
     for (int r = 0; r < kNR; ++r) {
       const uint64_t off = t0 + uint64_t(r) * 64 + lane;
-      const float v = norm_delta<HAS_BASE, I64>(a, i, ch.begin + (off < m ? off : m - 1));
+      const float v = norm_delta<HAS_BASE, I64>(x, b, ch.begin + (off < m ? off : m - 1));
       dst[r] = off < m ? v : 0.f;
     }
   };
   if (m) load_tile(0, cur);
   for (uint64_t t0 = 0; t0 < m; t0 += kNTile) {
+    // element 64r + lane of the tile is step 8r + lane/8 of chain lane%8
+#pragma unroll
+    for (int r = 0; r < kNR; ++r) rows[lane & 7][8 * r + (lane >> 3)] = cur[r];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     if (t0 + kNTile < m) load_tile(t0 + kNTile, nxt);
-#pragma unroll
-    for (int r = 0; r < kNR; ++r) {
-#pragma unroll
-      for (int q = 0; q < kNormLanes; ++q) {
-        const float v = __shfl(cur[r], q * kNormLanes + j, 64);
-        acc = __builtin_fmaf(v, v, acc);
+    if (lane < kNormLanes) {
+      const f4* row = reinterpret_cast<const f4*>(rows[lane]);
+#pragma unroll 8
+      for (int t = 0; t < kNTile / kNormLanes / 4; ++t) {
+        const f4 v = row[t];
+        acc = __builtin_fmaf(v.x, v.x, acc);
+        acc = __builtin_fmaf(v.y, v.y, acc);
+        acc = __builtin_fmaf(v.z, v.z, acc);
+        acc = __builtin_fmaf(v.w, v.w, acc);
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
     for (int r = 0; r < kNR; ++r) cur[r] = nxt[r];
   }
@@ -506,7 +524,7 @@ __device__ void norm_pair(const NormArgs& a, const Chunk ch, int i, int lane) {
   for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, l, 64);
   if (lane != 0) return;
   for (uint64_t e = m; e < n; ++e) {
-    const float v = norm_delta<HAS_BASE, I64>(a, i, ch.begin + e);
+    const float v = norm_delta<HAS_BASE, I64>(x, b, ch.begin + e);
     s = __builtin_fmaf(v, v, s);
   }
   if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
@@ -515,15 +533,17 @@ __device__ void norm_pair(const NormArgs& a, const Chunk ch, int i, int lane) {
 template <bool HAS_BASE>
 __global__ __launch_bounds__(kBlock) void entry_norms_kernel(NormArgs a) {
   // one wavefront per (entry, client), entry-major
-  const uint64_t pair = uint64_t(blockIdx.x) * (kBlock / 64) + (threadIdx.x >> 6);
+  __shared__ __attribute__((aligned(16))) float rows[kBlock / 64][kNormLanes][kNRow];
+  const int wave = threadIdx.x >> 6;
+  const uint64_t pair = uint64_t(blockIdx.x) * (kBlock / 64) + wave;
   const int lane = threadIdx.x & 63;
   if (pair >= uint64_t(a.nef + a.nei) * a.K) return;  // whole wavefronts exit together
   const uint32_t ent = uint32_t(pair / a.K);
   const int i = int(pair % a.K);
   if (ent < a.nef) {
-    norm_pair<HAS_BASE, false>(a, load_chunk(a.ef, ent, a.n_f32), i, lane);
+    norm_pair<HAS_BASE, false>(a, load_chunk(a.ef, ent, a.n_f32), i, lane, rows[wave]);
   } else {
-    norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane);
+    norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows[wave]);
   }
 }
 
