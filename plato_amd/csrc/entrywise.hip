@@ -437,12 +437,12 @@ __global__ __launch_bounds__(kBlock) void fedavg_entrywise_kernel(EwArgs a) {
 //
 // Each chain is serial (m/8 dependent fmas), so the kernel is built for
 // bytes in flight per chain: ONE wavefront per (entry, client).  All 64 lanes
-// load the delta, kNR elements each per tile (lane L, register r holds tile
-// element tile_elem(L, r)), prefetching the next tile while the current one
-// is consumed.  The tile is transposed through a wave-private LDS region so
-// that chain j's steps are contiguous (8 16-byte writes per lane per tile),
-// and lanes 0..7 walk their chain with 16-byte LDS reads, 4 fmas each.
-// Elements past m are fed as +0 (acc + 0*0 leaves a non-negative acc unchanged).
+// load the delta coalesced, kNR elements each per tile (lane L, register r
+// holds element 64r + L), prefetching the next tile while the current one is
+// consumed.  The tile is transposed through a wave-private LDS region so that
+// chain j's steps are contiguous (32 ds_write_b32 per lane per tile), and
+// lanes 0..7 walk their chain with 16-byte LDS reads, 4 fmas each.  Elements
+// past m are fed as +0 (acc + 0*0 leaves a non-negative acc unchanged).
 // ---------------------------------------------------------------------------
 constexpr int kNormLanes = 8;
 constexpr int kNR = 32;                 // elements per lane per tile
@@ -477,14 +477,6 @@ __device__ __forceinline__ float norm_delta(const void* x, const void* b, uint64
 // 16-byte reads hit distinct banks.
 constexpr int kNRow = kNTile / kNormLanes + 8;
 
-// Tile element held by (lane, register r = 4k + t): 256k + 32(lane/8) + 8t + lane%8,
-// i.e. step 32k + 4(lane/8) + t of chain lane%8.  For a fixed r the wavefront
-// loads 8 runs of 8 consecutive floats; per lane, 4 consecutive registers are
-// 4 consecutive steps of one chain (one 16-byte LDS write).
-__device__ __forceinline__ uint64_t tile_elem(int lane, int r) {
-  return uint64_t(256 * (r >> 2) + 32 * (lane >> 3) + 8 * (r & 3) + (lane & 7));
-}
-
 template <bool HAS_BASE, bool I64>
 __device__ void norm_pair(const NormArgs& a, const Chunk ch, int i, int lane, float (*rows)[kNRow]) {
   const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
@@ -496,19 +488,16 @@ __device__ void norm_pair(const NormArgs& a, const Chunk ch, int i, int lane, fl
     // clamp the address, zero the value: no branch around the loads (m > 0 here)
 #pragma unroll
     for (int r = 0; r < kNR; ++r) {
-      const uint64_t off = t0 + tile_elem(lane, r);
+      const uint64_t off = t0 + uint64_t(r) * 64 + lane;
       const float v = norm_delta<HAS_BASE, I64>(x, b, ch.begin + (off < m ? off : m - 1));
       dst[r] = off < m ? v : 0.f;
     }
   };
   if (m) load_tile(0, cur);
   for (uint64_t t0 = 0; t0 < m; t0 += kNTile) {
-    // registers 4k..4k+3 of a lane are 4 consecutive steps of chain lane%8
+    // element 64r + lane of the tile is step 8r + lane/8 of chain lane%8
 #pragma unroll
-    for (int k4 = 0; k4 < kNR / 4; ++k4) {
-      *reinterpret_cast<f4*>(&rows[lane & 7][32 * k4 + 4 * (lane >> 3)]) =
-          f4{cur[4 * k4], cur[4 * k4 + 1], cur[4 * k4 + 2], cur[4 * k4 + 3]};
-    }
+    for (int r = 0; r < kNR; ++r) rows[lane & 7][8 * r + (lane >> 3)] = cur[r];
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
