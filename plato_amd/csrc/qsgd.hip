@@ -32,7 +32,7 @@ typedef __attribute__((address_space(1))) const f4 gf4;
 typedef __attribute__((address_space(1))) f4 gf4w;
 typedef __attribute__((address_space(1))) const u4 gu4;
 
-constexpr int kBlock = 256;
+constexpr int kBlock = 512;  // 8 wavefronts share each decode table (built once per batch)
 constexpr int kU = 8;       // clients per LDS table batch
 constexpr int kG = 16;      // elements per lane group (one 16-byte code load)
 
@@ -89,7 +89,7 @@ __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
   const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
   const uint64_t g0 = ch.begin / kG, g1 = (uint64_t(ch.end) + kG - 1) / kG;
   const int K = a.K;
-  for (uint64_t gp = g0; gp < g1; gp += kBlock) {  // one pass for chunks <= 4096 elements
+  for (uint64_t gp = g0; gp < g1; gp += kBlock) {  // one pass for chunks <= 8192 elements
     const uint64_t g = gp + threadIdx.x;
     const bool have = g < g1;
     const uint64_t e0 = g * kG;
