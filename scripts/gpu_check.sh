@@ -15,10 +15,11 @@ run() {  # run <name> <timeout_s> <cmd...>
   if [ $rc -ge 124 ]; then echo "fatal rc=$rc in $name; stopping"; exit $rc; fi
   return 0
 }
-python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || { cat gpurun_out/build.log; exit 1; }
+# libraries are built in-tree before the call (never on the GPU box)
+for f in plato_amd/libplato_agg.so plato_amd/libplato_ingest.so; do [ -f $f ] || { echo "missing $f"; exit 1; }; done
 for step in "$@"; do
   case $step in
-    tests) run pytest_gpu 900 python -m pytest tests -m gpu -x -q ;;
+    tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     sweep) run sweep 600 python bench.py --sweep --steps 10 --no-cpu-baseline --no-host-inclusive ;;
     bench) run bench 900 python bench.py ;;
