@@ -251,7 +251,10 @@ int plato_agg_fedavg_entrywise(const float* const* d_x_f32, const int64_t* const
  * first n - n%8 elements, lanes added in order, tail fma'd, fp32 sqrt), so
  * the fp32 result equals the reference's bit for bit:
  *   d_out[i * n_entries + entry] = norm(d_i restricted to entry)
- * d_entries_* hold ONE piece per entry (ArenaLayout.chunk_tables(2**32)).
+ * d_entries_* hold ONE piece per entry (ArenaLayout.chunk_tables(2**32)), in
+ * any order: the table order is the dispatch order, and since each norm is one
+ * serial chain, passing the longest entries first shortens the launch (the
+ * engine does, FedAvgEngine._norm_tables).
  * FedAtt: examples/server_aggregation/fedatt/fedatt_algorithm.py:34-39.
  */
 int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,

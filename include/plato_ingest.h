@@ -37,7 +37,10 @@ extern "C" {
 #define PLATO_INGEST_EINVAL (-1)       /* bad argument                          */
 #define PLATO_INGEST_EFORMAT (-3)      /* malformed or truncated pickle         */
 #define PLATO_INGEST_EUNSUPPORTED (-4) /* valid pickle outside the accepted set */
-#define PLATO_INGEST_ECAPACITY (-5)    /* more tensors than the output array    */
+#define PLATO_INGEST_ECAPACITY (-5)    /* more tensors than the output array,
+                                          or a destination buffer too small     */
+#define PLATO_INGEST_ENOCODEC (-6)     /* libzstd.so.1 not available            */
+#define PLATO_INGEST_EUNKNOWNSIZE (-7) /* zstd frame without a content size     */
 
 /* dtype codes (torch storage classes) */
 #define PLATO_DT_F32 0  /* FloatStorage    */
@@ -85,6 +88,35 @@ int plato_ingest_parse(const uint8_t* buf, size_t len, plato_ingest_tensor* out,
  */
 int plato_ingest_gather(const uint8_t* buf, size_t len, const plato_ingest_tensor* t, int n,
                         const uint64_t* dst_byte_offset, uint8_t* dst, size_t dst_len, int threads);
+
+/*
+ * zstd-compressed payloads.  Plato's model_compress outbound processor sends
+ * zstd.compress(pickle.dumps(state_dict), level)
+ * (plato/processors/model_compress.py:25) and the server's model_decompress
+ * inbound processor runs pickle.loads(zstd.decompress(data))
+ * (plato/processors/model_decompress.py:24).  These entry points replace the
+ * zstd.decompress half (the pickle half is plato_ingest_parse / _gather) with
+ * the system libzstd.so.1, bound at first use (dlopen); without it they
+ * return PLATO_INGEST_ENOCODEC.  Standard zstd frames (RFC 8878), one or
+ * several concatenated.
+ */
+/* 1 if libzstd.so.1 could be bound, else 0 (plato_ingest_last_error says why). */
+int plato_ingest_zstd_available(void);
+
+/* Total decompressed size of the frames in [src, src + len), or
+ * PLATO_INGEST_EUNKNOWNSIZE when a frame header omits it, or an error. */
+int64_t plato_ingest_zstd_content_size(const uint8_t* src, size_t len);
+
+/* Decompress into dst (cap bytes); returns the decompressed size or an error
+ * (PLATO_INGEST_ECAPACITY if cap is too small). */
+int64_t plato_ingest_zstd_decompress(const uint8_t* src, size_t len, uint8_t* dst, size_t cap);
+
+/* Worst-case compressed size of len bytes (0 without libzstd). */
+size_t plato_ingest_zstd_bound(size_t len);
+
+/* One zstd frame (with content size) of [src, src + len) at `level`: what the
+ * clients' model_compress sends.  Returns the frame size or an error. */
+int64_t plato_ingest_zstd_compress(const uint8_t* src, size_t len, uint8_t* dst, size_t cap, int level);
 
 #ifdef __cplusplus
 }

@@ -7,6 +7,8 @@
 // Python objects and calls nothing: REDUCE is only accepted for the three
 // whitelisted callables, everything else is rejected.  All reads are bounds
 // checked against [buf, buf + len).
+#include <dlfcn.h>
+
 #include <algorithm>
 #include <atomic>
 #include <condition_variable>
@@ -17,6 +19,7 @@
 #include <memory>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <unordered_map>
 #include <utility>
 #include <vector>
@@ -518,11 +521,208 @@ void copy_strided(const uint8_t* base, const plato_ingest_tensor& t, uint8_t* ds
   }
 }
 
+// ----------------------------------------------------------------- zstd
+// Plato's model_compress / model_decompress processors wrap the pickled
+// payload in zstd frames (python-zstd's compress: a standard frame with the
+// content size in its header).  The codec is the system libzstd.so.1, bound
+// at first use with dlopen, so the library has no link-time dependency on it
+// (parse and gather work without it).  Only stable public entry points of the
+// zstd ABI are used.
+struct ZstdInBuf {
+  const void* src;
+  size_t size;
+  size_t pos;
+};
+struct ZstdOutBuf {
+  void* dst;
+  size_t size;
+  size_t pos;
+};
+
+struct Zstd {
+  size_t (*decompress)(void*, size_t, const void*, size_t) = nullptr;
+  size_t (*compress)(void*, size_t, const void*, size_t, int) = nullptr;
+  size_t (*bound)(size_t) = nullptr;
+  unsigned long long (*find_size)(const void*, size_t) = nullptr;
+  unsigned (*is_error)(size_t) = nullptr;
+  const char* (*error_name)(size_t) = nullptr;
+  void* (*create_dctx)() = nullptr;
+  size_t (*free_dctx)(void*) = nullptr;
+  size_t (*decompress_stream)(void*, ZstdOutBuf*, ZstdInBuf*) = nullptr;
+  std::string load_error;
+
+  static const Zstd& get() {
+    static Zstd* z = load();  // never destroyed: no teardown ordering at exit
+    return *z;
+  }
+
+  bool ok() const { return decompress != nullptr; }
+
+ private:
+  static Zstd* load() {
+    Zstd* z = new Zstd();
+    void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL);
+    if (!h) {
+      const char* e = dlerror();
+      z->load_error = std::string("libzstd.so.1 not loadable: ") + (e ? e : "?");
+      return z;
+    }
+    bool all = true;
+    auto bind = [&](auto& fn, const char* name) {
+      fn = reinterpret_cast<std::remove_reference_t<decltype(fn)>>(dlsym(h, name));
+      if (!fn) all = false;
+    };
+    decltype(z->decompress) d = nullptr;
+    bind(d, "ZSTD_decompress");
+    bind(z->compress, "ZSTD_compress");
+    bind(z->bound, "ZSTD_compressBound");
+    bind(z->find_size, "ZSTD_findDecompressedSize");
+    bind(z->is_error, "ZSTD_isError");
+    bind(z->error_name, "ZSTD_getErrorName");
+    bind(z->create_dctx, "ZSTD_createDCtx");
+    bind(z->free_dctx, "ZSTD_freeDCtx");
+    bind(z->decompress_stream, "ZSTD_decompressStream");
+    if (!all) {
+      z->load_error = "libzstd.so.1 lacks an expected ZSTD_* entry point";
+      return z;
+    }
+    z->decompress = d;  // set last: ok() means every entry point is bound
+    return z;
+  }
+};
+
+constexpr unsigned long long kZstdUnknown = ~0ull;        // ZSTD_CONTENTSIZE_UNKNOWN
+constexpr unsigned long long kZstdSizeError = ~0ull - 1;  // ZSTD_CONTENTSIZE_ERROR
+
+const Zstd* zstd_or_fail() {
+  const Zstd& z = Zstd::get();
+  if (!z.ok()) {
+    g_err = z.load_error;
+    return nullptr;
+  }
+  return &z;
+}
+
+// Frames without a content size (streaming compressors): decode until the
+// input is consumed; the destination must be large enough.
+int64_t zstd_stream(const Zstd& z, const uint8_t* src, size_t len, uint8_t* dst, size_t cap) {
+  void* dctx = z.create_dctx();
+  if (!dctx) {
+    g_err = "ZSTD_createDCtx failed";
+    return PLATO_INGEST_EFORMAT;
+  }
+  ZstdInBuf in{src, len, 0};
+  ZstdOutBuf out{dst, cap, 0};
+  size_t r = 1;
+  int64_t rc = 0;
+  for (;;) {
+    const size_t in0 = in.pos, out0 = out.pos;
+    r = z.decompress_stream(dctx, &out, &in);
+    if (z.is_error(r)) {
+      g_err = std::string("zstd: ") + z.error_name(r);
+      rc = PLATO_INGEST_EFORMAT;
+      break;
+    }
+    if (in.pos == in.size && r == 0) break;  // every frame complete
+    if (out.pos == out.size && (in.pos < in.size || r != 0)) {
+      g_err = "destination too small for the decompressed payload";
+      rc = PLATO_INGEST_ECAPACITY;
+      break;
+    }
+    if (in.pos == in0 && out.pos == out0) {
+      g_err = "truncated zstd frame";
+      rc = PLATO_INGEST_EFORMAT;
+      break;
+    }
+  }
+  z.free_dctx(dctx);
+  if (rc < 0) return rc;
+  g_err.clear();
+  return int64_t(out.pos);
+}
+
 }  // namespace
 
 extern "C" {
 
 const char* plato_ingest_last_error(void) { return g_err.c_str(); }
+
+int plato_ingest_zstd_available(void) { return zstd_or_fail() ? 1 : 0; }
+
+int64_t plato_ingest_zstd_content_size(const uint8_t* src, size_t len) {
+  const Zstd* z = zstd_or_fail();
+  if (!z) return PLATO_INGEST_ENOCODEC;
+  if (!src) {
+    g_err = "bad argument";
+    return PLATO_INGEST_EINVAL;
+  }
+  if (len == 0) {
+    g_err = "empty input: no zstd frame";
+    return PLATO_INGEST_EFORMAT;
+  }
+  const unsigned long long n = z->find_size(src, len);
+  if (n == kZstdUnknown) {
+    g_err = "zstd frame without a content size";
+    return PLATO_INGEST_EUNKNOWNSIZE;
+  }
+  if (n == kZstdSizeError || n > (unsigned long long)INT64_MAX) {
+    g_err = "not a complete sequence of zstd frames";
+    return PLATO_INGEST_EFORMAT;
+  }
+  g_err.clear();
+  return int64_t(n);
+}
+
+int64_t plato_ingest_zstd_decompress(const uint8_t* src, size_t len, uint8_t* dst, size_t cap) {
+  const Zstd* z = zstd_or_fail();
+  if (!z) return PLATO_INGEST_ENOCODEC;
+  if (!src || (cap && !dst)) {
+    g_err = "bad argument";
+    return PLATO_INGEST_EINVAL;
+  }
+  if (len == 0) {
+    g_err = "empty input: no zstd frame";
+    return PLATO_INGEST_EFORMAT;
+  }
+  const unsigned long long n = z->find_size(src, len);
+  if (n == kZstdUnknown) return zstd_stream(*z, src, len, dst, cap);
+  if (n == kZstdSizeError) {
+    g_err = "not a complete sequence of zstd frames";
+    return PLATO_INGEST_EFORMAT;
+  }
+  if (n > cap) {
+    g_err = "destination smaller than the frames' content size";
+    return PLATO_INGEST_ECAPACITY;
+  }
+  const size_t r = z->decompress(dst, cap, src, len);
+  if (z->is_error(r)) {
+    g_err = std::string("zstd: ") + z->error_name(r);
+    return PLATO_INGEST_EFORMAT;
+  }
+  g_err.clear();
+  return int64_t(r);
+}
+
+size_t plato_ingest_zstd_bound(size_t len) {
+  const Zstd* z = zstd_or_fail();
+  return z ? z->bound(len) : 0;
+}
+
+int64_t plato_ingest_zstd_compress(const uint8_t* src, size_t len, uint8_t* dst, size_t cap, int level) {
+  const Zstd* z = zstd_or_fail();
+  if (!z) return PLATO_INGEST_ENOCODEC;
+  if ((len && !src) || !dst) {
+    g_err = "bad argument";
+    return PLATO_INGEST_EINVAL;
+  }
+  const size_t r = z->compress(dst, cap, src, len, level);
+  if (z->is_error(r)) {
+    g_err = std::string("zstd: ") + z->error_name(r);
+    return PLATO_INGEST_ECAPACITY;
+  }
+  g_err.clear();
+  return int64_t(r);
+}
 
 int plato_ingest_parse(const uint8_t* buf, size_t len, plato_ingest_tensor* out, int max_tensors) {
   if (!buf || max_tensors < 0 || (max_tensors > 0 && !out)) {

@@ -238,6 +238,26 @@ class FedAvgEngine:
             layout._cache[key] = hit
         return hit
 
+    def _norm_tables(self, layout: ArenaLayout):
+        """One piece per entry, longest first (``plato_agg_entry_norms_f32``).
+
+        Each (client, entry) norm is one serial fma chain (torch's CPU order),
+        so the launch lasts at least as long as the longest chain; starting the
+        longest entries first lets the short ones fill in behind them instead
+        of delaying them (ResNet's largest convolutions come last in
+        ``state_dict`` order).  The output is indexed by each piece's entry, so
+        the table order changes only the schedule.
+        """
+        key = ("dev_norm_tables", str(self.device))
+        hit = layout._cache.get(key)
+        if hit is None:
+            ef, ei = layout.chunk_tables(1 << 32)
+            ef = ef[np.argsort(-(ef[:, 2].astype(np.int64) - ef[:, 1]), kind="stable")] if len(ef) else ef
+            hit = (torch.from_numpy(np.ascontiguousarray(ef).view(np.int32).copy()).to(self.device),
+                   torch.from_numpy(np.ascontiguousarray(ei).view(np.int32).copy()).to(self.device))
+            layout._cache[key] = hit
+        return hit
+
     def _f32_stager(self) -> "_Stager":
         st = self._stagers.get("f32")
         if st is None:
@@ -647,7 +667,7 @@ class AggregationRound:
             raise ValueError("baseline not staged")
         eng, lay = self.engine, self.layout
         k, n_e = len(slots), len(lay.entries)
-        ef, ei = eng._chunks(lay, 1 << 32)  # one piece per entry
+        ef, ei = eng._norm_tables(lay)  # one piece per entry, longest first
         pf = np.asarray([self._pf[i] for i in slots], dtype=np.int64)
         pi = np.asarray([self._pi[i] for i in slots], dtype=np.int64)
         tf, ti = eng._pointer_tables(pf, pi)

@@ -75,6 +75,16 @@ def lib():
             h.plato_ingest_gather.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(TensorInfo),
                                               ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
                                               ctypes.c_size_t, ctypes.c_int]
+            vp, sz = ctypes.c_void_p, ctypes.c_size_t
+            for name, res, args in (
+                ("plato_ingest_zstd_available", ctypes.c_int, []),
+                ("plato_ingest_zstd_content_size", ctypes.c_int64, [vp, sz]),
+                ("plato_ingest_zstd_decompress", ctypes.c_int64, [vp, sz, vp, sz]),
+                ("plato_ingest_zstd_bound", sz, [sz]),
+                ("plato_ingest_zstd_compress", ctypes.c_int64, [vp, sz, vp, sz, ctypes.c_int]),
+            ):
+                fn = getattr(h, name)
+                fn.restype, fn.argtypes = res, args
             _lib = h
     return _lib
 
@@ -194,6 +204,64 @@ def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: i
     out.arena_f32, out.arena_i64 = f32, i64
     out.layout_signature = layout.signature
     return out
+
+
+EFORMAT, ECAPACITY, ENOCODEC, EUNKNOWNSIZE = -3, -5, -6, -7
+
+
+def zstd_available() -> bool:
+    """True if the system libzstd.so.1 could be bound (model_compress payloads)."""
+    return bool(lib().plato_ingest_zstd_available())
+
+
+def _zstd_error(rc: int, what: str):
+    msg = lib().plato_ingest_last_error().decode(errors="replace")
+    if rc == ENOCODEC:
+        return RuntimeError(f"{what}: {msg}")
+    return IngestError(f"{what} failed ({rc}): {msg}")
+
+
+def zstd_decompress(data) -> np.ndarray:
+    """``zstd.decompress(data)`` (model_decompress.py:24) into a fresh uint8 array."""
+    addr, n, keep = _buffer(data)
+    h = lib()
+    size = h.plato_ingest_zstd_content_size(addr, n)
+    if size == EUNKNOWNSIZE:
+        cap = max(4 * n, 1 << 16)  # streamed frame: grow until it fits
+    elif size < 0:
+        raise _zstd_error(size, "zstd content size")
+    else:
+        cap = size
+    while True:
+        out = np.empty(max(cap, 1), dtype=np.uint8)
+        got = h.plato_ingest_zstd_decompress(addr, n, out.ctypes.data, cap)
+        if got == ECAPACITY and size == EUNKNOWNSIZE:
+            cap *= 4
+            continue
+        if got < 0:
+            raise _zstd_error(got, "zstd decompress")
+        del keep
+        return out[:got]
+
+
+def zstd_compress(data, level: int = 1) -> bytes:
+    """``zstd.compress(data, level)`` (model_compress.py:25): one frame with its content size."""
+    addr, n, keep = _buffer(data)
+    h = lib()
+    cap = h.plato_ingest_zstd_bound(n)
+    if cap == 0:
+        raise _zstd_error(ENOCODEC, "zstd compress")
+    out = np.empty(cap, dtype=np.uint8)
+    got = h.plato_ingest_zstd_compress(addr, n, out.ctypes.data, cap, int(level))
+    if got < 0:
+        raise _zstd_error(got, "zstd compress")
+    del keep
+    return out[:got].tobytes()
+
+
+def loads_compressed(data, layout: ArenaLayout | None = None, pin: bool = False, threads: int = 0):
+    """``pickle.loads(zstd.decompress(data))`` for a compressed ``state_dict``, natively."""
+    return loads(zstd_decompress(data), layout=layout, pin=pin, threads=threads)
 
 
 def load_file(path: str, layout: ArenaLayout | None = None, pin: bool = False) -> OrderedDict:

@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--clients", type=int, default=128)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default=None)
+    ap.add_argument("--qsgd-codes", default="qsgd", choices=["qsgd", "uniform"])
+    ap.add_argument("--norm-order", default="longest", choices=["longest", "layout"],
+                    help="entry order of the norms launch (longest first = the engine's)")
     args = ap.parse_args()
 
     from plato_amd import _lib, workloads
@@ -66,10 +69,24 @@ def main():
     def chunks(cap):
         return engine._chunks(layout, cap)
 
-    # QSGD codes: random bytes (every sign / magnitude), one max_v per (entry, client)
+    # QSGD codes, one max_v per (entry, client).  "qsgd": what the client quantizer
+    # (model_quantize_qsgd.py) makes of normally distributed deltas at level 64,
+    # |zeta| = floor(|x| / max_v * 63 + U[0,1)) with max_v ~ 5 sigma, random sign;
+    # "uniform": every byte equally likely (worst case for the LDS decode tables).
     qslab = ClientSlab(layout, k, dev, codec="qsgd")
-    qslab.f32.copy_(torch.randint(0, 256, qslab.f32.shape, dtype=torch.uint8, device=dev))
-    qslab.i64.copy_(torch.randint(0, 256, qslab.i64.shape, dtype=torch.uint8, device=dev))
+
+    def codes(shape):
+        if args.qsgd_codes == "uniform":
+            return torch.randint(0, 256, shape, dtype=torch.uint8, device=dev)
+        g = torch.Generator(device=dev).manual_seed(1)
+        mag = torch.floor(torch.randn(shape, device=dev, generator=g).abs() * (63 / 5)
+                          + torch.rand(shape, device=dev, generator=g)).clamp_(0, 127)
+        sign = (torch.rand(shape, device=dev, generator=g) < 0.5).to(torch.float32) * 128
+        return (mag + sign).to(torch.uint8)
+
+    for r in range(k):
+        qslab.f32[r].copy_(codes(qslab.f32[r].shape))
+    qslab.i64.copy_(codes(qslab.i64.shape))
     qpf, qpi = qslab.row_pointers(range(k))
     qtf = torch.from_numpy(qpf).to(dev)
     qti = torch.from_numpy(qpi).to(dev)
@@ -98,7 +115,7 @@ def main():
                   _ptr(stats_out), h)
 
     def run_norms():
-        ef, ei = chunks(1 << 32)
+        ef, ei = engine._norm_tables(layout) if args.norm_order == "longest" else chunks(1 << 32)
         _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64), _ptr(ef),
                   ef.shape[0], _ptr(ei), ei.shape[0], n_e, n_f, n_i, _ptr(norms_out), h)
 

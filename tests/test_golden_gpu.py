@@ -288,6 +288,28 @@ def test_wire_ingested_payloads_match_reference(engine):
     assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
 
 
+def test_zstd_compressed_payloads_match_reference(engine):
+    """model_compress'd payloads -> native zstd + pickle ingest (zstd Processor) -> engine: reference digest."""
+    from plato_amd import ingest
+    from plato_amd.processors import zstd as zp
+
+    if not ingest.zstd_available():
+        pytest.skip("libzstd.so.1 absent")
+    case = next(c for c in CASES if c["recipe"]["name"] == "resnet18_k16_permuted")
+    recipe, exp = case["recipe"], case["expected"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    order = G.order_of(recipe)
+    client = zp.CompressProcessor(compression_level=1)
+    wire = [client.process(type(payloads[c])((n, t.clone()) for n, t in payloads[c].items())) for c in order]
+    server = zp.Processor(server_id=0, layout=layout)
+    received = [server.process(w) for w in wire]
+    assert all(isinstance(r, ingest.ArenaStateDict) and r.arena_f32.is_pinned() for r in received)
+    weights, _ = G.weights_for(recipe, W)
+    updated = engine.aggregate_weights(baseline, received, weights)
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+
+
 def _bf16_payloads(recipe):
     layout, baseline, payloads = _host_payloads(recipe)
     # client side: Plato's model_quantize (.to(bfloat16)) of every entry
