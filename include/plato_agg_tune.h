@@ -14,6 +14,8 @@
 #include <stdint.h>
 #include <hip/hip_runtime_api.h>
 
+#include "plato_agg.h"
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -50,6 +52,19 @@ int plato_agg_tune_fedavg_bf16(int variant, const uint16_t* const* d_x_bf16,
  * streaming ceilings of the device next to the FedAvg kernel variants. */
 int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n,
                           int blocks, hipStream_t stream);
+
+/* plato_agg_entry_norms_f32 kernel variants (bitwise identical results):
+ *   0 = LDS-DMA ring, one workgroup per (entry, 2 clients) (default)
+ *   1 = one wavefront per (entry, client), one-tile register prefetch (first version)
+ *   2 = LDS-DMA ring, one workgroup per (entry, 4 clients): the baseline tile shared
+ *   3 = LDS-DMA ring, one single-wave workgroup per (entry, client)
+ *   4, 5 = variant 0 without the fma chains / without the loads: timing probes
+ *          only, their outputs are meaningless */
+int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+                               const float* d_base_f32, const int64_t* d_base_i64,
+                               const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
+                               const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
+                               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream);
 
 #ifdef __cplusplus
 }

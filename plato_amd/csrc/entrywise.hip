@@ -21,6 +21,7 @@
 
 #include "common.h"
 #include "plato_agg.h"
+#include "plato_agg_tune.h"
 
 namespace {
 
@@ -458,6 +459,8 @@ struct NormArgs {
   float* out;                 // [K][n_entries]
   uint64_t n_f32, n_i64;
   uint32_t nef, nei, n_entries;
+  uint32_t ngroups;           // ring kernel: ceil(K / G) client groups per entry
+  uint32_t probe;             // tuning only: bit 0 skips the chains, bit 1 skips the loads
   int K;
 };
 
@@ -544,6 +547,215 @@ __global__ __launch_bounds__(kBlock) void entry_norms_kernel(NormArgs a) {
     norm_pair<HAS_BASE, false>(a, load_chunk(a.ef, ent, a.n_f32), i, lane, rows[wave]);
   } else {
     norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows[wave]);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// entry_norms, ring version (the default): the same chains, fed through an
+// LDS ring by LDS-DMA.
+//
+// The per-wave version above keeps one 8 KiB tile in flight per chain, so the
+// largest ResNet entries (2.36 M elements per client) stream at ~4 GB/s per
+// (entry, client).  Here a workgroup of G waves owns one entry and G clients:
+// every stage holds a tile of the baseline and of the G client arenas (kRT
+// elements each, loaded with global_load_lds_dwordx4: no VGPRs, 1 KiB per
+// wave-instruction, spread over the G waves), kRS stages deep, so kRS - 1
+// stages stay in flight while one is consumed.  Per stage each wave forms
+// d = x - b for its client with all 64 lanes (in place, dwordx4 LDS traffic),
+// then walks its 8 chains over the tile (chain j reads positions j', j'+8, ...:
+// 8 consecutive dwords per step, no bank conflicts; whole tiles run on the
+// full wave, lanes 8..63 duplicating 0..7, because exec-masked fma chains ran
+// up to 2x slower, scripts/micro/fma_chain.hip).  The arithmetic and order
+// are exactly the per-wave version's (same chains, same lane sum, same tail),
+// so results are bitwise identical.  Tiles start on the arena's float4 grid;
+// `delta` = begin mod 4 shifts the chain positions.
+//
+// Measured: the launch is bound by the serial chain of the
+// largest entry (~15 cycles per step with the LDS traffic of the tile), not
+// by HBM; G = 2 is the fastest split.
+// ---------------------------------------------------------------------------
+constexpr int kRT = 1024;             // elements per operand per stage
+constexpr int kRS = 6;                // ring stages
+
+typedef __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(3))) void lvoid;
+
+// s_waitcnt with only vmcnt bounded (gfx9 encoding: vmcnt[3:0] | expcnt[6:4] |
+// lgkmcnt[11:8] | vmcnt[5:4] at [15:14]).
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// G = clients per workgroup (one wave each); stage = baseline tile + G client tiles
+template <int G, bool HAS_BASE>
+struct RingShape {
+  static constexpr int kRG = G;
+  static constexpr int kROps = 1 + G;                    // slots per stage (baseline first)
+  static constexpr int kOps = HAS_BASE ? kROps : kRG;  // operands loaded per stage
+  static constexpr int kChunks = kRT / 256;             // 1 KiB glds per operand
+  static constexpr int kPerWave = kOps * kChunks / G;   // glds per wave per stage
+  static_assert((kOps * kChunks) % G == 0, "stage must split evenly over the waves");
+};
+
+// This wave's glds sources: chunk r of every stage comes from operand
+// (wave + S::kRG * r) / kChunks, a fixed arena per wave (wave-uniform -> SGPRs).
+template <int G, bool HAS_BASE>
+__device__ __forceinline__ void ring_sources(const NormArgs& a, int grp, int wave,
+                                             const float* (&src)[RingShape<G, HAS_BASE>::kPerWave]) {
+  using S = RingShape<G, HAS_BASE>;
+#pragma unroll
+  for (int r = 0; r < S::kPerWave; ++r) {
+    const int o = (wave + S::kRG * r) / S::kChunks;
+    if (HAS_BASE && o == 0) {
+      src[r] = a.base_f;
+    } else {
+      const int i = grp * S::kRG + (HAS_BASE ? o - 1 : o);
+      src[r] = sld(a.xf, i < a.K ? i : a.K - 1);  // dead client slots load a live arena (never read)
+    }
+  }
+}
+
+// Issue this wave's share of one stage (tile starting at float4 group g0) into ring slot `slot`.
+template <int G, bool HAS_BASE>
+__device__ __forceinline__ void ring_issue(const float* const (&src)[RingShape<G, HAS_BASE>::kPerWave], float* ring,
+                                           uint32_t slot, uint64_t g0, uint64_t gmax, int wave, int lane) {
+  using S = RingShape<G, HAS_BASE>;
+#pragma unroll
+  for (int r = 0; r < S::kPerWave; ++r) {
+    const int q = wave + S::kRG * r;
+    const int o = q / S::kChunks, c = q % S::kChunks;
+    uint64_t g = g0 + uint64_t(c) * 64 + lane;
+    g = g < gmax ? g : gmax;
+    float* dst = ring + (slot * S::kROps + o) * kRT + c * 256;
+    __builtin_amdgcn_global_load_lds((gvoid*)(src[r] + 4 * g), (lvoid*)dst, 16, 0, 0);
+  }
+}
+
+template <int G, bool HAS_BASE>
+__device__ void norm_ring(const NormArgs& a, const Chunk ch, int grp, float* ring) {
+  using S = RingShape<G, HAS_BASE>;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  const int i = grp * S::kRG + wave;
+  const bool live = i < a.K;
+  const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+  const uint32_t delta = ch.begin & 3u;
+  const uint64_t g_first = ch.begin >> 2;                      // float4 group of the first element
+  const uint64_t ntiles = (delta + m + kRT - 1) / kRT;
+  const uint64_t gmax = (a.n_f32 >> 2) - 1;                    // last whole float4 group
+  const int op = HAS_BASE ? 1 + wave : wave;                   // this wave's client operand
+  const int pj = int((uint32_t(lane) + delta) & 7u);           // chain lane's position in each 8-block
+  const int64_t s_shift = (uint32_t(lane) + delta) >= 8u ? -1 : 0;
+  const int64_t s_end = int64_t(m / kNormLanes);
+  float acc = 0.f;
+  const float* src[S::kPerWave];
+  ring_sources<G, HAS_BASE>(a, grp, wave, src);
+
+#pragma unroll
+  for (int p = 0; p < kRS - 1; ++p)
+    if (uint64_t(p) < ntiles && !(a.probe & 2)) ring_issue<G, HAS_BASE>(src, ring, p, g_first + uint64_t(p) * (kRT / 4), gmax, wave, lane);
+
+  for (uint64_t tt = 0; tt < ntiles; ++tt) {
+    // stage tt complete for this wave, then for every wave
+    if (tt + kRS - 2 < ntiles) {
+      wait_vmcnt<(kRS - 2) * S::kPerWave>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    // slot (tt - 1) % kRS was consumed by every wave before the barrier
+    if (tt + kRS - 1 < ntiles && !(a.probe & 2))
+      ring_issue<G, HAS_BASE>(src, ring, uint32_t((tt + kRS - 1) % kRS), g_first + (tt + kRS - 1) * (kRT / 4), gmax,
+                           wave, lane);
+    float* col = ring + ((tt % kRS) * S::kROps + op) * kRT;
+    if (HAS_BASE) {
+      // d = x - b over the tile, in place (fp32, as compute_weight_deltas)
+      const float* bcol = ring + ((tt % kRS) * S::kROps) * kRT;
+#pragma unroll
+      for (int r = 0; r < kRT / 256; ++r) {
+        f4* px = reinterpret_cast<f4*>(col) + r * 64 + lane;
+        const f4 x = *px;
+        const f4 b = *(reinterpret_cast<const f4*>(bcol) + r * 64 + lane);
+        *px = x - b;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (a.probe & 1) continue;
+    const int64_t s0 = int64_t(tt) * (kRT / kNormLanes) + s_shift;
+    const float* p = col + pj;
+    if (tt >= 1 && int64_t(tt + 1) * (kRT / kNormLanes) <= s_end) {
+      // Whole tile for every chain (wave-uniform test).  All 64 lanes run the
+      // chain code, lanes 8..63 on copies of lanes 0..7's positions (LDS
+      // broadcast): an exec-masked fma chain ran up to 2x slower on MI355X
+      // than the same chain with the full wave active (scripts/micro/fma_chain.hip).
+      // Blocks of kCB steps, the next block's LDS reads in flight during this block's fmas.
+      constexpr int kCB = 16, kNB = kRT / kNormLanes / kCB;
+      float cur[kCB], nxt[kCB];
+#pragma unroll
+      for (int q = 0; q < kCB; ++q) cur[q] = p[8 * q];
+#pragma unroll
+      for (int blk = 0; blk < kNB; ++blk) {
+        if (blk + 1 < kNB) {
+#pragma unroll
+          for (int q = 0; q < kCB; ++q) nxt[q] = p[8 * (kCB * (blk + 1) + q)];
+        }
+        // keep the reads issued ahead of this block's chain (the scheduler would sink them)
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < kCB; ++q) acc = __builtin_fmaf(cur[q], cur[q], acc);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < kCB; ++q) cur[q] = nxt[q];
+      }
+    } else if (live && lane < kNormLanes) {
+      for (int u = 0; u < kRT / kNormLanes; ++u) {
+        const int64_t st = s0 + u;
+        if (st >= 0 && st < s_end) {
+          const float v = p[8 * u];
+          acc = __builtin_fmaf(v, v, acc);
+        }
+      }
+    }
+  }
+  if (!live) return;
+  // lanes added in order (ATen's buffer[0] + buffer[1] + ...), then the tail on top
+  float s = __shfl(acc, 0, 64);
+  for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, l, 64);
+  if (lane != 0) return;
+  const float* x = sld(a.xf, i);
+  for (uint64_t e = m; e < n; ++e) {
+    const uint64_t idx = ch.begin + e;
+    const float v = HAS_BASE ? x[idx] - a.base_f[idx] : x[idx];
+    s = __builtin_fmaf(v, v, s);
+  }
+  if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
+}
+
+template <int G, bool HAS_BASE>
+__global__ __launch_bounds__(64 * G) void entry_norms_ring_kernel(NormArgs a) {
+  using S = RingShape<G, HAS_BASE>;
+  __shared__ __attribute__((aligned(16))) float ring[kRS * S::kROps * kRT];
+  const uint32_t ng = a.ngroups;
+  const uint64_t blk = blockIdx.x;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  float(*rows)[kNRow] = reinterpret_cast<float(*)[kNRow]>(ring + wave * kNormLanes * kNRow);
+  if (blk < uint64_t(a.nef) * ng) {
+    const Chunk ch = load_chunk(a.ef, uint32_t(blk / ng), a.n_f32);
+    const int grp = int(blk % ng);
+    if (uint64_t(ch.end) > (a.n_f32 & ~3ull)) {
+      // reaches the arena's partial last float4 group: the per-wave path (scalar loads)
+      const int i = grp * S::kRG + wave;
+      if (i < a.K) norm_pair<HAS_BASE, false>(a, ch, i, lane, rows);
+      return;
+    }
+    norm_ring<G, HAS_BASE>(a, ch, grp, ring);
+  } else {
+    const uint64_t j = blk - uint64_t(a.nef) * ng;  // int64 entries: tiny, per-wave path
+    const int i = int(j % ng) * G + wave;
+    if (i < a.K) norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, uint32_t(j / ng), a.n_i64), i, lane, rows);
   }
 }
 
@@ -665,11 +877,14 @@ int plato_agg_fedavg_entrywise(const float* const* d_x_f32, const int64_t* const
   return launch_error("fedavg_entrywise launch");
 }
 
-int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
-                              const float* d_base_f32, const int64_t* d_base_i64,
-                              const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
-                              const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
-                              size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
+}  // extern "C"
+
+namespace {
+int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+              const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_chunk* d_entries_f32,
+              uint32_t n_entries_f32, const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
+              size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
+  if (variant < 0 || variant > 5) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (n_entries <= 0 || !d_out) return set_error(PLATO_AGG_EINVAL, "null output / no entries");
   if (n_entries_f32 && (!d_x_f32 || !d_entries_f32)) return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
@@ -694,13 +909,56 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
   a.nei = n_entries_i64;
   a.n_entries = uint32_t(n_entries);
   a.K = K;
-  const dim3 grid{uint32_t((threads + kBlock - 1) / kBlock)};
-  if (d_base_f32) {
-    hipLaunchKernelGGL(entry_norms_kernel<true>, grid, dim3(kBlock), 0, stream, a);
+  // ring variants: clients (waves) per workgroup (2 measured fastest on MI355X,
+  // DESIGN.md §10); 4 / 5 = variant 0 without the chains / without the loads
+  // (timing probes, wrong results)
+  static const int kGroup[] = {2, 0, 4, 1, 2, 2};
+  const int G = variant == 1 ? 1 : kGroup[variant];
+  a.probe = variant == 4 ? 1u : variant == 5 ? 2u : 0u;
+  a.ngroups = uint32_t((K + G - 1) / G);
+  if (variant == 1) {  // per-wave chains (the first version)
+    const dim3 grid{uint32_t((threads + kBlock - 1) / kBlock)};
+    if (d_base_f32) {
+      hipLaunchKernelGGL(entry_norms_kernel<true>, grid, dim3(kBlock), 0, stream, a);
+    } else {
+      hipLaunchKernelGGL(entry_norms_kernel<false>, grid, dim3(kBlock), 0, stream, a);
+    }
+    return launch_error("entry_norms launch");
+  }
+  const dim3 grid{uint32_t((uint64_t(n_entries_f32) + n_entries_i64) * a.ngroups)};
+  const dim3 block{uint32_t(64 * G)};
+  if (G == 1) {
+    if (d_base_f32) hipLaunchKernelGGL((entry_norms_ring_kernel<1, true>), grid, block, 0, stream, a);
+    else hipLaunchKernelGGL((entry_norms_ring_kernel<1, false>), grid, block, 0, stream, a);
+  } else if (G == 2) {
+    if (d_base_f32) hipLaunchKernelGGL((entry_norms_ring_kernel<2, true>), grid, block, 0, stream, a);
+    else hipLaunchKernelGGL((entry_norms_ring_kernel<2, false>), grid, block, 0, stream, a);
   } else {
-    hipLaunchKernelGGL(entry_norms_kernel<false>, grid, dim3(kBlock), 0, stream, a);
+    if (d_base_f32) hipLaunchKernelGGL((entry_norms_ring_kernel<4, true>), grid, block, 0, stream, a);
+    else hipLaunchKernelGGL((entry_norms_ring_kernel<4, false>), grid, block, 0, stream, a);
   }
   return launch_error("entry_norms launch");
+}
+}  // namespace
+
+extern "C" {
+
+int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+                              const float* d_base_f32, const int64_t* d_base_i64,
+                              const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
+                              const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
+                              size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
+  return run_norms(0, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32, d_entries_i64,
+                   n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
+}
+
+int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+                               const float* d_base_f32, const int64_t* d_base_i64,
+                               const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
+                               const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
+                               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
+  return run_norms(variant, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32,
+                   d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
 }
 
 }  // extern "C"

@@ -36,6 +36,7 @@ def main():
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--only", default=None)
     ap.add_argument("--qsgd-codes", default="qsgd", choices=["qsgd", "uniform"])
+    ap.add_argument("--norm-variants", action="store_true", help="also time each entry_norms kernel variant")
     ap.add_argument("--norm-order", default="longest", choices=["longest", "layout"],
                     help="entry order of the norms launch (longest first = the engine's)")
     args = ap.parse_args()
@@ -114,10 +115,14 @@ def main():
                   _ptr(out_i), _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], n_e, n_f, n_i, _ptr(ws_stats),
                   _ptr(stats_out), h)
 
-    def run_norms():
+    def run_norms(variant=None):
         ef, ei = engine._norm_tables(layout) if args.norm_order == "longest" else chunks(1 << 32)
-        _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64), _ptr(ef),
-                  ef.shape[0], _ptr(ei), ei.shape[0], n_e, n_f, n_i, _ptr(norms_out), h)
+        if variant is None:
+            _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64), _ptr(ef),
+                      ef.shape[0], _ptr(ei), ei.shape[0], n_e, n_f, n_i, _ptr(norms_out), h)
+        else:
+            _lib.call("plato_agg_tune_entry_norms", variant, _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64),
+                      _ptr(ef), ef.shape[0], _ptr(ei), ei.shape[0], n_e, n_f, n_i, _ptr(norms_out), h)
 
     def run_fedavg():
         engine.launch_fedavg(layout, tf, ti, w, None, k, base.f32, base.i64, out_f, out_i, stream)
@@ -129,8 +134,11 @@ def main():
         "norms": (run_norms, (k + 1) * n_f * 4 + (k + 1) * n_i * 8),
         "fedavg": (run_fedavg, layout.algorithmic_bytes(k)),
     }
+    if args.norm_variants:  # tuning: every plato_agg_tune_entry_norms variant
+        for v in range(6):
+            kernels[f"norms_v{v}"] = ((lambda v=v: run_norms(v)), kernels["norms"][1])
     for name, (fn, nbytes) in kernels.items():
-        if args.only and name not in args.only.split(","):
+        if args.only and name.split("_v")[0] not in args.only.split(","):
             continue
         fn()
         torch.cuda.synchronize(dev)

@@ -114,6 +114,54 @@ def test_entry_norms_follow_torch_cpu_order(engine):
             assert got[e_i].tolist() == [torch.linalg.norm(-t[i]).item() for i in range(k)], e.name
 
 
+RING_SPEC = [("a", (5,), "f32"), ("w", (33333,), "f32"), ("n", (), "i64"), ("v", (7,), "f32"),
+             ("u", (160, 128), "f32"), ("t", (9,), "f32"), ("m", (3,), "i64"), ("z", (12290,), "f32")]
+
+
+@pytest.mark.parametrize("k,deltas", [(5, False), (8, False), (3, True)])
+def test_entry_norm_kernels_agree_bitwise(engine, k, deltas):
+    """Ring kernel (default) == per-wave kernel == torch CPU order, across ring wrap-around,
+    unaligned entry starts, client groups with dead slots and both arena tails."""
+    from plato_amd import _lib
+
+    for spec in (RING_SPEC, RING_SPEC[:-1] + [("z", (12291,), "f32")]):  # n_f32 % 4 == 0 / == 3
+        layout = ArenaLayout.from_shapes(spec)
+        rng = np.random.default_rng(k)
+        dev = torch.device(DEV)
+        bf = rng.standard_normal(layout.row_f32).astype(np.float32)
+        bi = rng.integers(-1000, 1000, max(layout.row_i64, 1))
+        xs_f = np.stack([bf + 0.01 * rng.standard_normal(layout.row_f32).astype(np.float32) for _ in range(k)])
+        xs_i = np.stack([bi + rng.integers(0, 9, bi.size) for _ in range(k)])
+        xf = torch.from_numpy(xs_f).to(dev)
+        xi = torch.from_numpy(xs_i).to(dev)
+        tf = torch.tensor([xf[i].data_ptr() for i in range(k)], dtype=torch.int64, device=dev)
+        ti = torch.tensor([xi[i].data_ptr() for i in range(k)], dtype=torch.int64, device=dev)
+        b_f = torch.from_numpy(bf).to(dev)
+        b_i = torch.from_numpy(bi).to(dev)
+        ef, ei = engine._norm_tables(layout)
+        n_e = len(layout.entries)
+        outs = []
+        for variant in range(4):
+            out = torch.full((k * n_e,), float("nan"), device=dev)
+            _lib.call("plato_agg_tune_entry_norms", variant, tf.data_ptr(), ti.data_ptr(), k,
+                      None if deltas else b_f.data_ptr(), None if deltas else b_i.data_ptr(), ef.data_ptr(),
+                      ef.shape[0], ei.data_ptr(), ei.shape[0], n_e, layout.n_f32, layout.n_i64, out.data_ptr(),
+                      torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            outs.append(out.cpu().numpy().reshape(k, n_e))
+        for v in range(1, 4):
+            assert outs[0].tobytes() == outs[v].tobytes(), v
+        for e_i, e in enumerate(layout.entries):
+            if e.region == "f32":
+                rows = xs_f[:, e.offset:e.offset + e.numel]
+                if not deltas:
+                    rows = np.subtract(rows, bf[e.offset:e.offset + e.numel], dtype=np.float32)
+            else:
+                rows = xs_i[:, e.offset:e.offset + e.numel]
+                rows = (rows if deltas else rows - bi[e.offset:e.offset + e.numel]).astype(np.float32)
+            assert outs[0][:, e_i].tobytes() == ref.torch_cpu_norm_f32(np.ascontiguousarray(rows)).tobytes(), e.name
+
+
 # ------------------------------------------------------------------ hooks vs reference
 def _host(recipe):
     layout, base, pays, arenas = G.host_state_dicts(recipe)
