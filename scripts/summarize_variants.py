@@ -15,7 +15,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"qsgd": "fedavg_qsgd_kernel", "entrywise": "fedavg_entrywise_kernel",
-           "stats": "entry_stats_partial", "norms": "entry_norms_kernel", "fedavg": "fedavg_kernel"}
+           "stats": "entry_stats_partial", "norms": "entry_norms", "fedavg": "fedavg_kernel"}
 
 
 def per_kernel(path, name):
