@@ -570,7 +570,7 @@ __global__ __launch_bounds__(kBlock) void entry_norms_kernel(NormArgs a) {
 // so results are bitwise identical.  Tiles start on the arena's float4 grid;
 // `delta` = begin mod 4 shifts the chain positions.
 //
-// Measured (DESIGN.md §10): the launch is bound by the serial chain of the
+// Measured (DESIGN.md §11): the launch is bound by the serial chain of the
 // largest entry (~15 cycles per step with the LDS traffic of the tile), not
 // by HBM; G = 2 is the fastest split.
 // ---------------------------------------------------------------------------
@@ -910,7 +910,7 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
   a.n_entries = uint32_t(n_entries);
   a.K = K;
   // ring variants: clients (waves) per workgroup (2 measured fastest on MI355X,
-  // DESIGN.md §10); 4 / 5 = variant 0 without the chains / without the loads
+  // DESIGN.md §11); 4 / 5 = variant 0 without the chains / without the loads
   // (timing probes, wrong results)
   static const int kGroup[] = {2, 0, 4, 1, 2, 2};
   const int G = variant == 1 ? 1 : kGroup[variant];
