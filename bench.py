@@ -306,7 +306,7 @@ def main():
                 med = statistics.median(times[v])
                 print(json.dumps({"variant": v, "B": bs.value, "V": a.value, "U": b.value,
                                   "ntl": c.value & 1, "nts": (c.value >> 1) & 1, "pipe": (c.value >> 2) & 1,
-                                  "buf": (c.value >> 3) & 1, "persist": c.value >> 4,
+                                  "buf": (c.value >> 3) & 1, "persist": (c.value >> 4) & 255, "xcd": (c.value >> 12) & 1,
                                   "ms_median": med, "ms_min": min(times[v]),
                                   "GBps": alg_bytes / (med * 1e-3) / 1e9}), flush=True)
         return

@@ -128,7 +128,8 @@ struct AggArgs {
   uint64_t n_i64;
   uint32_t nb_vec;             // workgroups of the f4 body
   uint32_t nb_vec_full;        // of which fully in range (no bounds checks)
-  uint32_t nb_grid;            // PERSIST: workgroups striding over the chunks
+  uint32_t nb_grid;            // PERSIST: workgroups striding over the chunks; XCD: vector blocks in the grid
+  uint32_t xcd_per;            // XCD: chunks per XCD (contiguous range)
   int K;
 };
 
@@ -139,11 +140,15 @@ struct AggArgs {
 //   BUF   buffer_load_dwordx4 (SRD per client, 32-bit voffset) instead of global_load
 //   PERSIST  0: one workgroup per chunk; N: N workgroups per CU-slot grid-stride
 //            over the chunks (grid = min(chunks, 256*N))
-template <int B_, int V_, int U_, bool NTL_, bool NTS_, bool PIPE_, bool BUF_ = false, int PERSIST_ = 0>
+//   XCD   workgroups are dealt to the 8 XCDs round-robin by blockIdx; remap so
+//         that each XCD streams one contiguous eighth of the arena
+template <int B_, int V_, int U_, bool NTL_, bool NTS_, bool PIPE_, bool BUF_ = false, int PERSIST_ = 0,
+          bool XCD_ = false>
 struct Cfg {
   static constexpr int B = B_, V = V_, U = U_;
   static constexpr bool NTL = NTL_, NTS = NTS_, PIPE = PIPE_, BUF = BUF_;
   static constexpr int PERSIST = PERSIST_;
+  static constexpr bool XCD = XCD_;
 };
 
 template <bool NT>
@@ -308,7 +313,19 @@ __device__ __forceinline__ void scalar_item(const AggArgs& a, uint64_t j) {
 template <class C, bool HAS_BASE, bool TWO>
 __global__ __launch_bounds__(C::B) void fedavg_kernel(AggArgs a) {
   const uint32_t blk = blockIdx.x;
-  if constexpr (C::PERSIST > 0) {
+  if constexpr (C::XCD) {
+    if (blk < a.nb_grid) {
+      const uint32_t c = (blk % 8) * a.xcd_per + blk / 8;
+      if (c < a.nb_vec_full) {
+        vec_body<C, HAS_BASE, TWO, false>(a, c);
+      } else if (c < a.nb_vec) {
+        vec_body<C, HAS_BASE, TWO, true>(a, c);
+      }
+    } else {
+      const uint64_t j = uint64_t(blk - a.nb_grid) * C::B + threadIdx.x;
+      scalar_item<HAS_BASE, TWO>(a, j);
+    }
+  } else if constexpr (C::PERSIST > 0) {
     // a.nb_grid workgroups stride over the nb_vec chunks; the rest do scalars
     if (blk < a.nb_grid) {
       for (uint32_t c = blk; c < a.nb_vec; c += a.nb_grid) {
@@ -348,12 +365,13 @@ struct Variant {
   int B, V, U;
   bool NTL, NTS, PIPE, BUF;
   int PERSIST;
+  bool XCD;
   LaunchFn fn[2][2];  // [HAS_BASE][TWO]
 };
 
 template <class C>
 constexpr Variant make_variant() {
-  return Variant{C::B, C::V, C::U, C::NTL, C::NTS, C::PIPE, C::BUF, C::PERSIST,
+  return Variant{C::B, C::V, C::U, C::NTL, C::NTS, C::PIPE, C::BUF, C::PERSIST, C::XCD,
                  {{&launch_one<C, false, false>, &launch_one<C, false, true>},
                   {&launch_one<C, true, false>, &launch_one<C, true, true>}}};
 }
@@ -375,6 +393,10 @@ const Variant kVariants[] = {
     make_variant<Cfg<256, 1, 8, true, true, false, false, 4>>(),    // 11 persistent 4/CU
     make_variant<Cfg<256, 1, 8, true, true, false, true, 8>>(),     // 12 buffer + persistent 8/CU
     make_variant<Cfg<256, 1, 8, false, true, false, true>>(),       // 13 buffer, plain loads
+    make_variant<Cfg<256, 1, 8, true, true, false, false, 0, true>>(),   // 14 XCD-contiguous chunks
+    make_variant<Cfg<512, 1, 8, true, true, false, false, 0, true>>(),   // 15 XCD, 512 threads
+    make_variant<Cfg<1024, 1, 8, true, true, false, false, 0, true>>(),  // 16 XCD, 1024 threads
+    make_variant<Cfg<256, 1, 16, true, true, false, false, 0, true>>(),  // 17 XCD, U=16
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
@@ -417,6 +439,11 @@ int run_agg(int variant, bool has_base, const float* const* xf, const int64_t* c
   a.nb_vec = uint32_t(nb_vec);
   a.nb_vec_full = uint32_t(a.n4 / chunk);
   a.nb_grid = a.nb_vec;
+  a.xcd_per = 0;
+  if (vr.XCD) {
+    a.xcd_per = uint32_t((nb_vec + 7) / 8);
+    a.nb_grid = 8 * a.xcd_per;  // up to 7 vector blocks idle
+  }
   if (vr.PERSIST > 0) {
     const uint64_t cap = uint64_t(256) * vr.PERSIST;  // 256 CUs on MI355X
     a.nb_grid = uint32_t(nb_vec < cap ? nb_vec : cap);
@@ -869,7 +896,8 @@ int plato_agg_tune_describe(int variant, int* block, int* v, int* u, int* flags)
   *block = vr.B;
   *v = vr.V;
   *u = vr.U;
-  *flags = (vr.NTL ? 1 : 0) | (vr.NTS ? 2 : 0) | (vr.PIPE ? 4 : 0) | (vr.BUF ? 8 : 0) | (vr.PERSIST << 4);
+  *flags = (vr.NTL ? 1 : 0) | (vr.NTS ? 2 : 0) | (vr.PIPE ? 4 : 0) | (vr.BUF ? 8 : 0) | (vr.PERSIST << 4) |
+           (vr.XCD ? 1 << 12 : 0);
   return PLATO_AGG_OK;
 }
 
