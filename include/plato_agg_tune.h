@@ -67,6 +67,18 @@ int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const i
                                const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
                                size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream);
 
+/* plato_agg_fedavg_qsgd kernel variants (workgroup size x clients per decode-table
+ * batch; plato_agg_fedavg_qsgd uses 0).  plato_agg_tune_qsgd_chunk gives the
+ * chunk capacity (elements per workgroup pass) the variant is built for. */
+int plato_agg_tune_num_qsgd_variants(void);
+int plato_agg_tune_qsgd_chunk(int variant);
+int plato_agg_tune_fedavg_qsgd(int variant, const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64,
+                               int K, const float* d_max_v, int n_entries, float divisor, const float* d_w,
+                               const float* d_s, const plato_agg_chunk* d_chunks_f32, uint32_t n_chunks_f32,
+                               const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64, const float* d_base_f32,
+                               const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
+                               size_t n_i64, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -112,6 +112,14 @@ SIGNATURES = {
          _c_void_p, _c_void_p, _c_size_t, _c_size_t, _c_void_p],
     ),
     "plato_agg_tune_stream": (_c_int, [_c_int, _c_void_p, _c_void_p, _c_size_t, _c_int, _c_void_p]),
+    "plato_agg_tune_num_qsgd_variants": (_c_int, []),
+    "plato_agg_tune_qsgd_chunk": (_c_int, [_c_int]),
+    "plato_agg_tune_fedavg_qsgd": (
+        _c_int,
+        [_c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_int, _c_float, _c_void_p, _c_void_p, _c_void_p,
+         ctypes.c_uint32, _c_void_p, ctypes.c_uint32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+         _c_size_t, _c_size_t, _c_void_p],
+    ),
     "plato_agg_tune_entry_norms": (
         _c_int,
         [_c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_void_p,

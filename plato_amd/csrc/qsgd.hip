@@ -20,6 +20,7 @@
 
 #include "common.h"
 #include "plato_agg.h"
+#include "plato_agg_tune.h"
 
 namespace {
 
@@ -32,8 +33,11 @@ typedef __attribute__((address_space(1))) const f4 gf4;
 typedef __attribute__((address_space(1))) f4 gf4w;
 typedef __attribute__((address_space(1))) const u4 gu4;
 
-constexpr int kBlock = 512;  // 8 wavefronts share each decode table (built once per batch)
-constexpr int kU = 8;       // clients per LDS table batch
+// Kernel shape (tuning space, plato_agg_tune_fedavg_qsgd): B threads per
+// workgroup share each batch's decode tables, U clients per table batch.
+// The default (variant 0) is B = 512, U = 8 (the shape moves the
+// time by under 5 %, within box noise; probes without the code loads still
+// take ~80 % of the time: the decode/sum path, not HBM, bounds this kernel).
 constexpr int kG = 16;      // elements per lane group (one 16-byte code load)
 
 template <class T>
@@ -83,7 +87,7 @@ __device__ __forceinline__ float term(float x, float b, float w, float s, bool t
   return t;
 }
 
-template <bool TWO>
+template <int kBlock, int kU, bool TWO>
 __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
   const Chunk ch = load_chunk(a.tf, c, a.n_f32);
   const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
@@ -180,7 +184,7 @@ __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
   }
 }
 
-template <bool TWO>
+template <int kBlock, bool TWO>
 __device__ void qsgd_i64_chunk(const QArgs& a, uint32_t cc) {
   const Chunk ch = load_chunk(a.ti, cc, a.n_i64);
   const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
@@ -196,29 +200,45 @@ __device__ void qsgd_i64_chunk(const QArgs& a, uint32_t cc) {
   }
 }
 
-template <bool TWO>
+template <int kBlock, int kU, bool TWO>
 __global__ __launch_bounds__(kBlock) void fedavg_qsgd_kernel(QArgs a) {
   __shared__ float lut[kU][256];
   const uint32_t c = blockIdx.x;
   if (c < a.ncf) {
-    qsgd_f32_chunk<TWO>(a, c, lut);
+    qsgd_f32_chunk<kBlock, kU, TWO>(a, c, lut);
   } else {
-    qsgd_i64_chunk<TWO>(a, c - a.ncf);
+    qsgd_i64_chunk<kBlock, TWO>(a, c - a.ncf);
   }
 }
 
+using QFn = void (*)(const QArgs&, hipStream_t, uint32_t);
+template <int B, int U, bool TWO>
+void launch_q(const QArgs& a, hipStream_t st, uint32_t nc) {
+  hipLaunchKernelGGL((fedavg_qsgd_kernel<B, U, TWO>), dim3(nc), dim3(B), 0, st, a);
+}
+struct QVariant {
+  int block, u;
+  QFn fn[2];  // [TWO]
+};
+const QVariant kQVariants[] = {
+    {512, 8, {&launch_q<512, 8, false>, &launch_q<512, 8, true>}},      // 0 (default)
+    {256, 8, {&launch_q<256, 8, false>, &launch_q<256, 8, true>}},      // 1
+    {512, 16, {&launch_q<512, 16, false>, &launch_q<512, 16, true>}},   // 2
+    {256, 4, {&launch_q<256, 4, false>, &launch_q<256, 4, true>}},      // 3
+    {1024, 8, {&launch_q<1024, 8, false>, &launch_q<1024, 8, true>}},   // 4
+};
+constexpr int kNumQVariants = sizeof(kQVariants) / sizeof(kQVariants[0]);
+
 bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
 
-}  // namespace
 
-extern "C" {
-
-int plato_agg_fedavg_qsgd(const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64, int K,
+int run_qsgd(int variant, const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64, int K,
                           const float* d_max_v, int n_entries, float divisor, const float* d_w, const float* d_s,
                           const plato_agg_chunk* d_chunks_f32, uint32_t n_chunks_f32,
                           const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64, const float* d_base_f32,
                           const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
                           size_t n_i64, hipStream_t stream) {
+  if (variant < 0 || variant >= kNumQVariants) return set_error(PLATO_AGG_EINVAL, "bad qsgd variant");
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (n_entries <= 0 || !d_max_v || !d_w) return set_error(PLATO_AGG_EINVAL, "null max_v / weight table");
   if (!(divisor != 0.f)) return set_error(PLATO_AGG_EINVAL, "divisor (quantization_level - 1) must be non-zero");
@@ -251,14 +271,42 @@ int plato_agg_fedavg_qsgd(const uint8_t* const* d_codes_f32, const uint8_t* cons
   a.nci = n_chunks_i64;
   a.divisor = divisor;
   a.K = K;
-  if (d_s) {
-    hipLaunchKernelGGL(fedavg_qsgd_kernel<true>, dim3(uint32_t(nc)), dim3(kBlock), 0, stream, a);
-  } else {
-    hipLaunchKernelGGL(fedavg_qsgd_kernel<false>, dim3(uint32_t(nc)), dim3(kBlock), 0, stream, a);
-  }
+  kQVariants[variant].fn[d_s ? 1 : 0](a, stream, uint32_t(nc));
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(PLATO_AGG_EHIP, std::string("fedavg_qsgd launch: ") + hipGetErrorString(err));
   return clear_error();
+}
+
+}  // namespace
+
+extern "C" {
+
+int plato_agg_fedavg_qsgd(const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64, int K,
+                          const float* d_max_v, int n_entries, float divisor, const float* d_w, const float* d_s,
+                          const plato_agg_chunk* d_chunks_f32, uint32_t n_chunks_f32,
+                          const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64, const float* d_base_f32,
+                          const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
+                          size_t n_i64, hipStream_t stream) {
+  return run_qsgd(0, d_codes_f32, d_codes_i64, K, d_max_v, n_entries, divisor, d_w, d_s, d_chunks_f32, n_chunks_f32,
+                  d_chunks_i64, n_chunks_i64, d_base_f32, d_base_i64, d_out_f32, d_out_i64f, n_f32, n_i64, stream);
+}
+
+int plato_agg_tune_num_qsgd_variants(void) { return kNumQVariants; }
+
+int plato_agg_tune_qsgd_chunk(int variant) {
+  if (variant < 0 || variant >= kNumQVariants) return set_error(PLATO_AGG_EINVAL, "bad qsgd variant");
+  return kQVariants[variant].block * kG;
+}
+
+int plato_agg_tune_fedavg_qsgd(int variant, const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64,
+                               int K, const float* d_max_v, int n_entries, float divisor, const float* d_w,
+                               const float* d_s, const plato_agg_chunk* d_chunks_f32, uint32_t n_chunks_f32,
+                               const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64, const float* d_base_f32,
+                               const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
+                               size_t n_i64, hipStream_t stream) {
+  return run_qsgd(variant, d_codes_f32, d_codes_i64, K, d_max_v, n_entries, divisor, d_w, d_s, d_chunks_f32,
+                  n_chunks_f32, d_chunks_i64, n_chunks_i64, d_base_f32, d_base_i64, d_out_f32, d_out_i64f, n_f32,
+                  n_i64, stream);
 }
 
 }  // extern "C"

@@ -165,6 +165,9 @@ class _Stager:
 class FedAvgEngine:
     """HIP FedAvg aggregation on one GPU (one process per GPU)."""
 
+    #: QSGD kernel variant (tuning / tests; None = the library default)
+    qsgd_variant: int | None = None
+
     def __init__(self, device=None, variant: int | None = None):
         self.device = require_device(device)
         self.lib = _lib.lib()
@@ -581,10 +584,14 @@ class AggregationRound:
             mv = torch.from_numpy(np.ascontiguousarray(np.stack([self._mv[i] for i in order], axis=1))).to(eng.device)
             cf, ci = eng._chunks(lay, eng.QSGD_CHUNK)
             ncf, nci = int(cf.shape[0]), int(ci.shape[0])
-            _lib.call("plato_agg_fedavg_qsgd", _ptr(tf), _ptr(ti) if n_i else None, len(order), _ptr(mv),
-                      len(lay.entries), float(self._level - 1), _ptr(w), _ptr(s), _ptr(cf), ncf,
-                      _ptr(ci) if nci else None, nci, _ptr(eng._base.f32), _ptr(eng._base.i64) if n_i else None,
-                      _ptr(out_f), _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
+            args = (_ptr(tf), _ptr(ti) if n_i else None, len(order), _ptr(mv), len(lay.entries),
+                    float(self._level - 1), _ptr(w), _ptr(s), _ptr(cf), ncf, _ptr(ci) if nci else None, nci,
+                    _ptr(eng._base.f32), _ptr(eng._base.i64) if n_i else None, _ptr(out_f),
+                    _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
+            if eng.qsgd_variant is None:
+                _lib.call("plato_agg_fedavg_qsgd", *args)
+            else:  # tuning / tests
+                _lib.call("plato_agg_tune_fedavg_qsgd", eng.qsgd_variant, *args)
             w = (w, mv)
         elif self.codec == "bf16":
             n_i = lay.n_i64

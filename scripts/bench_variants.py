@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--qsgd-codes", default="qsgd", choices=["qsgd", "uniform"])
     ap.add_argument("--norm-variants", action="store_true", help="also time each entry_norms kernel variant")
+    ap.add_argument("--qsgd-variants", action="store_true", help="also time each fedavg_qsgd kernel variant")
     ap.add_argument("--norm-order", default="longest", choices=["longest", "layout"],
                     help="entry order of the norms launch (longest first = the engine's)")
     args = ap.parse_args()
@@ -97,10 +98,16 @@ def main():
     stats_out = torch.empty((2 * k + 1) * n_e, dtype=torch.float64, device=dev)
     norms_out = torch.empty(k * n_e, dtype=torch.float32, device=dev)
 
-    def run_qsgd():
-        cf, ci = chunks(engine.QSGD_CHUNK)
-        _lib.call("plato_agg_fedavg_qsgd", _ptr(qtf), _ptr(qti), k, _ptr(max_v), n_e, 63.0, _ptr(w), None,
-                  _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(out_f),
+    def run_qsgd(variant=None):
+        if variant is None:
+            cf, ci = chunks(engine.QSGD_CHUNK)
+            _lib.call("plato_agg_fedavg_qsgd", _ptr(qtf), _ptr(qti), k, _ptr(max_v), n_e, 63.0, _ptr(w), None,
+                      _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(out_f),
+                      _ptr(out_i), n_f, n_i, h)
+            return
+        cf, ci = chunks(_lib.lib().plato_agg_tune_qsgd_chunk(variant))
+        _lib.call("plato_agg_tune_fedavg_qsgd", variant, _ptr(qtf), _ptr(qti), k, _ptr(max_v), n_e, 63.0, _ptr(w),
+                  None, _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(out_f),
                   _ptr(out_i), n_f, n_i, h)
 
     def run_entrywise():
@@ -134,6 +141,9 @@ def main():
         "norms": (run_norms, (k + 1) * n_f * 4 + (k + 1) * n_i * 8),
         "fedavg": (run_fedavg, layout.algorithmic_bytes(k)),
     }
+    if args.qsgd_variants:  # tuning: every plato_agg_tune_fedavg_qsgd variant
+        for v in range(_lib.lib().plato_agg_tune_num_qsgd_variants()):
+            kernels[f"qsgd_v{v}"] = ((lambda v=v: run_qsgd(v)), kernels["qsgd"][1])
     if args.norm_variants:  # tuning: every plato_agg_tune_entry_norms variant
         for v in range(6):
             kernels[f"norms_v{v}"] = ((lambda v=v: run_norms(v)), kernels["norms"][1])
