@@ -572,7 +572,8 @@ __global__ __launch_bounds__(kBlock) void entry_norms_kernel(NormArgs a) {
 //
 // Measured: the launch is bound by the serial chain of the
 // largest entry (~15 cycles per step with the LDS traffic of the tile), not
-// by HBM; G = 2 is the fastest split.
+// by HBM; G = 2 is the fastest split of this design (variant 8); the
+// producer / consumer kernel below is faster and is the default.
 // ---------------------------------------------------------------------------
 constexpr int kRT = 1024;             // elements per operand per stage
 constexpr int kRS = 6;                // ring stages
@@ -759,6 +760,151 @@ __global__ __launch_bounds__(64 * G) void entry_norms_ring_kernel(NormArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// entry_norms, producer / consumer version: two waves per (entry, client).
+// The chain wave (wave 0) does nothing but walk its chains over ready tiles of
+// d = x - b; the producer wave (wave 1) streams x and b into a kPS-deep LDS ring
+// by LDS-DMA (the only reader of that ring, so reusing a slot needs no sync),
+// forms d for the next tile into a double-buffered d tile, and meets the chain
+// wave at one s_barrier per tile.  Same chains, same order as the kernels above.
+// ---------------------------------------------------------------------------
+
+// s_waitcnt lgkmcnt(0) alone (vmcnt left at its maximum: the glds stay in flight)
+__device__ __forceinline__ void wait_lgkm0() {
+  __builtin_amdgcn_s_waitcnt((63 & 15) | (7 << 4) | (0 << 8) | ((63 >> 4) << 14));
+}
+
+template <int T, bool HAS_BASE>
+__device__ __forceinline__ void pc_issue(const float* x, const float* b, float (*raw)[2][T], uint32_t slot,
+                                         uint64_t g0, uint64_t gmax, int lane) {
+#pragma unroll
+  for (int o = 0; o < (HAS_BASE ? 2 : 1); ++o) {
+    const float* src = o == 0 ? x : b;
+#pragma unroll
+    for (int c = 0; c < T / 256; ++c) {
+      uint64_t g = g0 + uint64_t(c) * 64 + lane;
+      g = g < gmax ? g : gmax;
+      __builtin_amdgcn_global_load_lds((gvoid*)(src + 4 * g), (lvoid*)&raw[slot][o][c * 256], 16, 0, 0);
+    }
+  }
+}
+
+template <int T, int PS, bool HAS_BASE>
+__device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int lane, float (*raw)[2][T],
+                        float (*dbuf)[T]) {
+  constexpr int kRT = T, kPS = PS;
+  constexpr int kPer = (HAS_BASE ? 2 : 1) * (kRT / 256);  // glds per stage
+  static_assert((kPS - 1) * kPer < 64, "vmcnt range");
+  const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+  const uint32_t delta = ch.begin & 3u;
+  const uint64_t g_first = ch.begin >> 2;
+  const uint64_t ntiles = (delta + m + kRT - 1) / kRT;
+  const uint64_t gmax = (a.n_f32 >> 2) - 1;
+  const float* x = sld(a.xf, i);
+  if (wave == 1) {  // producer
+#pragma unroll
+    for (int p = 0; p < kPS - 1; ++p)
+      if (uint64_t(p) < ntiles) pc_issue<T, HAS_BASE>(x, a.base_f, raw, p, g_first + uint64_t(p) * (kRT / 4), gmax, lane);
+    for (uint64_t tt = 0; tt < ntiles; ++tt) {
+      // slot (tt - 1) % kPS was read by this wave's previous d pass
+      if (tt + kPS - 1 < ntiles) {
+        pc_issue<T, HAS_BASE>(x, a.base_f, raw, uint32_t((tt + kPS - 1) % kPS), g_first + (tt + kPS - 1) * (kRT / 4),
+                           gmax, lane);
+        wait_vmcnt<(kPS - 1) * kPer>();
+      } else {
+        wait_vmcnt<0>();
+      }
+      const uint32_t slot = uint32_t(tt % kPS);
+      f4* d = reinterpret_cast<f4*>(dbuf[tt & 1]);
+#pragma unroll
+      for (int r = 0; r < kRT / 256; ++r) {
+        const f4 xv = *(reinterpret_cast<const f4*>(raw[slot][0]) + r * 64 + lane);
+        if (HAS_BASE) {
+          const f4 bv = *(reinterpret_cast<const f4*>(raw[slot][1]) + r * 64 + lane);
+          d[r * 64 + lane] = xv - bv;  // fp32, as compute_weight_deltas
+        } else {
+          d[r * 64 + lane] = xv;
+        }
+      }
+      wait_lgkm0();  // d tile written (the glds of later stages stay in flight)
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __builtin_amdgcn_s_barrier();  // tile tt ready; the chain wave is done with tile tt - 2
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+    wait_vmcnt<0>();
+    return;
+  }
+  // chain wave
+  const int pj = int((uint32_t(lane) + delta) & 7u);
+  const int64_t s_shift = (uint32_t(lane) + delta) >= 8u ? -1 : 0;
+  const int64_t s_end = int64_t(m / kNormLanes);
+  float acc = 0.f;
+  for (uint64_t tt = 0; tt < ntiles; ++tt) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const float* p = dbuf[tt & 1] + pj;
+    const int64_t s0 = int64_t(tt) * (kRT / kNormLanes) + s_shift;
+    if (tt >= 1 && int64_t(tt + 1) * (kRT / kNormLanes) <= s_end) {
+      constexpr int kCB = 16, kNB = kRT / kNormLanes / kCB;
+      float cur[kCB], nxt[kCB];
+#pragma unroll
+      for (int q = 0; q < kCB; ++q) cur[q] = p[8 * q];
+#pragma unroll
+      for (int blk = 0; blk < kNB; ++blk) {
+        if (blk + 1 < kNB) {
+#pragma unroll
+          for (int q = 0; q < kCB; ++q) nxt[q] = p[8 * (kCB * (blk + 1) + q)];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < kCB; ++q) acc = __builtin_fmaf(cur[q], cur[q], acc);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < kCB; ++q) cur[q] = nxt[q];
+      }
+    } else if (lane < kNormLanes) {
+      for (int u = 0; u < kRT / kNormLanes; ++u) {
+        const int64_t st = s0 + u;
+        if (st >= 0 && st < s_end) {
+          const float v = p[8 * u];
+          acc = __builtin_fmaf(v, v, acc);
+        }
+      }
+    }
+  }
+  float s = __shfl(acc, 0, 64);
+  for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, l, 64);
+  if (lane != 0) return;
+  for (uint64_t e = m; e < n; ++e) {
+    const uint64_t idx = ch.begin + e;
+    const float v = HAS_BASE ? x[idx] - a.base_f[idx] : x[idx];
+    s = __builtin_fmaf(v, v, s);
+  }
+  if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
+}
+
+template <int T, int PS, bool HAS_BASE>
+__global__ __launch_bounds__(128) void entry_norms_pc_kernel(NormArgs a) {
+  __shared__ __attribute__((aligned(16))) float raw[PS][2][T];
+  __shared__ __attribute__((aligned(16))) float dbuf[2][T];
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  const uint64_t pair = blockIdx.x;  // entry-major over the (longest-first) tables
+  const uint32_t ent = uint32_t(pair / uint64_t(a.K));
+  const int i = int(pair % uint64_t(a.K));
+  float(*rows)[kNRow] = reinterpret_cast<float(*)[kNRow]>(&raw[0][0][0]);
+  if (ent < a.nef) {
+    const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
+    if (uint64_t(ch.end) > (a.n_f32 & ~3ull)) {  // the arena's partial last float4 group: per-wave path
+      if (wave == 0) norm_pair<HAS_BASE, false>(a, ch, i, lane, rows);
+      return;
+    }
+    norm_pc<T, PS, HAS_BASE>(a, ch, i, wave, lane, raw, dbuf);
+  } else if (ent < a.nef + a.nei) {
+    if (wave == 0) norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows);
+  }
+}
+
 bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
 
 int launch_error(const char* what) {
@@ -884,7 +1030,7 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
               const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_chunk* d_entries_f32,
               uint32_t n_entries_f32, const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  if (variant < 0 || variant > 5) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
+  if (variant < 0 || variant > 8) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (n_entries <= 0 || !d_out) return set_error(PLATO_AGG_EINVAL, "null output / no entries");
   if (n_entries_f32 && (!d_x_f32 || !d_entries_f32)) return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
@@ -909,13 +1055,30 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
   a.nei = n_entries_i64;
   a.n_entries = uint32_t(n_entries);
   a.K = K;
-  // ring variants: clients (waves) per workgroup (2 measured fastest on MI355X,
-  // DESIGN.md §11); 4 / 5 = variant 0 without the chains / without the loads
-  // (timing probes, wrong results)
-  static const int kGroup[] = {2, 0, 4, 1, 2, 2};
-  const int G = variant == 1 ? 1 : kGroup[variant];
+  // Variants (include/plato_agg_tune.h): 0 producer/consumer with 512-element
+  // tiles, the fastest on MI355X; 1 per-wave; 2, 3, 8 LDS-DMA
+  // ring with 4 / 1 / 2 clients per workgroup; 4 / 5 variant 8 without the
+  // chains / without the loads (timing probes, wrong results); 6, 7
+  // producer/consumer with 1024- / 256-element tiles.
+  static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2};
+  const int G = kGroup[variant];
   a.probe = variant == 4 ? 1u : variant == 5 ? 2u : 0u;
-  a.ngroups = uint32_t((K + G - 1) / G);
+  if (variant == 0 || variant == 6 || variant == 7) {  // producer / consumer, one workgroup per (entry, client)
+    const dim3 grid{uint32_t((uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K))};
+    const bool hb = d_base_f32 != nullptr;
+    if (variant == 0) {
+      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true>), grid, dim3(128), 0, stream, a);
+      else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false>), grid, dim3(128), 0, stream, a);
+    } else if (variant == 6) {
+      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, true>), grid, dim3(128), 0, stream, a);
+      else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, false>), grid, dim3(128), 0, stream, a);
+    } else {
+      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<256, 12, true>), grid, dim3(128), 0, stream, a);
+      else hipLaunchKernelGGL((entry_norms_pc_kernel<256, 12, false>), grid, dim3(128), 0, stream, a);
+    }
+    return launch_error("entry_norms launch");
+  }
+  a.ngroups = uint32_t((K + (G ? G : 1) - 1) / (G ? G : 1));
   if (variant == 1) {  // per-wave chains (the first version)
     const dim3 grid{uint32_t((threads + kBlock - 1) / kBlock)};
     if (d_base_f32) {
