@@ -9,6 +9,9 @@ Modes:
                max|new - new_seq| / max|new_seq| <= 1e-6.
   gpu-bucket   gloo, every rank on cuda:0: BucketAggregator (HIP kernel) per
                rank, gathered model must equal the reference fixture digest.
+  gpu-rccl     nccl (= RCCL), one rank per GPU: gpu-bucket's all-gather on
+               device tensors, and the client-sharded reduce-scatter of HIP
+               deltas-kernel partials (normwise <= 1e-6).
 """
 
 import json
@@ -92,12 +95,45 @@ def gpu_bucket(rank, world, out):
     out["i64_match"] = G.sha(G.canon(ints.cpu().numpy())) == exp["updated_i64f_sha256"]
 
 
+def gpu_rccl(rank, world, out):
+    """RCCL (backend "nccl") on GPU tensors: the bucket all-gather + int64 broadcast
+    (gpu_bucket) and the client-sharded reduce-scatter of HIP-kernel partials."""
+    gpu_bucket(rank, world, out)
+    from plato_amd import weights as W
+    from plato_amd.engine import FedAvgEngine
+
+    layout, bf, bi, xs_f, xs_i = inputs(workloads.resnet(18), 8, 22)
+    w = W.fedavg(synth.num_samples(8, 22))
+    plan = BucketPlan.for_layout(layout, world)
+    mine = client_shard(8, world, rank)
+    eng = FedAvgEngine(f"cuda:{rank % torch.cuda.device_count()}")
+    deltas = [layout.unpack(torch.from_numpy(np.subtract(xs_f[c], bf, dtype=np.float32)),
+                            torch.from_numpy(xs_i[c] - bi)) for c in mine]
+    part = eng.aggregate_deltas(deltas, [w[c] for c in mine])   # HIP deltas-mode kernel
+    flat = torch.cat([part[e.name].reshape(-1) for e in layout.entries if e.region == "f32"]).to(eng.device)
+    bucket_sum = reduce_scatter_partials(plan, flat)             # RCCL reduce-scatter
+    out["reduce_scatter_on_gpu"] = bucket_sum.is_cuda
+    lo, hi = plan.f32_range(rank)
+    bucket = torch.zeros(plan.per, device=eng.device)
+    bucket[: hi - lo] = torch.from_numpy(bf[lo:hi]).to(eng.device) + bucket_sum[: hi - lo]
+    full, _ = gather_buckets(plan, bucket, torch.from_numpy(bi.astype(np.float32)).to(eng.device))
+    exp_f, _ = ref.fedavg_numpy(bf, bi, xs_f, xs_i, w)
+    diff = np.abs(full.cpu().numpy().astype(np.float64) - exp_f)
+    out["normwise"] = float(np.max(diff) / np.max(np.abs(exp_f)))
+
+
 def main():
     mode, out_dir = sys.argv[1], sys.argv[2]
-    dist.init_process_group("gloo")
+    if mode == "gpu-rccl":  # one process per GPU over RCCL
+        local = int(os.environ.get("LOCAL_RANK", "0"))
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     out = {"rank": rank, "world": world}
-    {"cpu-bucket": cpu_bucket, "cpu-client": cpu_client, "gpu-bucket": gpu_bucket}[mode](rank, world, out)
+    {"cpu-bucket": cpu_bucket, "cpu-client": cpu_client, "gpu-bucket": gpu_bucket,
+     "gpu-rccl": gpu_rccl}[mode](rank, world, out)
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
         json.dump(out, f)
     dist.barrier()

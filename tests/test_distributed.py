@@ -66,3 +66,14 @@ def test_two_ranks_bucket_aggregator_on_gpu(tmp_path):
     outs = _run("gpu-bucket", 2, tmp_path)
     for o in outs:
         assert o["f32_match"] and o["i64_match"], o
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_one_rank_per_gpu(tmp_path):
+    """The driver's multi-GPU runs use RCCL; on a one-GPU box this is world size 1."""
+    import torch
+
+    outs = _run("gpu-rccl", min(torch.cuda.device_count(), 8), tmp_path)
+    for o in outs:
+        assert o["f32_match"] and o["i64_match"] and o["reduce_scatter_on_gpu"], o
+        assert o["normwise"] <= 1e-6, o
