@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-host-inclusive", action="store_true")
     p.add_argument("--cpu-reps", type=int, default=3)
+    p.add_argument("--streaming", action="store_true",
+                   help="also time arrival staging and the trigger-to-result latency (C4, examples/async)")
     return p.parse_args()
 
 
@@ -381,6 +383,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_host_inclusive:
         result["host_inclusive"] = host_inclusive(engine, layout, base, slab, k, weights, dev)
 
+    if rank == 0 and world == 1 and args.streaming:
+        result["streaming"] = streaming(engine, layout, base, slab, k, weights, dev)
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(layout, base, slab, k, weights, out_f, out_i, args.cpu_reps,
                                               args.config)
@@ -454,6 +459,54 @@ def host_inclusive(engine, layout, base, slab, k, weights, dev):
         "note": "pickled payload bytes -> libplato_ingest parse + gather into pinned arenas -> H2D -> "
                 "kernel -> D2H (replaces pickle.loads at servers/base.py:822)"}
     return out
+
+
+def streaming(engine, layout, base, slab, k, weights, dev, reps=3):
+    """Async servers: stage each payload to HBM as it arrives, reduce at the trigger.
+
+    * arrival staging: K CPU state_dicts staged back to back (FedAvgEngine.prestage:
+      pack into the pinned ring, H2D on the copy stream), GB/s of payload bytes;
+    * trigger-to-result: the first K-1 payloads arrived (and were staged) earlier;
+      the last one arrives, then the round adopts every staged slot in
+      ``self.updates`` order, launches and returns the CPU state_dict — the
+      latency the server sees after the last report.
+    """
+    from plato_amd.arena import ArenaLayout
+
+    baseline, payloads = _host_state_dicts(layout, base, slab, k)
+    blay = ArenaLayout.from_state_dict(baseline)
+    per_client = layout.n_f32 * 4 + layout.n_i64 * 8
+    stage_s, trig_s = [], []
+    for r in range(reps + 1):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for p in payloads[:-1]:
+            engine.prestage(p, blay)
+        engine._copy_stream.synchronize()
+        t1 = time.perf_counter()
+        engine.prestage(payloads[-1], blay)  # the last report: trigger
+        rnd = engine.begin(baseline, k)
+        rnd.put_baseline(baseline)
+        for slot, p in enumerate(payloads):
+            if not rnd.adopt(slot, p):
+                raise RuntimeError("payload was not staged on arrival")
+        rnd.launch(weights)
+        rnd.result()
+        t2 = time.perf_counter()
+        engine.release_arrivals()
+        if r:
+            stage_s.append(t1 - t0)
+            trig_s.append(t2 - t1)
+    st = statistics.median(stage_s)
+    return {
+        "clients": k,
+        "arrival_staging_GBps": round((k - 1) * per_client / st / 1e9, 2),
+        "arrival_staging_ms_per_payload": round(st / (k - 1) * 1e3, 3),
+        "trigger_to_result_ms": round(statistics.median(trig_s) * 1e3, 2),
+        "note": "CPU state_dicts staged to HBM on arrival (pack -> pinned -> H2D); trigger-to-result = last "
+                "payload's staging + baseline H2D + kernel + D2H of the new state_dict; median of "
+                f"{reps} after 1 warm-up",
+    }
 
 
 def cpu_baseline(layout, base, slab, k, weights, out_f, out_i, reps, config):
