@@ -450,12 +450,25 @@ def host_inclusive(engine, layout, base, slab, k, weights, dev):
     for data in wire[:8]:
         pickle.loads(data)
     t_pickle = (time.perf_counter() - t0) / 8
+    # as the socket delivers it: 1 MiB chunks (servers/base.py:728-736, joined at :821)
+    chunked = [[d[i:i + 2**20] for i in range(0, len(d), 2**20)] for d in wire[:8]]
+    t0 = time.perf_counter()
+    for ch in chunked:
+        pickle.loads(b"".join(ch))
+    t_ref_chunks = (time.perf_counter() - t0) / 8
+    ingest.loads_chunks(chunked[0], layout=layout, pin=True)
+    t0 = time.perf_counter()
+    for ch in chunked:
+        ingest.loads_chunks(ch, layout=layout, pin=True)
+    t_chunks = (time.perf_counter() - t0) / 8
     med_w = statistics.median(t_wire[1:])
     out["from_wire"] = {
         "value": round(layout.algorithmic_bytes(k) / med_w / 1e9, 2), "unit": "GB/s",
         "ms": round(med_w * 1e3, 2),
         "native_parse_ms_per_payload": round(med_w * 1e3 / k, 3),
         "pickle_loads_ms_per_payload": round(t_pickle * 1e3, 3),
+        "socket_chunks": {"reference_join_pickle_loads_ms": round(t_ref_chunks * 1e3, 3),
+                          "native_join_parse_gather_ms": round(t_chunks * 1e3, 3)},
         "note": "pickled payload bytes -> libplato_ingest parse + gather into pinned arenas -> H2D -> "
                 "kernel -> D2H (replaces pickle.loads at servers/base.py:822)"}
     return out

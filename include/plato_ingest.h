@@ -90,6 +90,16 @@ int plato_ingest_gather(const uint8_t* buf, size_t len, const plato_ingest_tenso
                         const uint64_t* dst_byte_offset, uint8_t* dst, size_t dst_len, int threads);
 
 /*
+ * Join a payload's transport chunks (socket.io delivers 1 MiB chunks that the
+ * server concatenates with b"".join before unpickling, plato/servers/base.py:
+ * 813-822) into dst, on the same thread pool as plato_ingest_gather: one
+ * parallel copy instead of Python's single-threaded join.  dst may be the
+ * buffer plato_ingest_parse then reads.
+ */
+int plato_ingest_join(const uint8_t* const* chunks, const size_t* lens, int n, uint8_t* dst, size_t dst_len,
+                      int threads);
+
+/*
  * zstd-compressed payloads.  Plato's model_compress outbound processor sends
  * zstd.compress(pickle.dumps(state_dict), level)
  * (plato/processors/model_compress.py:25) and the server's model_decompress

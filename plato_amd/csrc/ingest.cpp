@@ -703,6 +703,41 @@ int64_t plato_ingest_zstd_decompress(const uint8_t* src, size_t len, uint8_t* ds
   return int64_t(r);
 }
 
+int plato_ingest_join(const uint8_t* const* chunks, const size_t* lens, int n, uint8_t* dst, size_t dst_len,
+                      int threads) {
+  if (n < 0 || (n > 0 && (!chunks || !lens)) || (!dst && dst_len)) {
+    g_err = "bad argument";
+    return PLATO_INGEST_EINVAL;
+  }
+  std::vector<Piece> pieces;
+  constexpr size_t kChunk = size_t(2) << 20;
+  size_t pos = 0;
+  for (int i = 0; i < n; ++i) {
+    if (lens[i] && !chunks[i]) {
+      g_err = "null chunk";
+      return PLATO_INGEST_EINVAL;
+    }
+    if (lens[i] > dst_len - pos) {
+      g_err = "chunks longer than the destination";
+      return PLATO_INGEST_ECAPACITY;
+    }
+    for (size_t o = 0; o < lens[i]; o += kChunk)
+      pieces.push_back({chunks[i] + o, dst + pos + o, std::min(kChunk, lens[i] - o)});
+    pos += lens[i];
+  }
+  int nt = threads > 0 ? threads : int(std::max(1u, std::thread::hardware_concurrency()));
+  nt = int(std::min<size_t>(size_t(nt), std::max<size_t>(1, pos / (size_t(4) << 20))));
+  nt = std::min(nt, 16);
+  if (nt <= 1 || pieces.size() <= 1) {
+    for (auto& p : pieces) std::memcpy(p.dst, p.src, p.bytes);
+  } else {
+    Pool::get().run(pieces.size(), nt,
+                    [&](size_t k) { std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].bytes); });
+  }
+  g_err.clear();
+  return 0;
+}
+
 size_t plato_ingest_zstd_bound(size_t len) {
   const Zstd* z = zstd_or_fail();
   return z ? z->bound(len) : 0;

@@ -76,6 +76,9 @@ def lib():
                                               ctypes.c_int, ctypes.POINTER(ctypes.c_uint64), ctypes.c_void_p,
                                               ctypes.c_size_t, ctypes.c_int]
             vp, sz = ctypes.c_void_p, ctypes.c_size_t
+            h.plato_ingest_join.restype = ctypes.c_int
+            h.plato_ingest_join.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
+                                            ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
             for name, res, args in (
                 ("plato_ingest_zstd_available", ctypes.c_int, []),
                 ("plato_ingest_zstd_content_size", ctypes.c_int64, [vp, sz]),
@@ -204,6 +207,26 @@ def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: i
     out.arena_f32, out.arena_i64 = f32, i64
     out.layout_signature = layout.signature
     return out
+
+
+def join(chunks, threads: int = 0) -> np.ndarray:
+    """``b"".join(chunks)`` (servers/base.py:821) as one parallel native copy into a fresh buffer."""
+    keeps = [_buffer(c) for c in chunks]
+    total = sum(k[1] for k in keeps)
+    out = np.empty(max(total, 1), dtype=np.uint8)
+    n = len(keeps)
+    ptrs = (ctypes.c_void_p * max(n, 1))(*[k[0] for k in keeps])
+    lens = (ctypes.c_size_t * max(n, 1))(*[k[1] for k in keeps])
+    rc = lib().plato_ingest_join(ptrs, lens, n, out.ctypes.data, total, threads)
+    if rc < 0:
+        raise IngestError(f"join failed ({rc}): {lib().plato_ingest_last_error().decode()}")
+    del keeps
+    return out[:total]
+
+
+def loads_chunks(chunks, layout: ArenaLayout | None = None, pin: bool = False, threads: int = 0):
+    """``pickle.loads(b"".join(chunks))`` for a chunked payload, natively (join + parse + gather)."""
+    return loads(join(chunks, threads), layout=layout, pin=pin, threads=threads)
 
 
 EFORMAT, ECAPACITY, ENOCODEC, EUNKNOWNSIZE = -3, -5, -6, -7

@@ -40,19 +40,23 @@ class WireIngestMixin:
         self._plato_amd_ingest_layout = layout
         return layout
 
-    def ingest_payload(self, payload: bytes):
-        """Native ``pickle.loads`` of one payload (falls back for non-tensor payloads)."""
+    def ingest_payload(self, payload):
+        """Native ``pickle.loads`` of one payload (falls back for non-tensor payloads).
+
+        ``payload`` is the payload's bytes, or the list of its transport chunks
+        (joined natively, in parallel, instead of ``b"".join``).
+        """
+        data = ingest.join(payload) if isinstance(payload, (list, tuple)) else payload
         try:
-            return ingest.loads(payload, layout=self._ingest_layout(), pin=self.ingest_pinned)
+            return ingest.loads(data, layout=self._ingest_layout(), pin=self.ingest_pinned)
         except (ingest.IngestError, KeyError, ValueError):
-            return pickle.loads(payload)
+            return pickle.loads(data)
 
     async def _client_payload_arrived(self, sid, client_id):
-        """plato/servers/base.py:817-831 with the unpickle done natively."""
+        """plato/servers/base.py:817-831 with the join and the unpickle done natively."""
         assert len(self.client_chunks[sid]) > 0 and client_id in self.training_clients
 
-        payload = b"".join(self.client_chunks[sid])
-        _data = self.ingest_payload(payload)
+        _data = self.ingest_payload(self.client_chunks[sid])
         self.client_chunks[sid] = []
         if self.stage_on_arrival and isinstance(_data, ingest.ArenaStateDict):
             layout = self._ingest_layout()
