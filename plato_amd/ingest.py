@@ -209,11 +209,19 @@ def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: i
     return out
 
 
-def join(chunks, threads: int = 0) -> np.ndarray:
-    """``b"".join(chunks)`` (servers/base.py:821) as one parallel native copy into a fresh buffer."""
+_scratch = threading.local()
+
+
+def join(chunks, threads: int = 0, out: np.ndarray | None = None) -> np.ndarray:
+    """``b"".join(chunks)`` (servers/base.py:821) as one parallel native copy.
+
+    Into ``out`` if it is large enough (its first bytes are returned), else
+    into a fresh buffer.
+    """
     keeps = [_buffer(c) for c in chunks]
     total = sum(k[1] for k in keeps)
-    out = np.empty(max(total, 1), dtype=np.uint8)
+    if out is None or out.size < total:
+        out = np.empty(max(total, 1), dtype=np.uint8)
     n = len(keeps)
     ptrs = (ctypes.c_void_p * max(n, 1))(*[k[0] for k in keeps])
     lens = (ctypes.c_size_t * max(n, 1))(*[k[1] for k in keeps])
@@ -225,8 +233,16 @@ def join(chunks, threads: int = 0) -> np.ndarray:
 
 
 def loads_chunks(chunks, layout: ArenaLayout | None = None, pin: bool = False, threads: int = 0):
-    """``pickle.loads(b"".join(chunks))`` for a chunked payload, natively (join + parse + gather)."""
-    return loads(join(chunks, threads), layout=layout, pin=pin, threads=threads)
+    """``pickle.loads(b"".join(chunks))`` for a chunked payload, natively (join + parse + gather).
+
+    The joined bytes go to a per-thread scratch buffer that is reused (the
+    tensors are gathered out of it), so steady-state joins take no page faults.
+    """
+    buf = getattr(_scratch, "buf", None)
+    data = join(chunks, threads, out=buf)
+    if buf is None or data.base is not buf:
+        _scratch.buf = data if data.base is None else data.base
+    return loads(data, layout=layout, pin=pin, threads=threads)
 
 
 EFORMAT, ECAPACITY, ENOCODEC, EUNKNOWNSIZE = -3, -5, -6, -7
