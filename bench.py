@@ -461,6 +461,14 @@ def host_inclusive(engine, layout, base, slab, k, weights, dev):
     for ch in chunked:
         ingest.loads_chunks(ch, layout=layout, pin=True)
     t_chunks = (time.perf_counter() - t0) / 8
+    # size accounting: the reference re-pickles each payload to log its size
+    # (servers/base.py:839-846); WireIngestMixin takes the wire length instead
+    loaded = [pickle.loads(d) for d in wire[:4]]
+    t0 = time.perf_counter()
+    for p in loaded:
+        sys.getsizeof(pickle.dumps(p))
+    t_resize = (time.perf_counter() - t0) / len(loaded)
+    del loaded
     med_w = statistics.median(t_wire[1:])
     out["from_wire"] = {
         "value": round(layout.algorithmic_bytes(k) / med_w / 1e9, 2), "unit": "GB/s",
@@ -469,6 +477,7 @@ def host_inclusive(engine, layout, base, slab, k, weights, dev):
         "pickle_loads_ms_per_payload": round(t_pickle * 1e3, 3),
         "socket_chunks": {"reference_join_pickle_loads_ms": round(t_ref_chunks * 1e3, 3),
                           "native_join_parse_gather_ms": round(t_chunks * 1e3, 3)},
+        "size_accounting": {"reference_repickle_ms": round(t_resize * 1e3, 3), "native": "wire length, no copy"},
         "note": "pickled payload bytes -> libplato_ingest parse + gather into pinned arenas -> H2D -> "
                 "kernel -> D2H (replaces pickle.loads at servers/base.py:822)"}
     return out

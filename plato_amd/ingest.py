@@ -19,7 +19,7 @@ from collections import OrderedDict
 import numpy as np
 import torch
 
-from .arena import CODECS, F32, ArenaLayout
+from .arena import CODECS, F32, I64, ArenaLayout
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libplato_ingest.so")
@@ -144,6 +144,19 @@ def _gather(keep, addr, n, infos, offsets, dst: torch.Tensor, threads: int):
         raise IngestError(f"gather failed ({rc}): {lib().plato_ingest_last_error().decode()}")
 
 
+def _owned_view(storage, byte_offset: int, nbytes: int, dtype, shape) -> torch.Tensor:
+    """A tensor over ``storage[byte_offset : byte_offset + nbytes]`` whose storage is that slice.
+
+    The slice shares the arena's memory (and keeps it alive), but the tensor
+    owns a storage of exactly its own bytes, as the tensors pickle.loads
+    builds do: re-pickling it (the reference sizes every payload with
+    pickle.dumps, servers/base.py:839-846) writes its own bytes, not the
+    whole arena once per tensor.
+    """
+    sub = storage[byte_offset : byte_offset + nbytes]
+    return torch.empty(0, dtype=dtype).set_(sub, 0, shape)
+
+
 def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: int = 0,
           codec: str | None = None) -> OrderedDict:
     """``pickle.loads`` for a pickled ``state_dict`` of CPU tensors, natively.
@@ -164,12 +177,11 @@ def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: i
             total += t.numel * t.element_size
         buf = torch.empty(max(total, 1), dtype=torch.uint8, pin_memory=pin)
         _gather(keep, addr, n, infos, offsets, buf, threads)
+        storage = buf.untyped_storage()
         out = OrderedDict()
         for key, t, off in zip(keys, infos, offsets):
-            dt = DTYPES[t.dtype]
-            shape = tuple(t.shape[: t.ndim])
-            view = buf[off : off + t.numel * t.element_size].view(dt).view(shape)
-            out[key] = view
+            out[key] = _owned_view(storage, off, t.numel * t.element_size, DTYPES[t.dtype],
+                                   tuple(t.shape[: t.ndim]))
         return out
 
     if len(keys) != len(layout.entries):
@@ -200,10 +212,11 @@ def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: i
     if i_infos:
         _gather(keep, addr, n, i_infos, i_offs, i64, threads)
     out = ArenaStateDict()
+    storages = {F32: (f32.untyped_storage(), es_f, dt_f), I64: (i64.untyped_storage(), es_i, dt_i)}
     for key in keys:
         e = layout[key]
-        src = f32 if e.region == F32 else i64
-        out[key] = src[e.offset : e.offset + e.numel].view(e.shape)
+        storage, es, dt = storages[e.region]
+        out[key] = _owned_view(storage, e.offset * es, e.numel * es, dt, e.shape)
     out.arena_f32, out.arena_i64 = f32, i64
     out.layout_signature = layout.signature
     return out

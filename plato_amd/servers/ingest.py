@@ -15,7 +15,9 @@ objects) are handed to ``pickle.loads`` exactly as the reference does.
 
 from __future__ import annotations
 
+import logging
 import pickle
+import sys
 
 from .. import ingest
 from ..arena import ArenaLayout
@@ -27,6 +29,8 @@ class WireIngestMixin:
     #: copy each payload to HBM as soon as it arrives (the aggregation hook then
     #: adopts it); payloads must not be modified in place after arrival
     stage_on_arrival = False
+    #: size payloads by their wire bytes instead of re-pickling them (see _wire_payload_size)
+    wire_size_accounting = True
 
     def _ingest_layout(self):
         try:
@@ -46,18 +50,28 @@ class WireIngestMixin:
         ``payload`` is the payload's bytes, or the list of its transport chunks
         (joined natively, in parallel, instead of ``b"".join``).
         """
+        return self._ingest(payload)[0]
+
+    def _ingest(self, payload):
+        """(data, wire length if parsed natively else None)."""
         data = ingest.join(payload) if isinstance(payload, (list, tuple)) else payload
         try:
-            return ingest.loads(data, layout=self._ingest_layout(), pin=self.ingest_pinned)
+            return ingest.loads(data, layout=self._ingest_layout(), pin=self.ingest_pinned), len(data)
         except (ingest.IngestError, KeyError, ValueError):
-            return pickle.loads(data)
+            return pickle.loads(data), None
 
     async def _client_payload_arrived(self, sid, client_id):
         """plato/servers/base.py:817-831 with the join and the unpickle done natively."""
         assert len(self.client_chunks[sid]) > 0 and client_id in self.training_clients
 
-        _data = self.ingest_payload(self.client_chunks[sid])
+        _data, wire_len = self._ingest(self.client_chunks[sid])
         self.client_chunks[sid] = []
+        sizes = self.__dict__.setdefault("_plato_amd_wire_sizes", {})
+        if self.client_payload[sid] is None:
+            sizes[sid] = []
+        if sizes.get(sid) is not None:
+            # the bytes this part arrived as, for the size accounting below
+            sizes[sid].append(wire_len)
         if self.stage_on_arrival and isinstance(_data, ingest.ArenaStateDict):
             layout = self._ingest_layout()
             if layout is not None:
@@ -70,3 +84,35 @@ class WireIngestMixin:
         else:
             self.client_payload[sid] = [self.client_payload[sid]]
             self.client_payload[sid].append(_data)
+
+    def _wire_payload_size(self, sid):
+        """``Σ sys.getsizeof(pickle.dumps(part))`` of a payload, from the bytes it arrived as.
+
+        The reference re-pickles every payload only to measure it
+        (servers/base.py:839-846), ~45-130 ms per ResNet-18 payload.  A dict of
+        tensors re-pickles to its wire length up to the decimal length of each
+        storage's address, which pickle writes as the storage key (so the
+        reference's own figure moves by a byte per tensor with where the
+        allocator placed it); None when a part was not a native-ingested dict.
+        """
+        parts = self.__dict__.get("_plato_amd_wire_sizes", {}).pop(sid, None)
+        payload = self.client_payload[sid]
+        count = len(payload) if isinstance(payload, list) else 1
+        if not self.wire_size_accounting or not parts or None in parts or len(parts) != count:
+            return None
+        return sum(n + sys.getsizeof(b"") for n in parts)
+
+    async def _client_payload_done(self, sid, client_id, s3_key=None):
+        """plato/servers/base.py:833-857 with the payload sized by its wire bytes, not re-pickled."""
+        payload_size = self._wire_payload_size(sid) if s3_key is None else None
+        if payload_size is None:
+            await super()._client_payload_done(sid, client_id, s3_key)
+            return
+        logging.info(
+            "[%s] Received %.2f MB of payload data from client #%d.",
+            self,
+            payload_size / 1024**2,
+            client_id,
+        )
+        self.comm_overhead += payload_size / 1024**2
+        await self.process_client_info(client_id, sid)

@@ -16,6 +16,7 @@ import json
 import os
 import sys
 import tempfile
+from collections import OrderedDict
 
 import numpy as np
 import torch
@@ -121,8 +122,60 @@ def main():
     same = all(torch.equal(state[n], exp[n].to(state[n].dtype)) for n in state)
     calls["model_matches_reference_chain"] = bool(same)
     calls["total_samples"] = server.total_samples == sum(ns)
+    # clones: each payload tensor with its own storage, as a client's state_dict has
+    calls["ingest"] = ingest_wiring(fedavg, model, [OrderedDict((n, t.clone()) for n, t in p.items())
+                                                    for p in payloads[:2]])
     with open(out_path, "w") as f:
         json.dump(calls, f)
+
+
+def ingest_wiring(fedavg, model, payloads):
+    """WireIngestMixin inside the reference's own arrival path (servers/base.py:775-857).
+
+    The reference's _client_report_arrived and _client_chunk_arrived run
+    unmodified; the mixin replaces the join + pickle.loads and the re-pickling
+    size accounting.  Compared with an unmodified reference server fed the same
+    socket chunks: the payload handed to process_client_info and comm_overhead.
+    """
+    import pickle
+    import types
+
+    from plato_amd.servers import WireIngestMixin
+
+    class Wire(WireIngestMixin, fedavg.Server):
+        ingest_pinned = False
+
+    def run(cls):
+        server = cls(model=lambda: model)
+        server.init_trainer()
+        handed = []
+
+        async def process_client_info(client_id, sid):
+            handed.append(server.client_payload[sid])
+
+        server.process_client_info = process_client_info
+        server.comm_simulation = False  # the socket.io path (servers/base.py:813-857)
+        server.comm_overhead = 0.0
+        for c, payload in enumerate(payloads):
+            sid = f"sid{c}"
+            server.training_clients[c + 1] = {"start_time": 0.0, "starting_round": 0}
+            report = types.SimpleNamespace(client_id=c + 1, num_samples=10, training_time=0.0,
+                                           processing_time=0.0, comm_time=0.0)
+            data = pickle.dumps(payload)
+            asyncio.run(server._client_report_arrived(sid, c + 1, pickle.dumps(report)))
+            for i in range(0, len(data), 2**20):
+                asyncio.run(server._client_chunk_arrived(sid, data[i:i + 2**20]))
+            asyncio.run(server._client_payload_arrived(sid, c + 1))
+            asyncio.run(server._client_payload_done(sid, c + 1))
+        return handed, server.comm_overhead
+
+    got, got_mb = run(Wire)
+    exp, exp_mb = run(fedavg.Server)
+    same = len(got) == len(exp) == len(payloads) and all(
+        list(g) == list(e) and all(torch.equal(g[k], e[k]) and g[k].dtype == e[k].dtype for k in e)
+        for g, e in zip(got, exp))
+    return {"payload_matches": bool(same), "arena_backed": all(type(g).__name__ == "ArenaStateDict" for g in got),
+            "comm_overhead_bytes": [got_mb * 1024**2, exp_mb * 1024**2]}
 
 
 if __name__ == "__main__":

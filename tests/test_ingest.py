@@ -225,3 +225,80 @@ def test_wire_ingest_mixin_replaces_pickle_loads():
     s.client_payload["sid"] = None
     asyncio.run(s._client_payload_arrived("sid", 3))
     assert s.client_payload["sid"] == ["features", 1, 2]
+
+
+def test_repickled_payload_is_payload_sized():
+    """Arena-backed tensors re-pickle their own bytes only (servers/base.py:839-846 sizes payloads so).
+
+    pickle writes each storage's address as its key, so sizes move by a byte
+    per tensor with where the allocator put the storage; nothing else differs.
+    """
+    spec = workloads.resnet(18)
+    sd = state_dict(spec, 7)
+    data = pickle.dumps(sd)
+    ref = len(pickle.dumps(pickle.loads(data)))
+    slack = 2 * len(sd) + 64
+    for got in (ingest.loads(data, layout=ArenaLayout.from_shapes(spec)), ingest.loads(data)):
+        n = len(pickle.dumps(got))
+        assert abs(n - ref) <= slack, (n, ref)
+        assert_same(pickle.loads(pickle.dumps(got)), sd)
+        # the storages are slices of the arena (no copy) and keep it alive
+        first = next(iter(got.values()))
+        assert first.untyped_storage().nbytes() == first.numel() * first.element_size()
+
+
+def test_wire_size_accounting_matches_repickling():
+    """_client_payload_done (servers/base.py:833-857): same log, comm_overhead and hand-off, no re-pickle."""
+    import asyncio
+
+    from plato_amd.servers import WireIngestMixin
+
+    spec = workloads.lenet5()
+    base = state_dict(spec, 8)
+    parts = [pickle.dumps(state_dict(spec, 9)), pickle.dumps(state_dict(spec, 10))]
+
+    class Algo:
+        def extract_weights(self):
+            return base
+
+    class Reference:  # the reference's sizing, as the mixin's fallback
+        async def _client_payload_done(self, sid, client_id, s3_key=None):
+            payload = self.client_payload[sid]
+            items = payload if isinstance(payload, list) else [payload]
+            self.comm_overhead += sum(sys.getsizeof(pickle.dumps(p)) for p in items) / 1024**2
+            await self.process_client_info(client_id, sid)
+
+    class S(WireIngestMixin, Reference):
+        ingest_pinned = False
+
+        def __init__(self, wire):
+            self.wire_size_accounting = wire
+            self.algorithm = Algo()
+            self.client_chunks = {"sid": []}
+            self.client_payload = {"sid": None}
+            self.training_clients = {3: 1}
+            self.comm_overhead = 0.0
+            self.handed = []
+
+        async def process_client_info(self, client_id, sid):
+            self.handed.append((client_id, sid))
+
+        async def receive(self, payload_parts):
+            for p in payload_parts:
+                self.client_chunks["sid"] = [p[i:i + 4096] for i in range(0, len(p), 4096)]
+                await self._client_payload_arrived("sid", 3)
+            await self._client_payload_done("sid", 3)
+
+    for n_parts in (1, 2):
+        fast, slow = S(True), S(False)
+        asyncio.run(fast.receive(parts[:n_parts]))
+        asyncio.run(slow.receive(parts[:n_parts]))
+        assert fast.handed == slow.handed == [(3, "sid")]
+        n_tensors = n_parts * len(spec)
+        assert abs(fast.comm_overhead - slow.comm_overhead) * 1024**2 <= 2 * n_tensors + 64
+        assert fast.comm_overhead * 1024**2 == sum(len(p) + sys.getsizeof(b"") for p in parts[:n_parts])
+    # a part that pickle.loads had to take is sized the reference's way (a list payload is
+    # taken as its parts there, servers/base.py:840-842)
+    s = S(True)
+    asyncio.run(s.receive([pickle.dumps(["features", 1, 2])]))
+    assert s.comm_overhead * 1024**2 == sum(sys.getsizeof(pickle.dumps(x)) for x in ["features", 1, 2])
