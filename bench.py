@@ -461,6 +461,23 @@ def host_inclusive(engine, layout, base, slab, k, weights, dev):
     for ch in chunked:
         ingest.loads_chunks(ch, layout=layout, pin=True)
     t_chunks = (time.perf_counter() - t0) / 8
+    # comm_simulation (Plato's default): the payload arrives as a file the client
+    # pickle.dump'ed (clients/base.py:372-386), pickle.load'ed at servers/base.py:791-792
+    import tempfile
+
+    with tempfile.NamedTemporaryFile(suffix=".pth") as f:
+        f.write(wire[0])
+        f.flush()
+        t_file_ref, t_file = [], []
+        ingest.load_file(f.name, layout=layout, pin=True)
+        for _ in range(4):
+            t0 = time.perf_counter()
+            with open(f.name, "rb") as fh:
+                pickle.load(fh)
+            t_file_ref.append(time.perf_counter() - t0)
+            t0 = time.perf_counter()
+            ingest.load_file(f.name, layout=layout, pin=True)
+            t_file.append(time.perf_counter() - t0)
     # size accounting: the reference re-pickles each payload to log its size
     # (servers/base.py:839-846); WireIngestMixin takes the wire length instead
     loaded = [pickle.loads(d) for d in wire[:4]]
@@ -477,6 +494,8 @@ def host_inclusive(engine, layout, base, slab, k, weights, dev):
         "pickle_loads_ms_per_payload": round(t_pickle * 1e3, 3),
         "socket_chunks": {"reference_join_pickle_loads_ms": round(t_ref_chunks * 1e3, 3),
                           "native_join_parse_gather_ms": round(t_chunks * 1e3, 3)},
+        "comm_simulation_file": {"reference_pickle_load_ms": round(statistics.median(t_file_ref) * 1e3, 3),
+                                 "native_read_parse_gather_ms": round(statistics.median(t_file) * 1e3, 3)},
         "size_accounting": {"reference_repickle_ms": round(t_resize * 1e3, 3), "native": "wire length, no copy"},
         "note": "pickled payload bytes -> libplato_ingest parse + gather into pinned arenas -> H2D -> "
                 "kernel -> D2H (replaces pickle.loads at servers/base.py:822)"}

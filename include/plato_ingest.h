@@ -41,6 +41,7 @@ extern "C" {
                                           or a destination buffer too small     */
 #define PLATO_INGEST_ENOCODEC (-6)     /* libzstd.so.1 not available            */
 #define PLATO_INGEST_EUNKNOWNSIZE (-7) /* zstd frame without a content size     */
+#define PLATO_INGEST_EIO (-8)          /* read error or short file              */
 
 /* dtype codes (torch storage classes) */
 #define PLATO_DT_F32 0  /* FloatStorage    */
@@ -98,6 +99,17 @@ int plato_ingest_gather(const uint8_t* buf, size_t len, const plato_ingest_tenso
  */
 int plato_ingest_join(const uint8_t* const* chunks, const size_t* lens, int n, uint8_t* dst, size_t dst_len,
                       int threads);
+
+/*
+ * Read the first len bytes of an open file (offset 0, pread, file position
+ * untouched) into dst, in 4 MiB pieces on the same thread pool.  Under
+ * comm_simulation (Plato's default, plato/clients/base.py:92-96) a client's
+ * payload reaches the server as a file it pickle.dump'ed
+ * (clients/base.py:372-386) and the server pickle.load's it
+ * (plato/servers/base.py:791-792); this is the read half of that, parse and
+ * gather being the rest.  Returns len, or PLATO_INGEST_EIO.
+ */
+int64_t plato_ingest_read_fd(int fd, uint8_t* dst, size_t len, int threads);
 
 /*
  * zstd-compressed payloads.  Plato's model_compress outbound processor sends

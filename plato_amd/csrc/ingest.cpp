@@ -8,6 +8,9 @@
 // whitelisted callables, everything else is rejected.  All reads are bounds
 // checked against [buf, buf + len).
 #include <dlfcn.h>
+#include <unistd.h>
+
+#include <cerrno>
 
 #include <algorithm>
 #include <atomic>
@@ -736,6 +739,44 @@ int plato_ingest_join(const uint8_t* const* chunks, const size_t* lens, int n, u
   }
   g_err.clear();
   return 0;
+}
+
+int64_t plato_ingest_read_fd(int fd, uint8_t* dst, size_t len, int threads) {
+  if (fd < 0 || (!dst && len)) {
+    g_err = "bad argument";
+    return PLATO_INGEST_EINVAL;
+  }
+  constexpr size_t kChunk = size_t(4) << 20;
+  const size_t n_pieces = (len + kChunk - 1) / kChunk;
+  std::atomic<int> failed{0};
+  auto read_piece = [&](size_t k) {
+    const size_t off = k * kChunk, want = std::min(kChunk, len - off);
+    size_t got = 0;
+    while (got < want) {
+      const ssize_t r = ::pread(fd, dst + off + got, want - got, off_t(off + got));
+      if (r > 0) {
+        got += size_t(r);
+      } else if (r < 0 && errno == EINTR) {
+        continue;
+      } else {  // error, or the file ended before len
+        failed.store(r < 0 ? errno : -1);
+        return;
+      }
+    }
+  };
+  int nt = threads > 0 ? threads : int(std::max(1u, std::thread::hardware_concurrency()));
+  nt = std::min({nt, 16, int(std::max<size_t>(1, n_pieces))});
+  if (nt <= 1) {
+    for (size_t k = 0; k < n_pieces; ++k) read_piece(k);
+  } else {
+    Pool::get().run(n_pieces, nt, read_piece);
+  }
+  if (const int e = failed.load()) {
+    g_err = e > 0 ? std::string("read: ") + std::strerror(e) : std::string("file shorter than expected");
+    return PLATO_INGEST_EIO;
+  }
+  g_err.clear();
+  return int64_t(len);
 }
 
 size_t plato_ingest_zstd_bound(size_t len) {

@@ -80,6 +80,7 @@ def lib():
             h.plato_ingest_join.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
                                             ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
             for name, res, args in (
+                ("plato_ingest_read_fd", ctypes.c_int64, [ctypes.c_int, vp, sz, ctypes.c_int]),
                 ("plato_ingest_zstd_available", ctypes.c_int, []),
                 ("plato_ingest_zstd_content_size", ctypes.c_int64, [vp, sz]),
                 ("plato_ingest_zstd_decompress", ctypes.c_int64, [vp, sz, vp, sz]),
@@ -245,20 +246,45 @@ def join(chunks, threads: int = 0, out: np.ndarray | None = None) -> np.ndarray:
     return out[:total]
 
 
-def loads_chunks(chunks, layout: ArenaLayout | None = None, pin: bool = False, threads: int = 0):
-    """``pickle.loads(b"".join(chunks))`` for a chunked payload, natively (join + parse + gather).
+def _scratch_buffer(nbytes: int) -> np.ndarray:
+    """This thread's reusable byte buffer, grown to at least ``nbytes``.
 
-    The joined bytes go to a per-thread scratch buffer that is reused (the
-    tensors are gathered out of it), so steady-state joins take no page faults.
+    Received bytes only live until their tensors are gathered out of them, so
+    one buffer per thread serves every payload and steady-state reads and
+    joins take no page faults.
     """
     buf = getattr(_scratch, "buf", None)
-    data = join(chunks, threads, out=buf)
-    if buf is None or data.base is not buf:
-        _scratch.buf = data if data.base is None else data.base
+    if buf is None or buf.size < nbytes:
+        buf = _scratch.buf = np.empty(max(nbytes, 1), dtype=np.uint8)
+    return buf
+
+
+def loads_chunks(chunks, layout: ArenaLayout | None = None, pin: bool = False, threads: int = 0):
+    """``pickle.loads(b"".join(chunks))`` for a chunked payload, natively (join + parse + gather)."""
+    total = sum(memoryview(c).nbytes for c in chunks)
+    data = join(chunks, threads, out=_scratch_buffer(total))
     return loads(data, layout=layout, pin=pin, threads=threads)
 
 
-EFORMAT, ECAPACITY, ENOCODEC, EUNKNOWNSIZE = -3, -5, -6, -7
+def read_file(path: str, out: np.ndarray | None = None, threads: int = 0) -> np.ndarray:
+    """The bytes of the file at ``path`` (parallel pread), into ``out`` if it is large enough.
+
+    Raises what ``open(path, "rb")`` raises for a missing or unreadable file.
+    """
+    fd = os.open(path, os.O_RDONLY)
+    try:
+        size = os.fstat(fd).st_size
+        if out is None or out.size < size:
+            out = np.empty(max(size, 1), dtype=np.uint8)
+        rc = lib().plato_ingest_read_fd(fd, out.ctypes.data, size, threads)
+        if rc < 0:
+            raise OSError(f"{path}: {lib().plato_ingest_last_error().decode()}")
+        return out[:size]
+    finally:
+        os.close(fd)
+
+
+EFORMAT, ECAPACITY, ENOCODEC, EUNKNOWNSIZE, EIO = -3, -5, -6, -7, -8
 
 
 def zstd_available() -> bool:
@@ -316,7 +342,11 @@ def loads_compressed(data, layout: ArenaLayout | None = None, pin: bool = False,
     return loads(zstd_decompress(data), layout=layout, pin=pin, threads=threads)
 
 
-def load_file(path: str, layout: ArenaLayout | None = None, pin: bool = False) -> OrderedDict:
-    """``pickle.load(open(path, 'rb'))`` of a comm_simulation payload file, natively."""
-    data = np.fromfile(path, dtype=np.uint8)
-    return loads(data, layout=layout, pin=pin)
+def load_file(path: str, layout: ArenaLayout | None = None, pin: bool = False, threads: int = 0) -> OrderedDict:
+    """``pickle.load(open(path, 'rb'))`` of a comm_simulation payload file, natively.
+
+    The file is read (in parallel) into this thread's scratch buffer and the
+    tensors are gathered out of it, as for :func:`loads_chunks`.
+    """
+    data = read_file(path, out=_scratch_buffer(os.path.getsize(path)), threads=threads)
+    return loads(data, layout=layout, pin=pin, threads=threads)

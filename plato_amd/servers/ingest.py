@@ -1,9 +1,12 @@
 """Server-side payload ingestion hook: native parsing of arriving payload bytes.
 
 The reference joins a client's socket.io chunks and calls ``pickle.loads``
-on them (plato/servers/base.py:817-831).  :class:`WireIngestMixin` overrides
-that one method so the bytes are parsed by libplato_ingest.so directly into a
-pinned arena laid out like the engine's (baseline key order).  The result is a
+on them (plato/servers/base.py:817-831), or, under comm_simulation (the
+default), ``pickle.load``s the file the client wrote (:775-811).
+:class:`WireIngestMixin` overrides those methods so the bytes are parsed by
+libplato_ingest.so directly into a pinned arena laid out like the engine's
+(baseline key order), and sizes payloads by the bytes they arrived as instead
+of re-pickling them (:794-796, :839-846).  The result is a
 real ``OrderedDict`` of CPU tensors (an :class:`~plato_amd.ingest.ArenaStateDict`),
 so every later step of the reference — inbound processors, ``weights_received``,
 size accounting, ``self.updates`` — sees what ``pickle.loads`` would have
@@ -16,6 +19,7 @@ objects) are handed to ``pickle.loads`` exactly as the reference does.
 from __future__ import annotations
 
 import logging
+import os
 import pickle
 import sys
 
@@ -59,6 +63,55 @@ class WireIngestMixin:
             return ingest.loads(data, layout=self._ingest_layout(), pin=self.ingest_pinned), len(data)
         except (ingest.IngestError, KeyError, ValueError):
             return pickle.loads(data), None
+
+    def _load_payload_file(self, path):
+        """(payload, file length if parsed natively else None) of a comm_simulation file."""
+        try:
+            return ingest.load_file(path, layout=self._ingest_layout(), pin=self.ingest_pinned), os.path.getsize(path)
+        except (ingest.IngestError, KeyError, ValueError):
+            with open(path, "rb") as payload_file:
+                return pickle.load(payload_file), None
+
+    async def _client_report_arrived(self, sid, client_id, report):
+        """plato/servers/base.py:775-811 with the payload file parsed natively and sized by its length.
+
+        ``comm_simulation`` (the default, clients/base.py:92-96) hands payloads
+        over as files the clients ``pickle.dump`` (clients/base.py:372-386); the
+        reference ``pickle.load``s one and re-pickles it to size it (:791-796).
+        """
+        if not self.comm_simulation:
+            await super()._client_report_arrived(sid, client_id, report)
+            return
+        from plato.config import Config
+
+        self.reports[sid] = pickle.loads(report)
+        self.client_payload[sid] = None
+        self.client_chunks[sid] = []
+
+        model_name = Config().trainer.model_name if hasattr(Config().trainer, "model_name") else "custom"
+        model_name = model_name.replace("/", "_")
+        checkpoint_path = Config().params["checkpoint_path"]
+        payload, file_len = self._load_payload_file(f"{checkpoint_path}/{model_name}_client_{client_id}.pth")
+        self.client_payload[sid] = payload
+        if self.stage_on_arrival and isinstance(payload, ingest.ArenaStateDict):
+            layout = self._ingest_layout()
+            if layout is not None:
+                self.aggregation_engine().prestage(payload, layout)
+
+        if self.wire_size_accounting and file_len is not None:
+            payload_size = (file_len + sys.getsizeof(b"")) / 1024**2
+        else:
+            payload_size = sys.getsizeof(pickle.dumps(payload)) / 1024**2
+        logging.info(
+            "[%s] Received %.2f MB of payload data from client #%d (simulated).",
+            self,
+            payload_size,
+            client_id,
+        )
+        self.comm_overhead += payload_size
+        self.uplink_comm_time[client_id] = payload_size / (self.uplink_bandwidth / 8)
+
+        await self.process_client_info(client_id, sid)
 
     async def _client_payload_arrived(self, sid, client_id):
         """plato/servers/base.py:817-831 with the join and the unpickle done natively."""

@@ -145,7 +145,9 @@ def ingest_wiring(fedavg, model, payloads):
     class Wire(WireIngestMixin, fedavg.Server):
         ingest_pinned = False
 
-    def run(cls):
+    def run(cls, simulated=False):
+        from plato.config import Config
+
         server = cls(model=lambda: model)
         server.init_trainer()
         handed = []
@@ -154,7 +156,7 @@ def ingest_wiring(fedavg, model, payloads):
             handed.append(server.client_payload[sid])
 
         server.process_client_info = process_client_info
-        server.comm_simulation = False  # the socket.io path (servers/base.py:813-857)
+        server.comm_simulation = simulated  # files (:775-811) or socket.io chunks (:813-857)
         server.comm_overhead = 0.0
         for c, payload in enumerate(payloads):
             sid = f"sid{c}"
@@ -162,6 +164,14 @@ def ingest_wiring(fedavg, model, payloads):
             report = types.SimpleNamespace(client_id=c + 1, num_samples=10, training_time=0.0,
                                            processing_time=0.0, comm_time=0.0)
             data = pickle.dumps(payload)
+            if simulated:  # what the client's _send writes (clients/base.py:372-386)
+                os.makedirs(Config().params["checkpoint_path"], exist_ok=True)
+                name = Config().trainer.model_name.replace("/", "_")
+                with open(f"{Config().params['checkpoint_path']}/{name}_client_{c + 1}.pth", "wb") as f:
+                    pickle.dump(payload, f)
+                server.uplink_comm_time = {}
+                asyncio.run(server._client_report_arrived(sid, c + 1, pickle.dumps(report)))
+                continue
             asyncio.run(server._client_report_arrived(sid, c + 1, pickle.dumps(report)))
             for i in range(0, len(data), 2**20):
                 asyncio.run(server._client_chunk_arrived(sid, data[i:i + 2**20]))
@@ -169,13 +179,17 @@ def ingest_wiring(fedavg, model, payloads):
             asyncio.run(server._client_payload_done(sid, c + 1))
         return handed, server.comm_overhead
 
-    got, got_mb = run(Wire)
-    exp, exp_mb = run(fedavg.Server)
-    same = len(got) == len(exp) == len(payloads) and all(
-        list(g) == list(e) and all(torch.equal(g[k], e[k]) and g[k].dtype == e[k].dtype for k in e)
-        for g, e in zip(got, exp))
-    return {"payload_matches": bool(same), "arena_backed": all(type(g).__name__ == "ArenaStateDict" for g in got),
-            "comm_overhead_bytes": [got_mb * 1024**2, exp_mb * 1024**2]}
+    result = {}
+    for mode, simulated in (("socket", False), ("simulated", True)):
+        got, got_mb = run(Wire, simulated)
+        exp, exp_mb = run(fedavg.Server, simulated)
+        same = len(got) == len(exp) == len(payloads) and all(
+            list(g) == list(e) and all(torch.equal(g[k], e[k]) and g[k].dtype == e[k].dtype for k in e)
+            for g, e in zip(got, exp))
+        result[mode] = {"payload_matches": bool(same),
+                        "arena_backed": all(type(g).__name__ == "ArenaStateDict" for g in got),
+                        "comm_overhead_bytes": [got_mb * 1024**2, exp_mb * 1024**2]}
+    return result
 
 
 if __name__ == "__main__":

@@ -30,7 +30,8 @@ def test_hook_dispatch_in_reference_process_reports(tmp_path):
     assert calls["cb_received"] == 1 and calls["cb_aggregated"] == 1
     assert calls["model_matches_reference_chain"]
     assert calls["total_samples"]
-    ing = calls["ingest"]              # WireIngestMixin in the reference's arrival path
-    assert ing["payload_matches"] and ing["arena_backed"]
-    got, exp = ing["comm_overhead_bytes"]
-    assert abs(got - exp) <= 2 * 2 * 122 + 64  # storage-key digits only (see test_ingest.py)
+    for mode in ("socket", "simulated"):  # WireIngestMixin in the reference's arrival paths
+        ing = calls["ingest"][mode]
+        assert ing["payload_matches"] and ing["arena_backed"], mode
+        got, exp = ing["comm_overhead_bytes"]
+        assert abs(got - exp) <= 2 * 2 * 122 + 64, mode  # storage-key digits only (see test_ingest.py)
