@@ -55,7 +55,7 @@ int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n,
                           int blocks, hipStream_t stream);
 
 /* plato_agg_entry_norms_f32 kernel variants (bitwise identical results):
- *   0 = producer / consumer (the default): per (entry, client) one wave streams
+ *   0 = producer / consumer: per (entry, client) one wave streams
  *       x and b into an 8-stage LDS ring (LDS-DMA) and forms the deltas of
  *       512-element tiles, the other wave only walks the chains
  *   1 = one wavefront per (entry, client), one-tile register prefetch (first version)
@@ -63,7 +63,10 @@ int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n,
  *       forming its own deltas and walking its chains
  *   4, 5 = variant 8 without the fma chains / without the loads: timing probes
  *          only, their outputs are meaningless
- *   6, 7 = producer / consumer with 1024- / 256-element tiles (6 / 12 stages) */
+ *   6, 7 = producer / consumer with 1024- / 256-element tiles (6 / 12 stages)
+ *   9, 10 = producer / consumer writing the delta tiles transposed (each chain's
+ *       steps contiguous), the chain wave reading 4 steps per ds_read_b128;
+ *       512- / 1024-element tiles; 9 is the default */
 int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
                                const float* d_base_f32, const int64_t* d_base_i64,
                                const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,

@@ -789,10 +789,25 @@ __device__ __forceinline__ void pc_issue(const float* x, const float* b, float (
   }
 }
 
-template <int T, int PS, bool HAS_BASE>
-__device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int lane, float (*raw)[2][T],
-                        float (*dbuf)[T]) {
-  constexpr int kRT = T, kPS = PS;
+// d tile layout: natural (element t of the tile at t), or transposed (TR): chain
+// c's steps contiguous in row c, rows kTS floats apart.  kTS = T/8 + 4 keeps the
+// producer's ds_write_b32 (32-lane groups, banks (a/4) mod 32) and the chain
+// wave's ds_read_b128 (16-lane groups, banks (a/4) mod 64) conflict-free, and
+// the chain wave reads 4 steps per instruction instead of 1.
+template <int T, bool TR>
+struct DTile {
+  static constexpr int kTS = T / 8 + 4;
+  static constexpr int kSize = TR ? 8 * kTS : T;
+};
+
+// Producer wave of the producer / consumer norms kernels: streams client x (and
+// the baseline) through its kPS-deep LDS-DMA ring `raw` and writes tile tt of
+// d = x - b to dtile + (tt & 1) * dstride (natural or transposed, DTile), then
+// meets the chain wave at one s_barrier per tile.
+template <int T, int PS, bool HAS_BASE, bool TR>
+__device__ void pc_produce(const NormArgs& a, const Chunk ch, const float* x, int lane, float (*raw)[2][T],
+                           float* dtile, int dstride) {
+  constexpr int kRT = T, kPS = PS, kTS = DTile<T, TR>::kTS;
   constexpr int kPer = (HAS_BASE ? 2 : 1) * (kRT / 256);  // glds per stage
   static_assert((kPS - 1) * kPer < 64, "vmcnt range");
   const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
@@ -800,52 +815,93 @@ __device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int 
   const uint64_t g_first = ch.begin >> 2;
   const uint64_t ntiles = (delta + m + kRT - 1) / kRT;
   const uint64_t gmax = (a.n_f32 >> 2) - 1;
-  const float* x = sld(a.xf, i);
-  if (wave == 1) {  // producer
 #pragma unroll
-    for (int p = 0; p < kPS - 1; ++p)
-      if (uint64_t(p) < ntiles) pc_issue<T, HAS_BASE>(x, a.base_f, raw, p, g_first + uint64_t(p) * (kRT / 4), gmax, lane);
-    for (uint64_t tt = 0; tt < ntiles; ++tt) {
-      // slot (tt - 1) % kPS was read by this wave's previous d pass
-      if (tt + kPS - 1 < ntiles) {
-        pc_issue<T, HAS_BASE>(x, a.base_f, raw, uint32_t((tt + kPS - 1) % kPS), g_first + (tt + kPS - 1) * (kRT / 4),
-                           gmax, lane);
-        wait_vmcnt<(kPS - 1) * kPer>();
-      } else {
-        wait_vmcnt<0>();
-      }
-      const uint32_t slot = uint32_t(tt % kPS);
-      f4* d = reinterpret_cast<f4*>(dbuf[tt & 1]);
-#pragma unroll
-      for (int r = 0; r < kRT / 256; ++r) {
-        const f4 xv = *(reinterpret_cast<const f4*>(raw[slot][0]) + r * 64 + lane);
-        if (HAS_BASE) {
-          const f4 bv = *(reinterpret_cast<const f4*>(raw[slot][1]) + r * 64 + lane);
-          d[r * 64 + lane] = xv - bv;  // fp32, as compute_weight_deltas
-        } else {
-          d[r * 64 + lane] = xv;
-        }
-      }
-      wait_lgkm0();  // d tile written (the glds of later stages stay in flight)
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      __builtin_amdgcn_s_barrier();  // tile tt ready; the chain wave is done with tile tt - 2
-      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+  for (int p = 0; p < kPS - 1; ++p)
+    if (uint64_t(p) < ntiles) pc_issue<T, HAS_BASE>(x, a.base_f, raw, p, g_first + uint64_t(p) * (kRT / 4), gmax, lane);
+  for (uint64_t tt = 0; tt < ntiles; ++tt) {
+    // slot (tt - 1) % kPS was read by this wave's previous d pass
+    if (tt + kPS - 1 < ntiles) {
+      pc_issue<T, HAS_BASE>(x, a.base_f, raw, uint32_t((tt + kPS - 1) % kPS), g_first + (tt + kPS - 1) * (kRT / 4),
+                         gmax, lane);
+      wait_vmcnt<(kPS - 1) * kPer>();
+    } else {
+      wait_vmcnt<0>();
     }
-    wait_vmcnt<0>();
-    return;
+    const uint32_t slot = uint32_t(tt % kPS);
+    float* dt = dtile + (tt & 1) * dstride;
+#pragma unroll
+    for (int r = 0; r < kRT / 256; ++r) {
+      f4 dv = *(reinterpret_cast<const f4*>(raw[slot][0]) + r * 64 + lane);
+      if (HAS_BASE) dv = dv - *(reinterpret_cast<const f4*>(raw[slot][1]) + r * 64 + lane);  // fp32, as
+                                                                                             // compute_weight_deltas
+      if constexpr (TR) {
+        // tile elements 256r + 4 lane + j: chain 4 (lane & 1) + j, step 32 r + lane / 2
+        float* col = dt + 32 * r + (lane >> 1) + 4 * (lane & 1) * kTS;
+        col[0] = dv.x;
+        col[kTS] = dv.y;
+        col[2 * kTS] = dv.z;
+        col[3 * kTS] = dv.w;
+      } else {
+        reinterpret_cast<f4*>(dt)[r * 64 + lane] = dv;
+      }
+    }
+    wait_lgkm0();  // d tile written (the glds of later stages stay in flight)
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_barrier();  // tile tt ready; the chain wave is done with tile tt - 2
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
   }
-  // chain wave
-  const int pj = int((uint32_t(lane) + delta) & 7u);
-  const int64_t s_shift = (uint32_t(lane) + delta) >= 8u ? -1 : 0;
+  wait_vmcnt<0>();
+}
+
+// Chain wave of the producer / consumer norms kernels: walks the 8 chains of G
+// clients at once (lanes 8g..8g+7 = client g, lanes >= 8G duplicating them),
+// client g's tile tt at dtile + (tt & 1) * dstride + g * gstride, one s_barrier
+// per tile.  Returns this lane's chain sum (torch's accumulator lane c & 7).
+template <int T, bool TR, int G>
+__device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstride, int gstride) {
+  constexpr int kRT = T, kTS = DTile<T, TR>::kTS;
+  const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+  const uint32_t delta = ch.begin & 3u;
+  const uint64_t ntiles = (delta + m + kRT - 1) / kRT;
+  const int c = lane & 7, g = (lane >> 3) % G;  // lanes 8g..8g+7: client g's chains
+  const int pj = int((uint32_t(c) + delta) & 7u);
+  const int64_t s_shift = (uint32_t(c) + delta) >= 8u ? -1 : 0;
   const int64_t s_end = int64_t(m / kNormLanes);
   float acc = 0.f;
   for (uint64_t tt = 0; tt < ntiles; ++tt) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_s_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const float* p = dbuf[tt & 1] + pj;
+    const float* tile = dtile + (tt & 1) * dstride + g * gstride;
+    const float* p = TR ? tile + pj * kTS : tile + pj;
+    constexpr int kStep = TR ? 1 : 8;  // floats between a chain's consecutive steps
     const int64_t s0 = int64_t(tt) * (kRT / kNormLanes) + s_shift;
-    if (tt >= 1 && int64_t(tt + 1) * (kRT / kNormLanes) <= s_end) {
+    if (TR && tt >= 1 && int64_t(tt + 1) * (kRT / kNormLanes) <= s_end) {
+      // 16 steps per block as 4 ds_read_b128, the next block's in flight
+      constexpr int kNB = kRT / kNormLanes / 16;
+      const f4* q4 = reinterpret_cast<const f4*>(p);
+      f4 cur[4], nxt[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cur[q] = q4[q];
+#pragma unroll
+      for (int blk = 0; blk < kNB; ++blk) {
+        if (blk + 1 < kNB) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) nxt[q] = q4[4 * (blk + 1) + q];
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc = __builtin_fmaf(cur[q].x, cur[q].x, acc);
+          acc = __builtin_fmaf(cur[q].y, cur[q].y, acc);
+          acc = __builtin_fmaf(cur[q].z, cur[q].z, acc);
+          acc = __builtin_fmaf(cur[q].w, cur[q].w, acc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
+      }
+    } else if (!TR && tt >= 1 && int64_t(tt + 1) * (kRT / kNormLanes) <= s_end) {
       constexpr int kCB = 16, kNB = kRT / kNormLanes / kCB;
       float cur[kCB], nxt[kCB];
 #pragma unroll
@@ -863,16 +919,29 @@ __device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int 
 #pragma unroll
         for (int q = 0; q < kCB; ++q) cur[q] = nxt[q];
       }
-    } else if (lane < kNormLanes) {
+    } else if (lane < kNormLanes * G) {
       for (int u = 0; u < kRT / kNormLanes; ++u) {
         const int64_t st = s0 + u;
         if (st >= 0 && st < s_end) {
-          const float v = p[8 * u];
+          const float v = p[kStep * u];
           acc = __builtin_fmaf(v, v, acc);
         }
       }
     }
   }
+  return acc;
+}
+
+template <int T, int PS, bool HAS_BASE, bool TR = false>
+__device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int lane, float (*raw)[2][T],
+                        float (*dbuf)[DTile<T, TR>::kSize]) {
+  const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+  const float* x = sld(a.xf, i);
+  if (wave == 1) {  // producer
+    pc_produce<T, PS, HAS_BASE, TR>(a, ch, x, lane, raw, dbuf[0], DTile<T, TR>::kSize);
+    return;
+  }
+  const float acc = pc_chain<T, TR, 1>(ch, lane, dbuf[0], DTile<T, TR>::kSize, 0);
   float s = __shfl(acc, 0, 64);
   for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, l, 64);
   if (lane != 0) return;
@@ -884,10 +953,10 @@ __device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int 
   if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
 }
 
-template <int T, int PS, bool HAS_BASE>
+template <int T, int PS, bool HAS_BASE, bool TR = false>
 __global__ __launch_bounds__(128) void entry_norms_pc_kernel(NormArgs a) {
   __shared__ __attribute__((aligned(16))) float raw[PS][2][T];
-  __shared__ __attribute__((aligned(16))) float dbuf[2][T];
+  __shared__ __attribute__((aligned(16))) float dbuf[2][DTile<T, TR>::kSize];
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const uint64_t pair = blockIdx.x;  // entry-major over the (longest-first) tables
   const uint32_t ent = uint32_t(pair / uint64_t(a.K));
@@ -899,7 +968,7 @@ __global__ __launch_bounds__(128) void entry_norms_pc_kernel(NormArgs a) {
       if (wave == 0) norm_pair<HAS_BASE, false>(a, ch, i, lane, rows);
       return;
     }
-    norm_pc<T, PS, HAS_BASE>(a, ch, i, wave, lane, raw, dbuf);
+    norm_pc<T, PS, HAS_BASE, TR>(a, ch, i, wave, lane, raw, dbuf);
   } else if (ent < a.nef + a.nei) {
     if (wave == 0) norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows);
   }
@@ -1030,7 +1099,7 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
               const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_chunk* d_entries_f32,
               uint32_t n_entries_f32, const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  if (variant < 0 || variant > 8) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
+  if (variant < 0 || variant > 10) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (n_entries <= 0 || !d_out) return set_error(PLATO_AGG_EINVAL, "null output / no entries");
   if (n_entries_f32 && (!d_x_f32 || !d_entries_f32)) return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
@@ -1055,20 +1124,29 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
   a.nei = n_entries_i64;
   a.n_entries = uint32_t(n_entries);
   a.K = K;
-  // Variants (include/plato_agg_tune.h): 0 producer/consumer with 512-element
-  // tiles, the fastest on MI355X; 1 per-wave; 2, 3, 8 LDS-DMA
+  // Variants (include/plato_agg_tune.h): 9 (the default) producer/consumer with
+  // transposed 512-element tiles, the fastest on MI355X; 0 the
+  // same with natural tiles; 1 per-wave; 2, 3, 8 LDS-DMA
   // ring with 4 / 1 / 2 clients per workgroup; 4 / 5 variant 8 without the
   // chains / without the loads (timing probes, wrong results); 6, 7
-  // producer/consumer with 1024- / 256-element tiles.
-  static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2};
+  // producer/consumer with 1024- / 256-element tiles; 9, 10 producer/consumer
+  // with transposed d tiles (512 / 1,024 elements).
+  static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2, 0, 0};
   const int G = kGroup[variant];
   a.probe = variant == 4 ? 1u : variant == 5 ? 2u : 0u;
-  if (variant == 0 || variant == 6 || variant == 7) {  // producer / consumer, one workgroup per (entry, client)
+  if (variant == 0 || variant == 6 || variant == 7 || variant == 9 || variant == 10) {
+    // producer / consumer, one workgroup per (entry, client)
     const dim3 grid{uint32_t((uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K))};
     const bool hb = d_base_f32 != nullptr;
     if (variant == 0) {
       if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true>), grid, dim3(128), 0, stream, a);
       else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false>), grid, dim3(128), 0, stream, a);
+    } else if (variant == 9) {
+      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true>), grid, dim3(128), 0, stream, a);
+      else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true>), grid, dim3(128), 0, stream, a);
+    } else if (variant == 10) {
+      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, true, true>), grid, dim3(128), 0, stream, a);
+      else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, false, true>), grid, dim3(128), 0, stream, a);
     } else if (variant == 6) {
       if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, true>), grid, dim3(128), 0, stream, a);
       else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, false>), grid, dim3(128), 0, stream, a);
@@ -1111,7 +1189,7 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
                               const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
                               const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
                               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  return run_norms(0, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32, d_entries_i64,
+  return run_norms(9, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32, d_entries_i64,
                    n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
 }
 
