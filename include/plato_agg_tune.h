@@ -73,9 +73,12 @@ int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const i
                                const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
                                size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream);
 
-/* plato_agg_fedavg_qsgd kernel variants (workgroup size x clients per decode-table
- * batch; plato_agg_fedavg_qsgd uses 0).  plato_agg_tune_qsgd_chunk gives the
- * chunk capacity (elements per workgroup pass) the variant is built for. */
+/* plato_agg_fedavg_qsgd kernel variants, workgroup size x clients per decode-table
+ * batch x elements per lane: 0 = 1024x8x8 (plato_agg_fedavg_qsgd), 1 = 256x8x16,
+ * 2 = 512x16x16, 3 = 256x4x16, 4 = 1024x8x16, 5 = 256x8x8, 6 = 512x8x8,
+ * 7 = 128x8x16, 8 = 512x16x8, 9 = 512x8x4, 10 = 512x8x16 (the first default),
+ * 11 = 256x16x8, 12 = 1024x16x8, 13 = 1024x4x8.  plato_agg_tune_qsgd_chunk gives
+ * the chunk capacity (elements per workgroup pass) the variant is built for. */
 int plato_agg_tune_num_qsgd_variants(void);
 int plato_agg_tune_qsgd_chunk(int variant);
 int plato_agg_tune_fedavg_qsgd(int variant, const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64,

@@ -18,6 +18,8 @@
 #include <cstdint>
 #include <string>
 
+#include <type_traits>
+
 #include "common.h"
 #include "plato_agg.h"
 #include "plato_agg_tune.h"
@@ -29,16 +31,21 @@ using plato_agg_internal::set_error;
 
 typedef float f4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u1 __attribute__((ext_vector_type(1)));
 typedef __attribute__((address_space(1))) const f4 gf4;
 typedef __attribute__((address_space(1))) f4 gf4w;
 typedef __attribute__((address_space(1))) const u4 gu4;
+typedef __attribute__((address_space(1))) const u2 gu2;
+typedef __attribute__((address_space(1))) const u1 gu1;
 
 // Kernel shape (tuning space, plato_agg_tune_fedavg_qsgd): B threads per
-// workgroup share each batch's decode tables, U clients per table batch.
-// The default (variant 0) is B = 512, U = 8 (the shape moves the
-// time by under 5 %, within box noise; probes without the code loads still
-// take ~80 % of the time: the decode/sum path, not HBM, bounds this kernel).
-constexpr int kG = 16;      // elements per lane group (one 16-byte code load)
+// workgroup share each batch's decode tables, U clients per table batch, G
+// elements per lane (one 16/8/4-byte code load per client).  The default
+// (variant 0) is B = 1024, U = 8, G = 8: 8,192-element chunks as before, but
+// half the per-lane work and twice the waves to cover each batch's code
+// loads, 0.43 -> 0.33 ms on C2-sized inputs.
+constexpr int kG = 16;      // elements per lane group (one 16-byte code load) of the default
 
 template <class T>
 __device__ __forceinline__ T sld(const T* p, uint64_t i) {
@@ -87,8 +94,9 @@ __device__ __forceinline__ float term(float x, float b, float w, float s, bool t
   return t;
 }
 
-template <int kBlock, int kU, bool TWO>
+template <int kBlock, int kU, bool TWO, int kG = ::kG>
 __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
+  static_assert(kG == 16 || kG == 8 || kG == 4, "one 16-, 8- or 4-byte code load per lane");
   const Chunk ch = load_chunk(a.tf, c, a.n_f32);
   const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
   const uint64_t g0 = ch.begin / kG, g1 = (uint64_t(ch.end) + kG - 1) / kG;
@@ -135,11 +143,13 @@ __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
       }
       __syncthreads();
       if (full) {
-        u4 code[kU];
+        using CodeT = std::conditional_t<kG == 16, u4, std::conditional_t<kG == 8, u2, u1>>;
+        using GCodeT = std::conditional_t<kG == 16, gu4, std::conditional_t<kG == 8, gu2, gu1>>;
+        CodeT code[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
           const int i = i0 + u < K ? i0 + u : K - 1;
-          code[u] = __builtin_nontemporal_load((gu4*)(sld(a.cf, i) + e0));
+          code[u] = __builtin_nontemporal_load((GCodeT*)(sld(a.cf, i) + e0));
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -200,32 +210,41 @@ __device__ void qsgd_i64_chunk(const QArgs& a, uint32_t cc) {
   }
 }
 
-template <int kBlock, int kU, bool TWO>
+template <int kBlock, int kU, bool TWO, int kGE = kG>
 __global__ __launch_bounds__(kBlock) void fedavg_qsgd_kernel(QArgs a) {
   __shared__ float lut[kU][256];
   const uint32_t c = blockIdx.x;
   if (c < a.ncf) {
-    qsgd_f32_chunk<kBlock, kU, TWO>(a, c, lut);
+    qsgd_f32_chunk<kBlock, kU, TWO, kGE>(a, c, lut);
   } else {
     qsgd_i64_chunk<kBlock, TWO>(a, c - a.ncf);
   }
 }
 
 using QFn = void (*)(const QArgs&, hipStream_t, uint32_t);
-template <int B, int U, bool TWO>
+template <int B, int U, bool TWO, int G = kG>
 void launch_q(const QArgs& a, hipStream_t st, uint32_t nc) {
-  hipLaunchKernelGGL((fedavg_qsgd_kernel<B, U, TWO>), dim3(nc), dim3(B), 0, st, a);
+  hipLaunchKernelGGL((fedavg_qsgd_kernel<B, U, TWO, G>), dim3(nc), dim3(B), 0, st, a);
 }
 struct QVariant {
-  int block, u;
-  QFn fn[2];  // [TWO]
+  int block, u, g;  // threads, clients per table batch, elements per lane
+  QFn fn[2];        // [TWO]
 };
 const QVariant kQVariants[] = {
-    {512, 8, {&launch_q<512, 8, false>, &launch_q<512, 8, true>}},      // 0 (default)
-    {256, 8, {&launch_q<256, 8, false>, &launch_q<256, 8, true>}},      // 1
-    {512, 16, {&launch_q<512, 16, false>, &launch_q<512, 16, true>}},   // 2
-    {256, 4, {&launch_q<256, 4, false>, &launch_q<256, 4, true>}},      // 3
-    {1024, 8, {&launch_q<1024, 8, false>, &launch_q<1024, 8, true>}},   // 4
+    {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},  // 0 (default)
+    {256, 8, 16, {&launch_q<256, 8, false>, &launch_q<256, 8, true>}},      // 1
+    {512, 16, 16, {&launch_q<512, 16, false>, &launch_q<512, 16, true>}},   // 2
+    {256, 4, 16, {&launch_q<256, 4, false>, &launch_q<256, 4, true>}},      // 3
+    {1024, 8, 16, {&launch_q<1024, 8, false>, &launch_q<1024, 8, true>}},   // 4
+    {256, 8, 8, {&launch_q<256, 8, false, 8>, &launch_q<256, 8, true, 8>}},  // 5
+    {512, 8, 8, {&launch_q<512, 8, false, 8>, &launch_q<512, 8, true, 8>}},  // 6
+    {128, 8, 16, {&launch_q<128, 8, false>, &launch_q<128, 8, true>}},      // 7
+    {512, 16, 8, {&launch_q<512, 16, false, 8>, &launch_q<512, 16, true, 8>}},  // 8
+    {512, 8, 4, {&launch_q<512, 8, false, 4>, &launch_q<512, 8, true, 4>}},    // 9
+    {512, 8, 16, {&launch_q<512, 8, false>, &launch_q<512, 8, true>}},      // 10 (the first default)
+    {256, 16, 8, {&launch_q<256, 16, false, 8>, &launch_q<256, 16, true, 8>}},  // 11
+    {1024, 16, 8, {&launch_q<1024, 16, false, 8>, &launch_q<1024, 16, true, 8>}},  // 12
+    {1024, 4, 8, {&launch_q<1024, 4, false, 8>, &launch_q<1024, 4, true, 8>}},  // 13
 };
 constexpr int kNumQVariants = sizeof(kQVariants) / sizeof(kQVariants[0]);
 
@@ -295,7 +314,7 @@ int plato_agg_tune_num_qsgd_variants(void) { return kNumQVariants; }
 
 int plato_agg_tune_qsgd_chunk(int variant) {
   if (variant < 0 || variant >= kNumQVariants) return set_error(PLATO_AGG_EINVAL, "bad qsgd variant");
-  return kQVariants[variant].block * kG;
+  return kQVariants[variant].block * kQVariants[variant].g;
 }
 
 int plato_agg_tune_fedavg_qsgd(int variant, const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64,
