@@ -66,7 +66,11 @@ int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n,
  *   6, 7 = producer / consumer with 1024- / 256-element tiles (6 / 12 stages)
  *   9, 10 = producer / consumer writing the delta tiles transposed (each chain's
  *       steps contiguous), the chain wave reading 4 steps per ds_read_b128;
- *       512- / 1024-element tiles; 9 is the default */
+ *       512- / 1024-element tiles
+ *   11 = variant 9 with the chain wave at s_setprio 3
+ *   12 = variant 9 with the chain waves of the entries at least half as long as
+ *        the table's first at s_setprio 3, the others at 1 (the default; the
+ *        engine passes the table longest first) */
 int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
                                const float* d_base_f32, const int64_t* d_base_i64,
                                const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,

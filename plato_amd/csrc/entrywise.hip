@@ -932,7 +932,7 @@ __device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstr
   return acc;
 }
 
-template <int T, int PS, bool HAS_BASE, bool TR = false>
+template <int T, int PS, bool HAS_BASE, bool TR = false, int PRIO = 0>
 __device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int lane, float (*raw)[2][T],
                         float (*dbuf)[DTile<T, TR>::kSize]) {
   const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
@@ -940,6 +940,15 @@ __device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int 
   if (wave == 1) {  // producer
     pc_produce<T, PS, HAS_BASE, TR>(a, ch, x, lane, raw, dbuf[0], DTile<T, TR>::kSize);
     return;
+  }
+  if constexpr (PRIO > 0) {
+    __builtin_amdgcn_s_setprio(PRIO);  // the chain wave issues first
+  } else if constexpr (PRIO < 0) {
+    // the longest chains (the launch's critical path) first: entries at least half as long
+    // as the table's first (longest-first order) at priority 3, the rest at 1
+    const Chunk c0 = load_chunk(a.ef, 0, a.n_f32);
+    if (2 * n >= uint64_t(c0.end - c0.begin)) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(1);
   }
   const float acc = pc_chain<T, TR, 1>(ch, lane, dbuf[0], DTile<T, TR>::kSize, 0);
   float s = __shfl(acc, 0, 64);
@@ -953,7 +962,7 @@ __device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int 
   if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
 }
 
-template <int T, int PS, bool HAS_BASE, bool TR = false>
+template <int T, int PS, bool HAS_BASE, bool TR = false, int PRIO = 0>
 __global__ __launch_bounds__(128) void entry_norms_pc_kernel(NormArgs a) {
   __shared__ __attribute__((aligned(16))) float raw[PS][2][T];
   __shared__ __attribute__((aligned(16))) float dbuf[2][DTile<T, TR>::kSize];
@@ -968,7 +977,7 @@ __global__ __launch_bounds__(128) void entry_norms_pc_kernel(NormArgs a) {
       if (wave == 0) norm_pair<HAS_BASE, false>(a, ch, i, lane, rows);
       return;
     }
-    norm_pc<T, PS, HAS_BASE, TR>(a, ch, i, wave, lane, raw, dbuf);
+    norm_pc<T, PS, HAS_BASE, TR, PRIO>(a, ch, i, wave, lane, raw, dbuf);
   } else if (ent < a.nef + a.nei) {
     if (wave == 0) norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows);
   }
@@ -1099,7 +1108,7 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
               const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_chunk* d_entries_f32,
               uint32_t n_entries_f32, const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  if (variant < 0 || variant > 10) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
+  if (variant < 0 || variant > 12) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (n_entries <= 0 || !d_out) return set_error(PLATO_AGG_EINVAL, "null output / no entries");
   if (n_entries_f32 && (!d_x_f32 || !d_entries_f32)) return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
@@ -1124,17 +1133,18 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
   a.nei = n_entries_i64;
   a.n_entries = uint32_t(n_entries);
   a.K = K;
-  // Variants (include/plato_agg_tune.h): 9 (the default) producer/consumer with
-  // transposed 512-element tiles, the fastest on MI355X; 0 the
-  // same with natural tiles; 1 per-wave; 2, 3, 8 LDS-DMA
+  // Variants (include/plato_agg_tune.h): 12 (the default) producer/consumer with
+  // transposed 512-element tiles and the long chains' waves at raised priority,
+  // the fastest on MI355X; 9, 11 the same without / with a flat
+  // raised priority; 0 natural tiles; 1 per-wave; 2, 3, 8 LDS-DMA
   // ring with 4 / 1 / 2 clients per workgroup; 4 / 5 variant 8 without the
   // chains / without the loads (timing probes, wrong results); 6, 7
   // producer/consumer with 1024- / 256-element tiles; 9, 10 producer/consumer
   // with transposed d tiles (512 / 1,024 elements).
-  static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2, 0, 0};
+  static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2, 0, 0, 0, 0};
   const int G = kGroup[variant];
   a.probe = variant == 4 ? 1u : variant == 5 ? 2u : 0u;
-  if (variant == 0 || variant == 6 || variant == 7 || variant == 9 || variant == 10) {
+  if (variant == 0 || variant == 6 || variant == 7 || variant >= 9) {
     // producer / consumer, one workgroup per (entry, client)
     const dim3 grid{uint32_t((uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K))};
     const bool hb = d_base_f32 != nullptr;
@@ -1144,6 +1154,12 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
     } else if (variant == 9) {
       if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true>), grid, dim3(128), 0, stream, a);
       else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true>), grid, dim3(128), 0, stream, a);
+    } else if (variant == 11) {
+      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true, 3>), grid, dim3(128), 0, stream, a);
+      else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true, 3>), grid, dim3(128), 0, stream, a);
+    } else if (variant == 12) {
+      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true, -1>), grid, dim3(128), 0, stream, a);
+      else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true, -1>), grid, dim3(128), 0, stream, a);
     } else if (variant == 10) {
       if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, true, true>), grid, dim3(128), 0, stream, a);
       else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, false, true>), grid, dim3(128), 0, stream, a);
@@ -1189,7 +1205,7 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
                               const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
                               const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
                               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  return run_norms(9, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32, d_entries_i64,
+  return run_norms(12, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32, d_entries_i64,
                    n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
 }
 
