@@ -938,12 +938,16 @@ __device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int 
   const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
   const float* x = sld(a.xf, i);
   if (wave == 1) {  // producer
+    if constexpr (PRIO == -2) {  // the long entries' producers above every chain but their own
+      const Chunk c0 = load_chunk(a.ef, 0, a.n_f32);
+      if (2 * n >= uint64_t(c0.end - c0.begin)) __builtin_amdgcn_s_setprio(2);
+    }
     pc_produce<T, PS, HAS_BASE, TR>(a, ch, x, lane, raw, dbuf[0], DTile<T, TR>::kSize);
     return;
   }
   if constexpr (PRIO > 0) {
     __builtin_amdgcn_s_setprio(PRIO);  // the chain wave issues first
-  } else if constexpr (PRIO < 0) {
+  } else if constexpr (PRIO < 0) {  // -1, -2
     // the longest chains (the launch's critical path) first: entries at least half as long
     // as the table's first (longest-first order) at priority 3, the rest at 1
     const Chunk c0 = load_chunk(a.ef, 0, a.n_f32);
@@ -1108,7 +1112,7 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
               const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_chunk* d_entries_f32,
               uint32_t n_entries_f32, const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  if (variant < 0 || variant > 12) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
+  if (variant < 0 || variant > 13) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (n_entries <= 0 || !d_out) return set_error(PLATO_AGG_EINVAL, "null output / no entries");
   if (n_entries_f32 && (!d_x_f32 || !d_entries_f32)) return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
@@ -1141,7 +1145,7 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
   // chains / without the loads (timing probes, wrong results); 6, 7
   // producer/consumer with 1024- / 256-element tiles; 9, 10 producer/consumer
   // with transposed d tiles (512 / 1,024 elements).
-  static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2, 0, 0, 0, 0};
+  static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2, 0, 0, 0, 0, 0};
   const int G = kGroup[variant];
   a.probe = variant == 4 ? 1u : variant == 5 ? 2u : 0u;
   if (variant == 0 || variant == 6 || variant == 7 || variant >= 9) {
@@ -1160,6 +1164,9 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
     } else if (variant == 12) {
       if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true, -1>), grid, dim3(128), 0, stream, a);
       else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true, -1>), grid, dim3(128), 0, stream, a);
+    } else if (variant == 13) {
+      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true, -2>), grid, dim3(128), 0, stream, a);
+      else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true, -2>), grid, dim3(128), 0, stream, a);
     } else if (variant == 10) {
       if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, true, true>), grid, dim3(128), 0, stream, a);
       else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, false, true>), grid, dim3(128), 0, stream, a);
