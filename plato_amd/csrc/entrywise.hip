@@ -853,17 +853,17 @@ __device__ void pc_produce(const NormArgs& a, const Chunk ch, const float* x, in
   wait_vmcnt<0>();
 }
 
-// Chain wave of the producer / consumer norms kernels: walks the 8 chains of G
-// clients at once (lanes 8g..8g+7 = client g, lanes >= 8G duplicating them),
-// client g's tile tt at dtile + (tt & 1) * dstride + g * gstride, one s_barrier
-// per tile.  Returns this lane's chain sum (torch's accumulator lane c & 7).
-template <int T, bool TR, int G>
-__device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstride, int gstride) {
+// Chain wave of the producer / consumer norms kernels: walks the 8 chains
+// (lanes 8..63 duplicating lanes 0..7) over tile tt at dtile + (tt & 1) *
+// dstride, one s_barrier per tile.  Returns this lane's chain sum (torch's
+// accumulator lane & 7).
+template <int T, bool TR>
+__device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstride) {
   constexpr int kRT = T, kTS = DTile<T, TR>::kTS;
   const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
   const uint32_t delta = ch.begin & 3u;
   const uint64_t ntiles = (delta + m + kRT - 1) / kRT;
-  const int c = lane & 7, g = (lane >> 3) % G;  // lanes 8g..8g+7: client g's chains
+  const int c = lane & 7;
   const int pj = int((uint32_t(c) + delta) & 7u);
   const int64_t s_shift = (uint32_t(c) + delta) >= 8u ? -1 : 0;
   const int64_t s_end = int64_t(m / kNormLanes);
@@ -872,7 +872,7 @@ __device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstr
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_s_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    const float* tile = dtile + (tt & 1) * dstride + g * gstride;
+    const float* tile = dtile + (tt & 1) * dstride;
     const float* p = TR ? tile + pj * kTS : tile + pj;
     constexpr int kStep = TR ? 1 : 8;  // floats between a chain's consecutive steps
     const int64_t s0 = int64_t(tt) * (kRT / kNormLanes) + s_shift;
@@ -919,7 +919,7 @@ __device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstr
 #pragma unroll
         for (int q = 0; q < kCB; ++q) cur[q] = nxt[q];
       }
-    } else if (lane < kNormLanes * G) {
+    } else if (lane < kNormLanes) {
       for (int u = 0; u < kRT / kNormLanes; ++u) {
         const int64_t st = s0 + u;
         if (st >= 0 && st < s_end) {
@@ -954,7 +954,7 @@ __device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int 
     if (2 * n >= uint64_t(c0.end - c0.begin)) __builtin_amdgcn_s_setprio(3);
     else __builtin_amdgcn_s_setprio(1);
   }
-  const float acc = pc_chain<T, TR, 1>(ch, lane, dbuf[0], DTile<T, TR>::kSize, 0);
+  const float acc = pc_chain<T, TR>(ch, lane, dbuf[0], DTile<T, TR>::kSize);
   float s = __shfl(acc, 0, 64);
   for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, l, 64);
   if (lane != 0) return;
