@@ -584,11 +584,37 @@ def cpu_baseline(layout, base, slab, k, weights, out_f, out_i, reps, config):
         exact = bool(torch.equal(gpu_f.view(torch.int32), exp_f.view(torch.int32))
                      and torch.equal(gpu_i.view(torch.int32), exp_i.view(torch.int32)))
         parity = "bit-exact vs CPU reference op sequence" if exact else "MISMATCH vs CPU reference"
+    # the same sequence on 1 thread (first 8 clients), and the
+    # host's STREAM-style copy rate (1 GiB fp32, read + write bytes) at `threads`
+    k1 = min(k_s, 8)
+    t1 = []
+    torch.set_num_threads(1)
+    try:
+        for r in range(3):
+            t0 = time.perf_counter()
+            ref.fedavg_torch_ops(baseline, payloads[:k1], weights=w_s[:k1])
+            if r:
+                t1.append(time.perf_counter() - t0)
+    finally:
+        torch.set_num_threads(threads)
+    src = torch.ones(1 << 28, dtype=torch.float32)
+    dst = torch.empty_like(src)
+    tc = []
+    for r in range(4):
+        t0 = time.perf_counter()
+        dst.copy_(src)
+        if r:
+            tc.append(time.perf_counter() - t0)
+    stream_gbps = 2 * src.numel() * 4 / statistics.median(tc) / 1e9
+    del src, dst
     return {
         "value": round(layout.algorithmic_bytes(k_s) / med / 1e9, 3),
         "unit": "GB/s",
         "cores": threads,
         "kind": "port",
+        "one_thread": {"value": round(layout.algorithmic_bytes(k1) / statistics.median(t1) / 1e9, 3),
+                       "unit": "GB/s", "sample": f"first {k1} clients, median of 2 after 1 warm-up"},
+        "host_copy_GBps": round(stream_gbps, 1),
         "sample": f"{config}: {k_s} of {k} clients x {layout.n_f32 + layout.n_i64} params; the "
                   f"reference's torch CPU op sequence sub->mul->add_->add per tensor, median of {reps} "
                   f"after 1 warm-up, {threads} threads on {cpu_model()} (nproc {os.cpu_count()})",
