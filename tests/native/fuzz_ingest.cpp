@@ -1,7 +1,13 @@
 // Sanitizer fuzz driver for plato_ingest_parse / plato_ingest_gather (host code).
 // Built by tests/test_ingest_sanitize.py with -fsanitize=address,undefined
 // together with plato_amd/csrc/ingest.cpp.  For every sample file: parse all
-// prefixes and thousands of random byte mutations; gather whatever parses.
+// prefixes and thousands of random byte mutations; gather whatever parses;
+// read the file back through plato_ingest_read_fd (short and exact lengths)
+// and re-join it from random chunkings with plato_ingest_join.
+#include <fcntl.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -43,6 +49,34 @@ int main(int argc, char** argv) {
     for (size_t cut = 0; cut <= data.size(); cut += (data.size() > 4096 ? 7 : 1)) {
       std::vector<uint8_t> p(data.begin(), data.begin() + long(cut));
       exercise(p, &ok, &err);
+    }
+    // read_fd: whole file on 1 and 4 threads, then one byte past the end (must fail)
+    const int fd = ::open(argv[a], O_RDONLY);
+    if (fd < 0) return 3;
+    for (int threads : {1, 4}) {
+      std::vector<uint8_t> back(data.size() + 1);
+      if (plato_ingest_read_fd(fd, back.data(), data.size(), threads) != int64_t(data.size())) return 4;
+      if (std::memcmp(back.data(), data.data(), data.size()) != 0) return 5;
+      if (plato_ingest_read_fd(fd, back.data(), data.size() + 1, threads) != PLATO_INGEST_EIO) return 6;
+    }
+    ::close(fd);
+    // join: random chunkings of the file reassemble it byte for byte
+    for (int rep = 0; rep < 50; ++rep) {
+      std::vector<const uint8_t*> ptrs;
+      std::vector<size_t> lens;
+      for (size_t pos = 0; pos < data.size();) {
+        const size_t len = std::min(data.size() - pos, size_t(1 + rng() % 5000));
+        ptrs.push_back(data.data() + pos);
+        lens.push_back(len);
+        pos += len;
+      }
+      std::vector<uint8_t> joined(data.size());
+      if (plato_ingest_join(ptrs.data(), lens.data(), int(ptrs.size()), joined.data(), joined.size(), 4) != 0) return 7;
+      if (joined != data) return 8;
+      if (!ptrs.empty() &&
+          plato_ingest_join(ptrs.data(), lens.data(), int(ptrs.size()), joined.data(), joined.size() - 1, 4) !=
+              PLATO_INGEST_ECAPACITY)
+        return 9;
     }
     for (int m = 0; m < 4000; ++m) {
       std::vector<uint8_t> p = data;
