@@ -22,6 +22,12 @@ extern "C" {
 
 int plato_agg_tune_num_variants(void);
 
+// Largest fp32 range (in groups of 4 elements) one FedAvg launch covers;
+// 0 restores the default (the 4 GiB reach of 32-bit lane offsets).  Arenas
+// above it run as consecutive launches.  Tests lower it to exercise the split
+// on small arenas; process-wide, not thread-safe against concurrent launches.
+void plato_agg_tune_set_launch_groups(uint64_t groups);
+
 /* Writes the variant's workgroup size, V (float4 per lane), U (clients per
  * batch) and flags: bit 0 non-temporal loads, bit 1 non-temporal stores,
  * bit 2 software-pipelined batches, bit 3 buffer loads, bits 4..11 persistent

@@ -100,6 +100,7 @@ SIGNATURES = {
     ),
     # tuning / benchmarking (include/plato_agg_tune.h)
     "plato_agg_tune_num_variants": (_c_int, []),
+    "plato_agg_tune_set_launch_groups": (None, [_c_u64]),
     "plato_agg_tune_describe": (
         _c_int,
         [_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),

@@ -130,6 +130,7 @@ struct AggArgs {
   uint32_t nb_vec_full;        // of which fully in range (no bounds checks)
   uint32_t nb_grid;            // PERSIST: workgroups striding over the chunks; XCD: vector blocks in the grid
   uint32_t xcd_per;            // XCD: chunks per XCD (contiguous range)
+  uint64_t x_off;              // element offset of this launch's range in every client arena
   int K;
 };
 
@@ -200,7 +201,7 @@ __device__ __forceinline__ void load_batch(f4 (&x)[C::U][C::V], const AggArgs& a
                                            const uint32_t (&off)[C::V]) {
 #pragma unroll
   for (int u = 0; u < C::U; ++u) {
-    const float* p = sld(a.xf, i0 + u);
+    const float* p = sld(a.xf, i0 + u) + a.x_off;
 #pragma unroll
     for (int v = 0; v < C::V; ++v) x[u][v] = ld_client<C>(p, off[v], a);
   }
@@ -254,7 +255,7 @@ __device__ __forceinline__ void vec_body(const AggArgs& a, uint32_t blk) {
     }
   }
   for (int i = nbatch * U; i < K; ++i) {
-    const float* p = sld(a.xf, i);
+    const float* p = sld(a.xf, i) + a.x_off;
     const float wu = sld(a.w, i);
     float su = 1.f;
     if constexpr (TWO) su = sld(a.s, i);
@@ -284,7 +285,7 @@ __device__ __forceinline__ void scalar_item(const AggArgs& a, uint64_t j) {
     const float b = HAS_BASE ? a.base_f[e] : 0.f;
     float acc = 0.f;
     for (int i = 0; i < K; ++i) {
-      const float x = sld(a.xf, i)[e];
+      const float x = sld(a.xf, i)[a.x_off + e];
       const float d = HAS_BASE ? x - b : x;
       float t = d * sld(a.w, i);
       if constexpr (TWO) t = t * sld(a.s, i);
@@ -400,6 +401,14 @@ const Variant kVariants[] = {
 };
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
+// Tuning/test knob: f4 groups per launch (0 = the 4 GiB limit); lets tests
+// exercise the split path on small arenas.
+uint64_t g_launch_groups = 0;
+
+int run_agg_range(const Variant& vr, bool has_base, const float* const* xf, const int64_t* const* xi,
+                  const float* w, const float* s, int K, const float* base_f, const int64_t* base_i,
+                  float* out_f, float* out_if, size_t n_f32, size_t n_i64, uint64_t x_off, hipStream_t st);
+
 int run_agg(int variant, bool has_base, const float* const* xf, const int64_t* const* xi,
             const float* w, const float* s, int K, const float* base_f, const int64_t* base_i,
             float* out_f, float* out_if, size_t n_f32, size_t n_i64, hipStream_t st) {
@@ -417,7 +426,35 @@ int run_agg(int variant, bool has_base, const float* const* xf, const int64_t* c
     return PLATO_AGG_OK;
   }
   const Variant& vr = kVariants[variant];
+  // Lanes address their element groups with 32-bit byte offsets, so one launch
+  // covers < 4 GiB of the fp32 arena; larger arenas (models > ~1 B parameters)
+  // run as consecutive launches over whole-chunk ranges, each offsetting the
+  // client pointers in the kernel (x_off) and the baseline/output on the host.
+  // Every element still sums its K clients in order: results do not depend on
+  // the split.
+  const uint64_t chunk = uint64_t(vr.B) * vr.V;
+  const uint64_t n4_all = n_f32 / 4;
+  const uint64_t range = g_launch_groups ? (g_launch_groups + chunk - 1) / chunk * chunk
+                                         : ((0xffffffffull / 16) / chunk) * chunk;
+  uint64_t g0 = 0;
+  for (; n4_all - g0 > range; g0 += range) {
+    const int rc = run_agg_range(vr, has_base, xf, nullptr, w, s, K, base_f ? base_f + 4 * g0 : nullptr, nullptr,
+                                 out_f + 4 * g0, nullptr, 4 * range, 0, 4 * g0, st);
+    if (rc != PLATO_AGG_OK) return rc;
+  }
+  return run_agg_range(vr, has_base, xf, xi, w, s, K, base_f ? base_f + 4 * g0 : nullptr, base_i,
+                       n_f32 ? out_f + 4 * g0 : out_f, out_if, n_f32 - 4 * g0, n_i64, 4 * g0, st);
+}
+
+int run_agg_range(const Variant& vr, bool has_base, const float* const* xf, const int64_t* const* xi,
+                  const float* w, const float* s, int K, const float* base_f, const int64_t* base_i,
+                  float* out_f, float* out_if, size_t n_f32, size_t n_i64, uint64_t x_off, hipStream_t st) {
+  if (n_f32 == 0 && n_i64 == 0) {
+    g_last_error.clear();
+    return PLATO_AGG_OK;
+  }
   AggArgs a{};
+  a.x_off = x_off;
   a.xf = xf;
   a.xi = xi;
   a.w = w;
@@ -435,7 +472,7 @@ int run_agg(int variant, bool has_base, const float* const* xf, const int64_t* c
   const uint64_t n_scalar = (n_f32 - 4 * a.n4) + n_i64;
   const uint64_t nb_scalar = (n_scalar + vr.B - 1) / vr.B;
   if (nb_vec + nb_scalar > 0x7fffffffull || a.n4 * 16ull > 0xffffffffull)
-    return fail(PLATO_AGG_EINVAL, "fp32 arena must be < 4 GiB per launch (split it into buckets)");
+    return fail(PLATO_AGG_EINVAL, "launch range exceeds 4 GiB (internal split error)");
   a.nb_vec = uint32_t(nb_vec);
   a.nb_vec_full = uint32_t(a.n4 / chunk);
   a.nb_grid = a.nb_vec;
@@ -484,6 +521,7 @@ struct Bf16Args {
   float* out_if;
   uint64_t n8, n_f32, n_i64;
   uint32_t nb_vec, nb_vec_full;
+  uint64_t x_off;  // element offset of this launch's range in every client arena
   int K;
 };
 
@@ -503,7 +541,7 @@ __device__ __forceinline__ void bf16_body(const Bf16Args& a, uint32_t blk) {
     u4 q[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint16_t* p = sld(a.xf, i + u);
+      const uint16_t* p = sld(a.xf, i + u) + a.x_off;
       q[u] = __builtin_nontemporal_load((gu4*)((__attribute__((address_space(1))) const char*)p + xoff));
     }
 #pragma unroll
@@ -523,7 +561,7 @@ __device__ __forceinline__ void bf16_body(const Bf16Args& a, uint32_t blk) {
     }
   }
   for (; i < K; ++i) {
-    const uint16_t* p = sld(a.xf, i);
+    const uint16_t* p = sld(a.xf, i) + a.x_off;
     const u4 q = __builtin_nontemporal_load((gu4*)((__attribute__((address_space(1))) const char*)p + xoff));
     const float wu = sld(a.w, i);
     float su = 1.f;
@@ -566,7 +604,7 @@ __device__ __forceinline__ void bf16_body4(const Bf16Args& a, uint32_t blk) {
     u2 q[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const uint16_t* p = sld(a.xf, i + u);
+      const uint16_t* p = sld(a.xf, i + u) + a.x_off;
       q[u] = __builtin_nontemporal_load((gu2*)((__attribute__((address_space(1))) const char*)p + xoff));
     }
 #pragma unroll
@@ -579,7 +617,7 @@ __device__ __forceinline__ void bf16_body4(const Bf16Args& a, uint32_t blk) {
     }
   }
   for (; i < K; ++i) {
-    const uint16_t* p = sld(a.xf, i);
+    const uint16_t* p = sld(a.xf, i) + a.x_off;
     const u2 q = __builtin_nontemporal_load((gu2*)((__attribute__((address_space(1))) const char*)p + xoff));
     const f4 x = f4{bf16_lo(q.x), bf16_hi(q.x), bf16_lo(q.y), bf16_hi(q.y)};
     f4 t = f4_scale(x - b, sld(a.w, i));
@@ -598,7 +636,7 @@ __device__ __forceinline__ void bf16_scalar(const Bf16Args& a, uint64_t j) {
     const float b = a.base_f[e];
     float acc = 0.f;
     for (int i = 0; i < K; ++i) {
-      float t = (bf16_at(sld(a.xf, i), e) - b) * sld(a.w, i);
+      float t = (bf16_at(sld(a.xf, i), a.x_off + e) - b) * sld(a.w, i);
       if constexpr (TWO) t = t * sld(a.s, i);
       acc = acc + t;
     }
@@ -832,6 +870,11 @@ int plato_agg_fedavg_deltas(const float* const* d_d_f32, const int64_t* const* d
 }
 
 namespace {
+int run_bf16_range(const Bf16Variant& vr, const uint16_t* const* d_x_bf16, const uint16_t* const* d_x_i64_bf16,
+                   const float* d_w, const float* d_s, int K, const float* d_base_f32, const int64_t* d_base_i64,
+                   float* d_out_f32, float* d_out_i64f, size_t n_f32, size_t n_i64, uint64_t x_off,
+                   hipStream_t stream);
+
 int run_bf16(int variant, const uint16_t* const* d_x_bf16, const uint16_t* const* d_x_i64_bf16, const float* d_w,
              const float* d_s, int K, const float* d_base_f32, const int64_t* d_base_i64, float* d_out_f32,
              float* d_out_i64f, size_t n_f32, size_t n_i64, hipStream_t stream) {
@@ -844,7 +887,29 @@ int run_bf16(int variant, const uint16_t* const* d_x_bf16, const uint16_t* const
     return fail(PLATO_AGG_EINVAL, "fp32 baseline/output must be 16-byte aligned");
   if (n_f32 + n_i64 == 0) return plato_agg_internal::clear_error();
   const Bf16Variant& vr = kBf16Variants[variant];
+  // < 4 GiB of fp32 output per launch (32-bit lane offsets): larger arenas run
+  // as consecutive whole-block ranges, as in run_agg.
+  const uint64_t n8_all = n_f32 / 8;
+  const uint64_t range8 = g_launch_groups ? (g_launch_groups / 2 + 255) / 256 * 256
+                                          : ((0xffffffffull / 32) / 256) * 256;
+  uint64_t g0 = 0;
+  for (; n8_all - g0 > range8; g0 += range8) {
+    const int rc = run_bf16_range(vr, d_x_bf16, nullptr, d_w, d_s, K, d_base_f32 + 8 * g0, nullptr,
+                                  d_out_f32 + 8 * g0, nullptr, 8 * range8, 0, 8 * g0, stream);
+    if (rc != PLATO_AGG_OK) return rc;
+  }
+  return run_bf16_range(vr, d_x_bf16, d_x_i64_bf16, d_w, d_s, K, n_f32 ? d_base_f32 + 8 * g0 : d_base_f32,
+                        d_base_i64, n_f32 ? d_out_f32 + 8 * g0 : d_out_f32, d_out_i64f, n_f32 - 8 * g0, n_i64,
+                        8 * g0, stream);
+}
+
+int run_bf16_range(const Bf16Variant& vr, const uint16_t* const* d_x_bf16, const uint16_t* const* d_x_i64_bf16,
+                   const float* d_w, const float* d_s, int K, const float* d_base_f32, const int64_t* d_base_i64,
+                   float* d_out_f32, float* d_out_i64f, size_t n_f32, size_t n_i64, uint64_t x_off,
+                   hipStream_t stream) {
+  if (n_f32 + n_i64 == 0) return plato_agg_internal::clear_error();
   Bf16Args a{};
+  a.x_off = x_off;
   a.xf = d_x_bf16;
   a.xi = d_x_i64_bf16;
   a.w = d_w;
@@ -862,7 +927,7 @@ int run_bf16(int variant, const uint16_t* const* d_x_bf16, const uint16_t* const
   const uint64_t n_scalar = (n_f32 - 8 * a.n8) + n_i64;
   const uint64_t nb_scalar = (n_scalar + 255) / 256;
   if (nb_vec + nb_scalar > 0x7fffffffull || a.n8 * 32ull > 0xffffffffull)
-    return fail(PLATO_AGG_EINVAL, "fp32 arena must be < 4 GiB per launch (split it into buckets)");
+    return fail(PLATO_AGG_EINVAL, "launch range exceeds 4 GiB (internal split error)");
   a.nb_vec = uint32_t(nb_vec);
   a.nb_vec_full = uint32_t(groups / 256);
   vr.fn[d_s ? 1 : 0](a, dim3(uint32_t(nb_vec + nb_scalar)), stream);
@@ -889,6 +954,8 @@ int plato_agg_tune_fedavg_bf16(int variant, const uint16_t* const* d_x_bf16, con
 }
 
 int plato_agg_tune_num_variants(void) { return kNumVariants; }
+
+void plato_agg_tune_set_launch_groups(uint64_t groups) { g_launch_groups = groups; }
 
 int plato_agg_tune_describe(int variant, int* block, int* v, int* u, int* flags) {
   if (variant < 0 || variant >= kNumVariants) return fail(PLATO_AGG_EINVAL, "bad variant");

@@ -44,7 +44,11 @@ struct Error {
 enum class K { None, Bool, Int, Float, Str, Bytes, Global, Tuple, List, Dict, Mark, Storage, Tensor };
 
 struct Val;
-using P = std::shared_ptr<Val>;
+// Values are owned by the parse's Ctx::pool and referenced by raw pointer:
+// a hostile pickle can nest containers arbitrarily deep or build reference
+// cycles (memo GET + APPEND), and a pool is freed iteratively either way
+// (shared_ptr chains would recurse on destruction and leak on cycles).
+using P = Val*;
 
 struct Val {
   K k = K::None;
@@ -56,11 +60,6 @@ struct Val {
   std::vector<std::pair<P, P>> dict;  // Dict (insertion order)
 };
 
-P mk(K k) {
-  auto p = std::make_shared<Val>();
-  p->k = k;
-  return p;
-}
 
 struct Storage {
   int32_t dtype = -1;
@@ -76,6 +75,8 @@ struct Ctx {
   size_t len;
   std::vector<Storage> storages;
   std::vector<plato_ingest_tensor> tensors;
+  std::vector<std::unique_ptr<Val>> pool;  // every Val of this parse
+  int record_depth = 0;                     // nested _load_from_bytes records
 
   std::string str(const Val& v) const { return std::string(reinterpret_cast<const char*>(buf + v.off), v.len); }
 };
@@ -106,6 +107,13 @@ struct Reader {
     return s;
   }
 };
+
+P mk(Ctx& c, K k) {
+  c.pool.push_back(std::make_unique<Val>());
+  P p = c.pool.back().get();
+  p->k = k;
+  return p;
+}
 
 int dtype_of_storage(const std::string& mod, const std::string& name, int32_t* elem) {
   if (mod != "torch") return -1;
@@ -138,6 +146,7 @@ struct Persistent {
 };
 
 P parse_legacy_record(Ctx& c, uint64_t off, uint64_t len);
+bool tensor_in_storage(const plato_ingest_tensor& t);
 
 // Runs one pickle from r.pos to its STOP; returns the top of the stack.
 P run(Ctx& c, Reader& r, Persistent* pers) {
@@ -171,7 +180,7 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
   };
   auto push_view = [&](K k, uint64_t n) {
     r.need(size_t(n));
-    P v = mk(k);
+    P v = mk(c, k);
     v->off = r.pos;
     v->len = n;
     r.pos += size_t(n);
@@ -188,13 +197,13 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
     switch (op) {
       case 0x80: r.u8(); break;                       // PROTO
       case 0x95: r.le(8); break;                      // FRAME (transparent)
-      case '.': return st.empty() ? mk(K::None) : st.back();  // STOP
+      case '.': return st.empty() ? mk(c, K::None) : st.back();  // STOP
       case '(': marks.push_back(st.size()); break;    // MARK
-      case '}': st.push_back(mk(K::Dict)); break;     // EMPTY_DICT
-      case ']': st.push_back(mk(K::List)); break;     // EMPTY_LIST
-      case ')': st.push_back(mk(K::Tuple)); break;    // EMPTY_TUPLE
+      case '}': st.push_back(mk(c, K::Dict)); break;     // EMPTY_DICT
+      case ']': st.push_back(mk(c, K::List)); break;     // EMPTY_LIST
+      case ')': st.push_back(mk(c, K::Tuple)); break;    // EMPTY_TUPLE
       case 't': {                                     // TUPLE
-        P t = mk(K::Tuple);
+        P t = mk(c, K::Tuple);
         t->items = pop_mark();
         st.push_back(t);
         break;
@@ -202,7 +211,7 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
       case 0x85: case 0x86: case 0x87: {              // TUPLE1..3
         const int n = op - 0x84;
         if (st.size() < size_t(n)) fail(PLATO_INGEST_EFORMAT, "stack underflow");
-        P t = mk(K::Tuple);
+        P t = mk(c, K::Tuple);
         t->items.assign(st.end() - n, st.end());
         st.resize(st.size() - size_t(n));
         st.push_back(t);
@@ -233,13 +242,13 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
         set_items(st.back(), kv);
         break;
       }
-      case 'J': { P v = mk(K::Int); v->i = int32_t(uint32_t(r.le(4))); st.push_back(v); break; }
-      case 'K': { P v = mk(K::Int); v->i = r.u8(); st.push_back(v); break; }
-      case 'M': { P v = mk(K::Int); v->i = int64_t(r.le(2)); st.push_back(v); break; }
+      case 'J': { P v = mk(c, K::Int); v->i = int32_t(uint32_t(r.le(4))); st.push_back(v); break; }
+      case 'K': { P v = mk(c, K::Int); v->i = r.u8(); st.push_back(v); break; }
+      case 'M': { P v = mk(c, K::Int); v->i = int64_t(r.le(2)); st.push_back(v); break; }
       case 0x8a: case 0x8b: {                         // LONG1 / LONG4
         const uint64_t n = op == 0x8a ? r.u8() : r.le(4);
         r.need(size_t(n));
-        P v = mk(K::Int);
+        P v = mk(c, K::Int);
         v->off = r.pos;
         if (n > 8) {
           // only the legacy magic number is this long: keep its low bits
@@ -257,15 +266,15 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
         st.push_back(v);
         break;
       }
-      case 'N': st.push_back(mk(K::None)); break;
-      case 0x88: { P v = mk(K::Bool); v->i = 1; st.push_back(v); break; }
-      case 0x89: { P v = mk(K::Bool); v->i = 0; st.push_back(v); break; }
+      case 'N': st.push_back(mk(c, K::None)); break;
+      case 0x88: { P v = mk(c, K::Bool); v->i = 1; st.push_back(v); break; }
+      case 0x89: { P v = mk(c, K::Bool); v->i = 0; st.push_back(v); break; }
       case 'G': {                                     // BINFLOAT (big endian)
         r.need(8);
         uint64_t x = 0;
         for (int b = 0; b < 8; ++b) x = (x << 8) | c.buf[r.pos + size_t(b)];
         r.pos += 8;
-        P v = mk(K::Float);
+        P v = mk(c, K::Float);
         std::memcpy(&v->f, &x, 8);
         st.push_back(v);
         break;
@@ -285,7 +294,7 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
       case 'h': memo_get(r.u8()); break;              // BINGET
       case 'j': memo_get(size_t(r.le(4))); break;     // LONG_BINGET
       case 'c': {                                     // GLOBAL
-        P g = mk(K::Global);
+        P g = mk(c, K::Global);
         g->mod = r.line();
         g->name = r.line();
         st.push_back(g);
@@ -295,7 +304,7 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
         P name = pop();
         P mod = pop();
         if (mod->k != K::Str || name->k != K::Str) fail(PLATO_INGEST_EFORMAT, "STACK_GLOBAL needs strings");
-        P g = mk(K::Global);
+        P g = mk(c, K::Global);
         g->mod = c.str(*mod);
         g->name = c.str(*name);
         st.push_back(g);
@@ -326,7 +335,7 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
         } else {
           idx = it->second;
         }
-        P v = mk(K::Storage);
+        P v = mk(c, K::Storage);
         v->i = idx;
         st.push_back(v);
         break;
@@ -336,7 +345,7 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
         P fn = pop();
         if (fn->k != K::Global || args->k != K::Tuple) fail(PLATO_INGEST_EUNSUPPORTED, "REDUCE of a non-global");
         if ((fn->mod == "collections" && fn->name == "OrderedDict") && args->items.empty()) {
-          st.push_back(mk(K::Dict));
+          st.push_back(mk(c, K::Dict));
         } else if (fn->mod == "torch.storage" && fn->name == "_load_from_bytes") {
           if (args->items.size() != 1 || args->items[0]->k != K::Bytes)
             fail(PLATO_INGEST_EFORMAT, "_load_from_bytes(bytes) expected");
@@ -359,7 +368,7 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
           if (nd > PLATO_INGEST_MAX_DIMS || a[3]->items.size() != nd)
             fail(PLATO_INGEST_EUNSUPPORTED, "tensor rank > 8 or size/stride mismatch");
           t.ndim = int32_t(nd);
-          uint64_t numel = 1, span = 0;
+          uint64_t numel = 1;
           bool contig = true;
           int64_t expect = 1;
           for (size_t d = 0; d < nd; ++d) {
@@ -374,12 +383,11 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
           for (size_t d = nd; d-- > 0;) {
             if (t.shape[d] != 1 && t.stride[d] != expect) contig = false;
             expect *= t.shape[d];
-            if (t.shape[d] > 0) span += uint64_t(t.shape[d] - 1) * uint64_t(t.stride[d]);
           }
           t.numel = numel;
           t.contiguous = contig ? 1 : 0;
-          if (numel > 0 && t.storage_offset + span >= s.numel) fail(PLATO_INGEST_EFORMAT, "tensor outside its storage");
-          P v = mk(K::Tensor);
+          if (!tensor_in_storage(t)) fail(PLATO_INGEST_EFORMAT, "tensor outside its storage");
+          P v = mk(c, K::Tensor);
           v->i = int64_t(c.tensors.size());
           c.tensors.push_back(t);
           st.push_back(v);
@@ -399,6 +407,15 @@ P run(Ctx& c, Reader& r, Persistent* pers) {
 
 // torch.save(storage, _use_new_zipfile_serialization=False) record.
 P parse_legacy_record(Ctx& c, uint64_t off, uint64_t len) {
+  // A state_dict pickle holds records one level deep; a record whose storage
+  // pickle calls _load_from_bytes again is never produced by torch.
+  struct Depth {
+    Ctx& c;
+    explicit Depth(Ctx& cc) : c(cc) {
+      if (++c.record_depth > 2) fail(PLATO_INGEST_EUNSUPPORTED, "nested torch.save records");
+    }
+    ~Depth() { --c.record_depth; }
+  } depth(c);
   Reader r{c, size_t(off), size_t(off + len)};
   Persistent pers;
   P magic = run(c, r, nullptr);
@@ -509,6 +526,33 @@ class Pool {
   int remaining_ = 0;
   uint64_t gen_ = 0;
 };
+
+// True when every element of t lies inside its storage: storage_offset +
+// sum((shape[d]-1) * stride[d]) < storage_numel, with no step of the sum
+// wrapping (a hostile record may carry strides up to 2^63-1), and numel equal
+// to the product of the shape.  Checked by the parser and again by the gather
+// (its descriptors come through the C ABI).
+bool tensor_in_storage(const plato_ingest_tensor& t) {
+  if (t.ndim < 0 || t.ndim > PLATO_INGEST_MAX_DIMS) return false;
+  uint64_t numel = 1, span = 0;
+  for (int d = 0; d < t.ndim; ++d) {
+    if (t.shape[d] < 0 || t.stride[d] < 0) return false;
+    if (__builtin_mul_overflow(numel, uint64_t(t.shape[d]), &numel)) return false;
+  }
+  if (numel != t.numel) return false;
+  if (numel == 0) return true;  // an empty tensor reads nothing, whatever its strides
+  for (int d = 0; d < t.ndim; ++d) {
+    if (t.shape[d] > 1) {
+      uint64_t ext = 0;
+      if (uint64_t(t.stride[d]) >= t.storage_numel) return false;
+      if (__builtin_mul_overflow(uint64_t(t.shape[d] - 1), uint64_t(t.stride[d]), &ext) ||
+          __builtin_add_overflow(span, ext, &span))
+        return false;
+    }
+  }
+  uint64_t last = 0;
+  return !__builtin_add_overflow(t.storage_offset, span, &last) && last < t.storage_numel;
+}
 
 void copy_strided(const uint8_t* base, const plato_ingest_tensor& t, uint8_t* dst) {
   const size_t es = size_t(t.element_size);
@@ -846,8 +890,9 @@ int plato_ingest_gather(const uint8_t* buf, size_t len, const plato_ingest_tenso
     const plato_ingest_tensor& x = t[i];
     const size_t es = size_t(x.element_size);
     const size_t bytes = size_t(x.numel) * es;
-    const uint64_t storage_bytes = x.storage_numel * es;
-    if (x.data_offset > len || storage_bytes > len - x.data_offset || dst_byte_offset[i] > dst_len ||
+    uint64_t storage_bytes = 0;
+    if (es == 0 || es > 16 || !tensor_in_storage(x) || __builtin_mul_overflow(x.storage_numel, es, &storage_bytes) ||
+        x.data_offset > len || storage_bytes > len - x.data_offset || dst_byte_offset[i] > dst_len ||
         bytes > dst_len - dst_byte_offset[i]) {
       g_err = "tensor or destination out of range";
       return PLATO_INGEST_EINVAL;

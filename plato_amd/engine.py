@@ -772,7 +772,9 @@ class AggregationRound:
         h = _stream_handle(stream)
         _lib.call("plato_agg_compute_deltas", _ptr(eng._base.f32), _ptr(eng._base.i64), _ptr(prev.f32),
                   _ptr(prev.i64), _ptr(v.f32), _ptr(v.i64), lay.n_f32, lay.n_i64, h)
-        pf, pi = self.slab.row_pointers(slots)
+        # slots adopted from arrival staging live outside the round slab
+        pf = np.asarray([self._pf[i] for i in slots], dtype=np.int64)
+        pi = np.asarray([self._pi[i] for i in slots], dtype=np.int64)
         tf, ti = eng._pointer_tables(pf, pi)
         k = len(slots)
         ws_bytes = self.engine.lib.plato_agg_client_dots_workspace(k, lay.n_f32)

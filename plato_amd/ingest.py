@@ -108,6 +108,46 @@ class ArenaStateDict(OrderedDict):
     def __reduce__(self):  # pickles (e.g. for payload-size accounting) as a plain OrderedDict
         return (OrderedDict, (list(self.items()),))
 
+    # Any change to the mapping (a processor or weights_received hook replacing
+    # an entry) detaches the arena: the stager then packs the dict's current
+    # tensors instead of copying stale arena bytes.  In-place writes to the
+    # tensors themselves land in the arena and need nothing.
+    def _detach_arena(self) -> None:
+        self.arena_f32 = self.arena_i64 = self.layout_signature = None
+
+    def __setitem__(self, key, value):
+        self._detach_arena()
+        super().__setitem__(key, value)
+
+    def __delitem__(self, key):
+        self._detach_arena()
+        super().__delitem__(key)
+
+    def pop(self, *args):
+        self._detach_arena()
+        return super().pop(*args)
+
+    def popitem(self, last=True):
+        self._detach_arena()
+        return super().popitem(last)
+
+    def setdefault(self, key, default=None):
+        if key not in self:
+            self._detach_arena()
+        return super().setdefault(key, default)
+
+    def update(self, *args, **kwargs):
+        self._detach_arena()
+        super().update(*args, **kwargs)
+
+    def clear(self):
+        self._detach_arena()
+        super().clear()
+
+    def __ior__(self, other):
+        self._detach_arena()
+        return super().__ior__(other)
+
 
 def _buffer(data):
     """(address, length, keepalive) of a bytes-like object without copying."""
@@ -212,12 +252,12 @@ def loads(data, layout: ArenaLayout | None = None, pin: bool = False, threads: i
         _gather(keep, addr, n, f_infos, f_offs, f32, threads)
     if i_infos:
         _gather(keep, addr, n, i_infos, i_offs, i64, threads)
-    out = ArenaStateDict()
     storages = {F32: (f32.untyped_storage(), es_f, dt_f), I64: (i64.untyped_storage(), es_i, dt_i)}
+    out = ArenaStateDict()
     for key in keys:
         e = layout[key]
         storage, es, dt = storages[e.region]
-        out[key] = _owned_view(storage, e.offset * es, e.numel * es, dt, e.shape)
+        OrderedDict.__setitem__(out, key, _owned_view(storage, e.offset * es, e.numel * es, dt, e.shape))
     out.arena_f32, out.arena_i64 = f32, i64
     out.layout_signature = layout.signature
     return out

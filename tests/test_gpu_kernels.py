@@ -159,3 +159,70 @@ def test_compute_deltas_and_update(engine):
     exp = ref.fedavg_torch_ops(base_sd, payloads, num_samples=ns)
     for name in exp:
         assert torch.equal(upd[name], exp[name]), name
+
+
+@pytest.mark.parametrize("groups", [1000, 4096, 777777])
+def test_split_launch_ranges_bit_exact(engine, groups):
+    """Arenas beyond one launch's 4 GiB reach run as consecutive ranges; emulate with a small range."""
+    spec = workloads.resnet(18)
+    k, seed = 7, 12
+    layout, base, slab = _device_case(spec, k, seed)
+    weights = ref.fedavg_weights(synth.num_samples(k, seed))
+    scales = [1.0 / (1 + 0.11 * i) for i in range(k)]
+    bf, bi, xs_f, xs_i = host_inputs(layout.n_f32, layout.n_i64, seed, k)
+    lib = _lib.lib()
+    lib.plato_agg_tune_set_launch_groups(groups)
+    try:
+        for v in (None, 14, 10):
+            got_f, got_i = _run(engine, layout, base, slab, k, weights, scales=scales, variant=v)
+            exp_f, exp_i = ref.fedavg_numpy(bf, bi, xs_f, xs_i, weights, scales)
+            assert bits_equal(got_f, exp_f), (v, first_mismatch(got_f, exp_f))
+            assert bits_equal(got_i, exp_i), v
+        # bf16 payloads take the same split
+        slab16 = ClientSlab(layout, k, base.f32.device, codec="bf16")
+        slab16.f32.copy_(slab.f32.to(torch.bfloat16))
+        slab16.i64.copy_(slab.i64.to(torch.bfloat16))
+        pf, pi = slab16.row_pointers(range(k))
+        dev = base.f32.device
+        tf, ti = torch.from_numpy(pf).to(dev), torch.from_numpy(pi).to(dev)
+        w = torch.from_numpy(ref.fp32(weights)).to(dev)
+        out_f = torch.full((layout.row_f32,), float("nan"), device=dev)
+        out_i = torch.full((layout.row_i64,), float("nan"), device=dev)
+        _lib.call("plato_agg_fedavg_weights_bf16", tf.data_ptr(), ti.data_ptr(), w.data_ptr(), None, k,
+                  base.f32.data_ptr(), base.i64.data_ptr(), out_f.data_ptr(), out_i.data_ptr(),
+                  layout.n_f32, layout.n_i64, torch.cuda.current_stream().cuda_stream)
+        lib.plato_agg_tune_set_launch_groups(0)
+        ref_f = torch.full_like(out_f, float("nan"))
+        ref_i = torch.full_like(out_i, float("nan"))
+        _lib.call("plato_agg_fedavg_weights_bf16", tf.data_ptr(), ti.data_ptr(), w.data_ptr(), None, k,
+                  base.f32.data_ptr(), base.i64.data_ptr(), ref_f.data_ptr(), ref_i.data_ptr(),
+                  layout.n_f32, layout.n_i64, torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert torch.equal(out_f[: layout.n_f32].view(torch.int32), ref_f[: layout.n_f32].view(torch.int32))
+        assert torch.equal(out_i[: layout.n_i64].view(torch.int32), ref_i[: layout.n_i64].view(torch.int32))
+    finally:
+        lib.plato_agg_tune_set_launch_groups(0)
+        engine.variant = None
+
+
+def test_arena_beyond_4gib_one_launch_call(engine):
+    """A 1.1 G-parameter fp32 arena (4.4 GB per client) through the public entry point; sampled check."""
+    n = (1 << 30) + 12345  # > 4 GiB of fp32, with a ragged tail
+    layout = ArenaLayout.from_shapes([("w", (n,), "f32"), ("c", (3,), "i64")])
+    k, seed = 2, 21
+    dev = torch.device("cuda:0")
+    base = DeviceArena(layout, dev)
+    slab = ClientSlab(layout, k, dev)
+    fill_baseline(base, seed)
+    fill_clients(slab, base, seed, k)
+    weights = [0.25, 0.75]
+    got_f, got_i = _run(engine, layout, base, slab, k, weights)
+    rng = np.random.default_rng(0)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 4096), np.arange(n - 64, n),
+                                    np.arange((1 << 30) - 64, (1 << 30) + 64)]))
+    bf = base.f32[: n].cpu().numpy()[idx]
+    xs = [slab.f32[c, : n].cpu().numpy()[idx] for c in range(k)]
+    exp_f, _ = ref.fedavg_numpy(bf, np.zeros(0, np.int64), xs, [np.zeros(0, np.int64)] * k, weights)
+    assert bits_equal(got_f[idx], exp_f)
+    del slab, base
+    torch.cuda.empty_cache()

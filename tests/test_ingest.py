@@ -121,6 +121,79 @@ def test_never_executes_and_rejects_foreign_objects():
     assert not os.path.exists("/tmp/plato_ingest_pwned")
 
 
+class _StridedTensor:
+    """Pickles as _rebuild_tensor_v2(storage, offset, size, stride, ...) with chosen geometry."""
+
+    def __init__(self, storage, offset, size, stride):
+        self.args = (storage, offset, size, stride, False, OrderedDict())
+
+    def __reduce__(self):
+        return (torch._utils._rebuild_tensor_v2, self.args)
+
+
+def _hostile_geometry_payloads():
+    big = 2**63 - 1
+    u8 = torch.zeros(2, dtype=torch.uint8)._typed_storage()
+    f32 = torch.zeros(16)._typed_storage()
+    yield _StridedTensor(u8, 0, (2, 2, 2), (big, big, 3))     # extents wrap to 1
+    yield _StridedTensor(u8, 0, (2,), (big,))                # one huge stride
+    yield _StridedTensor(f32, 2**62, (1,), (1,))             # offset far outside
+    yield _StridedTensor(f32, 15, (2,), (1,))                # one past the end
+    yield _StridedTensor(f32, 1, (2, 2), (2**62, 2**62))     # 2*2^62 wraps to 0 in a 64-bit sum
+    yield _StridedTensor(f32, 0, (4, 5), (5, 1))             # 20 > 16 elements
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_hostile_strides_and_offsets_are_rejected(case):
+    """Geometry that would read outside the storage (wrapping extents included) is a format error."""
+    obj = list(_hostile_geometry_payloads())[case]
+    data = pickle.dumps(OrderedDict(w=obj), protocol=4)
+    with pytest.raises(ingest.IngestError, match="outside its storage"):
+        ingest.loads(data)
+
+
+def test_legal_strided_tensor_still_loads():
+    base = torch.arange(24, dtype=torch.float32)
+    data = pickle.dumps(OrderedDict(w=_StridedTensor(base._typed_storage(), 2, (3, 4), (1, 5))), protocol=4)
+    got = ingest.loads(data)
+    assert torch.equal(got["w"], base.as_strided((3, 4), (1, 5), 2))
+
+
+def test_deep_nesting_is_refused_without_recursion():
+    """200k nested 1-tuples: parsed into a pool and refused (not a dict), no stack overflow."""
+    code = r"""
+import sys
+sys.path.insert(0, sys.argv[1])
+from plato_amd import ingest
+for body in (b")" + b"\x85" * 200000, b"]" + b"\x94" + b"h\x00a" * 100000):
+    try:
+        ingest.loads(b"\x80\x04" + body + b".")
+    except ingest.IngestError:
+        pass
+    else:
+        raise SystemExit("accepted")
+print("OK")
+"""
+    proc = subprocess.run([sys.executable, "-c", code, ROOT], capture_output=True, text=True, timeout=300)
+    assert proc.returncode == 0 and "OK" in proc.stdout, proc.stderr[-2000:]
+
+
+def test_mutating_an_arena_payload_detaches_its_arena():
+    spec = workloads.lenet5(10)
+    layout = ArenaLayout.from_shapes(spec)
+    sd = state_dict(spec, 3)
+    got = ingest.loads(pickle.dumps(sd), layout=layout)
+    assert got.layout_signature == layout.signature and got.arena_f32 is not None
+    key = next(iter(got))
+    got[key] = torch.zeros_like(got[key])
+    assert got.layout_signature is None and got.arena_f32 is None
+    for mutate in (lambda d: d.pop(key), lambda d: d.update({key: d[key]}), lambda d: d.clear(),
+                   lambda d: d.popitem()):
+        fresh = ingest.loads(pickle.dumps(sd), layout=layout)
+        mutate(fresh)
+        assert fresh.layout_signature is None
+
+
 def test_truncation_and_corruption_fuzz():
     """Every prefix and random byte flips: error or a result, never a crash (subprocess)."""
     code = r'''

@@ -29,6 +29,16 @@ def test_parser_under_address_and_ub_sanitizers(tmp_path):
         path = tmp_path / f"sd{proto}.pkl"
         path.write_bytes(pickle.dumps(sd, protocol=proto))
         samples.append(str(path))
+    # crafted geometry that reads outside its storage (wrapping extents), and deep nesting
+    from tests.test_ingest import _hostile_geometry_payloads
+
+    for i, obj in enumerate(_hostile_geometry_payloads()):
+        path = tmp_path / f"hostile{i}.pkl"
+        path.write_bytes(pickle.dumps(OrderedDict(w=obj), protocol=4))
+        samples.append(str(path))
+    deep = tmp_path / "deep.pkl"
+    deep.write_bytes(b"\x80\x04)" + b"\x85" * 20000 + b".")
+    samples.append(str(deep))
     run = subprocess.run([str(exe), *samples], capture_output=True, text=True, timeout=600,
                          env=dict(os.environ, ASAN_OPTIONS="detect_leaks=0"))
     assert run.returncode == 0 and "FUZZ_OK" in run.stdout, run.stderr[-3000:]
