@@ -81,6 +81,7 @@ extern "C" {
 #define PLATO_AGG_OK 0
 #define PLATO_AGG_EINVAL (-1)   /* bad argument (null, misaligned, K <= 0) */
 #define PLATO_AGG_EHIP (-2)     /* HIP runtime error (launch / copy)      */
+#define PLATO_AGG_ERCCL (-3)    /* RCCL unavailable or a collective failed */
 
 /* ABI version of the loaded library (== PLATO_AGG_ABI_VERSION). */
 int plato_agg_abi_version(void);
@@ -299,6 +300,33 @@ int plato_agg_fill_synth_f32(float* d_out, const float* d_add, size_t n,
 int plato_agg_fill_synth_i64(int64_t* d_out, const int64_t* d_add, size_t n,
                              uint64_t seed, uint64_t stream_id, uint64_t modulus,
                              hipStream_t stream);
+
+/*
+ * Single-process RCCL communicator over the GPUs one Plato server drives.
+ * The reference has no collectives (aggregation runs on one CPU
+ * process); these serve the multi-GPU engine behind the same
+ * aggregate_weights hook (plato/servers/fedavg.py:171-182), which bucket-
+ * shards the arena over the node's GPUs.  Rank g is
+ * devices[g]; every collective is issued for all ranks inside one
+ * ncclGroupStart/End, each on its own stream (streams[g] on devices[g]).
+ * RCCL is bound at run time (dlopen "librccl.so.1"): PLATO_AGG_ERCCL if absent.
+ */
+typedef struct plato_agg_comm plato_agg_comm;
+
+/* ncclCommInitAll over `ndev` distinct device ordinals. */
+int plato_agg_comm_create(int ndev, const int* devices, plato_agg_comm** out);
+int plato_agg_comm_destroy(plato_agg_comm* comm);
+int plato_agg_comm_size(const plato_agg_comm* comm);
+
+/* d_recv[g][r*count .. (r+1)*count) = d_send[r][0 .. count) for every rank r:
+ * assembles the bucket-sharded new model on every GPU. */
+int plato_agg_comm_allgather_f32(plato_agg_comm* comm, const float* const* d_send, float* const* d_recv,
+                                 size_t count, const hipStream_t* streams);
+
+/* d_recv[g][0 .. count) = sum over ranks r of d_send[r][g*count .. (g+1)*count)
+ * (client-sharded tolerance mode: per-GPU partial weighted sums -> bucket g). */
+int plato_agg_comm_reduce_scatter_f32(plato_agg_comm* comm, const float* const* d_send, float* const* d_recv,
+                                      size_t count, const hipStream_t* streams);
 
 #ifdef __cplusplus
 }

@@ -90,6 +90,17 @@ int plato_ingest_parse(const uint8_t* buf, size_t len, plato_ingest_tensor* out,
 int plato_ingest_gather(const uint8_t* buf, size_t len, const plato_ingest_tensor* t, int n,
                         const uint64_t* dst_byte_offset, uint8_t* dst, size_t dst_len, int threads);
 
+/* Packs n contiguous host pieces into one destination (the engine's pinned
+ * staging arena) on the same thread pool: piece i is bytes[i] bytes copied
+ * from src[i] to dst + dst_off[i].  It replaces the per-tensor pack of a CPU
+ * state_dict into the flat arena before its H2D copy (the reference keeps the
+ * tensors apart and reads them one by one in aggregate_deltas,
+ * plato/servers/fedavg.py:148-154).  threads <= 0: up to 16 pool threads.
+ * Returns 0, PLATO_INGEST_EINVAL or PLATO_INGEST_ECAPACITY (a piece outside
+ * dst). */
+int plato_ingest_pack(const void* const* src, const uint64_t* bytes, const uint64_t* dst_off, int n, void* dst,
+                      size_t dst_len, int threads);
+
 /*
  * Join a payload's transport chunks (socket.io delivers 1 MiB chunks that the
  * server concatenates with b"".join before unpickling, plato/servers/base.py:

@@ -18,6 +18,7 @@ ABI_VERSION = 1
 PLATO_AGG_OK = 0
 PLATO_AGG_EINVAL = -1
 PLATO_AGG_EHIP = -2
+PLATO_AGG_ERCCL = -3
 PLATO_AGG_ADD_BASE = 1
 
 _c_void_p = ctypes.c_void_p
@@ -98,6 +99,11 @@ SIGNATURES = {
          ctypes.c_uint32, _c_void_p, ctypes.c_uint32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
          _c_size_t, _c_size_t, _c_void_p],
     ),
+    "plato_agg_comm_create": (_c_int, [_c_int, _c_void_p, ctypes.POINTER(_c_void_p)]),
+    "plato_agg_comm_destroy": (_c_int, [_c_void_p]),
+    "plato_agg_comm_size": (_c_int, [_c_void_p]),
+    "plato_agg_comm_allgather_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_void_p]),
+    "plato_agg_comm_reduce_scatter_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     # tuning / benchmarking (include/plato_agg_tune.h)
     "plato_agg_tune_num_variants": (_c_int, []),
     "plato_agg_tune_set_launch_groups": (None, [_c_u64]),

@@ -785,6 +785,43 @@ int plato_ingest_join(const uint8_t* const* chunks, const size_t* lens, int n, u
   return 0;
 }
 
+int plato_ingest_pack(const void* const* src, const uint64_t* bytes, const uint64_t* dst_off, int n, void* dst,
+                      size_t dst_len, int threads) {
+  if (n < 0 || (n > 0 && (!src || !bytes || !dst_off)) || (!dst && dst_len)) {
+    g_err = "bad argument";
+    return PLATO_INGEST_EINVAL;
+  }
+  uint8_t* out = static_cast<uint8_t*>(dst);
+  std::vector<Piece> pieces;
+  constexpr size_t kChunk = size_t(1) << 20;
+  size_t total = 0;
+  for (int i = 0; i < n; ++i) {
+    if (bytes[i] && !src[i]) {
+      g_err = "null source";
+      return PLATO_INGEST_EINVAL;
+    }
+    if (dst_off[i] > dst_len || bytes[i] > dst_len - dst_off[i]) {
+      g_err = "piece outside the destination";
+      return PLATO_INGEST_ECAPACITY;
+    }
+    const uint8_t* from = static_cast<const uint8_t*>(src[i]);
+    for (size_t o = 0; o < bytes[i]; o += kChunk)
+      pieces.push_back({from + o, out + dst_off[i] + o, std::min<size_t>(kChunk, bytes[i] - o)});
+    total += bytes[i];
+  }
+  int nt = threads > 0 ? threads : int(std::max(1u, std::thread::hardware_concurrency()));
+  nt = int(std::min<size_t>(size_t(nt), std::max<size_t>(1, total / (size_t(2) << 20))));
+  nt = std::min(nt, 16);
+  if (nt <= 1 || pieces.size() <= 1) {
+    for (auto& p : pieces) std::memcpy(p.dst, p.src, p.bytes);
+  } else {
+    Pool::get().run(pieces.size(), nt,
+                    [&](size_t k) { std::memcpy(pieces[k].dst, pieces[k].src, pieces[k].bytes); });
+  }
+  g_err.clear();
+  return 0;
+}
+
 int64_t plato_ingest_read_fd(int fd, uint8_t* dst, size_t len, int threads) {
   if (fd < 0 || (!dst && len)) {
     g_err = "bad argument";

@@ -80,6 +80,7 @@ def lib():
             h.plato_ingest_join.argtypes = [ctypes.POINTER(ctypes.c_void_p), ctypes.POINTER(ctypes.c_size_t),
                                             ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
             for name, res, args in (
+                ("plato_ingest_pack", ctypes.c_int, [vp, vp, vp, ctypes.c_int, vp, sz, ctypes.c_int]),
                 ("plato_ingest_read_fd", ctypes.c_int64, [ctypes.c_int, vp, sz, ctypes.c_int]),
                 ("plato_ingest_zstd_available", ctypes.c_int, []),
                 ("plato_ingest_zstd_content_size", ctypes.c_int64, [vp, sz]),

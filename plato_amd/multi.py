@@ -1,0 +1,444 @@
+"""Multi-GPU aggregation inside one Plato server process (parameter-bucket sharding).
+
+Plato's server is a single process on one asyncio event loop
+(plato/servers/base.py:323-327) that calls ``aggregate_weights`` once per round
+(plato/servers/fedavg.py:171-182).  :class:`MultiDeviceEngine` keeps that
+contract and drives every GPU of the node from the server process:
+
+* the flat fp32 arena is cut into one contiguous, 256-byte-aligned bucket per
+  GPU (:class:`~plato_amd.distributed.BucketPlan`; the int64 counters ride
+  with bucket 0);
+* each payload is packed once into a pinned host slot (or used in place when
+  it arrived through native ingestion) and GPU g receives only bucket g of it,
+  on its own copy stream: the N PCIe links each carry 1/N of every payload;
+* GPU g runs the same sequential-K FedAvg kernel on its bucket.  Every element
+  still sums its K clients in ``self.updates`` order, so the result is
+  bit-identical to the one-GPU and CPU-reference results — there is no
+  cross-GPU arithmetic;
+* the new model is assembled by a per-bucket D2H into one pinned host result
+  (what ``load_weights`` consumes), and, when it should stay device-resident,
+  by an RCCL all-gather over xGMI (``plato_agg_comm_allgather_f32``, one
+  communicator per GPU from ``ncclCommInitAll``).
+
+Rounds whose weights need reductions over the whole staged model (Port's
+similarity, FedAdp, FedAtt, Polaris) or per-entry scales (QSGD payloads) run on
+the first device's single-GPU engine (:attr:`MultiDeviceEngine.primary`).
+"""
+
+from __future__ import annotations
+
+import ctypes
+import time
+from collections import OrderedDict
+from typing import Mapping, Sequence
+
+import numpy as np
+import torch
+
+from . import _lib
+from .arena import CODECS, ArenaLayout, payload_codec
+from .distributed import BucketPlan
+from .engine import FedAvgEngine, fp32_weights, require_device
+from .staging import HostPacker, PinnedRing, ResultPool, arena_source
+
+MULTI_CODECS = ("native", "bf16")
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+class _Shard:
+    """Bucket ``index`` of the arena on one GPU: baseline, client rows, result, streams."""
+
+    def __init__(self, index: int, device: torch.device, plan: BucketPlan):
+        self.index = index
+        self.device = device
+        self.lo, self.hi = plan.f32_range(index)
+        self.ilo, self.ihi = plan.i64_range(index)
+        self.n = self.hi - self.lo
+        self.ni = self.ihi - self.ilo
+        self.per = plan.per
+        self.layout = ArenaLayout([], self.n, self.ni)  # kernel sizes of this bucket
+        with torch.cuda.device(device):
+            self.copy_stream = torch.cuda.Stream(device)
+            self.stream = torch.cuda.Stream(device)
+        self.base_f = torch.empty(self.per, dtype=torch.float32, device=device)
+        self.base_i = torch.empty(max(self.ni, 1), dtype=torch.int64, device=device)
+        self.slabs: dict[str, tuple[torch.Tensor, torch.Tensor]] = {}
+        self.arrival_slabs: dict[str, list] = {}
+
+    def slab(self, codec: str, capacity: int):
+        hit = self.slabs.get(codec)
+        if hit is None or hit[0].shape[0] < capacity:
+            self.slabs.pop(codec, None)
+            dt_f, dt_i = CODECS[codec]
+            hit = (torch.empty((capacity, self.per), dtype=dt_f, device=self.device),
+                   torch.empty((capacity, max(self.ni, 1)), dtype=dt_i, device=self.device))
+            self.slabs[codec] = hit
+        return hit
+
+    def new_arrival_slab(self, codec: str, rows: int):
+        dt_f, dt_i = CODECS[codec]
+        slab = (torch.empty((rows, self.per), dtype=dt_f, device=self.device),
+                torch.empty((rows, max(self.ni, 1)), dtype=dt_i, device=self.device))
+        self.arrival_slabs.setdefault(codec, []).append(slab)
+        return slab
+
+    def copy_in(self, host_f: torch.Tensor, host_i: torch.Tensor, dst_f: torch.Tensor, dst_i: torch.Tensor):
+        """Bucket slice of a full host arena -> this GPU (on the copy stream)."""
+        with torch.cuda.stream(self.copy_stream):
+            if self.n:
+                dst_f[: self.n].copy_(host_f[self.lo:self.hi], non_blocking=True)
+            if self.ni:
+                dst_i[: self.ni].copy_(host_i[self.ilo:self.ihi], non_blocking=True)
+
+
+def _row_ptr(t: torch.Tensor, row: int) -> int:
+    return t.data_ptr() + row * t.stride(0) * t.element_size()
+
+
+class MultiDeviceEngine:
+    """Bucket-sharded FedAvg over several GPUs of one node, driven from one process."""
+
+    ARRIVAL_CHUNK = 16
+
+    def __init__(self, devices: Sequence, variant: int | None = None, ring_depth: int = 4):
+        if not devices:
+            raise ValueError("MultiDeviceEngine needs at least one device")
+        self.devices = [require_device(d) for d in devices]
+        self.lib = _lib.lib()
+        self.variant = variant
+        self.ring_depth = ring_depth
+        self.primary = FedAvgEngine(self.devices[0], variant=variant)
+        self._layout: ArenaLayout | None = None
+        self._plan: BucketPlan | None = None
+        self._shards: list[_Shard] = []
+        self._rings: dict[str, PinnedRing] = {}
+        self._packers: dict[str, HostPacker] = {}
+        self._results: ResultPool | None = None
+        self._arrivals: dict = {}
+        self._arrival_free: dict = {}
+        self._comm = None
+
+    @property
+    def world(self) -> int:
+        return len(self.devices)
+
+    # ------------------------------------------------------------ layout
+    def _prepare(self, template: Mapping[str, torch.Tensor] | ArenaLayout) -> ArenaLayout:
+        layout = template if isinstance(template, ArenaLayout) else ArenaLayout.from_state_dict(template)
+        if self._layout is None or self._layout.signature != layout.signature:
+            self._layout = layout
+            self._plan = BucketPlan.for_layout(layout, self.world)
+            self._shards = [_Shard(g, d, self._plan) for g, d in enumerate(self.devices)]
+            self._rings, self._packers = {}, {}
+            self._results = ResultPool(layout)
+            self._arrivals, self._arrival_free = {}, {}
+        return self._layout
+
+    def _ring(self, codec: str) -> tuple[PinnedRing, HostPacker]:
+        if codec not in self._rings:
+            self._rings[codec] = PinnedRing(self._layout, codec, self.ring_depth)
+            self._packers[codec] = HostPacker(self._layout, codec)
+        return self._rings[codec], self._packers[codec]
+
+    def _stage(self, payload, codec: str, rows) -> None:
+        """Send bucket g of ``payload`` to ``rows[g] = (dst_f row, dst_i row)`` on every GPU."""
+        src = arena_source(payload, self._layout, codec)
+        if src is not None:
+            for shard, (df, di) in zip(self._shards, rows):
+                shard.copy_in(src[0], src[1], df, di)
+            return
+        ring, packer = self._ring(codec)
+        j = ring.acquire()
+        hf, hi = ring.slots[j]
+        packer.pack(payload, hf, hi)
+        events = []
+        for shard, (df, di) in zip(self._shards, rows):
+            shard.copy_in(hf, hi, df, di)
+            ev = torch.cuda.Event()
+            ev.record(shard.copy_stream)
+            events.append(ev)
+        ring.fence(j, events)
+
+    # ------------------------------------------------------------ rounds
+    def begin(self, template, capacity: int, codec: str = "native") -> "MultiRound":
+        if capacity <= 0:
+            raise ValueError("no client payloads to aggregate")
+        if codec not in MULTI_CODECS:
+            raise ValueError(f"codec {codec!r} is aggregated on one device (use .primary)")
+        layout = self._prepare(template)
+        for shard in self._shards:
+            shard.slab(codec, capacity)
+            # the previous round's kernel may still read this round's rows
+            shard.copy_stream.wait_stream(shard.stream)
+        return MultiRound(self, layout, capacity, codec)
+
+    def prestage(self, payload: Mapping[str, torch.Tensor], baseline_layout: ArenaLayout) -> bool:
+        """Copy an arriving payload's buckets to their GPUs now (adopted by the next round)."""
+        codec = payload_codec(payload)
+        if codec not in MULTI_CODECS:
+            return self.primary.prestage(payload, baseline_layout)
+        try:
+            baseline_layout.check_compatible(payload, "arriving payload", codec)
+        except (KeyError, ValueError):
+            return False
+        self._prepare(baseline_layout)
+        free = self._arrival_free.setdefault(codec, [])
+        if not free:
+            slabs = [s.new_arrival_slab(codec, self.ARRIVAL_CHUNK) for s in self._shards]
+            free.extend((slabs, r) for r in range(self.ARRIVAL_CHUNK))
+        slabs, row = free.pop()
+        self._stage(payload, codec, [(f[row], i[row]) for f, i in slabs])
+        ptrs = [(_row_ptr(f, row), _row_ptr(i, row)) for f, i in slabs]
+        self._arrivals[id(payload)] = (payload, codec, self._layout.signature, ptrs, slabs, row)
+        return True
+
+    def _arrival_rows(self, payload, layout: ArenaLayout, codec: str):
+        hit = self._arrivals.get(id(payload))
+        if hit is None or hit[0] is not payload or hit[1] != codec or hit[2] != layout.signature:
+            return None
+        return hit[3]
+
+    def release_arrivals(self) -> None:
+        for _, codec, _, _, slabs, row in self._arrivals.values():
+            self._arrival_free.setdefault(codec, []).append((slabs, row))
+        self._arrivals = {}
+        self.primary.release_arrivals()
+
+    def comm(self):
+        """The RCCL communicator over the engine's devices (distinct GPUs only)."""
+        if self._comm is None:
+            ids = [d.index for d in self.devices]
+            if len(set(ids)) != len(ids):
+                return None
+            handle = ctypes.c_void_p()
+            arr = (ctypes.c_int * len(ids))(*ids)
+            _lib.call("plato_agg_comm_create", len(ids), ctypes.cast(arr, ctypes.c_void_p), ctypes.byref(handle))
+            self._comm = handle
+        return self._comm
+
+    def close(self) -> None:
+        if self._comm is not None:
+            _lib.call("plato_agg_comm_destroy", self._comm)
+            self._comm = None
+
+    def __del__(self):  # pragma: no cover - interpreter teardown order varies
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------- convenience API
+    def aggregate_weights(self, baseline, weights_received, weights, scales=None):
+        """``update_weights(aggregate_deltas(compute_weight_deltas(b, X)))`` over the GPUs."""
+        k = len(weights_received)
+        if k == 0:
+            raise ValueError("no client payloads to aggregate")
+        if len(weights) != k:
+            raise ValueError("weights must have one entry per client")
+        codec = payload_codec(weights_received[0])
+        if codec not in MULTI_CODECS:
+            return self.primary.aggregate_weights(baseline, weights_received, weights, scales)
+        rnd = self.begin(baseline, k, codec)
+        rnd.put_baseline(baseline)
+        for i, sd in enumerate(weights_received):
+            if not rnd.adopt(i, sd):
+                rnd.put_client(i, sd)
+        rnd.launch(weights, scales)
+        return rnd.result()
+
+    def aggregate_deltas(self, deltas_received, weights, scales=None):
+        k = len(deltas_received)
+        if k == 0:
+            raise ValueError("no client deltas to aggregate")
+        if len(weights) != k:
+            raise ValueError("weights must have one entry per client")
+        rnd = self.begin(deltas_received[0], k)
+        for i, sd in enumerate(deltas_received):
+            rnd.put_client(i, sd, what="deltas_received")
+        rnd.launch(weights, scales, deltas=True)
+        return rnd.result()
+
+
+class MultiRound:
+    """One bucket-sharded aggregation: stage (any order), launch on every GPU, assemble."""
+
+    def __init__(self, engine: MultiDeviceEngine, layout: ArenaLayout, capacity: int, codec: str):
+        self.engine = engine
+        self.layout = layout
+        self.capacity = capacity
+        self.codec = codec
+        self.staged = [False] * capacity
+        self._ptrs: list = [None] * capacity  # per slot: per shard (fp32 row ptr, int64 row ptr)
+        self.has_baseline = False
+        self.events: list = []
+        self._out = None
+        self._keep = None
+        self._device_results = None
+        self._t0 = time.perf_counter()
+        self.timings: dict = {}
+        self._k = 0
+
+    def put_baseline(self, baseline: Mapping[str, torch.Tensor]) -> None:
+        self.layout.check_compatible(baseline, "baseline_weights")
+        eng = self.engine
+        eng._stage(baseline, "native", [(s.base_f, s.base_i) for s in eng._shards])
+        self.has_baseline = True
+
+    def put_client(self, slot: int, payload, what: str = "weights_received") -> None:
+        if not 0 <= slot < self.capacity:
+            raise IndexError(f"slot {slot} outside [0, {self.capacity})")
+        self.layout.check_compatible(payload, f"{what}[{slot}]", self.codec)
+        eng = self.engine
+        rows = []
+        ptrs = []
+        for s in eng._shards:
+            f, i = s.slabs[self.codec]
+            rows.append((f[slot], i[slot]))
+            ptrs.append((_row_ptr(f, slot), _row_ptr(i, slot)))
+        eng._stage(payload, self.codec, rows)
+        self._ptrs[slot] = ptrs
+        self.staged[slot] = True
+
+    def adopt(self, slot: int, payload) -> bool:
+        if not 0 <= slot < self.capacity:
+            raise IndexError(f"slot {slot} outside [0, {self.capacity})")
+        hit = self.engine._arrival_rows(payload, self.layout, self.codec)
+        if hit is None:
+            return False
+        self._ptrs[slot] = hit
+        self.staged[slot] = True
+        return True
+
+    def launch(self, weights: Sequence[float], scales: Sequence[float] | None = None,
+               order: Sequence[int] | None = None, deltas: bool = False, gather: bool = False) -> None:
+        """Enqueue every GPU's bucket kernel, then the per-bucket D2H (and the all-gather if ``gather``)."""
+        order = list(range(len(weights))) if order is None else list(order)
+        if len(order) != len(weights):
+            raise ValueError("order and weights must have the same length")
+        for slot in order:
+            if not (0 <= slot < self.capacity and self.staged[slot]):
+                raise ValueError(f"client slot {slot} was not staged")
+        if not deltas and not self.has_baseline:
+            raise ValueError("baseline not staged")
+        if deltas and self.codec != "native":
+            raise ValueError("deltas are fp32 (x - b promotes coded payloads); use the native codec")
+        if scales is not None and len(scales) != len(weights):
+            raise ValueError("scales must have one entry per client")
+        eng = self.engine
+        k = len(order)
+        self._k = k
+        w_host = torch.from_numpy(fp32_weights(weights)).pin_memory()
+        s_host = None if scales is None else torch.from_numpy(fp32_weights(scales)).pin_memory()
+        host_f, host_i = eng._results.get()
+        keep = [w_host, s_host]
+        self.timings["stage_ms"] = (time.perf_counter() - self._t0) * 1e3
+        self.events, kernel_events = [], []
+        outs = []
+        for s in eng._shards:
+            pf = np.asarray([self._ptrs[i][s.index][0] for i in order], dtype=np.int64)
+            pi = np.asarray([self._ptrs[i][s.index][1] for i in order], dtype=np.int64)
+            with torch.cuda.device(s.device), torch.cuda.stream(s.stream):
+                s.stream.wait_stream(s.copy_stream)
+                w = w_host.to(s.device, non_blocking=True)
+                sc = None if s_host is None else s_host.to(s.device, non_blocking=True)
+                tf = torch.from_numpy(pf).pin_memory().to(s.device, non_blocking=True)
+                ti = torch.from_numpy(pi).pin_memory().to(s.device, non_blocking=True)
+                out_f = torch.empty(s.per, dtype=torch.float32, device=s.device)
+                out_i = torch.empty(max(s.ni, 1), dtype=torch.float32, device=s.device)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(s.stream)
+                h = s.stream.cuda_stream
+                n_i = s.ni
+                if self.codec == "bf16":
+                    _lib.call("plato_agg_fedavg_weights_bf16", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w),
+                              _ptr(sc), k, _ptr(s.base_f), _ptr(s.base_i) if n_i else None, _ptr(out_f),
+                              _ptr(out_i) if n_i else None, s.n, n_i, h)
+                elif eng.variant is not None:
+                    _lib.call("plato_agg_tune_fedavg", eng.variant, int(not deltas), _ptr(tf),
+                              _ptr(ti) if n_i else None, _ptr(w), _ptr(sc), k,
+                              None if deltas else _ptr(s.base_f), None if (deltas or not n_i) else _ptr(s.base_i),
+                              _ptr(out_f), _ptr(out_i) if n_i else None, s.n, n_i, h)
+                elif deltas:
+                    _lib.call("plato_agg_fedavg_deltas", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w), _ptr(sc),
+                              k, _ptr(out_f), _ptr(out_i) if n_i else None, s.n, n_i, h)
+                else:
+                    _lib.call("plato_agg_fedavg_weights", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w), _ptr(sc),
+                              k, _ptr(s.base_f), _ptr(s.base_i) if n_i else None, _ptr(out_f),
+                              _ptr(out_i) if n_i else None, s.n, n_i, h)
+                e1.record(s.stream)
+                kernel_events.append((e0, e1))
+                keep.extend((w, sc, tf, ti))
+                outs.append((out_f, out_i))
+        if gather:
+            self._device_results = self._gather(outs)
+        for s, (out_f, out_i) in zip(eng._shards, outs):
+            with torch.cuda.device(s.device), torch.cuda.stream(s.stream):
+                if s.n:
+                    host_f[s.lo:s.hi].copy_(out_f[: s.n], non_blocking=True)
+                if s.ni:
+                    host_i[s.ilo:s.ihi].copy_(out_i[: s.ni], non_blocking=True)
+                ev = torch.cuda.Event(enable_timing=True)
+                ev.record(s.stream)
+                self.events.append(ev)
+        self._kernel_events = kernel_events
+        self._out = (host_f, host_i)
+        self._keep = (keep, outs)
+
+    def _gather(self, outs):
+        """Every GPU gets the whole new model: RCCL all-gather of the buckets (device copies if GPUs repeat)."""
+        eng = self.engine
+        per, world = eng._plan.per, eng.world
+        fulls = [torch.empty(per * world, dtype=torch.float32, device=s.device) for s in eng._shards]
+        comm = eng.comm() if world > 1 else None
+        if comm is not None:
+            send = (ctypes.c_void_p * world)(*[o[0].data_ptr() for o in outs])
+            recv = (ctypes.c_void_p * world)(*[f.data_ptr() for f in fulls])
+            streams = (ctypes.c_void_p * world)(*[s.stream.cuda_stream for s in eng._shards])
+            _lib.call("plato_agg_comm_allgather_f32", comm, ctypes.cast(send, ctypes.c_void_p),
+                      ctypes.cast(recv, ctypes.c_void_p), per, ctypes.cast(streams, ctypes.c_void_p))
+        else:
+            for g, s in enumerate(eng._shards):
+                with torch.cuda.device(s.device), torch.cuda.stream(s.stream):
+                    for r, src in enumerate(eng._shards):
+                        if r != g:
+                            s.stream.wait_stream(src.stream)
+                        fulls[g][r * per:(r + 1) * per].copy_(outs[r][0], non_blocking=True)
+        ints = []
+        s0 = eng._shards[0]
+        for s in eng._shards:
+            with torch.cuda.device(s.device), torch.cuda.stream(s.stream):
+                s.stream.wait_stream(s0.stream)
+                ints.append(outs[0][1][: s0.ni].to(s.device, non_blocking=True))
+        return [(f[: self.layout.n_f32], i) for f, i in zip(fulls, ints)]
+
+    def device_result(self, g: int = 0):
+        """(fp32 arena, fp32 values of the int64 entries) of the new model on GPU ``g`` (``gather=True``)."""
+        if self._device_results is None:
+            raise RuntimeError("launch(..., gather=True) first")
+        return self._device_results[g]
+
+    def algorithmic_bytes(self) -> int:
+        return self.layout.algorithmic_bytes(self._k)
+
+    def ready(self) -> bool:
+        return bool(self.events) and all(ev.query() for ev in self.events)
+
+    def wait(self) -> None:
+        for ev in self.events:
+            ev.synchronize()
+
+    def result(self) -> "OrderedDict[str, torch.Tensor]":
+        if not self.events:
+            raise RuntimeError("launch() first")
+        self.wait()
+        self.timings["kernel_ms"] = max(a.elapsed_time(b) for a, b in self._kernel_events)
+        self.timings["d2h_ms"] = max(b.elapsed_time(ev) for (_, b), ev in zip(self._kernel_events, self.events))
+        self.timings["total_ms"] = (time.perf_counter() - self._t0) * 1e3
+        host_f, host_i = self._out
+        self._out = None
+        self._keep = None
+        return self.layout.unpack(host_f, host_i)

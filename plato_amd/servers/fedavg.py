@@ -22,26 +22,70 @@ the classes in by hand: ``class Server(FusedAggregationMixin, fedavg.Server)``.
 from __future__ import annotations
 
 import asyncio
+import concurrent.futures
 
+from .. import tracing
 from .. import weights as W
 from ..arena import payload_codec
 from ..engine import FedAvgEngine
 
 
 class _EngineHolder:
-    """Lazily created per-server GPU engine (one process per GPU)."""
+    """Lazily created per-server GPU engine: one GPU, or every GPU of ``aggregation_devices``."""
 
     #: torch device string for the engine, e.g. "cuda:0" (None: current device)
     aggregation_device = None
+    #: several devices ("cuda:0", "cuda:1", ... or ordinals): the model is
+    #: bucket-sharded over them from this one server process (plato_amd.multi)
+    aggregation_devices = None
     #: kernel variant override (tuning only; None = library default)
     aggregation_variant = None
+    #: weights computed from the staged payloads (Port, FedAdp, Polaris): such
+    #: rounds run on one GPU (the multi-GPU engine's first device)
+    needs_staged_round = False
 
-    def aggregation_engine(self) -> FedAvgEngine:
+    def aggregation_engine(self):
         eng = getattr(self, "_plato_amd_engine", None)
         if eng is None:
-            eng = FedAvgEngine(self.aggregation_device, variant=self.aggregation_variant)
+            devices = self.aggregation_devices
+            if devices is not None and len(devices) > 1:
+                from ..multi import MultiDeviceEngine
+
+                eng = MultiDeviceEngine([f"cuda:{d}" if isinstance(d, int) else d for d in devices],
+                                        variant=self.aggregation_variant)
+            else:
+                device = devices[0] if devices else self.aggregation_device
+                device = f"cuda:{device}" if isinstance(device, int) else device
+                eng = FedAvgEngine(device, variant=self.aggregation_variant)
             self._plato_amd_engine = eng
         return eng
+
+    def round_engine(self, codec: str):
+        """The engine one round runs on (multi-GPU unless the round needs one device)."""
+        eng = self.aggregation_engine()
+        primary = getattr(eng, "primary", None)
+        if primary is not None and (self.needs_staged_round or codec not in ("native", "bf16")):
+            return primary
+        return eng
+
+    def aggregation_executor(self) -> concurrent.futures.ThreadPoolExecutor:
+        """One worker thread that packs and copies payloads, off the server's event loop."""
+        ex = getattr(self, "_plato_amd_executor", None)
+        if ex is None:
+            ex = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="plato-amd-stage")
+            self._plato_amd_executor = ex
+        return ex
+
+    async def _off_loop(self, fn, *args):
+        return await asyncio.get_running_loop().run_in_executor(self.aggregation_executor(), fn, *args)
+
+    async def _finish(self, rnd):
+        """Wait for the round's result on the worker thread (a HIP event wait, no busy polling)."""
+        await self._off_loop(rnd.wait)
+        result = rnd.result()
+        self._plato_amd_timings = dict(rnd.timings, bytes=rnd.algorithmic_bytes(),
+                                       gpus=getattr(getattr(rnd, "engine", None), "world", 1))
+        return result
 
     def aggregation_weights(self, updates):
         """Per-update (weights, second scalars or None), in ``updates`` order.
@@ -52,32 +96,59 @@ class _EngineHolder:
         self.total_samples = sum(update.report.num_samples for update in updates)
         return W.fedavg([update.report.num_samples for update in updates]), None
 
+    def get_logged_items(self) -> dict:
+        """The reference's CSV items (``servers/fedavg.py:234-252``) plus the last aggregation's timings.
+
+        ``aggregation_stage_ms`` (pack + H2D issue, host wall), ``aggregation_kernel_ms``
+        (HIP events, max over GPUs), ``aggregation_d2h_ms``, ``aggregation_total_ms``
+        (hook entry to result), ``aggregation_GBps`` (algorithmic bytes / kernel time)
+        and ``aggregation_gpus``; list them in ``results.types`` to record them.
+        """
+        items = super().get_logged_items() if hasattr(super(), "get_logged_items") else {}
+        t = getattr(self, "_plato_amd_timings", None) or {}
+        kernel = t.get("kernel_ms")
+        items.update({
+            "aggregation_stage_ms": t.get("stage_ms"),
+            "aggregation_kernel_ms": kernel,
+            "aggregation_d2h_ms": t.get("d2h_ms"),
+            "aggregation_total_ms": t.get("total_ms"),
+            "aggregation_GBps": (t["bytes"] / (kernel * 1e-3) / 1e9) if kernel else None,
+            "aggregation_gpus": t.get("gpus"),
+        })
+        return items
+
 
 class FusedAggregationMixin(_EngineHolder):
-    """``aggregate_weights`` hook: fused deltas -> weighted sum -> update on the GPU."""
+    """``aggregate_weights`` hook: fused deltas -> weighted sum -> update on the GPU(s)."""
 
     async def aggregate_weights(self, updates, baseline_weights, weights_received):
-        engine = self.aggregation_engine()
         # bf16 payloads (model_quantize on the clients) stay bf16 on the device
-        rnd = engine.begin(baseline_weights, len(weights_received), payload_codec(weights_received[0]))
-        rnd.put_baseline(baseline_weights)
-        for slot, payload in enumerate(weights_received):
-            # payloads staged at arrival (WireIngestMixin.stage_on_arrival) are adopted in place
-            if not rnd.adopt(slot, payload):
-                rnd.put_client(slot, payload)
-            # Yield to other tasks in the server between clients, as the
-            # reference does per client (servers/fedavg.py:157).
-            await asyncio.sleep(0)
-        # weights may need the staged arenas (Port's similarity reduction)
+        codec = payload_codec(weights_received[0])
+        engine = self.round_engine(codec)
+        rnd = engine.begin(baseline_weights, len(weights_received), codec)
+
+        def stage():
+            with tracing.range("plato_amd.stage"):
+                rnd.put_baseline(baseline_weights)
+                for slot, payload in enumerate(weights_received):
+                    # payloads staged at arrival (WireIngestMixin.stage_on_arrival) are adopted in place
+                    if not rnd.adopt(slot, payload):
+                        rnd.put_client(slot, payload)
+
+        # Pack + H2D run on a worker thread: the event loop keeps serving the
+        # clients meanwhile (the reference yields per client, servers/fedavg.py:157).
+        await self._off_loop(stage)
+        # weights may need the staged arenas (Port's similarity reduction); the
+        # hook runs on the event loop thread like the reference's
         self._plato_amd_round = rnd
         try:
             weights, scales = self.aggregation_weights(updates)
         finally:
             self._plato_amd_round = None
-        rnd.launch(weights, scales)
-        while not rnd.ready():
-            await asyncio.sleep(0)
-        result = rnd.result()
+        with tracing.range("plato_amd.launch"):
+            rnd.launch(weights, scales)
+        with tracing.range("plato_amd.fetch"):
+            result = await self._finish(rnd)
         engine.release_arrivals()
         return result
 
@@ -87,15 +158,19 @@ class DeltasAggregationMixin(_EngineHolder):
 
     async def aggregate_deltas(self, updates, deltas_received):
         weights, scales = self.aggregation_weights(updates)
-        engine = self.aggregation_engine()
+        engine = self.round_engine("native")
         rnd = engine.begin(deltas_received[0], len(deltas_received))
-        for slot, delta in enumerate(deltas_received):
-            rnd.put_client(slot, delta, what="deltas_received")
-            await asyncio.sleep(0)
-        rnd.launch(weights, scales, deltas=True)
-        while not rnd.ready():
-            await asyncio.sleep(0)
-        return rnd.result()
+
+        def stage():
+            with tracing.range("plato_amd.stage"):
+                for slot, delta in enumerate(deltas_received):
+                    rnd.put_client(slot, delta, what="deltas_received")
+
+        await self._off_loop(stage)
+        with tracing.range("plato_amd.launch"):
+            rnd.launch(weights, scales, deltas=True)
+        with tracing.range("plato_amd.fetch"):
+            return await self._finish(rnd)
 
 
 def make_server(base=None, mixin=FusedAggregationMixin, name: str = "Server"):

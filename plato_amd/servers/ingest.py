@@ -24,7 +24,7 @@ import pickle
 import sys
 
 from .. import ingest
-from ..arena import ArenaLayout
+from ..arena import ArenaLayout, payload_codec
 
 
 class WireIngestMixin:
@@ -96,7 +96,7 @@ class WireIngestMixin:
         if self.stage_on_arrival and isinstance(payload, ingest.ArenaStateDict):
             layout = self._ingest_layout()
             if layout is not None:
-                self.aggregation_engine().prestage(payload, layout)
+                self.round_engine(payload_codec(payload)).prestage(payload, layout)
 
         if self.wire_size_accounting and file_len is not None:
             payload_size = (file_len + sys.getsizeof(b"")) / 1024**2
@@ -128,7 +128,7 @@ class WireIngestMixin:
         if self.stage_on_arrival and isinstance(_data, ingest.ArenaStateDict):
             layout = self._ingest_layout()
             if layout is not None:
-                self.aggregation_engine().prestage(_data, layout)
+                self.round_engine(payload_codec(_data)).prestage(_data, layout)
 
         if self.client_payload[sid] is None:
             self.client_payload[sid] = _data

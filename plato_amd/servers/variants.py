@@ -76,6 +76,8 @@ class PortWeights(_EngineHolder):
             out[i] = sim
         return out
 
+    needs_staged_round = True
+
     #: Port hyper-parameters; None = Config().server.<name>, else the reference default
     similarity_weight = None
     staleness_weight = None
@@ -132,8 +134,9 @@ class FedAsyncMixing(_EngineHolder):
                 self.mixing_hyperparam = W.fedasync_mixing(
                     self.mixing_hyperparam, updates[0].staleness, fn.type,
                     getattr(fn, "a", 1), getattr(fn, "b", 0))
-        return self.aggregation_engine().mix_weights(baseline_weights, weights_received[0],
-                                                     self.mixing_hyperparam)
+        engine = self.aggregation_engine()
+        engine = getattr(engine, "primary", engine)  # one model-sized elementwise pass: one GPU
+        return engine.mix_weights(baseline_weights, weights_received[0], self.mixing_hyperparam)
 
 
 class GanDeltasAggregationMixin(_EngineHolder):
@@ -145,7 +148,6 @@ class GanDeltasAggregationMixin(_EngineHolder):
     """
 
     async def aggregate_deltas(self, updates, deltas_received):
-        import asyncio
         from collections import OrderedDict
 
         weights, scales = self.aggregation_weights(updates)
@@ -154,15 +156,16 @@ class GanDeltasAggregationMixin(_EngineHolder):
             d = OrderedDict((f"g.{n}", t) for n, t in gen.items())
             d.update((f"d.{n}", t) for n, t in disc.items())
             combined.append(d)
-        engine = self.aggregation_engine()
+        engine = self.round_engine("native")
         rnd = engine.begin(combined[0], len(combined))
-        for slot, d in enumerate(combined):
-            rnd.put_client(slot, d, what="deltas_received")
-            await asyncio.sleep(0)
+
+        def stage():
+            for slot, d in enumerate(combined):
+                rnd.put_client(slot, d, what="deltas_received")
+
+        await self._off_loop(stage)
         rnd.launch(weights, scales, deltas=True)
-        while not rnd.ready():
-            await asyncio.sleep(0)
-        avg = rnd.result()
+        avg = await self._finish(rnd)
         gen = {n[2:]: t for n, t in avg.items() if n.startswith("g.")}
         disc = {n[2:]: t for n, t in avg.items() if n.startswith("d.")}
         return gen, disc
@@ -206,6 +209,8 @@ class FedAdpWeights(_EngineHolder):
     come from the server.
     """
 
+    needs_staged_round = True
+
     #: FedAdp's alpha; None = Config().algorithm.alpha, else 5 (fedadp_server.py:112-114)
     fedadp_alpha = None
     #: learning rate of process_grad; None = Config().parameters.optimizer.lr
@@ -245,6 +250,8 @@ class PolarisWeights(_EngineHolder):
     from one ``plato_agg_entry_stats`` pass over the staged payloads.  The
     solver itself (cvxopt/mosek, ``:129-186``) stays the reference's.
     """
+
+    needs_staged_round = True
 
     def aggregation_weights(self, updates):
         weights, scales = super().aggregation_weights(updates)  # FedAvg n_i/N, sets total_samples

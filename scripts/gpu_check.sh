@@ -25,6 +25,9 @@ for step in "$@"; do
     bench) run bench 900 python bench.py ;;
     dist2) run bench_dist2 600 env PLATO_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 3 ;;
     dist2c3) run bench_dist2_c3 600 env PLATO_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node=2 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 2 --config C3 --clients 256 --steps 5 --warmup 2 ;;
+    multi1) run bench_multi1 600 python bench.py --engine-devices 1 --steps 3 --warmup 1 ;;
+    multi4) run bench_multi4 600 python bench.py --engine-devices 4 --steps 3 --warmup 1 ;;
+    profile) run profile 900 bash scripts/profile.sh ${PROFILE_TAG:-r02} ;;
     bf16) run bench_bf16 600 python bench.py --codec bf16 --steps 20 ;;
     bf16sweep) run sweep_bf16 600 python bench.py --codec bf16 --sweep --steps 10 ;;
     variants) run bench_variants 600 python scripts/bench_variants.py ;;

@@ -57,6 +57,14 @@ class OracleRound:
     def ready(self):
         return True
 
+    def wait(self):
+        pass
+
+    timings = {}
+
+    def algorithmic_bytes(self):
+        return 0
+
     def result(self):
         return self.out
 

@@ -47,7 +47,7 @@ def test_ingest_library_exports_its_header():
     handle = ctypes.CDLL(ingest.LIB_PATH)
     names = declared_symbols("plato_ingest.h")
     assert names == {"plato_ingest_last_error", "plato_ingest_parse", "plato_ingest_gather", "plato_ingest_join",
-                     "plato_ingest_read_fd",
+                     "plato_ingest_read_fd", "plato_ingest_pack",
                      "plato_ingest_zstd_available", "plato_ingest_zstd_content_size",
                      "plato_ingest_zstd_decompress", "plato_ingest_zstd_bound", "plato_ingest_zstd_compress"}
     for name in names:

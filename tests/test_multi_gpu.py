@@ -1,0 +1,253 @@
+"""Multi-GPU engine in one server process (plato_amd.multi) against the reference fixtures.
+
+``MultiDeviceEngine`` bucket-shards the arena over a device list; the result
+must be bit-identical to the reference for any bucket count.  On a one-GPU
+box the device list repeats cuda:0 (every bucket still gets its own arenas,
+streams and copies, so the sharding, the per-bucket H2D/D2H assembly and the
+pointer tables are all exercised); the RCCL communicator needs distinct GPUs
+and runs when the box has them.
+"""
+
+import asyncio
+import pickle
+
+import numpy as np
+import pytest
+import torch
+
+from plato_amd import weights as W
+from tests import golden_cases as G
+from tests.test_golden_gpu import CASES, _bf16_payloads, _flat, _host_payloads, _updates
+
+pytestmark = pytest.mark.gpu
+
+
+def _devices(n):
+    count = torch.cuda.device_count()
+    return [f"cuda:{g % count}" for g in range(n)] if count >= 2 else ["cuda:0"] * n
+
+
+def _case(name):
+    return next(c for c in CASES if c["recipe"]["name"] == name)
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("name", ["resnet18_k16_permuted", "resnet18_k5_int64_edges", "lenet5_k7_edge_values",
+                                  "C3_resnet50_200cls_k8", "resnet18_k1"])
+def test_multi_device_hook_matches_reference(name, n):
+    """FusedAggregationMixin with aggregation_devices: the reference digest for every bucket count."""
+    from plato_amd.servers import FusedAggregationMixin
+
+    case = _case(name)
+    recipe, exp = case["recipe"], case["expected"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    updates = _updates(recipe, payloads)
+
+    class Server(FusedAggregationMixin):
+        aggregation_devices = _devices(n)
+
+    server = Server()
+    updated = asyncio.run(server.aggregate_weights(updates, baseline, [u.payload for u in updates]))
+    assert server.aggregation_engine().world == n
+    assert list(updated.keys()) == [e.name for e in layout.entries]
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+    assert server.total_samples == sum(recipe["num_samples"])
+    items = server.get_logged_items()
+    assert items["aggregation_gpus"] == n and items["aggregation_kernel_ms"] > 0
+    assert items["aggregation_GBps"] > 0 and items["aggregation_total_ms"] >= items["aggregation_kernel_ms"]
+
+
+@pytest.mark.parametrize("n", [2, 5])
+def test_multi_device_deltas_and_variants(n):
+    """aggregate_deltas (deltas mode), FedBuff and Pisces (second scalar) through the multi engine."""
+    from plato_amd.servers import DeltasAggregationMixin
+    from plato_amd.servers import variants as V
+
+    for name, mixin in (("lenet5_k7_edge_values", DeltasAggregationMixin),
+                        ("fedbuff_resnet18_k16", V.FedBuffServerMixin),
+                        ("pisces_resnet18_k8", V.PiscesServerMixin)):
+        case = _case(name)
+        recipe, exp = case["recipe"], case["expected"]
+        layout, baseline, payloads = _host_payloads(recipe)
+        updates = _updates(recipe, payloads)
+
+        class Server(mixin):
+            aggregation_devices = _devices(n)
+            staleness_factor = 0.5
+
+            def __init__(self):
+                self.client_staleness = {}
+                self.current_round = 0
+
+        server = Server()
+        received = [u.payload for u in updates]
+        if hasattr(server, "aggregate_weights"):
+            updated = asyncio.run(server.aggregate_weights(updates, baseline, received))
+        else:
+            deltas = [{k: p[k] - baseline[k] for k in p} for p in received]
+            avg = asyncio.run(server.aggregate_deltas(updates, deltas))
+            assert G.sha(G.canon(_flat(layout, avg, "f32"))) == exp["avg_f32_sha256"], name
+            updated = {k: baseline[k] + avg[k] for k in baseline}
+        assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"], name
+        assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"], name
+
+
+def test_multi_device_routes_staged_round_variants_to_one_gpu():
+    """Port needs the whole staged model: it runs on the first device's engine, same digest."""
+    from plato_amd.servers import variants as V
+
+    case = _case("port_resnet18_k16")
+    recipe, exp = case["recipe"], case["expected"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    updates = _updates(recipe, payloads)
+
+    class Server(V.PortServerMixin):
+        aggregation_devices = _devices(4)
+        staleness_weight = 3
+
+        def __init__(self):
+            self.current_round = 0
+
+    server = Server()
+    updated = asyncio.run(server.aggregate_weights(updates, baseline, [u.payload for u in updates]))
+    assert server.round_engine("native") is server.aggregation_engine().primary
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+
+
+@pytest.mark.parametrize("name", ["bf16_codec_resnet18_k16", "bf16_codec_lenet5_k9"])
+def test_multi_device_bf16_payloads(name):
+    from plato_amd.multi import MultiDeviceEngine
+
+    case = _case(name)
+    recipe, exp = case["recipe"], case["expected"]
+    layout, baseline, payloads = _bf16_payloads(recipe)
+    weights, _ = G.weights_for(recipe, W)
+    eng = MultiDeviceEngine(_devices(3))
+    updated = eng.aggregate_weights(baseline, [payloads[c] for c in G.order_of(recipe)], weights)
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+
+
+def test_multi_device_wire_payloads_staged_on_arrival():
+    """Native-ingested payloads prestaged bucket by bucket as they arrive, adopted in updates order."""
+    from plato_amd import ingest
+    from plato_amd.servers import FusedAggregationMixin, WireIngestMixin
+
+    case = _case("resnet18_k16_permuted")
+    recipe, exp = case["recipe"], case["expected"]
+    layout, baseline, payloads = _host_payloads(recipe)
+
+    class Algo:
+        def extract_weights(self):
+            return baseline
+
+    class Server(WireIngestMixin, FusedAggregationMixin):
+        aggregation_devices = _devices(4)
+        stage_on_arrival = True
+
+        def __init__(self):
+            self.algorithm = Algo()
+            self.client_chunks, self.client_payload, self.training_clients = {}, {}, {}
+
+    server = Server()
+    arrived = {}
+    for c in reversed(range(recipe["k"])):
+        sid = f"s{c}"
+        server.client_chunks[sid] = [pickle.dumps(type(payloads[c])((n, t.clone()) for n, t in payloads[c].items()))]
+        server.client_payload[sid] = None
+        server.training_clients[c + 1] = True
+        asyncio.run(server._client_payload_arrived(sid, c + 1))
+        arrived[c] = server.client_payload[sid]
+        assert isinstance(arrived[c], ingest.ArenaStateDict)
+    eng = server.aggregation_engine()
+    assert len(eng._arrivals) == recipe["k"]
+    updates = _updates(recipe, [arrived[c] for c in range(recipe["k"])])
+    updated = asyncio.run(server.aggregate_weights(updates, baseline, [u.payload for u in updates]))
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+    assert len(eng._arrivals) == 0
+
+
+def test_multi_device_gather_leaves_the_model_on_every_gpu():
+    from plato_amd.multi import MultiDeviceEngine
+
+    case = _case("C3_resnet50_200cls_k8")
+    recipe, exp = case["recipe"], case["expected"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    weights, _ = G.weights_for(recipe, W)
+    eng = MultiDeviceEngine(_devices(4))
+    rnd = eng.begin(baseline, recipe["k"])
+    rnd.put_baseline(baseline)
+    for slot, c in enumerate(G.order_of(recipe)):
+        rnd.put_client(slot, payloads[c])
+    rnd.launch(weights, gather=True)
+    host = rnd.result()
+    flat = _flat(layout, host, "f32")
+    assert G.sha(G.canon(flat)) == exp["updated_f32_sha256"]
+    for g in range(eng.world):
+        dev_f, dev_i = rnd.device_result(g)
+        assert dev_f.device == eng.devices[g]
+        assert np.array_equal(dev_f.cpu().numpy().view(np.uint32), flat.view(np.uint32))
+        assert np.array_equal(dev_i.cpu().numpy().view(np.uint32), _flat(layout, host, "i64").view(np.uint32))
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="RCCL communicator needs two or more GPUs")
+def test_rccl_allgather_and_reduce_scatter_in_process():
+    import ctypes
+
+    from plato_amd import _lib
+    from plato_amd.multi import MultiDeviceEngine
+
+    n = torch.cuda.device_count()
+    eng = MultiDeviceEngine([f"cuda:{g}" for g in range(n)])
+    comm = eng.comm()
+    assert comm is not None and _lib.lib().plato_agg_comm_size(comm) == n
+    count = 1000
+    send = [torch.full((count,), float(g + 1), device=f"cuda:{g}") for g in range(n)]
+    recv = [torch.empty(count * n, device=f"cuda:{g}") for g in range(n)]
+    streams = [torch.cuda.current_stream(g).cuda_stream for g in range(n)]
+    arr = lambda xs: ctypes.cast((ctypes.c_void_p * n)(*xs), ctypes.c_void_p)  # noqa: E731
+    _lib.call("plato_agg_comm_allgather_f32", comm, arr([t.data_ptr() for t in send]),
+              arr([t.data_ptr() for t in recv]), count, arr(streams))
+    for g in range(n):
+        torch.cuda.synchronize(g)
+        assert torch.equal(recv[g].cpu(), torch.arange(1, n + 1).float().repeat_interleave(count))
+    part = [torch.full((count * n,), 1.0, device=f"cuda:{g}") for g in range(n)]
+    out = [torch.empty(count, device=f"cuda:{g}") for g in range(n)]
+    _lib.call("plato_agg_comm_reduce_scatter_f32", comm, arr([t.data_ptr() for t in part]),
+              arr([t.data_ptr() for t in out]), count, arr(streams))
+    for g in range(n):
+        torch.cuda.synchronize(g)
+        assert torch.all(out[g].cpu() == float(n))
+    eng.close()
+
+
+def test_rccl_refuses_repeated_devices():
+    import ctypes
+
+    from plato_amd import _lib
+
+    arr = (ctypes.c_int * 2)(0, 0)
+    handle = ctypes.c_void_p()
+    with pytest.raises(ValueError, match="distinct"):
+        _lib.call("plato_agg_comm_create", 2, ctypes.cast(arr, ctypes.c_void_p), ctypes.byref(handle))
+
+
+def test_result_buffers_are_not_recycled_under_a_kept_result():
+    """Pinned result buffers are pooled, but never reused while an earlier result is referenced."""
+    from plato_amd.engine import FedAvgEngine
+
+    case = _case("resnet18_k16")
+    recipe = case["recipe"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    eng = FedAvgEngine("cuda:0")
+    weights, _ = G.weights_for(recipe, W)
+    first = eng.aggregate_weights(baseline, payloads, weights)
+    snapshot = {k: v.clone() for k, v in first.items()}
+    for _ in range(3):
+        eng.aggregate_weights(baseline, payloads[::-1], weights)
+    for k in first:
+        assert torch.equal(first[k], snapshot[k]), k
+    ptrs = {eng.aggregate_weights(baseline, payloads, weights)[layout.entries[0].name].data_ptr() for _ in range(3)}
+    assert len(ptrs) <= 2  # dropped results give their buffer back to the pool
