@@ -172,6 +172,32 @@ def pmc_traffic(alg_bytes: int, kernel: str):
     return summ["pmc"]["hbm_bytes"], os.path.relpath(path, ROOT), summ.get("avg_duration_ms")
 
 
+def cpus_available() -> int:
+    """CPUs this process can actually use: its affinity set, capped by a cgroup CPU quota.
+
+    On a shared GPU box nproc shows every CPU of the machine while the job's
+    cgroup grants a share of them; oversubscribing that share only slows the
+    baseline down.
+    """
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, -(-int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def progress(msg: str) -> None:
+    """A line on stderr per phase (the JSON result line stays the only stdout line)."""
+    print(f"[bench] {msg}", file=sys.stderr, flush=True)
+
+
 def cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -367,6 +393,7 @@ def main():
                                   "GBps": alg_bytes / (med * 1e-3) / 1e9}), flush=True)
         return
 
+    progress(f"rank {rank}: inputs ready, {args.warmup} warmup + {args.steps} timed steps")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
@@ -446,12 +473,14 @@ def main():
     if args.codec != "native":
         args.no_host_inclusive = args.no_cpu_baseline = True
     if rank == 0 and world == 1 and not args.no_host_inclusive:
+        progress("host-inclusive leg")
         result["host_inclusive"] = host_inclusive(engine, layout, base, slab, k, weights, dev)
 
     if rank == 0 and world == 1 and args.streaming:
         result["streaming"] = streaming(engine, layout, base, slab, k, weights, dev)
 
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("cpu baseline leg")
         result["cpu_baseline"] = cpu_baseline(layout, base, slab, k, weights, out_f, out_i, args.cpu_reps,
                                               args.config)
         result["parity"] = result["cpu_baseline"].pop("parity")
@@ -703,22 +732,22 @@ def cpu_baseline(layout, base, slab, k, weights, out_f, out_i, reps, config):
     w_s = weights[:k_s]
     default_threads = torch.get_num_threads()
     # time the reference sequence with the host's CPUs as well as torch's
-    # default pool; the CPUs this process may run on (nproc counts the whole machine)
-    try:
-        avail = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        avail = os.cpu_count() or default_threads
+    # default pool; the CPUs this process may use (nproc counts the whole machine)
+    avail = cpus_available() or default_threads
     by_threads = {}
     upd = None
     for threads in sorted({default_threads, avail}):
+        progress(f"cpu baseline: {k_s} clients on {threads} threads")
         torch.set_num_threads(threads)
         times = []
         for r in range(reps + 1):
             t0 = time.perf_counter()
             upd = ref.fedavg_torch_ops(baseline, payloads, weights=w_s)
             dt = time.perf_counter() - t0
-            if r:
+            if r or dt > 20:  # a slow pool: its first pass is the measurement (bounded leg)
                 times.append(dt)
+            if dt > 20:
+                break
         by_threads[threads] = statistics.median(times)
     torch.set_num_threads(default_threads)
     threads = min(by_threads, key=by_threads.get)  # the faster pool is the baseline
