@@ -302,6 +302,64 @@ int plato_agg_fill_synth_i64(int64_t* d_out, const int64_t* d_add, size_t n,
                              hipStream_t stream);
 
 /*
+ * Flattened-model reductions of the variant servers, in the reference's own
+ * float32 order (bit-exact; CPU restatements in oracle/reductions.c).
+ *
+ * plato_agg_flatten writes K flat fp32 vectors: position p of vector k lies in
+ * segment s (the last with flat_offset <= p), element e = src_offset +
+ * (p - flat_offset) of its region, and is
+ *   PLATO_AGG_FLAT_DELTA      fp32: x_k[e] - b[e];   int64: fp32(x_k[e] - b[e])
+ *   PLATO_AGG_FLAT_CAST_DIFF  fp32: x_k[e] - b[e];   int64: fp32(x_k[e]) - fp32(b[e])
+ *   PLATO_AGG_FLAT_RAW        fp32: x_k[e];          int64 region given as fp32 values
+ * and, with PLATO_AGG_SEG_NEG_DIV, (-v) / lr instead (int64 deltas: the int64
+ * negation, then the cast and the division).  Port concatenates the entries in
+ * state_dict order (examples/async/port/port_server.py:36-48, CAST_DIFF for
+ * current - previous, DELTA for the update); FedAdp sorts them by name.lower()
+ * and divides all but the first by -lr (examples/server_aggregation/fedadp/
+ * fedadp_server.py:122-133, RAW for the global gradient, DELTA for a client).
+ * d_src_*: K device pointers; d_out: K device pointers to n_flat floats.
+ */
+typedef struct plato_agg_segment {
+  uint64_t flat_offset;
+  uint64_t src_offset;
+  uint64_t numel;
+  uint32_t region;  /* 0: fp32 region, 1: int64 region */
+  uint32_t flags;   /* PLATO_AGG_SEG_NEG_DIV */
+} plato_agg_segment;
+#define PLATO_AGG_FLAT_DELTA 0
+#define PLATO_AGG_FLAT_CAST_DIFF 1
+#define PLATO_AGG_FLAT_RAW 2
+#define PLATO_AGG_SEG_NEG_DIV 1u
+int plato_agg_flatten(int mode, const void* const* d_src_f32, const void* const* d_src_i64, int K,
+                      const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
+                      uint32_t n_segs, size_t n_flat, float lr, float* const* d_out, hipStream_t stream);
+
+/*
+ * numpy's float32 np.inner(x_j, y_j) (and y_j . y_j if d_out_yy) for n_pairs
+ * pairs of flat vectors, in the order of numpy's bundled OpenBLAS 0.3.29
+ * sdot_k_SKYLAKEX (the x86-64 AVX-512 kernel; cblas_sdot calls it unthreaded):
+ * FedAdp's inner products and norms (fedadp_server.py:95-99; np.linalg.norm
+ * is sqrt of the float32 self dot).  Vectors 16-byte aligned.
+ */
+int plato_agg_sdot_pairs(const float* const* d_x, const float* const* d_y, int n_pairs, size_t n,
+                         float* d_out_xy, float* d_out_yy, hipStream_t stream);
+
+/*
+ * The sum in Port's F.cosine_similarity(a, b_k, dim=0) (port_server.py:50),
+ * as x86-64 PyTorch 2.10 forms it on `threads` CPU threads:
+ *   q = (a / max(|a|, eps)) * (b_k / max(|b_k|, eps)),  out[k] = sum(q)
+ * in TensorIterator's two-pass order (min(threads, ceil(n/32768)) chunks;
+ * one pass below 32768 elements or on one thread), each chunk by ATen's
+ * cascade sum.  |a|, |b_k|: device floats, e.g. plato_agg_entry_norms_f32 of
+ * the flat vectors with no baseline (torch.linalg.vector_norm's order).
+ * d_workspace: plato_agg_torch_cosine_workspace(K, threads) bytes.
+ */
+size_t plato_agg_torch_cosine_workspace(int K, int threads);
+int plato_agg_torch_cosine_sum(const float* d_a, const float* const* d_b, int K, size_t n, const float* d_norm_a,
+                               const float* d_norm_b, float eps, int threads, void* d_workspace, float* d_out,
+                               hipStream_t stream);
+
+/*
  * Single-process RCCL communicator over the GPUs one Plato server drives.
  * The reference has no collectives (aggregation runs on one CPU
  * process); these serve the multi-GPU engine behind the same

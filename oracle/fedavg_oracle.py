@@ -334,7 +334,11 @@ def torch_cpu_norm_f32(rows: np.ndarray) -> np.ndarray:
     """``torch.linalg.norm`` of each row of an fp32 ``[K, n]`` matrix, in x86-64
     PyTorch's CPU order (ATen's vectorised last-dim 2-norm, as measured for
     torch 2.10 here): 8 lanes of fp32 fma(v, v, acc) over the first n - n%8
-    elements, lanes summed in order, the tail fma'd, fp32 sqrt."""
+    elements, lanes summed in order, then the tail: 4 separately rounded
+    products added in order if 4+ remain, the last 1-3 fma'd; fp32 sqrt.
+    (The fma below is emulated in float64: exact product, one rounding of the
+    sum to float64, then to float32 — double rounding can flip a last bit in
+    rare ties; oracle/reductions.c has the exact fmaf version.)"""
     rows = np.asarray(rows, dtype=np.float32)
     k, n = rows.shape
     m = n - n % 8
@@ -346,8 +350,11 @@ def torch_cpu_norm_f32(rows: np.ndarray) -> np.ndarray:
     for j in range(1, 8):
         s = np.add(s, acc[:, j], dtype=np.float32)
     for e in range(m, n):
-        v = rows[:, e].astype(np.float64)
-        s = (s + v * v).astype(np.float32)
+        if n - m >= 4 and e < m + 4:  # 4 products of one SSE multiply, added in order
+            s = np.add(s, np.multiply(rows[:, e], rows[:, e], dtype=np.float32), dtype=np.float32)
+        else:  # the last 1-3: vfmadd231ss
+            v = rows[:, e].astype(np.float64)
+            s = (s + v * v).astype(np.float32)
     return np.sqrt(s, dtype=np.float32)
 
 

@@ -20,6 +20,10 @@ PLATO_AGG_EINVAL = -1
 PLATO_AGG_EHIP = -2
 PLATO_AGG_ERCCL = -3
 PLATO_AGG_ADD_BASE = 1
+PLATO_AGG_FLAT_DELTA = 0
+PLATO_AGG_FLAT_CAST_DIFF = 1
+PLATO_AGG_FLAT_RAW = 2
+PLATO_AGG_SEG_NEG_DIV = 1
 
 _c_void_p = ctypes.c_void_p
 _c_size_t = ctypes.c_size_t
@@ -98,6 +102,18 @@ SIGNATURES = {
         [_c_void_p, _c_void_p, _c_int, _c_void_p, _c_int, _c_float, _c_void_p, _c_void_p, _c_void_p,
          ctypes.c_uint32, _c_void_p, ctypes.c_uint32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
          _c_size_t, _c_size_t, _c_void_p],
+    ),
+    "plato_agg_flatten": (
+        _c_int,
+        [_c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,
+         _c_float, _c_void_p, _c_void_p],
+    ),
+    "plato_agg_sdot_pairs": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p, _c_void_p, _c_void_p]),
+    "plato_agg_torch_cosine_workspace": (_c_size_t, [_c_int, _c_int]),
+    "plato_agg_torch_cosine_sum": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p, _c_void_p, _c_float, _c_int, _c_void_p, _c_void_p,
+         _c_void_p],
     ),
     "plato_agg_comm_create": (_c_int, [_c_int, _c_void_p, ctypes.POINTER(_c_void_p)]),
     "plato_agg_comm_destroy": (_c_int, [_c_void_p]),

@@ -465,6 +465,17 @@ struct NormArgs {
 };
 
 // one client's delta at element e of its region (pointers hoisted by the caller)
+
+// ATen's scalar tail of the last-dim 2-norm (`buffer[0] += v * v` after the
+// 8-lane part), as x86-64 PyTorch 2.10 compiled it: while 4 or more remain,
+// the four products come from one SSE multiply and are added in order
+// (separately rounded); the last 1-3 are fused (vfmadd231ss).  Pinned against
+// torch on ragged sizes in tests/test_reductions.py (oracle/reductions.c).
+__device__ __forceinline__ float torch_norm_tail_step(float s, float v, uint64_t e, uint64_t m, uint64_t n) {
+  if (n - m >= 4 && e < m + 4) return s + v * v;
+  return __builtin_fmaf(v, v, s);
+}
+
 template <bool HAS_BASE, bool I64>
 __device__ __forceinline__ float norm_delta(const void* x, const void* b, uint64_t e) {
   if constexpr (I64) {
@@ -528,7 +539,7 @@ __device__ void norm_pair(const NormArgs& a, const Chunk ch, int i, int lane, fl
   if (lane != 0) return;
   for (uint64_t e = m; e < n; ++e) {
     const float v = norm_delta<HAS_BASE, I64>(x, b, ch.begin + e);
-    s = __builtin_fmaf(v, v, s);
+    s = torch_norm_tail_step(s, v, e, m, n);
   }
   if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
 }
@@ -730,7 +741,7 @@ __device__ void norm_ring(const NormArgs& a, const Chunk ch, int grp, float* rin
   for (uint64_t e = m; e < n; ++e) {
     const uint64_t idx = ch.begin + e;
     const float v = HAS_BASE ? x[idx] - a.base_f[idx] : x[idx];
-    s = __builtin_fmaf(v, v, s);
+    s = torch_norm_tail_step(s, v, e, m, n);
   }
   if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
 }
@@ -961,7 +972,7 @@ __device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int 
   for (uint64_t e = m; e < n; ++e) {
     const uint64_t idx = ch.begin + e;
     const float v = HAS_BASE ? x[idx] - a.base_f[idx] : x[idx];
-    s = __builtin_fmaf(v, v, s);
+    s = torch_norm_tail_step(s, v, e, m, n);
   }
   if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
 }

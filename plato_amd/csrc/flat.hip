@@ -1,0 +1,508 @@
+// flat.hip — the reductions Plato's variant servers run over flattened models,
+// in the reference's own float32 evaluation order (bit-exact), for gfx950.
+// C ABI: include/plato_agg.h (plato_agg_flatten, plato_agg_sdot_pairs,
+// plato_agg_torch_cosine_sum).  CPU restatements: oracle/reductions.c.
+//
+// * plato_agg_flatten gathers a model (or a client delta) into the flat
+//   float32 vector the reference builds: Port concatenates every entry in
+//   state_dict order (port_server.py:36-48); FedAdp sorts the entries by
+//   name.lower() and divides all but the first by -lr (fedadp_server.py:
+//   122-133).  One launch covers K vectors.
+// * plato_agg_sdot_pairs is numpy's float32 np.inner / dot on x86-64 AVX-512
+//   hosts (OpenBLAS 0.3.29 sdot_k_SKYLAKEX): 64 fma chains (4 x 16 lanes) over
+//   the 64-element blocks, folded to 4 x 8, one more 32-block, a fixed
+//   horizontal sum, and a float64 tail.  One 64-lane wavefront holds exactly
+//   the 64 chains; the other waves of the workgroup stream the two vectors
+//   into a double-buffered LDS tile.
+// * plato_agg_torch_cosine_sum is the sum in F.cosine_similarity
+//   (port_server.py:50): q = (a/|a|)*(b/|b|) summed by PyTorch's CPU
+//   two-pass reduction over T OpenMP chunks, each a 4-level cascade of 8-wide
+//   vectors x 4 rows of ILP (ATen SumKernel.cpp).  A workgroup computes one
+//   (client, chunk): the level-0 groups in parallel, the higher levels in
+//   order; a second launch combines the T partials.  (The norms |a|, |b| are
+//   plato_agg_entry_norms_f32 over the flattened vectors.)
+// Compiled with -ffp-contract=off: fmaf where the reference fuses, separate
+// roundings everywhere else; divisions are IEEE (correctly rounded).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "common.h"
+#include "plato_agg.h"
+
+using plato_agg_internal::clear_error;
+using plato_agg_internal::set_error;
+
+namespace {
+
+int check_launch(const char* what) {
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(PLATO_AGG_EHIP, std::string(what) + ": " + hipGetErrorString(err));
+  return clear_error();
+}
+
+template <class T>
+__device__ __forceinline__ T sld(const T* p, int i) {
+  return ((__attribute__((address_space(4))) const T*)p)[i];
+}
+
+// ------------------------------------------------------------------ flatten
+struct FlatArgs {
+  const void* const* src_f;   // K pointers: fp32 region
+  const void* const* src_i;   // K pointers: int64 region (fp32 values in RAW mode)
+  const float* base_f;
+  const int64_t* base_i;
+  const plato_agg_segment* segs;
+  uint32_t n_segs;
+  uint64_t n_flat;
+  float lr;
+  float* const* out;
+  int mode;
+};
+
+__device__ __forceinline__ uint32_t find_segment(const plato_agg_segment* segs, uint32_t n, uint64_t p) {
+  uint32_t lo = 0, hi = n;  // last segment with flat_offset <= p
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (segs[mid].flat_offset <= p) lo = mid; else hi = mid;
+  }
+  return lo;
+}
+
+constexpr int kFlatPer = 8;  // positions per thread
+
+__global__ __launch_bounds__(256) void flatten_kernel(FlatArgs a) {
+  const int k = blockIdx.y;
+  const void* xf = sld(a.src_f, k);
+  const void* xi = sld(a.src_i, k);
+  float* out = sld(a.out, k);
+  const uint64_t p0 = uint64_t(blockIdx.x) * (256 * kFlatPer) + threadIdx.x;
+  uint32_t s = 0;
+  for (int j = 0; j < kFlatPer; ++j) {
+    const uint64_t p = p0 + uint64_t(j) * 256;
+    if (p >= a.n_flat) return;
+    if (j == 0) {
+      s = find_segment(a.segs, a.n_segs, p);
+    } else {
+      while (s + 1 < a.n_segs && a.segs[s + 1].flat_offset <= p) ++s;
+    }
+    const plato_agg_segment g = a.segs[s];
+    const uint64_t e = g.src_offset + (p - g.flat_offset);
+    float v;
+    if (g.region == 0) {
+      const float x = static_cast<const float*>(xf)[e];
+      v = a.mode == PLATO_AGG_FLAT_RAW ? x : x - a.base_f[e];
+      if (g.flags & PLATO_AGG_SEG_NEG_DIV) v = (-v) / a.lr;
+    } else if (a.mode == PLATO_AGG_FLAT_RAW) {
+      v = static_cast<const float*>(xi)[e];
+      if (g.flags & PLATO_AGG_SEG_NEG_DIV) v = (-v) / a.lr;
+    } else if (a.mode == PLATO_AGG_FLAT_CAST_DIFF) {
+      // torch.cat casts each int64 entry to fp32 before the subtraction
+      v = float(static_cast<const int64_t*>(xi)[e]) - float(a.base_i[e]);
+      if (g.flags & PLATO_AGG_SEG_NEG_DIV) v = (-v) / a.lr;
+    } else {
+      // int64 delta, exact (wrapping) in int64; -delta too, then the cast
+      uint64_t d = uint64_t(static_cast<const int64_t*>(xi)[e]) - uint64_t(a.base_i[e]);
+      if (g.flags & PLATO_AGG_SEG_NEG_DIV) {
+        v = float(int64_t(uint64_t(0) - d)) / a.lr;
+      } else {
+        v = float(int64_t(d));
+      }
+    }
+    out[p] = v;
+  }
+}
+
+// ------------------------------------------------------------- sdot (SKX)
+constexpr int kSdotThreads = 512;        // wave 0: the 64 chains; waves 1..7: the tile stream
+constexpr int kSdotTS = 64;              // steps (64-element blocks) per tile
+constexpr int kSdotTile = kSdotTS * 64;  // floats per tile per vector
+
+struct SdotArgs {
+  const float* const* x;
+  const float* const* y;
+  uint64_t n;
+  float* out_xy;
+  float* out_yy;
+};
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void sdot_load_tile(const float* x, const float* y, uint64_t base, uint32_t cnt,
+                                               float* lx, float* ly, int ptid, int nprod) {
+  // cnt is a multiple of 64; base a multiple of kSdotTile (16-byte aligned vectors)
+  for (uint32_t e = uint32_t(ptid) * 4; e < cnt; e += uint32_t(nprod) * 4) {
+    const f4 vx = *reinterpret_cast<const f4*>(x + base + e);
+    const f4 vy = *reinterpret_cast<const f4*>(y + base + e);
+    *reinterpret_cast<f4*>(lx + e) = vx;
+    *reinterpret_cast<f4*>(ly + e) = vy;
+  }
+}
+
+__global__ __launch_bounds__(kSdotThreads) void sdot_skx_kernel(SdotArgs a) {
+  __shared__ __attribute__((aligned(16))) float tx[2][kSdotTile];
+  __shared__ __attribute__((aligned(16))) float ty[2][kSdotTile];
+  const int pair = blockIdx.x;
+  const float* x = sld(a.x, pair);
+  const float* y = sld(a.y, pair);
+  const uint64_t n = a.n;
+  const uint64_t n1 = n & ~uint64_t(31);
+  const uint64_t n64 = n1 & ~uint64_t(63);
+  const uint64_t ntiles = (n64 + kSdotTile - 1) / kSdotTile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nprod = kSdotThreads - 64, ptid = tid - 64;
+  float axy = 0.f, ayy = 0.f;  // chain `lane` = 16 r + l of the 512-bit accumulators
+  if (wave != 0 && ntiles) {
+    sdot_load_tile(x, y, 0, uint32_t(n64 < kSdotTile ? n64 : kSdotTile), tx[0], ty[0], ptid, nprod);
+  }
+  __syncthreads();
+  for (uint64_t t = 0; t < ntiles; ++t) {
+    const int cur = int(t & 1);
+    if (wave != 0) {
+      if (t + 1 < ntiles) {
+        const uint64_t base = (t + 1) * kSdotTile;
+        const uint64_t left = n64 - base;
+        sdot_load_tile(x, y, base, uint32_t(left < kSdotTile ? left : kSdotTile), tx[cur ^ 1], ty[cur ^ 1],
+                       ptid, nprod);
+      }
+    } else {
+      const uint64_t base = t * kSdotTile;
+      const uint64_t left = n64 - base;
+      const int steps = int((left < kSdotTile ? left : kSdotTile) / 64);
+      const float* lx = tx[cur];
+      const float* ly = ty[cur];
+      for (int s = 0; s < steps; ++s) {
+        const float xv = lx[s * 64 + lane];
+        const float yv = ly[s * 64 + lane];
+        axy = __builtin_fmaf(xv, yv, axy);
+        ayy = __builtin_fmaf(yv, yv, ayy);
+      }
+    }
+    __syncthreads();
+  }
+  if (wave != 0) return;
+  // fold the 4 x 16 accumulators to 4 x 8: a[r][l] = acc[r][l] + acc[r][l+8]
+  const float hxy = __shfl(axy, (lane + 8) & 63, 64);
+  const float hyy = __shfl(ayy, (lane + 8) & 63, 64);
+  const int r = lane >> 4, l = lane & 15;
+  float bxy = 0.f, byy = 0.f;
+  if (l < 8) {
+    bxy = axy + hxy;
+    byy = ayy + hyy;
+    if (n1 > n64) {  // one 32-element block left: 4 x 8 lanes
+      const float xv = x[n64 + 8 * r + l];
+      const float yv = y[n64 + 8 * r + l];
+      bxy = __builtin_fmaf(xv, yv, bxy);
+      byy = __builtin_fmaf(yv, yv, byy);
+    }
+  }
+  // s[l] = ((a0 + a1) + a2) + a3 over r, then h[l] = s[l] + s[l+4], (h0 + h1) + (h2 + h3)
+  const float xy1 = __shfl(bxy, 16 + l, 64), xy2 = __shfl(bxy, 32 + l, 64), xy3 = __shfl(bxy, 48 + l, 64);
+  const float yy1 = __shfl(byy, 16 + l, 64), yy2 = __shfl(byy, 32 + l, 64), yy3 = __shfl(byy, 48 + l, 64);
+  const float sxy = ((bxy + xy1) + xy2) + xy3;
+  const float syy = ((byy + yy1) + yy2) + yy3;
+  const float sxy4 = __shfl(sxy, (lane + 4) & 63, 64);
+  const float syy4 = __shfl(syy, (lane + 4) & 63, 64);
+  const float hx = sxy + sxy4, hy = syy + syy4;  // valid on lanes 0..3
+  const float hx1 = __shfl(hx, 1, 64), hx2 = __shfl(hx, 2, 64), hx3 = __shfl(hx, 3, 64);
+  const float hy1 = __shfl(hy, 1, 64), hy2 = __shfl(hy, 2, 64), hy3 = __shfl(hy, 3, 64);
+  if (lane != 0) return;
+  double kxy = 0.0, kyy = 0.0;
+  if (n1) {
+    kxy = double((hx + hx1) + (hx2 + hx3));
+    kyy = double((hy + hy1) + (hy2 + hy3));
+  }
+  double txy = 0.0, tyy = 0.0;  // the scalar tail in float64, products rounded to fp32 first
+  for (uint64_t i = n1; i < n; ++i) {
+    const float xv = x[i], yv = y[i];
+    txy += double(yv * xv);
+    tyy += double(yv * yv);
+  }
+  a.out_xy[pair] = float(txy + kxy);
+  if (a.out_yy) a.out_yy[pair] = float(tyy + kyy);
+}
+
+// ------------------------------------------------- torch cascade sum (cos)
+constexpr int kSumThreads = 256;
+
+struct CosArgs {
+  const float* av;            // shared vector a (Port: current - previous)
+  const float* const* bv;     // K vectors b
+  const float* norm_a;        // |a| (1 float)
+  const float* norm_b;        // |b_k| (K floats)
+  float eps;
+  uint64_t n;
+  uint64_t chunk;             // elements per thread chunk
+  int nt;                     // chunks (<= T)
+  int T;                      // torch threads: partial-buffer length
+  int single;                 // one pass (n < grain or T == 1): partial[0] is the result
+  float* partial;             // [K][T]
+  float* out;                 // [K]
+};
+
+__device__ __forceinline__ int ceil_log2_u64(uint64_t x) {
+  int r = 0;
+  while ((uint64_t(1) << r) < x) ++r;
+  return r;
+}
+
+struct QSrc {
+  const float* a;
+  const float* b;
+  float na, nb;
+  __device__ __forceinline__ float operator()(uint64_t p) const { return (a[p] / na) * (b[p] / nb); }
+};
+
+// One chunk [b0, b0+size0) -> final_acc of vectorized_inner_sum (size0 >= 8).
+// Level-0 groups (L rows of 32 values: 4 ILP rows x 8 lanes) are summed in
+// parallel by the workgroup, the higher levels in order by lanes 0..31 of wave 0.
+__device__ float chunk_cascade(const QSrc& q, uint64_t b0, uint64_t size0, float* lds_s0) {
+  const uint64_t vec_size = size0 / 8;
+  const uint64_t size_ilp = vec_size / 4;
+  int lp = ceil_log2_u64(size_ilp) / 4;
+  if (lp < 4) lp = 4;
+  const uint64_t L = uint64_t(1) << lp;
+  const uint64_t G0 = size_ilp / L;  // full level-0 groups
+  const uint64_t G1 = G0 / L;        // full level-1 groups
+  const int tid = threadIdx.x;
+  const int acc_id = tid & 31;       // (ILP row k, lane l) = (acc_id / 8, acc_id % 8)
+  const int gslot = tid >> 5;        // 8 level-0 groups per pass
+  float acc2 = 0.f, acc3 = 0.f;      // running on lanes 0..31 of wave 0
+  auto s0_of = [&](uint64_t g0) {
+    float s = 0.f;
+    const uint64_t row0 = g0 * L;
+    for (uint64_t i = 0; i < L; ++i) s += q(b0 + (row0 + i) * 32 + uint64_t(acc_id));
+    return s;
+  };
+  for (uint64_t g1 = 0; g1 < G1; ++g1) {
+    for (uint64_t j = uint64_t(gslot); j < L; j += kSumThreads / 32)
+      lds_s0[j * 32 + uint64_t(acc_id)] = s0_of(g1 * L + j);
+    __syncthreads();
+    if (tid < 32) {
+      float s1 = 0.f;
+      for (uint64_t j = 0; j < L; ++j) s1 += lds_s0[j * 32 + uint64_t(tid)];
+      acc2 += s1;
+      if ((g1 + 1) % L == 0) {
+        acc3 += acc2;
+        acc2 = 0.f;
+      }
+    }
+    __syncthreads();
+  }
+  // the partial level-1 group: its complete level-0 groups, in order
+  const uint64_t rem0 = G0 - G1 * L;
+  for (uint64_t j = uint64_t(gslot); j < rem0; j += kSumThreads / 32)
+    lds_s0[j * 32 + uint64_t(acc_id)] = s0_of(G1 * L + j);
+  __syncthreads();
+  float result = 0.f;
+  if (tid < 32) {
+    float acc1 = 0.f;
+    for (uint64_t j = 0; j < rem0; ++j) acc1 += lds_s0[j * 32 + uint64_t(tid)];
+    float acc0 = 0.f;  // the rows after the last complete level-0 group
+    for (uint64_t i = G0 * L; i < size_ilp; ++i) acc0 += q(b0 + i * 32 + uint64_t(tid));
+    float ps = acc0;
+    ps += acc1;
+    ps += acc2;
+    ps += acc3;
+    lds_s0[tid] = ps;  // ps[k][l] at k*8 + l
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float ps0[8];
+    for (int l = 0; l < 8; ++l) ps0[l] = lds_s0[l];
+    for (uint64_t v = size_ilp * 4; v < vec_size; ++v)
+      for (int l = 0; l < 8; ++l) ps0[l] += q(b0 + v * 8 + uint64_t(l));
+    for (int k = 1; k < 4; ++k)
+      for (int l = 0; l < 8; ++l) ps0[l] += lds_s0[k * 8 + l];
+    float final_acc = 0.f;
+    for (uint64_t e = vec_size * 8; e < size0; ++e) final_acc += q(b0 + e);
+    for (int l = 0; l < 8; ++l) final_acc += ps0[l];
+    result = final_acc;
+  }
+  __syncthreads();
+  return result;
+}
+
+// scalar_inner_sum / vectorized_inner_sum of a short array (single thread)
+__device__ float small_inner_sum(const float* in, int n) {
+  float ps[4][8];
+  for (int k = 0; k < 4; ++k)
+    for (int l = 0; l < 8; ++l) ps[k][l] = 0.f;
+  const int W = n >= 8 ? 8 : 1;
+  const int vec_size = n / W;
+  const int size_ilp = vec_size / 4;
+  int lp = ceil_log2_u64(uint64_t(size_ilp)) / 4;
+  if (lp < 4) lp = 4;
+  const int L = 1 << lp;
+  float acc[4][4][8];
+  for (int j = 0; j < 4; ++j)
+    for (int k = 0; k < 4; ++k)
+      for (int l = 0; l < 8; ++l) acc[j][k][l] = 0.f;
+  int i = 0;
+  for (; i + L <= size_ilp;) {
+    for (int j = 0; j < L; ++j, ++i)
+      for (int k = 0; k < 4; ++k)
+        for (int l = 0; l < W; ++l) acc[0][k][l] += in[(i * 4 + k) * W + l];
+    for (int j = 1; j < 4; ++j) {
+      for (int k = 0; k < 4; ++k)
+        for (int l = 0; l < W; ++l) {
+          acc[j][k][l] += acc[j - 1][k][l];
+          acc[j - 1][k][l] = 0.f;
+        }
+      if ((uint64_t(i) & (uint64_t(L - 1) << (j * lp))) != 0) break;
+    }
+  }
+  for (; i < size_ilp; ++i)
+    for (int k = 0; k < 4; ++k)
+      for (int l = 0; l < W; ++l) acc[0][k][l] += in[(i * 4 + k) * W + l];
+  for (int j = 1; j < 4; ++j)
+    for (int k = 0; k < 4; ++k)
+      for (int l = 0; l < W; ++l) acc[0][k][l] += acc[j][k][l];
+  for (int k = 0; k < 4; ++k)
+    for (int l = 0; l < W; ++l) ps[k][l] = acc[0][k][l];
+  if (W == 8) {
+    for (int v = size_ilp * 4; v < vec_size; ++v)
+      for (int l = 0; l < 8; ++l) ps[0][l] += in[v * 8 + l];
+    for (int k = 1; k < 4; ++k)
+      for (int l = 0; l < 8; ++l) ps[0][l] += ps[k][l];
+    float final_acc = 0.f;
+    for (int e = vec_size * 8; e < n; ++e) final_acc += in[e];
+    for (int l = 0; l < 8; ++l) final_acc += ps[0][l];
+    return final_acc;
+  }
+  for (int v = size_ilp * 4; v < n; ++v) ps[0][0] += in[v];
+  for (int k = 1; k < 4; ++k) ps[0][0] += ps[k][0];
+  return ps[0][0];
+}
+
+__global__ __launch_bounds__(kSumThreads) void cosine_chunks_kernel(CosArgs a) {
+  __shared__ float lds_s0[64 * 32];  // L <= 64 level-0 groups of 32 values
+  const int k = blockIdx.y, t = blockIdx.x;
+  const uint64_t b0 = uint64_t(t) * a.chunk;
+  if (b0 >= a.n) return;
+  const uint64_t e0 = b0 + a.chunk < a.n ? b0 + a.chunk : a.n;
+  QSrc q;
+  q.a = a.av;
+  q.b = sld(a.bv, k);
+  q.na = a.norm_a[0];
+  q.nb = a.norm_b[k];
+  if (q.na < a.eps) q.na = a.eps;  // clamp_min_: NaN stays NaN
+  if (q.nb < a.eps) q.nb = a.eps;
+  const uint64_t size0 = e0 - b0;
+  float r;
+  if (size0 >= 8) {
+    r = chunk_cascade(q, b0, size0, lds_s0);
+  } else {
+    r = 0.f;
+    if (threadIdx.x == 0) {
+      float tmp[8];
+      for (uint64_t e = 0; e < size0; ++e) tmp[e] = q(b0 + e);
+      r = small_inner_sum(tmp, int(size0));
+    }
+  }
+  if (threadIdx.x == 0) a.partial[uint64_t(k) * a.T + t] = 0.f + r;
+}
+
+__global__ void cosine_combine_kernel(CosArgs a, int K) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= K) return;
+  float* buf = a.partial + uint64_t(k) * a.T;
+  if (a.single) {
+    a.out[k] = buf[0];  // one pass: 0 + inner_sum, already formed
+    return;
+  }
+  for (int t = a.nt; t < a.T; ++t) buf[t] = 0.f;
+  a.out[k] = 0.f + small_inner_sum(buf, a.T);
+}
+
+}  // namespace
+
+extern "C" {
+
+int plato_agg_flatten(int mode, const void* const* d_src_f32, const void* const* d_src_i64, int K,
+                      const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
+                      uint32_t n_segs, size_t n_flat, float lr, float* const* d_out, hipStream_t stream) {
+  if (mode < PLATO_AGG_FLAT_DELTA || mode > PLATO_AGG_FLAT_RAW) return set_error(PLATO_AGG_EINVAL, "bad mode");
+  if (K <= 0 || K > 65535) return set_error(PLATO_AGG_EINVAL, "K must be in [1, 65535]");
+  if (n_flat == 0) return clear_error();
+  if (!d_src_f32 || !d_src_i64 || !d_segs || !n_segs || !d_out)
+    return set_error(PLATO_AGG_EINVAL, "null pointer");
+  if (mode != PLATO_AGG_FLAT_RAW && (!d_base_f32 || !d_base_i64))
+    return set_error(PLATO_AGG_EINVAL, "the delta modes need the baseline");
+  FlatArgs a{};
+  a.src_f = d_src_f32;
+  a.src_i = d_src_i64;
+  a.base_f = d_base_f32;
+  a.base_i = d_base_i64;
+  a.segs = d_segs;
+  a.n_segs = n_segs;
+  a.n_flat = n_flat;
+  a.lr = lr;
+  a.out = d_out;
+  a.mode = mode;
+  const uint64_t blocks = (uint64_t(n_flat) + 256 * kFlatPer - 1) / (256 * kFlatPer);
+  if (blocks > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "vector too long");
+  hipLaunchKernelGGL(flatten_kernel, dim3(uint32_t(blocks), uint32_t(K)), dim3(256), 0, stream, a);
+  return check_launch("flatten launch");
+}
+
+int plato_agg_sdot_pairs(const float* const* d_x, const float* const* d_y, int n_pairs, size_t n, float* d_out_xy,
+                         float* d_out_yy, hipStream_t stream) {
+  if (n_pairs <= 0) return set_error(PLATO_AGG_EINVAL, "no pairs");
+  if (!d_x || !d_y || !d_out_xy) return set_error(PLATO_AGG_EINVAL, "null pointer");
+  SdotArgs a{d_x, d_y, uint64_t(n), d_out_xy, d_out_yy};
+  hipLaunchKernelGGL(sdot_skx_kernel, dim3(uint32_t(n_pairs)), dim3(kSdotThreads), 0, stream, a);
+  return check_launch("sdot launch");
+}
+
+size_t plato_agg_torch_cosine_workspace(int K, int threads) {
+  return size_t(K > 0 ? K : 0) * size_t(threads > 0 ? threads : 1) * sizeof(float);
+}
+
+int plato_agg_torch_cosine_sum(const float* d_a, const float* const* d_b, int K, size_t n, const float* d_norm_a,
+                               const float* d_norm_b, float eps, int threads, void* d_workspace, float* d_out,
+                               hipStream_t stream) {
+  if (K <= 0 || K > 65535) return set_error(PLATO_AGG_EINVAL, "K must be in [1, 65535]");
+  if (threads < 1 || threads > 1024) return set_error(PLATO_AGG_EINVAL, "threads must be in [1, 1024]");
+  if (!d_a || !d_b || !d_norm_a || !d_norm_b || !d_workspace || !d_out)
+    return set_error(PLATO_AGG_EINVAL, "null pointer");
+  if (n == 0) return set_error(PLATO_AGG_EINVAL, "empty vectors");
+  CosArgs a{};
+  a.av = d_a;
+  a.bv = d_b;
+  a.norm_a = d_norm_a;
+  a.norm_b = d_norm_b;
+  a.eps = eps;
+  a.n = n;
+  a.T = threads;
+  a.partial = static_cast<float*>(d_workspace);
+  a.out = d_out;
+  // TensorIterator's parallel_reduce: one pass below the grain or on one
+  // thread, else two passes over min(T, ceil(n / 32768)) OpenMP chunks
+  const uint64_t grain = 32768;
+  a.single = (n < grain || threads == 1) ? 1 : 0;
+  if (a.single) {
+    a.nt = 1;
+    a.chunk = n;
+  } else {
+    uint64_t nt = uint64_t(threads);
+    const uint64_t by_grain = (n + grain - 1) / grain;
+    if (by_grain < nt) nt = by_grain;
+    a.chunk = (n + nt - 1) / nt;
+    a.nt = int((n + a.chunk - 1) / a.chunk);
+  }
+  // the level-0 sums of one level-1 group are staged in LDS: L = 2^lp <= 64 rows
+  {
+    const uint64_t size_ilp = (a.chunk / 8) / 4;
+    int r = 0;
+    while ((uint64_t(1) << r) < size_ilp) ++r;
+    if (r / 4 > 6) return set_error(PLATO_AGG_EINVAL, "thread chunk too long (> 2^33 elements)");
+  }
+  hipLaunchKernelGGL(cosine_chunks_kernel, dim3(uint32_t(a.nt), uint32_t(K)), dim3(kSumThreads), 0, stream, a);
+  if (int rc = check_launch("cosine chunks launch")) return rc;
+  hipLaunchKernelGGL(cosine_combine_kernel, dim3(uint32_t((K + 63) / 64)), dim3(64), 0, stream, a, K);
+  return check_launch("cosine combine launch");
+}
+
+}  // extern "C"

@@ -747,15 +747,106 @@ class AggregationRound:
         self._fetch(stream, out_f, out_i, (tf, ti, dw, nz))
         return None
 
+    # ------------------------------------------- flattened-model reductions
+    def _flat_segments(self, order: Sequence[int], neg_div_after_first: bool) -> torch.Tensor:
+        """plato_agg_segment rows for the layout's entries in ``order`` (device, cached)."""
+        lay, eng = self.layout, self.engine
+        key = ("flat_segments", tuple(order), neg_div_after_first, str(eng.device))
+        hit = lay._cache.get(key)
+        if hit is None:
+            rows = np.zeros((len(order), 4), dtype=np.uint64)
+            flat = 0
+            for j, idx in enumerate(order):
+                e = lay.entries[idx]
+                flags = 1 if (neg_div_after_first and j > 0) else 0
+                region = 0 if e.region == F32 else 1
+                rows[j, 0], rows[j, 1], rows[j, 2] = flat, e.offset, e.numel
+                rows[j, 3] = np.uint64(region | (flags << 32))
+                flat += e.numel
+            hit = (torch.from_numpy(rows.view(np.int64).copy()).to(eng.device), flat)
+            lay._cache[key] = hit
+        return hit
+
+    def _flatten(self, mode: int, segs, n_segs: int, n_flat: int, src_f: Sequence[int], src_i: Sequence[int],
+                 base: tuple | None, lr: float, stream) -> tuple[torch.Tensor, int]:
+        """K flat vectors (rows of a [K, stride] buffer, stride 64-aligned) from device arenas."""
+        eng = self.engine
+        k = len(src_f)
+        stride = max(64, -(-n_flat // 64) * 64)
+        out = torch.empty((k, stride), dtype=torch.float32, device=eng.device)
+        ptrs = torch.from_numpy(np.asarray(list(src_f) + list(src_i) +
+                                           [out.data_ptr() + r * stride * 4 for r in range(k)],
+                                           dtype=np.int64)).to(eng.device)
+        base_f, base_i = (None, None) if base is None else base
+        _lib.call("plato_agg_flatten", mode, ptrs.data_ptr(), ptrs.data_ptr() + 8 * k, k, base_f, base_i,
+                  segs.data_ptr(), n_segs, n_flat, float(lr), ptrs.data_ptr() + 16 * k, _stream_handle(stream))
+        self._keep_flat = ptrs
+        return out, stride
+
+    def fedadp_dots(self, grads: tuple[torch.Tensor, torch.Tensor], slots: Sequence[int], lr: float,
+                    batch_bytes: float = 4e9):
+        """FedAdp's float32 reductions of process_grad's flattened vectors, bit-exact.
+
+        ``grads`` is the device global gradient (fp32 arena, fp32 values of the
+        int64 entries), e.g. :meth:`launch_entrywise` with ``device=True``.
+        Returns ``(inner[K], g_sq, l_sq[K])`` as numpy float32: ``np.inner(g,
+        loc_k)``, ``g.dot(g)``, ``loc_k.dot(loc_k)`` exactly as numpy's OpenBLAS
+        forms them (examples/server_aggregation/fedadp/fedadp_server.py:91-99,
+        ``plato_agg_flatten`` + ``plato_agg_sdot_pairs``).
+        """
+        slots = self._check_slots(slots)
+        if not self.has_baseline:
+            raise ValueError("baseline not staged")
+        eng, lay = self.engine, self.layout
+        names = lay.keys()
+        order = sorted(range(len(names)), key=lambda i: names[i].lower())
+        if order and lay.entries[order[0]].region != F32:
+            raise ValueError("FedAdp: the first entry in name order is int64, so the reference flattens to "
+                             "float64 (np.append) and takes float64 dots; the device path reproduces the "
+                             "float32 case only")
+        segs, n_flat = self._flat_segments(order, True)
+        stream = torch.cuda.current_stream(eng.device)
+        self.stager.fence(stream)
+        g_flat, stride = self._flatten(_lib.PLATO_AGG_FLAT_RAW, segs, len(order), n_flat, [grads[0].data_ptr()],
+                                       [grads[1].data_ptr()], None, lr, stream)
+        k = len(slots)
+        inner = torch.empty(k, dtype=torch.float32, device=eng.device)
+        l_sq = torch.empty(k, dtype=torch.float32, device=eng.device)
+        g_sq = torch.empty(1, dtype=torch.float32, device=eng.device)
+        gp = torch.tensor([g_flat.data_ptr()], dtype=torch.int64, device=eng.device)
+        _lib.call("plato_agg_sdot_pairs", gp.data_ptr(), gp.data_ptr(), 1, n_flat, g_sq.data_ptr(), None,
+                  _stream_handle(stream))
+        per = max(1, int(batch_bytes // (stride * 4)))
+        base = (_ptr(eng._base.f32), _ptr(eng._base.i64))
+        keep = [gp]
+        for s0 in range(0, k, per):
+            part = slots[s0:s0 + per]
+            locs, _ = self._flatten(_lib.PLATO_AGG_FLAT_DELTA, segs, len(order), n_flat,
+                                    [self._pf[i] for i in part], [self._pi[i] for i in part], base, lr, stream)
+            xs = torch.from_numpy(np.full(len(part), g_flat.data_ptr(), dtype=np.int64)).to(eng.device)
+            ys = torch.from_numpy(np.asarray([locs.data_ptr() + r * stride * 4 for r in range(len(part))],
+                                             dtype=np.int64)).to(eng.device)
+            _lib.call("plato_agg_sdot_pairs", xs.data_ptr(), ys.data_ptr(), len(part), n_flat,
+                      inner.data_ptr() + 4 * s0, l_sq.data_ptr() + 4 * s0, _stream_handle(stream))
+            keep.append((locs, xs, ys))
+            if s0 + per < k:
+                stream.synchronize()  # bound the flat buffers to one batch
+                keep = [gp]
+        stream.synchronize()
+        return inner.cpu().numpy(), g_sq.cpu().numpy()[0], l_sq.cpu().numpy()
+
     def model_similarities(self, reference: Mapping[str, torch.Tensor], slots: Sequence[int],
-                           eps: float = 1e-8) -> list[np.float32]:
-        """Port's cosine similarity of each client delta with ``baseline - reference``.
+                           eps: float = 1e-8, threads: int | None = None) -> list[np.float32]:
+        """Port's cosine similarity of each client delta with ``baseline - reference``, bit-exact.
 
         ``F.cosine_similarity(current - previous, delta, dim=0)`` over the
-        flattened models (examples/async/port/port_server.py:38-50), from the
-        device reductions of ``plato_agg_client_dots`` (fp64, fixed order):
-        ``dot / (max(|v|, eps) * max(|d|, eps))``, returned as fp32 like the
-        reference's 0-dim tensor.
+        models flattened by ``torch.cat`` in state_dict order
+        (examples/async/port/port_server.py:24-52), computed on the device in
+        the order x86-64 PyTorch 2.10 uses on ``threads`` CPU threads (default
+        ``torch.get_num_threads()``: what the reference's call would use in this
+        process): ``plato_agg_flatten`` -> ``plato_agg_entry_norms_f32`` (the
+        vector norms) -> ``plato_agg_torch_cosine_sum``.  Returned as fp32 like
+        the reference's 0-dim tensor.
         """
         if not self.has_baseline:
             raise ValueError("baseline not staged")
@@ -765,8 +856,8 @@ class AggregationRound:
                 raise ValueError(f"client slot {slot} was not staged")
         if not slots:
             return []
-        if self.codec != "native":
-            raise NotImplementedError("similarities of bf16-coded payloads are not on the device path yet")
+        slots = self._check_slots(slots)
+        threads = torch.get_num_threads() if threads is None else int(threads)
         eng = self.engine
         lay = self.layout
         lay.check_compatible(reference, "reference model")
@@ -774,28 +865,31 @@ class AggregationRound:
         prev = DeviceArena(lay, eng.device)
         eng._stager.put(reference, prev.f32, prev.i64)
         eng._stager.fence(stream)
-        v = DeviceArena(lay, eng.device)
-        h = _stream_handle(stream)
-        _lib.call("plato_agg_compute_deltas", _ptr(eng._base.f32), _ptr(eng._base.i64), _ptr(prev.f32),
-                  _ptr(prev.i64), _ptr(v.f32), _ptr(v.i64), lay.n_f32, lay.n_i64, h)
-        # slots adopted from arrival staging live outside the round slab
-        pf = np.asarray([self._pf[i] for i in slots], dtype=np.int64)
-        pi = np.asarray([self._pi[i] for i in slots], dtype=np.int64)
-        tf, ti = eng._pointer_tables(pf, pi)
+        self.stager.fence(stream)
+        segs, n_flat = self._flat_segments(list(range(len(lay.entries))), False)
+        n_segs = len(lay.entries)
+        # current - previous, then each client's delta, as torch.cat lays them out
+        cur, stride = self._flatten(_lib.PLATO_AGG_FLAT_CAST_DIFF, segs, n_segs, n_flat, [_ptr(eng._base.f32)],
+                                    [_ptr(eng._base.i64)], (_ptr(prev.f32), _ptr(prev.i64)), 0.0, stream)
         k = len(slots)
-        ws_bytes = self.engine.lib.plato_agg_client_dots_workspace(k, lay.n_f32)
-        ws = torch.empty((ws_bytes + 7) // 8, dtype=torch.float64, device=eng.device)
-        out = torch.empty(2 * k + 1, dtype=torch.float64, device=eng.device)
-        _lib.call("plato_agg_client_dots", _ptr(tf), _ptr(ti) if lay.n_i64 else None, k, _ptr(eng._base.f32),
-                  _ptr(eng._base.i64) if lay.n_i64 else None, _ptr(v.f32), _ptr(v.i64) if lay.n_i64 else None,
-                  lay.n_f32, lay.n_i64, _ptr(ws), _ptr(out), h)
-        res = out.cpu().numpy()
-        vnorm = max(float(np.sqrt(res[2 * k])), eps)
-        sims = []
-        for i in range(k):
-            dnorm = max(float(np.sqrt(res[k + i])), eps)
-            sims.append(np.float32(res[i] / (vnorm * dnorm)))
-        return sims
+        deltas, _ = self._flatten(_lib.PLATO_AGG_FLAT_DELTA, segs, n_segs, n_flat, [self._pf[i] for i in slots],
+                                  [self._pi[i] for i in slots], (_ptr(eng._base.f32), _ptr(eng._base.i64)), 0.0,
+                                  stream)
+        rows = [cur.data_ptr()] + [deltas.data_ptr() + r * stride * 4 for r in range(k)]
+        tab = torch.from_numpy(np.asarray(rows, dtype=np.int64)).to(eng.device)
+        chunk = torch.from_numpy(np.asarray([[0, 0, n_flat, 0]], dtype=np.uint32).view(np.int32)).to(eng.device)
+        norms = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
+        h = _stream_handle(stream)
+        _lib.call("plato_agg_entry_norms_f32", tab.data_ptr(), None, k + 1, None, None, chunk.data_ptr(), 1, None,
+                  0, 1, n_flat, 0, norms.data_ptr(), h)
+        ws = torch.empty(max(1, eng.lib.plato_agg_torch_cosine_workspace(k, threads) // 4), dtype=torch.float32,
+                         device=eng.device)
+        out = torch.empty(k, dtype=torch.float32, device=eng.device)
+        _lib.call("plato_agg_torch_cosine_sum", cur.data_ptr(), tab.data_ptr() + 8, k, n_flat, norms.data_ptr(),
+                  norms.data_ptr() + 4, float(eps), threads, ws.data_ptr(), out.data_ptr(), h)
+        stream.synchronize()
+        self.last_norms = norms.cpu().numpy()
+        return [np.float32(v) for v in out.cpu().numpy()]
 
     def ready(self) -> bool:
         return self.event is not None and self.event.query()

@@ -70,13 +70,16 @@ class PortWeights(_EngineHolder):
         import torch
 
         previous = torch.load(path, map_location="cpu", weights_only=True)
-        sims = rnd.model_similarities(previous, need)
+        sims = rnd.model_similarities(previous, need, threads=self.port_threads)
         out = [1.0] * len(updates)
         for i, sim in zip(need, sims):
             out[i] = sim
         return out
 
     needs_staged_round = True
+    #: CPU threads whose reduction order F.cosine_similarity follows; None =
+    #: torch.get_num_threads(), the pool the reference's call would use here
+    port_threads = None
 
     #: Port hyper-parameters; None = Config().server.<name>, else the reference default
     similarity_weight = None
@@ -198,9 +201,10 @@ class FedAdpWeights(_EngineHolder):
 
     1. ``global_grads`` = one ``fedavg_entrywise`` pass (no baseline added),
        left in HBM, bit-exact with the reference's;
-    2. ``plato_agg_entry_stats`` gives per (client, entry) ``d.g`` and ``d.d``
-       plus per-entry ``g.g``; ``process_grad``'s ``-x/lr`` scaling folds into
-       per-entry factors (weights.fedadp_process_scales);
+    2. ``process_grad``'s flattening (sorted by ``name.lower()``, ``-x/lr``
+       after the first entry) and numpy's float32 ``np.inner`` /
+       ``np.linalg.norm`` in OpenBLAS's order (``AggregationRound.fedadp_dots``):
+       the same float32 values the reference computes;
     3. the host runs the reference's scalar code (weights.fedadp_*), and the
        fused kernel does the final ``b + sum_i delta_i * w_i``.
 
@@ -226,7 +230,6 @@ class FedAdpWeights(_EngineHolder):
         names = lay.keys()
         w1 = np.tile(np.asarray(W.fedavg(num_samples), dtype=np.float64), (len(names), 1))
         grads = rnd.launch_entrywise(w1, add_base=False, device=True)
-        dv, dd, vv = rnd.entry_stats(range(k), v=grads)
         lr = self.fedadp_lr
         if lr is None:
             lr = _config_attr("parameters", "optimizer", None)
@@ -234,7 +237,8 @@ class FedAdpWeights(_EngineHolder):
             if lr is None:
                 raise ValueError("FedAdp needs parameters.optimizer.lr (or set fedadp_lr)")
         alpha = self.fedadp_alpha if self.fedadp_alpha is not None else _config_attr("algorithm", "alpha", 5)
-        angles = W.fedadp_angles(dv, dd, vv, W.fedadp_process_scales(names, lr))
+        inner, g_sq, l_sq = rnd.fedadp_dots(grads, range(k), lr)
+        angles = W.fedadp_angles_from_dots(inner, g_sq, l_sq)
         contribs = W.fedadp_contributions(angles, self.selected_clients, self.local_angles,
                                           self.current_round, alpha)
         self.adaptive_weighting = W.fedadp_weighting(contribs, num_samples)

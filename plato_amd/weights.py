@@ -178,6 +178,22 @@ def fedadp_angles(dv: np.ndarray, dd: np.ndarray, vv: np.ndarray, scales: np.nda
     return angles
 
 
+def fedadp_angles_from_dots(inner: Sequence, g_sq, l_sq: Sequence) -> list:
+    """fedadp_server.py:94-99 from the reference's own float32 reductions, computed on the device.
+
+    ``inner[k] = np.inner(g, loc_k)``, ``g_sq = g.dot(g)``, ``l_sq[k] = loc_k.dot(loc_k)`` are the
+    float32 values numpy's BLAS produces (``plato_agg_flat_dots``, bit-exact);
+    ``np.linalg.norm`` is ``sqrt`` of such a dot in float32, and the rest is
+    the reference's numpy scalar code on those float32 values.
+    """
+    g_norm = np.sqrt(np.float32(g_sq))
+    angles = []
+    for k in range(len(inner)):
+        norms = g_norm * np.sqrt(np.float32(l_sq[k]))
+        angles.append(np.arccos(np.clip(np.float32(inner[k]) / norms, -1.0, 1.0)))
+    return angles
+
+
 def fedadp_contributions(angles, selected_clients, local_angles: dict, current_round: int,
                          alpha: float = 5) -> list:
     """fedadp_server.py:101-120: smoothed angles (updated in ``local_angles``) -> contributions."""

@@ -1,0 +1,88 @@
+"""GPU parity of the flattened-model reductions (plato_amd/csrc/flat.hip) vs oracle/reductions.c.
+
+The oracle is pinned to numpy / torch on the CPU (tests/test_reductions.py)
+and to the reference's fixtures; here the device kernels must equal it bit
+for bit on ragged sizes (every tail case of the 64- and 32-element blocks, the
+cascade's partial groups, one- and two-pass thread splits).
+"""
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import reductions as R
+from plato_amd import _lib
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+SIZES = [1, 5, 31, 32, 33, 63, 64, 65, 95, 96, 100, 127, 129, 4095, 4096, 4097, 8191, 32767, 32768, 32769,
+         100003, 262144 + 37]
+
+
+def _rows(vecs):
+    """[len, stride] device buffer (64-float aligned rows) and its row pointer table."""
+    n = max(v.size for v in vecs)
+    stride = max(64, -(-n // 64) * 64)
+    buf = torch.zeros((len(vecs), stride), dtype=torch.float32, device=DEV)
+    for r, v in enumerate(vecs):
+        buf[r, : v.size] = torch.from_numpy(v)
+    ptrs = torch.tensor([buf.data_ptr() + r * stride * 4 for r in range(len(vecs))], dtype=torch.int64, device=DEV)
+    return buf, ptrs
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_sdot_pairs_equal_openblas_order(n):
+    rng = np.random.default_rng(n)
+    xs = [rng.standard_normal(n).astype(np.float32) for _ in range(3)]
+    ys = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(3)]
+    bx, px = _rows(xs)
+    by, py = _rows(ys)
+    out_xy = torch.full((3,), float("nan"), device=DEV)
+    out_yy = torch.full((3,), float("nan"), device=DEV)
+    _lib.call("plato_agg_sdot_pairs", px.data_ptr(), py.data_ptr(), 3, n, out_xy.data_ptr(), out_yy.data_ptr(),
+              torch.cuda.current_stream().cuda_stream)
+    got_xy, got_yy = out_xy.cpu().numpy(), out_yy.cpu().numpy()
+    for j in range(3):
+        assert got_xy[j].tobytes() == R.sdot(xs[j], ys[j]).tobytes(), (n, j)
+        assert got_yy[j].tobytes() == R.sdot(ys[j], ys[j]).tobytes(), (n, j)
+
+
+@pytest.mark.parametrize("n", SIZES + [1 << 20, (1 << 20) + 3])
+def test_norms_and_cosine_sum_equal_torch_order(n):
+    rng = np.random.default_rng(n + 1)
+    a = (rng.standard_normal(n) * 1e-2).astype(np.float32)
+    bs = [(rng.standard_normal(n) * 3e-2).astype(np.float32) + a for _ in range(2)]
+    buf, ptrs = _rows([a] + bs)
+    chunk = torch.from_numpy(np.asarray([[0, 0, n, 0]], dtype=np.uint32).view(np.int32)).to(DEV)
+    norms = torch.empty(3, dtype=torch.float32, device=DEV)
+    h = torch.cuda.current_stream().cuda_stream
+    _lib.call("plato_agg_entry_norms_f32", ptrs.data_ptr(), None, 3, None, None, chunk.data_ptr(), 1, None, 0, 1,
+              n, 0, norms.data_ptr(), h)
+    got_n = norms.cpu().numpy()
+    for j, v in enumerate([a] + bs):
+        assert got_n[j].tobytes() == R.torch_norm(v).tobytes(), (n, j)
+    for threads in (1, 3, 8, 16, 64):
+        ws = torch.empty(_lib.lib().plato_agg_torch_cosine_workspace(2, threads) // 4 + 1, device=DEV)
+        out = torch.full((2,), float("nan"), device=DEV)
+        _lib.call("plato_agg_torch_cosine_sum", buf.data_ptr(), ptrs.data_ptr() + 8, 2, n, norms.data_ptr(),
+                  norms.data_ptr() + 4, 1e-8, threads, ws.data_ptr(), out.data_ptr(), h)
+        got = out.cpu().numpy()
+        for j in range(2):
+            assert got[j].tobytes() == R.torch_cosine(a, bs[j], threads).tobytes(), (n, threads, j)
+
+
+def test_cosine_of_a_zero_vector_uses_eps():
+    n = 1000
+    a = np.zeros(n, np.float32)
+    b = np.random.default_rng(0).standard_normal(n).astype(np.float32)
+    buf, ptrs = _rows([a, b])
+    chunk = torch.from_numpy(np.asarray([[0, 0, n, 0]], dtype=np.uint32).view(np.int32)).to(DEV)
+    norms = torch.empty(2, dtype=torch.float32, device=DEV)
+    h = torch.cuda.current_stream().cuda_stream
+    _lib.call("plato_agg_entry_norms_f32", ptrs.data_ptr(), None, 2, None, None, chunk.data_ptr(), 1, None, 0, 1,
+              n, 0, norms.data_ptr(), h)
+    ws = torch.empty(64, device=DEV)
+    out = torch.empty(1, device=DEV)
+    _lib.call("plato_agg_torch_cosine_sum", buf.data_ptr(), ptrs.data_ptr() + 8, 1, n, norms.data_ptr(),
+              norms.data_ptr() + 4, 1e-8, 8, ws.data_ptr(), out.data_ptr(), h)
+    assert out.item() == float(R.torch_cosine(a, b, 8)) == 0.0
