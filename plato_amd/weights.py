@@ -145,39 +145,6 @@ def fedatt_attention(norms: np.ndarray) -> np.ndarray:
     return torch.softmax(t, dim=1).numpy()
 
 
-def fedadp_process_scales(names: Sequence[str], lr: float) -> np.ndarray:
-    """Per-entry factor of FedAdp's flattening on products of two flattened vectors.
-
-    ``process_grad`` (examples/server_aggregation/fedadp/fedadp_server.py:122-133)
-    sorts the entries by ``name.lower()``, keeps the first as is and divides
-    every other by ``-lr``; a product of two such vectors therefore weighs
-    entry e by 1 (first) or 1/lr^2.
-    """
-    order = sorted(range(len(names)), key=lambda i: names[i].lower())
-    scales = np.full(len(names), 1.0 / (lr * lr))
-    if order:
-        scales[order[0]] = 1.0
-    return scales
-
-
-def fedadp_angles(dv: np.ndarray, dd: np.ndarray, vv: np.ndarray, scales: np.ndarray) -> list:
-    """Angles between each client's flattened delta and the global one (fedadp_server.py:94-99).
-
-    The reference forms ``np.inner`` and ``np.linalg.norm`` of float32 arrays
-    (float32 results), then ``np.arccos(np.clip(inner / norms, -1.0, 1.0))``
-    in float32; here the sums come from the device in fp64 and are rounded to
-    float32 where the reference holds float32 values.
-    """
-    g_norm = np.float32(np.sqrt(float(np.dot(vv, scales))))
-    angles = []
-    for k in range(dv.shape[0]):
-        inner = np.float32(float(np.dot(dv[k], scales)))
-        l_norm = np.float32(np.sqrt(float(np.dot(dd[k], scales))))
-        norms = g_norm * l_norm
-        angles.append(np.arccos(np.clip(inner / norms, -1.0, 1.0)))
-    return angles
-
-
 def fedadp_angles_from_dots(inner: Sequence, g_sq, l_sq: Sequence) -> list:
     """fedadp_server.py:94-99 from the reference's own float32 reductions, computed on the device.
 
