@@ -360,6 +360,20 @@ int plato_agg_torch_cosine_sum(const float* d_a, const float* const* d_b, int K,
                                hipStream_t stream);
 
 /*
+ * numpy's float32 np.sum(np.square(x_k - b)) of each fp32 piece (one per
+ * entry, d_pieces rows (entry, begin, end)): the ufunc reduction's 8192-element
+ * inner loops, out += pairwise_sum(chunk) from 0, pairwise_sum as numpy's
+ * (8 partial sums up to 128 elements, halved at multiples of 8 above).
+ * Polaris' per-layer squared deltas (examples/client_selection/polaris/
+ * polaris_server.py:78-81).  d_first_chunk[p] = sum over earlier pieces of
+ * ceil(len / 8192); n_chunks the total.  d_out: [K][n_pieces] floats.
+ */
+size_t plato_agg_np_sumsq_workspace(int K, uint32_t n_chunks);
+int plato_agg_np_sumsq(const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
+                       const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
+                       float* d_out, hipStream_t stream);
+
+/*
  * Single-process RCCL communicator over the GPUs one Plato server drives.
  * The reference has no collectives (aggregation runs on one CPU
  * process); these serve the multi-GPU engine behind the same

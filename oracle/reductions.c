@@ -181,3 +181,35 @@ float plato_oracle_torch_cosine(const float* a, const float* b, int64_t n, int t
   for (int64_t i = 0; i < n; ++i) tmp[i] = (a[i] / na) * (b[i] / nb);
   return plato_oracle_torch_sum(tmp, n, threads);
 }
+
+/* ------------------------------------------------------------------ numpy */
+/* 3. Polaris (examples/client_selection/polaris/polaris_server.py:78-81):
+ *    np.sum(np.square(d)) of a float32 array = the ufunc reduction's inner
+ *    loops over 8192-element buffer chunks, out += pairwise_sum(chunk) from
+ *    0, with numpy's pairwise_sum (numpy/_core/src/umath/loops_utils.h). */
+static float pairwise(const float* a, int64_t n) {
+  if (n < 8) {
+    float res = 0.f;
+    for (int64_t i = 0; i < n; ++i) res += a[i];
+    return res;
+  }
+  if (n <= 128) {
+    float r[8];
+    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    int64_t i = 8;
+    for (; i < n - (n % 8); i += 8)
+      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; i < n; ++i) res += a[i];
+    return res;
+  }
+  int64_t n2 = n / 2;
+  n2 -= n2 % 8;
+  return pairwise(a, n2) + pairwise(a + n2, n - n2);
+}
+
+float plato_oracle_np_sum(const float* a, int64_t n) {
+  float out = 0.f;
+  for (int64_t s = 0; s < n; s += 8192) out += pairwise(a + s, n - s < 8192 ? n - s : 8192);
+  return out;
+}

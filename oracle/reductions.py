@@ -30,6 +30,7 @@ def lib():
             ("plato_oracle_torch_norm", ctypes.c_float, [vp, i64]),
             ("plato_oracle_torch_sum", ctypes.c_float, [vp, i64, ctypes.c_int]),
             ("plato_oracle_torch_cosine", ctypes.c_float, [vp, vp, i64, ctypes.c_int, ctypes.c_float, vp]),
+            ("plato_oracle_np_sum", ctypes.c_float, [vp, i64]),
         ):
             fn = getattr(h, name)
             fn.restype, fn.argtypes = res, args
@@ -67,6 +68,12 @@ def torch_cosine(a, b, threads: int, eps: float = 1e-8) -> np.float32:
     tmp = np.empty(a.size, dtype=np.float32)
     return np.float32(lib().plato_oracle_torch_cosine(a.ctypes.data, b.ctypes.data, a.size, threads, eps,
                                                       tmp.ctypes.data))
+
+
+def np_sum(x) -> np.float32:
+    """numpy's float32 ``np.sum`` (8192-element inner loops of pairwise sums)."""
+    x = _f32(x)
+    return np.float32(lib().plato_oracle_np_sum(x.ctypes.data, x.size))
 
 
 # --------------------------------------------------------------------------

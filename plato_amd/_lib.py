@@ -115,6 +115,12 @@ SIGNATURES = {
         [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p, _c_void_p, _c_float, _c_int, _c_void_p, _c_void_p,
          _c_void_p],
     ),
+    "plato_agg_np_sumsq_workspace": (_c_size_t, [_c_int, ctypes.c_uint32]),
+    "plato_agg_np_sumsq": (
+        _c_int,
+        [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, ctypes.c_uint32, _c_void_p,
+         _c_void_p, _c_void_p],
+    ),
     "plato_agg_comm_create": (_c_int, [_c_int, _c_void_p, ctypes.POINTER(_c_void_p)]),
     "plato_agg_comm_destroy": (_c_int, [_c_void_p]),
     "plato_agg_comm_size": (_c_int, [_c_void_p]),

@@ -416,9 +416,160 @@ __global__ void cosine_combine_kernel(CosArgs a, int K) {
   a.out[k] = 0.f + small_inner_sum(buf, a.T);
 }
 
+// ------------------------------------------------- numpy pairwise sum of squares
+// numpy's float32 add.reduce: the inner loop gets at most 8192 elements (the
+// ufunc buffer), each loop does out += pairwise_sum(chunk), and pairwise_sum
+// (numpy/_core/src/umath/loops_utils.h) is: n < 8 sequential from 0; n <= 128
+// eight partial sums r[j] over the multiples of 8, ((r0+r1)+(r2+r3)) +
+// ((r4+r5)+(r6+r7)), then the rest; else split at n2 = n/2 - (n/2)%8.
+constexpr int kPW = 128;
+
+struct SqSrc {
+  const float* x;
+  const float* b;
+  __device__ __forceinline__ float operator()(uint64_t i) const {
+    const float d = x[i] - b[i];
+    return d * d;
+  }
+};
+
+__device__ float pw_leaf(const SqSrc& v, uint64_t off, uint64_t n) {
+  if (n < 8) {
+    float res = 0.f;
+    for (uint64_t i = 0; i < n; ++i) res += v(off + i);
+    return res;
+  }
+  float r[8];
+  for (int j = 0; j < 8; ++j) r[j] = v(off + j);
+  uint64_t i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += v(off + i + j);
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += v(off + i);
+  return res;
+}
+
+// The recursion, post-order, on an explicit stack (depth <= 7 for 8192 elements).
+__device__ float pw_sum(const SqSrc& v, uint64_t off, uint64_t n) {
+  uint64_t so[16], sn[16];
+  float sl[16];
+  int stage[16];
+  int sp = 0;
+  so[0] = off;
+  sn[0] = n;
+  stage[0] = 0;
+  float ret = 0.f;
+  bool have = false;  // `ret` holds the value of the node just finished
+  for (;;) {
+    if (!have) {
+      if (sn[sp] <= kPW) {
+        ret = pw_leaf(v, so[sp], sn[sp]);
+        have = true;
+        --sp;
+      } else {  // descend into the left half
+        uint64_t n2 = sn[sp] / 2;
+        n2 -= n2 % 8;
+        so[sp + 1] = so[sp];
+        sn[sp + 1] = n2;
+        stage[sp + 1] = 0;
+        stage[sp] = 1;
+        ++sp;
+        continue;
+      }
+    }
+    if (sp < 0) return ret;
+    if (stage[sp] == 1) {  // left done: remember it, descend right
+      uint64_t n2 = sn[sp] / 2;
+      n2 -= n2 % 8;
+      sl[sp] = ret;
+      stage[sp] = 2;
+      so[sp + 1] = so[sp] + n2;
+      sn[sp + 1] = sn[sp] - n2;
+      stage[sp + 1] = 0;
+      ++sp;
+      have = false;
+    } else {  // right done: left + right
+      ret = sl[sp] + ret;
+      --sp;
+    }
+  }
+}
+
+constexpr uint64_t kNpBuf = 8192;
+
+struct SumsqArgs {
+  const float* const* x;
+  const float* base;
+  const plato_agg_chunk* pieces;  // one per entry: (entry, begin, end)
+  const uint32_t* first_chunk;    // per piece: index of its first 8192-chunk (prefix sums)
+  uint32_t n_pieces;
+  uint32_t n_chunks;
+  int K;
+  float* chunk_sums;              // [K][n_chunks]
+  float* out;                     // [K][n_pieces]
+};
+
+__global__ __launch_bounds__(256) void np_sumsq_chunks_kernel(SumsqArgs a) {
+  const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= uint64_t(a.n_chunks) * uint64_t(a.K)) return;
+  const uint32_t k = uint32_t(t / a.n_chunks), c = uint32_t(t % a.n_chunks);
+  uint32_t lo = 0, hi = a.n_pieces;  // the piece holding chunk c
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.first_chunk[mid] <= c) lo = mid; else hi = mid;
+  }
+  const plato_agg_chunk p = a.pieces[lo];
+  const uint64_t begin = uint64_t(p.begin) + uint64_t(c - a.first_chunk[lo]) * kNpBuf;
+  const uint64_t end = begin + kNpBuf < uint64_t(p.end) ? begin + kNpBuf : uint64_t(p.end);
+  SqSrc v{a.x[k], a.base};
+  a.chunk_sums[uint64_t(k) * a.n_chunks + c] = pw_sum(v, begin, end - begin);
+}
+
+__global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
+  const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  if (t >= uint64_t(a.n_pieces) * uint64_t(a.K)) return;
+  const uint32_t k = uint32_t(t / a.n_pieces), pc = uint32_t(t % a.n_pieces);
+  const uint32_t c0 = a.first_chunk[pc];
+  const uint32_t c1 = pc + 1 < a.n_pieces ? a.first_chunk[pc + 1] : a.n_chunks;
+  float out = 0.f;  // the reduction's identity, then out += pairwise(chunk) per inner loop
+  for (uint32_t c = c0; c < c1; ++c) out += a.chunk_sums[uint64_t(k) * a.n_chunks + c];
+  a.out[uint64_t(k) * a.n_pieces + pc] = out;
+}
+
 }  // namespace
 
 extern "C" {
+
+size_t plato_agg_np_sumsq_workspace(int K, uint32_t n_chunks) {
+  return size_t(K > 0 ? K : 0) * size_t(n_chunks) * sizeof(float);
+}
+
+int plato_agg_np_sumsq(const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
+                       const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
+                       float* d_out, hipStream_t stream) {
+  if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
+  if (!n_pieces) return clear_error();
+  if (!d_x || !d_base || !d_pieces || !d_first_chunk || !d_workspace || !d_out)
+    return set_error(PLATO_AGG_EINVAL, "null pointer");
+  SumsqArgs a{};
+  a.x = d_x;
+  a.base = d_base;
+  a.pieces = d_pieces;
+  a.first_chunk = d_first_chunk;
+  a.n_pieces = n_pieces;
+  a.n_chunks = n_chunks;
+  a.K = K;
+  a.chunk_sums = static_cast<float*>(d_workspace);
+  a.out = d_out;
+  const uint64_t t1 = uint64_t(n_chunks) * uint64_t(K), t2 = uint64_t(n_pieces) * uint64_t(K);
+  if (t1) {
+    hipLaunchKernelGGL(np_sumsq_chunks_kernel, dim3(uint32_t((t1 + 255) / 256)), dim3(256), 0, stream, a);
+    if (int rc = check_launch("np_sumsq chunks launch")) return rc;
+  }
+  hipLaunchKernelGGL(np_sumsq_pieces_kernel, dim3(uint32_t((t2 + 255) / 256)), dim3(256), 0, stream, a);
+  return check_launch("np_sumsq pieces launch");
+}
+
 
 int plato_agg_flatten(int mode, const void* const* d_src_f32, const void* const* d_src_i64, int K,
                       const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,

@@ -835,6 +835,47 @@ class AggregationRound:
         stream.synchronize()
         return inner.cpu().numpy(), g_sq.cpu().numpy()[0], l_sq.cpu().numpy()
 
+    def np_sumsq(self, slots: Sequence[int]) -> np.ndarray:
+        """numpy's float32 ``np.sum(np.square(x - b))`` of every fp32 entry, per client, bit-exact.
+
+        Polaris' per-layer squared deltas (examples/client_selection/polaris/
+        polaris_server.py:78-81) in numpy's own order (``plato_agg_np_sumsq``).
+        Returns ``[K, E]`` float32 (entries in layout order; int64 entries 0).
+        """
+        slots = self._check_slots(slots)
+        if not self.has_baseline:
+            raise ValueError("baseline not staged")
+        eng, lay = self.engine, self.layout
+        key = ("np_sumsq_pieces", str(eng.device))
+        hit = lay._cache.get(key)
+        if hit is None:
+            rows, first, n_chunks = [], [], 0
+            for idx, e in enumerate(lay.entries):
+                if e.region == F32 and e.numel:
+                    rows.append((idx, e.offset, e.offset + e.numel, 0))
+                    first.append(n_chunks)
+                    n_chunks += -(-e.numel // 8192)
+            pieces = np.asarray(rows, dtype=np.uint32).reshape(-1, 4)
+            hit = (torch.from_numpy(pieces.view(np.int32).copy()).to(eng.device),
+                   torch.from_numpy(np.asarray(first, dtype=np.uint32).view(np.int32)).to(eng.device),
+                   pieces[:, 0].astype(np.int64), n_chunks)
+            lay._cache[key] = hit
+        pieces, first, entry_of, n_chunks = hit
+        k, n_p = len(slots), int(entry_of.size)
+        out = np.zeros((k, len(lay.entries)), dtype=np.float32)
+        if n_p == 0:
+            return out
+        stream = torch.cuda.current_stream(eng.device)
+        self.stager.fence(stream)
+        tf = torch.from_numpy(np.asarray([self._pf[i] for i in slots], dtype=np.int64)).to(eng.device)
+        ws = torch.empty(max(1, eng.lib.plato_agg_np_sumsq_workspace(k, n_chunks) // 4), dtype=torch.float32,
+                         device=eng.device)
+        dev_out = torch.empty((k, n_p), dtype=torch.float32, device=eng.device)
+        _lib.call("plato_agg_np_sumsq", tf.data_ptr(), k, _ptr(eng._base.f32), pieces.data_ptr(), first.data_ptr(),
+                  n_p, n_chunks, ws.data_ptr(), dev_out.data_ptr(), _stream_handle(stream))
+        out[:, entry_of] = dev_out.cpu().numpy()
+        return out
+
     def model_similarities(self, reference: Mapping[str, torch.Tensor], slots: Sequence[int],
                            eps: float = 1e-8, threads: int | None = None) -> list[np.float32]:
         """Port's cosine similarity of each client delta with ``baseline - reference``, bit-exact.

@@ -250,9 +250,11 @@ class PolarisWeights(_EngineHolder):
 
     FedAvg weights, plus the per-client norm of the conv-layer deltas the
     reference records for its client-selection solver
-    (``self.squared_deltas_current_round``, ``self.unexplored_clients``),
-    from one ``plato_agg_entry_stats`` pass over the staged payloads.  The
-    solver itself (cvxopt/mosek, ``:129-186``) stays the reference's.
+    (``self.squared_deltas_current_round``, ``self.unexplored_clients``):
+    each layer's ``np.sum(np.square(delta))`` in numpy's own float32 order on
+    the device (``AggregationRound.np_sumsq``), then the reference's float32
+    scalar code.  The solver itself (cvxopt/mosek, ``:129-186``) stays the
+    reference's.
     """
 
     needs_staged_round = True
@@ -260,8 +262,8 @@ class PolarisWeights(_EngineHolder):
     def aggregation_weights(self, updates):
         weights, scales = super().aggregation_weights(updates)  # FedAvg n_i/N, sets total_samples
         rnd = _staged_round(self, "Polaris")
-        _, dd, _ = rnd.entry_stats(range(len(updates)))
-        norms = W.polaris_delta_norms(dd, rnd.layout.keys())
+        sums = rnd.np_sumsq(range(len(updates)))  # numpy's float32 np.sum(np.square(delta)) per layer
+        norms = W.polaris_delta_norms(sums, rnd.layout.keys())
         self.squared_deltas_current_round = np.zeros(self.number_of_client)
         sum_deltas_current_round = 0
         deltas_counter = 0

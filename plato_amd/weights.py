@@ -191,8 +191,9 @@ def polaris_delta_norms(dd: np.ndarray, names: Sequence[str]) -> list:
     """Per client ``sqrt(sum over 'conv' layers of np.sum(np.square(delta)))``.
 
     examples/client_selection/polaris/polaris_server.py:76-89: each layer's
-    ``np.sum`` is a float32 scalar and they are added in float32
-    (``0 + np.float32``), then ``np.sqrt`` in float32.
+    ``np.sum`` is a float32 scalar (``dd[k, e]``, from the device in numpy's
+    order) and they are added in float32 (``0 + np.float32``), then
+    ``np.sqrt`` in float32.
     """
     conv = [e for e, name in enumerate(names) if "conv" in name]
     out = []

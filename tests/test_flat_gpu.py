@@ -86,3 +86,31 @@ def test_cosine_of_a_zero_vector_uses_eps():
     _lib.call("plato_agg_torch_cosine_sum", buf.data_ptr(), ptrs.data_ptr() + 8, 1, n, norms.data_ptr(),
               norms.data_ptr() + 4, 1e-8, 8, ws.data_ptr(), out.data_ptr(), h)
     assert out.item() == float(R.torch_cosine(a, b, 8)) == 0.0
+
+
+def test_np_sumsq_equals_numpy_order():
+    from oracle import fedavg_oracle as ref
+    from plato_amd.arena import ArenaLayout
+    from plato_amd.engine import FedAvgEngine
+
+    spec = [("conv.a", (7,), "f32"), ("conv.b", (129,), "f32"), ("n", (2,), "i64"), ("conv.c", (8192,), "f32"),
+            ("conv.d", (8193,), "f32"), ("fc", (100003,), "f32"), ("conv.e", (512, 256, 3, 3), "f32")]
+    layout = ArenaLayout.from_shapes(spec)
+    rng = np.random.default_rng(4)
+    bf = rng.standard_normal(layout.n_f32).astype(np.float32)
+    bi = rng.integers(0, 100, layout.n_i64)
+    xs = [((rng.standard_normal(layout.n_f32) * 1e-2).astype(np.float32) + bf, bi + 1) for _ in range(3)]
+    eng = FedAvgEngine(DEV)
+    rnd = eng.begin(layout.unpack(torch.from_numpy(bf), torch.from_numpy(bi)), 3)
+    rnd.put_baseline(layout.unpack(torch.from_numpy(bf), torch.from_numpy(bi)))
+    for c, (xf, xi) in enumerate(xs):
+        rnd.put_client(c, layout.unpack(torch.from_numpy(xf), torch.from_numpy(xi)))
+    got = rnd.np_sumsq(range(3))
+    for c, (xf, _) in enumerate(xs):
+        for e_i, e in enumerate(layout.entries):
+            if e.region != "f32":
+                assert got[c, e_i] == 0
+                continue
+            d = np.subtract(xf[e.offset:e.offset + e.numel], bf[e.offset:e.offset + e.numel], dtype=np.float32)
+            assert got[c, e_i].tobytes() == np.sum(np.square(d.reshape(e.shape))).tobytes(), (c, e.name)
+            assert got[c, e_i].tobytes() == R.np_sum(np.square(d)).tobytes()

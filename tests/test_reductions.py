@@ -135,3 +135,34 @@ def test_fedadp_weights_from_restated_dots_reproduce_reference_bits(name):
     aw = W.fedadp_weighting(contribs, ns)
     assert [float(x).hex() for x in aw] == exp["adaptive_weighting"]
     assert {str(c): "%08x" % np.float32(a).view(np.uint32) for c, a in local.items()} == exp["local_angles"]
+
+
+def test_numpy_sum_restatement_equals_np_sum_of_squares():
+    rng = np.random.default_rng(11)
+    for shape in [(1,), (7,), (8,), (100,), (129,), (8192,), (8193,), (20000,), (100003,), (64, 3, 3, 3),
+                  (512, 256, 3, 3)]:
+        d = (rng.standard_normal(shape) * 1e-2).astype(np.float32)
+        assert R.np_sum(np.square(d).ravel()) == np.sum(np.square(d)), shape
+
+
+def test_polaris_norms_from_restated_sums_reproduce_reference_bits():
+    case = CASES["polaris_resnet18_k8"]
+    recipe, exp = case["recipe"], case["expected"]
+    layout, base, pays, (bf, bi, xs_f, xs_i) = G.host_state_dicts(recipe)
+    names = layout.keys()
+    got = {}
+    for c, x in zip(G.order_of(recipe), pays):
+        sums = np.zeros(len(names), dtype=np.float32)
+        for e_i, e in enumerate(layout.entries):
+            if e.region == "f32" and "conv" in e.name:
+                d = np.subtract(x[e.name].numpy(), base[e.name].numpy(), dtype=np.float32)
+                sums[e_i] = R.np_sum(np.square(d).ravel())
+        got[c] = W.polaris_delta_norms(sums[None, :], names)[0]
+    want = {int(c): float.fromhex(v) for c, v in exp["squared_deltas"].items()}
+    assert {c: float(v).hex() for c, v in got.items()} == {c: float(want[c]).hex() for c in got}
+    # unexplored clients get alpha * the mean norm, accumulated like the reference (float32 norms)
+    total = 0
+    for c in got:
+        total += got[c]
+    expect = 10 * (total / len(got))  # alpha of the fixture config
+    assert all(float(want[c]).hex() == float(expect).hex() for c in want if c not in got)
