@@ -76,7 +76,7 @@
 extern "C" {
 #endif
 
-#define PLATO_AGG_ABI_VERSION 1
+#define PLATO_AGG_ABI_VERSION 2
 
 #define PLATO_AGG_OK 0
 #define PLATO_AGG_EINVAL (-1)   /* bad argument (null, misaligned, K <= 0) */
@@ -300,6 +300,36 @@ int plato_agg_fill_synth_f32(float* d_out, const float* d_add, size_t n,
 int plato_agg_fill_synth_i64(int64_t* d_out, const int64_t* d_add, size_t n,
                              uint64_t seed, uint64_t stream_id, uint64_t modulus,
                              hipStream_t stream);
+
+/*
+ * FedAvg with float64 weights on the fp32 entries (ABI 2): for every fp32
+ * element, clients in order,
+ *   d = x_i - b (fp32; d = x_i when d_base_* are NULL: deltas mode)
+ *   acc = fp32( double(acc) + double(d) * d_w64[i] )      (one double rounding
+ *         for the product, one for the sum, then the cast: torch's in-place add
+ *         of a float64 tensor into an fp32 one)
+ *   new = fp32(b + acc)            (deltas mode: acc)
+ * and for the int64 entries the fp32 chain with d_w_i64[i] (fp32):
+ *   acc = acc + fp32(fp32(x_i - b) * w_i64),  new = fp32(b) + acc.
+ * Replaces the RL server's smart weighting (plato/utils/reinforcement_learning/
+ * rl_server.py:66-71: `delta * smart_weighting[i]` with a float64 [K, 1]
+ * action for the fp32 entries, `delta * smart_weighting[i][0]` for the int64
+ * ones).  Arena < 4 GiB per call.
+ */
+int plato_agg_fedavg_w64(const float* const* d_x_f32, const int64_t* const* d_x_i64, const double* d_w64,
+                         const float* d_w_i64, int K, const float* d_base_f32, const int64_t* d_base_i64,
+                         float* d_out_f32, float* d_out_i64f, size_t n_f32, size_t n_i64, hipStream_t stream);
+
+/*
+ * float64 weighted sum of K float64 vectors (16-byte aligned):
+ *   out[e] = (((0 + x_0[e]*w_0) + x_1[e]*w_1) + ...)   float64, separately rounded.
+ * The plaintext half of HE hybrid FedAvg (plato/servers/fedavg_he.py:88-98):
+ * the unencrypted weights are float64 numpy vectors (homo_enc.py:50-63), so
+ * `unencrypted_avg_update += unenc_w * (n_i / N)` runs in numpy float64 and
+ * turns the fp32 zeros into a float64 accumulator.
+ */
+int plato_agg_weighted_sum_f64(const double* const* d_x, const double* d_w, int K, double* d_out, size_t n,
+                               hipStream_t stream);
 
 /*
  * Flattened-model reductions of the variant servers, in the reference's own

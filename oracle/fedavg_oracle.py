@@ -155,6 +155,30 @@ def deltas_numpy(deltas_f32, deltas_i64, weights, scales=None):
     return acc, acc_i
 
 
+def w64_numpy(xs_f32, xs_i64, weights64, weights_i64, base_f32=None, base_i64=None):
+    """Float64 weights on fp32 entries (rl_server.py:66-71 with a float64 action,
+    fedavg_he.py:88-98 on float64 plaintext vectors): the product in float64,
+    the in-place add into the fp32 average in float64, then the cast;
+    int64 entries keep the fp32 chain with fp32(weights_i64[i])."""
+    n_f = xs_f32[0].size if xs_f32 else 0
+    acc = np.zeros(n_f, dtype=np.float32)
+    for x, w in zip(xs_f32, weights64):
+        d = x if base_f32 is None else np.subtract(x, base_f32, dtype=np.float32)
+        acc = (acc.astype(np.float64) + d.astype(np.float64) * float(w)).astype(np.float32)
+    n_i = xs_i64[0].size if xs_i64 else 0
+    acc_i = np.zeros(n_i, dtype=np.float32)
+    for x, w in zip(xs_i64, weights_i64):
+        with np.errstate(over="ignore"):
+            d = x.astype(np.int64) if base_i64 is None else x.astype(np.int64) - base_i64.astype(np.int64)
+        acc_i = np.add(acc_i, np.multiply(d.astype(np.float32), np.float32(float(w)), dtype=np.float32),
+                       dtype=np.float32)
+    if base_f32 is not None:
+        acc = np.add(base_f32, acc, dtype=np.float32)
+    if base_i64 is not None:
+        acc_i = np.add(base_i64.astype(np.float32), acc_i, dtype=np.float32)
+    return acc, acc_i
+
+
 def mix_numpy(base_f32, base_i64, x_f32, x_i64, mixing: float):
     """FedAsync (fedasync_algorithm.py:15-18): b * fp32(1-m) + x * fp32(m)."""
     om = np.float32(1 - mixing)

@@ -13,7 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libplato_agg.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 PLATO_AGG_OK = 0
 PLATO_AGG_EINVAL = -1
@@ -101,6 +101,12 @@ SIGNATURES = {
         _c_int,
         [_c_void_p, _c_void_p, _c_int, _c_void_p, _c_int, _c_float, _c_void_p, _c_void_p, _c_void_p,
          ctypes.c_uint32, _c_void_p, ctypes.c_uint32, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
+         _c_size_t, _c_size_t, _c_void_p],
+    ),
+    "plato_agg_weighted_sum_f64": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_void_p, _c_size_t, _c_void_p]),
+    "plato_agg_fedavg_w64": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p,
          _c_size_t, _c_size_t, _c_void_p],
     ),
     "plato_agg_flatten": (

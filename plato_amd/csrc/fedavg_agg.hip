@@ -869,6 +869,180 @@ int plato_agg_fedavg_deltas(const float* const* d_d_f32, const int64_t* const* d
                  stream);
 }
 
+}  // extern "C"
+
+namespace {
+// ---------------------------------------------------------------------------
+// float64 weights on the fp32 entries (the reference's numpy/torch promotion):
+//   acc = fp32( double(acc) + double(d) * w64_i )      d = x - b (fp32) or x
+// int64 entries keep the fp32 chain with their own weights w_i64:
+//   acc = acc + fp32(fp32(d) * w_i64_i)
+// RL server: `delta * self.smart_weighting[i]` with a float64 [K, 1] numpy
+// action (rl_server.py:66-71) is a float64 tensor added into the fp32 average
+// (in-place add in float64, then cast); its int64 entries use
+// smart_weighting[i][0] as a Python scalar.
+// Streaming shape of the fp32 kernel: a float4 group per lane, clients in
+// order, 4 clients' loads in flight; HBM-bound (fp64 is cheap on MI355X).
+// ---------------------------------------------------------------------------
+struct W64Args {
+  const float* const* xf;
+  const int64_t* const* xi;
+  const double* w64;
+  const float* wi;
+  const float* base_f;
+  const int64_t* base_i;
+  float* out_f;
+  float* out_if;
+  uint64_t n4, n_f32, n_i64;
+  uint32_t nb_vec;
+  int K;
+};
+
+template <bool HAS_BASE>
+__global__ __launch_bounds__(256) void fedavg_w64_kernel(W64Args a) {
+  const uint32_t blk = blockIdx.x;
+  if (blk < a.nb_vec) {
+    const uint64_t g = uint64_t(blk) * 256 + threadIdx.x;
+    if (g >= a.n4) return;
+    const uint32_t off = uint32_t(g * 16u);
+    const f4 b = HAS_BASE ? ld4_off<false>(a.base_f, off) : f4_zero();
+    f4 acc = f4_zero();
+    int i = 0;
+    for (; i + 4 <= a.K; i += 4) {
+      f4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = ld4_off<true>(sld(a.xf, i + u), off);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double w = sld(a.w64, i + u);
+        const f4 d = HAS_BASE ? f4_sub(x[u], b) : x[u];
+        acc.x = float(double(acc.x) + double(d.x) * w);
+        acc.y = float(double(acc.y) + double(d.y) * w);
+        acc.z = float(double(acc.z) + double(d.z) * w);
+        acc.w = float(double(acc.w) + double(d.w) * w);
+      }
+    }
+    for (; i < a.K; ++i) {
+      const f4 x = ld4_off<true>(sld(a.xf, i), off);
+      const double w = sld(a.w64, i);
+      const f4 d = HAS_BASE ? f4_sub(x, b) : x;
+      acc.x = float(double(acc.x) + double(d.x) * w);
+      acc.y = float(double(acc.y) + double(d.y) * w);
+      acc.z = float(double(acc.z) + double(d.z) * w);
+      acc.w = float(double(acc.w) + double(d.w) * w);
+    }
+    st4_off<true>(a.out_f, off, HAS_BASE ? f4_add(b, acc) : acc);
+    return;
+  }
+  const uint64_t j = uint64_t(blk - a.nb_vec) * 256 + threadIdx.x;
+  const uint64_t tail = a.n_f32 - 4 * a.n4;
+  if (j < tail) {
+    const uint64_t e = 4 * a.n4 + j;
+    const float b = HAS_BASE ? a.base_f[e] : 0.f;
+    float acc = 0.f;
+    for (int i = 0; i < a.K; ++i) {
+      const float x = sld(a.xf, i)[e];
+      const float d = HAS_BASE ? x - b : x;
+      acc = float(double(acc) + double(d) * sld(a.w64, i));
+    }
+    a.out_f[e] = HAS_BASE ? b + acc : acc;
+    return;
+  }
+  const uint64_t e = j - tail;
+  if (e >= a.n_i64) return;
+  const int64_t b = HAS_BASE ? a.base_i[e] : 0;
+  float acc = 0.f;
+  for (int i = 0; i < a.K; ++i) {
+    const int64_t x = sld(a.xi, i)[e];
+    const int64_t d = HAS_BASE ? (int64_t)((uint64_t)x - (uint64_t)b) : x;
+    acc = acc + (float)d * sld(a.wi, i);
+  }
+  a.out_if[e] = HAS_BASE ? (float)b + acc : acc;
+}
+}  // namespace
+
+namespace {
+// float64 weighted sum (HE plaintext half): acc = acc + x_i * w_i, float64,
+// separately rounded, clients in order; two doubles per lane (16-byte loads).
+typedef double d2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(1))) const d2 gd2;
+
+__global__ __launch_bounds__(256) void weighted_sum_f64_kernel(const double* const* xs, const double* w, int K,
+                                                               double* out, uint64_t n) {
+  const uint64_t g = uint64_t(blockIdx.x) * 256 + threadIdx.x;
+  const uint64_t n2 = n / 2;
+  if (g < n2) {
+    d2 acc = d2{0.0, 0.0};
+    int i = 0;
+    for (; i + 4 <= K; i += 4) {
+      d2 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = __builtin_nontemporal_load((gd2*)(sld(xs, i + u)) + g);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) acc = acc + x[u] * sld(w, i + u);
+    }
+    for (; i < K; ++i) acc = acc + __builtin_nontemporal_load((gd2*)(sld(xs, i)) + g) * sld(w, i);
+    ((__attribute__((address_space(1))) d2*)out)[g] = acc;
+  } else if (g == n2 && (n & 1)) {
+    double acc = 0.0;
+    for (int i = 0; i < K; ++i) acc = acc + sld(xs, i)[n - 1] * sld(w, i);
+    out[n - 1] = acc;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int plato_agg_weighted_sum_f64(const double* const* d_x, const double* d_w, int K, double* d_out, size_t n,
+                               hipStream_t stream) {
+  if (K <= 0) return fail(PLATO_AGG_EINVAL, "K must be >= 1");
+  if (!n) return plato_agg_internal::clear_error();
+  if (!d_x || !d_w || !d_out) return fail(PLATO_AGG_EINVAL, "null pointer");
+  if (!aligned16(d_out)) return fail(PLATO_AGG_EINVAL, "output must be 16-byte aligned");
+  const uint64_t threads = n / 2 + 1;
+  hipLaunchKernelGGL(weighted_sum_f64_kernel, dim3(uint32_t((threads + 255) / 256)), dim3(256), 0, stream, d_x,
+                     d_w, K, d_out, uint64_t(n));
+  return check_launch("weighted_sum_f64 launch");
+}
+
+int plato_agg_fedavg_w64(const float* const* d_x_f32, const int64_t* const* d_x_i64, const double* d_w64,
+                         const float* d_w_i64, int K, const float* d_base_f32, const int64_t* d_base_i64,
+                         float* d_out_f32, float* d_out_i64f, size_t n_f32, size_t n_i64, hipStream_t stream) {
+  if (K <= 0) return fail(PLATO_AGG_EINVAL, "K must be >= 1");
+  if (n_f32 && (!d_x_f32 || !d_w64 || !d_out_f32)) return fail(PLATO_AGG_EINVAL, "null fp32 pointer");
+  if (n_i64 && (!d_x_i64 || !d_w_i64 || !d_out_i64f)) return fail(PLATO_AGG_EINVAL, "null int64 pointer");
+  const bool has_base = d_base_f32 != nullptr || d_base_i64 != nullptr;
+  if (has_base && ((n_f32 && !d_base_f32) || (n_i64 && !d_base_i64)))
+    return fail(PLATO_AGG_EINVAL, "baseline given for one region only");
+  if (n_f32 && (!aligned16(d_out_f32) || (has_base && !aligned16(d_base_f32))))
+    return fail(PLATO_AGG_EINVAL, "fp32 baseline/output must be 16-byte aligned");
+  if (n_f32 + n_i64 == 0) return plato_agg_internal::clear_error();
+  W64Args a{};
+  a.xf = d_x_f32;
+  a.xi = d_x_i64;
+  a.w64 = d_w64;
+  a.wi = d_w_i64;
+  a.base_f = d_base_f32;
+  a.base_i = d_base_i64;
+  a.out_f = d_out_f32;
+  a.out_if = d_out_i64f;
+  a.n4 = n_f32 / 4;
+  a.n_f32 = n_f32;
+  a.n_i64 = n_i64;
+  a.K = K;
+  if (a.n4 * 16ull > 0xffffffffull) return fail(PLATO_AGG_EINVAL, "fp32 arena must be < 4 GiB for float64 weights");
+  const uint64_t nb_vec = (a.n4 + 255) / 256;
+  const uint64_t nb_scalar = ((n_f32 - 4 * a.n4) + n_i64 + 255) / 256;
+  a.nb_vec = uint32_t(nb_vec);
+  const dim3 grid(uint32_t(nb_vec + nb_scalar));
+  if (has_base) {
+    hipLaunchKernelGGL(fedavg_w64_kernel<true>, grid, dim3(256), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL(fedavg_w64_kernel<false>, grid, dim3(256), 0, stream, a);
+  }
+  return check_launch("fedavg_w64 launch");
+}
+
 namespace {
 int run_bf16_range(const Bf16Variant& vr, const uint16_t* const* d_x_bf16, const uint16_t* const* d_x_i64_bf16,
                    const float* d_w, const float* d_s, int K, const float* d_base_f32, const int64_t* d_base_i64,

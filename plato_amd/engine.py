@@ -406,17 +406,46 @@ class FedAvgEngine:
         rnd.launch(weights, scales, deltas=True)
         return rnd.result()
 
-    def weighted_sum(self, tensors: Sequence[torch.Tensor], weights: Sequence[float]) -> torch.Tensor:
-        """``avg = zeros; avg += t_i * w_i`` over same-shape fp32 CPU tensors, in order.
+    def weighted_sum(self, tensors: Sequence, weights: Sequence[float]) -> torch.Tensor:
+        """``avg = trainer.zeros(n); avg += t_i * w_i`` over same-size vectors, in order.
 
-        The plaintext half of the HE server's hybrid FedAvg
-        (plato/servers/fedavg_he.py:88-98) and any flat weighted sum; one
-        deltas-mode launch (bit-exact with the sequential fp32 loop).
+        fp32 tensors follow torch's fp32 chain (one deltas-mode launch, fp32
+        result).  float64 numpy vectors follow the reference's numpy promotion
+        — the plaintext half of HE hybrid FedAvg (plato/servers/fedavg_he.py:
+        88-98), whose vectors come from ``np.append`` into float64 arrays
+        (plato/utils/homo_enc.py:50-63): ``avg += unenc_w * w`` falls back to
+        numpy and the accumulator becomes float64, so the sum runs in float64
+        (``plato_agg_weighted_sum_f64``) and the result is a float64 tensor.
         """
-        if not tensors:
+        if len(tensors) == 0:
             raise ValueError("no tensors to sum")
-        sds = [OrderedDict(v=t) for t in tensors]
+        if len(weights) != len(tensors):
+            raise ValueError("weights must have one entry per vector")
+        first = tensors[0]
+        if (isinstance(first, np.ndarray) and first.dtype == np.float64) or \
+                (isinstance(first, torch.Tensor) and first.dtype == torch.float64):
+            return self._weighted_sum_f64(tensors, weights)
+        sds = [OrderedDict(v=torch.as_tensor(t)) for t in tensors]
         return self.aggregate_deltas(sds, weights)["v"]
+
+    def _weighted_sum_f64(self, vectors, weights) -> torch.Tensor:
+        """float64 vectors: ``((0 + x_0*w_0) + x_1*w_1) + ...`` in float64 (``plato_agg_weighted_sum_f64``)."""
+        n = int(np.asarray(vectors[0]).size)
+        host = torch.empty((len(vectors), max(2, -(-n // 2) * 2)), dtype=torch.float64, pin_memory=True)
+        for r, v in enumerate(vectors):
+            v = torch.as_tensor(np.asarray(v, dtype=np.float64)).reshape(-1)
+            if v.numel() != n:
+                raise ValueError("vectors must have the same length")
+            host[r, :n].copy_(v)
+        dev = host.to(self.device, non_blocking=True)
+        w = torch.tensor([float(x) for x in weights], dtype=torch.float64).to(self.device)
+        ptrs = torch.tensor([dev.data_ptr() + r * dev.stride(0) * 8 for r in range(len(vectors))],
+                            dtype=torch.int64).to(self.device)
+        out = torch.empty(max(2, n), dtype=torch.float64, device=self.device)
+        stream = torch.cuda.current_stream(self.device)
+        _lib.call("plato_agg_weighted_sum_f64", _ptr(ptrs), _ptr(w), len(vectors), _ptr(out), n,
+                  _stream_handle(stream))
+        return out[:n].cpu()
 
     def compute_weight_deltas(self, baseline: Mapping[str, torch.Tensor],
                               weights_received: Sequence[Mapping[str, torch.Tensor]]
@@ -609,6 +638,46 @@ class AggregationRound:
         e1.record(stream)
         self._kernel_events = (e0, e1)
         self._fetch(stream, out_f, out_i, (tf, ti, w, s))
+
+    def launch_w64(self, weights64: Sequence[float], weights_i64: Sequence[float] | None = None,
+                   order: Sequence[int] | None = None, deltas: bool = False) -> None:
+        """FedAvg with float64 weights on the fp32 entries (``plato_agg_fedavg_w64``).
+
+        ``acc = fp32(double(acc) + double(d) * w64[i])`` for fp32 entries,
+        ``acc += fp32(fp32(d) * fp32(w_i64[i]))`` for int64 entries (default:
+        ``w_i64 = weights64``): the RL server's float64 smart weighting
+        (rl_server.py:66-71) and HE's float64 plaintext vectors (fedavg_he.py:88-98).
+        """
+        order = list(range(len(weights64))) if order is None else list(order)
+        if len(order) != len(weights64):
+            raise ValueError("order and weights must have the same length")
+        slots = self._check_slots(order)
+        if not deltas and not self.has_baseline:
+            raise ValueError("baseline not staged")
+        eng, lay = self.engine, self.layout
+        self.timings["stage_ms"] = (time.perf_counter() - self._t0) * 1e3
+        self._k = len(order)
+        w64 = torch.from_numpy(np.asarray([float(w) for w in weights64], dtype=np.float64)).to(eng.device)
+        wi = fp32_weights(weights64 if weights_i64 is None else weights_i64)
+        if len(wi) != len(order):
+            raise ValueError("weights_i64 must have one entry per client")
+        wi = torch.from_numpy(wi).to(eng.device)
+        pf = np.asarray([self._pf[i] for i in slots], dtype=np.int64)
+        pi = np.asarray([self._pi[i] for i in slots], dtype=np.int64)
+        tf, ti = eng._pointer_tables(pf, pi)
+        stream = torch.cuda.current_stream(eng.device)
+        self.stager.fence(stream)
+        out_f = torch.empty(lay.row_f32, dtype=torch.float32, device=eng.device)
+        out_i = torch.empty(lay.row_i64, dtype=torch.float32, device=eng.device)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        n_i = lay.n_i64
+        _lib.call("plato_agg_fedavg_w64", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w64), _ptr(wi), len(order),
+                  None if deltas else _ptr(eng._base.f32), None if (deltas or not n_i) else _ptr(eng._base.i64),
+                  _ptr(out_f), _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
+        e1.record(stream)
+        self._kernel_events = (e0, e1)
+        self._fetch(stream, out_f, out_i, (tf, ti, w64, wi))
 
     def _fetch(self, stream, out_f: torch.Tensor, out_i: torch.Tensor, keep=()) -> None:
         """D2H into pooled pinned buffers, stream-ordered; result() only waits."""

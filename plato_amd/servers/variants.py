@@ -299,3 +299,95 @@ class FedAdpServerMixin(FedAdpWeights, FusedAggregationMixin):
 
 class PolarisServerMixin(PolarisWeights, FusedAggregationMixin):
     pass
+
+
+def rl_smart_weights(smart_weighting, k: int, has_int64: bool):
+    """How the RL server's ``smart_weighting`` multiplies each kind of entry (rl_server.py:66-71).
+
+    Returns ``(weights for fp32 entries, weights for int64 entries, float64?)``:
+    ``delta * smart_weighting[i]`` for float entries — a float64 row of a
+    [K, 1] array makes the product float64 (numpy promotion) and the in-place
+    add then runs in float64; a float32 row or a scalar keeps torch's fp32
+    chain — and ``delta * smart_weighting[i][0]`` (a scalar: fp32 chain) for
+    int64 entries.
+    """
+    sw = np.asarray(smart_weighting)
+    if sw.shape[0] != k:
+        raise ValueError(f"smart_weighting has {sw.shape[0]} rows for {k} updates")
+    if sw.ndim == 1:
+        if has_int64:
+            raise TypeError("the reference indexes smart_weighting[i][0] for int64 entries: a [K, m] array is needed")
+        return [float(v) for v in sw], None, False
+    if sw.ndim != 2 or sw.shape[1] != 1:
+        raise ValueError("smart_weighting rows must hold one number ([K, 1]); wider rows broadcast per element")
+    col = [float(v) for v in sw[:, 0]]
+    return col, col, sw.dtype == np.float64
+
+
+class RLDeltasAggregationMixin(_EngineHolder):
+    """plato/utils/reinforcement_learning/rl_server.py:45-80: smart-weighted aggregate_deltas on the GPU.
+
+    The agent handshake (``update_state``, ``agent.prep_agent_update``,
+    ``update_action`` -> ``apply_action``) runs exactly as in the reference;
+    the weighted sum of the deltas runs on the device with the reference's
+    per-entry-type weight semantics (:func:`rl_smart_weights`): a float64
+    action puts the fp32 entries on float64 arithmetic
+    (``plato_agg_fedavg_w64``), while the int64 entries keep fp32 weights.
+    Compose as ``class Server(RLDeltasAggregationMixin, MyRLServer)``.
+    """
+
+    async def aggregate_deltas(self, updates, deltas_received):
+        self.update_state()
+        num_samples = [update.report.num_samples for update in updates]
+        self.total_samples = sum(num_samples)
+        self.agent.num_samples = num_samples
+        await self.agent.prep_agent_update()
+        await self.update_action()
+
+        engine = self.round_engine("native")
+        engine = getattr(engine, "primary", engine)  # float64 weights: one device
+        rnd = engine.begin(deltas_received[0], len(deltas_received))
+        w, w_i64, f64 = rl_smart_weights(self.smart_weighting, len(deltas_received), rnd.layout.n_i64 > 0)
+
+        def stage():
+            for slot, delta in enumerate(deltas_received):
+                rnd.put_client(slot, delta, what="deltas_received")
+
+        await self._off_loop(stage)
+        if f64:
+            rnd.launch_w64(w, w_i64, deltas=True)
+        else:
+            rnd.launch(w, None, deltas=True)
+        return await self._finish(rnd)
+
+
+class HEHybridMixin(_EngineHolder):
+    """plato/servers/fedavg_he.py:66-106: the plaintext half of hybrid FedAvg on the GPU.
+
+    The CKKS half (tenseal vectors) stays the reference's; the unencrypted
+    float64 vectors are summed by :meth:`FedAvgEngine.weighted_sum` with the
+    reference's float64 promotion.  Compose as
+    ``class Server(HEHybridMixin, fedavg_he.Server)``.
+    """
+
+    def _fedavg_hybrid(self, updates):
+        from plato.utils import homo_enc
+
+        weights_received = [homo_enc.deserialize_weights(update.payload, self.context) for update in updates]
+        unencrypted_weights = [homo_enc.extract_encrypted_model(x)[0] for x in weights_received]
+        encrypted_weights = [homo_enc.extract_encrypted_model(x)[1] for x in weights_received]
+        indices = [homo_enc.extract_encrypted_model(x)[2] for x in weights_received]
+        for i in range(1, len(indices)):
+            assert indices[i] == indices[0]
+        encrypt_indices = indices[0]
+        self.total_samples = sum(update.report.num_samples for update in updates)
+        factors = [update.report.num_samples / self.total_samples for update in updates]
+        engine = self.aggregation_engine()
+        engine = getattr(engine, "primary", engine)
+        unencrypted_avg_update = engine.weighted_sum(unencrypted_weights, factors)
+        encrypted_avg_update = self.trainer.zeros(encrypted_weights[0].size())
+        for enc_w, factor in zip(encrypted_weights, factors):
+            encrypted_avg_update += enc_w * factor
+        if len(encrypt_indices) == 0:
+            encrypted_avg_update = None
+        return homo_enc.wrap_encrypted_model(unencrypted_avg_update, encrypted_avg_update, encrypt_indices)

@@ -22,6 +22,10 @@ Reference code paths exercised (file:line in the reference):
   * Pisces aggregate_deltas                   examples/client_selection/pisces/pisces_server.py:73-99
   * FedAsync aggregate_weights                examples/async/fedasync/fedasync_server.py:67-78,
                                               fedasync_algorithm.py:9-20
+  * async simulated-wall-time ordering        plato/servers/base.py:925-1091 (_process_clients)
+  * cross-silo _process_reports               plato/servers/fedavg_cs.py:161-199
+  * RL smart-weighted aggregate_deltas        plato/utils/reinforcement_learning/rl_server.py:45-80
+  * HE hybrid FedAvg (plaintext half)         plato/servers/fedavg_he.py:66-106
   * the reference's own known-answer test     tests/fedavg_tests.py:44-175
 Missing third-party packages that the reference imports but this path never
 uses (socketio, torchvision, zstd, ...) are replaced by inert module stubs.
@@ -253,7 +257,148 @@ def server_class(mode):
     if mode == "polaris":
         import polaris_server
         return polaris_server.Server
+    if mode == "cross_silo":
+        from plato.servers import fedavg_cs
+        return fedavg_cs.Server
+    if mode == "async_wall":
+        from plato.servers import fedavg
+        return fedavg.Server
+    if mode in ("rl", "rl_f32"):
+        return rl_server_class()
     raise ValueError(mode)
+
+
+class _StubAgent:
+    """The RL agent surface rl_server.RLServer.aggregate_deltas touches (rl_server.py:45-90)."""
+
+    def __init__(self, action):
+        self.current_step = 0
+        self.planned = action
+        self.action = None
+        self.num_samples = None
+
+    def prep_action(self):
+        self.action = self.planned
+
+    async def prep_agent_update(self):
+        return None
+
+    def process_env_update(self):
+        return None
+
+
+async def drive_async_wall_time(server, case, payloads):
+    """base.Server._process_clients in asynchronous mode with simulated wall time
+    (plato/servers/base.py:925-1091): every client has reported (heap of
+    (finish_time, client_id, info), :896-910); the server pops the
+    minimum_clients earliest finishers, then the clients that violate the
+    staleness bound, in finish-time order (:1007-1079), and aggregates them in
+    that order.  Returns the client indices in the order the updates were formed.
+    """
+    import heapq
+
+    k = case["k"]
+    finish = case["finish_times"]
+    starting = case["starting_rounds"]
+    server.asynchronous_mode = True
+    server.simulate_wall_time = True
+    server.request_update = False
+    server.minimum_clients = case["minimum_clients"]
+    server.staleness_bound = case["staleness_bound"]
+    server.selected_clients = list(range(1, k + 1))
+    server.current_reported_clients = {}
+    server.current_processed_clients = {}
+    server.reported_clients = []
+    server.updates = []
+    server.training_clients = {}
+    info = None
+    for c in case["arrival_order"]:
+        report = types.SimpleNamespace(client_id=c + 1, num_samples=case["num_samples"][c], accuracy=0.5,
+                                       training_time=0, processing_time=0, comm_time=0, update_response=False,
+                                       statistical_utility=1.0, start_round=starting[c])
+        info = (float(finish[c]), c + 1, {"client_id": c + 1, "sid": f"s{c}", "starting_round": starting[c],
+                                         "start_time": 0.0, "report": report, "payload": payloads[c]})
+        heapq.heappush(server.reported_clients, info)
+        server.current_reported_clients[c + 1] = True
+
+    async def nothing(*a, **kw):
+        return None
+
+    server.wrap_up = nothing
+    server._select_clients = nothing
+    order = []
+    orig = server._process_reports
+
+    async def spy():
+        order.extend(u.client_id - 1 for u in server.updates)
+        return await orig()
+
+    server._process_reports = spy
+    await server._process_clients(info)
+    return order
+
+
+def rl_server_class():
+    from plato.utils.reinforcement_learning import rl_server
+
+    class GoldenRLServer(rl_server.RLServer):
+        action_dtype = np.float64
+
+        def prep_state(self):
+            return None
+
+        def apply_action(self):
+            # what examples/outdated/fei/fei_server.py:43 does with the agent's action
+            self.smart_weighting = np.array(self.agent.action, dtype=self.action_dtype)
+
+    return GoldenRLServer
+
+
+def rl_action(case):
+    return [[float.fromhex(h)] for h in case["action"]]
+
+
+def run_he_case(case):
+    """fedavg_he.Server._fedavg_hybrid (servers/fedavg_he.py:66-106) on float64 plaintext vectors.
+
+    The vectors are built as homo_enc.encrypt_weights builds them
+    (homo_enc.py:50-63: np.append of every weight into a float64 vector, the
+    encrypted indices deleted); the encrypted half is an fp32 torch stand-in
+    (tenseal is absent), recorded but not part of the check.
+    """
+    from plato.servers import fedavg_he
+    from plato.utils import homo_enc
+
+    model = make_model(case["model"])
+    entries, nf, ni = layout_of(model.state_dict())
+    k, seed = case["k"], case["seed"]
+    bf, bi = synth.baseline_arena(nf, ni, seed)
+    enc_idx = list(case["encrypt_indices"])
+    msgs = []
+    for c in range(k):
+        xf, xi = synth.client_arena(bf, bi, seed, c)
+        sd = unpack(entries, torch.from_numpy(xf), torch.from_numpy(xi))
+        vec = np.array([])
+        for w in sd.values():
+            vec = np.append(vec, w)
+        msgs.append({"unencrypted_weights": np.delete(vec, enc_idx),
+                     "encrypted_weights": torch.from_numpy(vec[enc_idx].astype(np.float32)),
+                     "indices": list(enc_idx)})
+    updates = make_updates(case["num_samples"], msgs, list(range(k)), [0] * k)
+    fake = types.SimpleNamespace(context=None, trainer=types.SimpleNamespace(
+        zeros=lambda shape: torch.zeros(shape)))
+    orig = homo_enc.deserialize_weights
+    homo_enc.deserialize_weights = lambda w, ctx: w
+    try:
+        res = fedavg_he.Server._fedavg_hybrid(fake, updates)
+    finally:
+        homo_enc.deserialize_weights = orig
+    unenc = res["unencrypted_weights"]
+    out = {"unencrypted_avg_sha256": sha(np.ascontiguousarray(unenc.numpy())), "dtype": str(unenc.dtype),
+           "n_unencrypted": int(unenc.numel()), "total_samples": fake.total_samples}
+    if case.get("full"):
+        out["_full"] = {"unencrypted_avg": unenc.numpy()}
+    return out, entries
 
 
 def run_case(case):
@@ -304,6 +449,10 @@ def run_case(case):
         import fedatt_algorithm
 
         server = cls(model=lambda: model, algorithm=fedatt_algorithm.Algorithm)
+        server.init_trainer()
+    elif mode in ("rl", "rl_f32"):
+        server = cls(agent=_StubAgent(rl_action(case)), model=lambda: model)
+        server.action_dtype = np.float64 if mode == "rl" else np.float32
         server.init_trainer()
     else:
         server = cls(model=lambda: model)
@@ -381,7 +530,19 @@ def run_case(case):
         return orig_load(weights)
     server.algorithm.load_weights = spy_load
 
-    if mode in ("fedavg", "fedbuff", "port", "fedasync", "fedatt", "fedadp", "polaris"):
+    if mode == "cross_silo":
+        # fedavg_cs.get_logged_items reads algorithm.local_rounds, which only a cross-silo
+        # config carries; the CSV row written after the aggregation is not part of the check
+        orig_event = server.callback_handler.call_event
+
+        def call_event(event, *a, **kw):
+            if event != "on_clients_processed":
+                return orig_event(event, *a, **kw)
+        server.callback_handler.call_event = call_event
+    if mode == "async_wall":
+        captured["order"] = asyncio.run(drive_async_wall_time(server, case, payloads))
+    elif mode in ("fedavg", "fedbuff", "port", "fedasync", "fedatt", "fedadp", "polaris", "cross_silo", "rl",
+                  "rl_f32"):
         asyncio.run(server._process_reports())
     else:  # pisces: drive the hot path directly (its weights_aggregated needs client selection state)
         weights_received = [u.payload for u in server.updates]
@@ -417,6 +578,10 @@ def run_case(case):
         out["global_grads_i64f_sha256"] = sha(canon(flatten(entries, gg, "i64", torch.float32)))
         out["adaptive_weighting"] = captured["adaptive"]
         out["local_angles"] = {str(c): f32hex(a) for c, a in server.local_angles.items()}
+    if mode in ("cross_silo", "rl", "rl_f32", "async_wall"):
+        out["total_samples"] = server.total_samples
+    if mode == "async_wall":
+        out["updates_order"] = captured["order"]  # client index per position of self.updates
     if mode == "polaris":
         sq = server.squared_deltas_current_round
         out["squared_deltas"] = {str(i): float(sq[i]).hex() for i in range(len(sq)) if sq[i] != 0}
@@ -508,7 +673,33 @@ def cases():
              num_samples=synth.num_samples(3, 25), order=[2, 0, 1]),
         dict(name="C4_port_resnet18_k256", model="resnet18", k=256, seed=13, mode="port",
              num_samples=synth.num_samples(256, 13), staleness=[(7 * i) % 11 for i in range(256)]),
+        dict(name="async_wall_resnet18_k12", model="resnet18", k=12, seed=33, mode="async_wall",
+             num_samples=synth.num_samples(12, 33), current_round=20, minimum_clients=5, staleness_bound=6,
+             finish_times=[7.5, 3.25, 9.0, 1.5, 12.0, 3.25, 6.0, 15.5, 2.75, 11.0, 8.25, 4.0],
+             starting_rounds=[19, 18, 11, 20, 17, 19, 16, 10, 19, 18, 20, 17],
+             arrival_order=[4, 0, 7, 2, 9, 1, 11, 3, 6, 10, 5, 8]),
+        dict(name="cross_silo_resnet18_k6", model="resnet18", k=6, seed=26, mode="cross_silo",
+             num_samples=synth.num_samples(6, 26), order=[4, 1, 0, 5, 2, 3]),
+        dict(name="cross_silo_lenet5_k4_edges", model="lenet5", k=4, seed=27, mode="cross_silo",
+             num_samples=[20000 * 3, 20000 * 2, 20000 * 4, 20000], full=True),
+        dict(name="rl_float64_resnet18_k6", model="resnet18", k=6, seed=28, mode="rl",
+             num_samples=synth.num_samples(6, 28), action=rl_weights(6, 28)),
+        dict(name="rl_float64_lenet5_k5", model="lenet5", k=5, seed=29, mode="rl",
+             num_samples=synth.num_samples(5, 29), action=rl_weights(5, 29), full=True),
+        dict(name="rl_float32_resnet18_k4", model="resnet18", k=4, seed=30, mode="rl_f32",
+             num_samples=synth.num_samples(4, 30), action=rl_weights(4, 30)),
+        dict(name="he_plain_lenet5_k5", model="lenet5", k=5, seed=31, mode="he",
+             num_samples=synth.num_samples(5, 31), encrypt_indices=list(range(0, 61706, 97)), full=True),
+        dict(name="he_plain_resnet18_k3", model="resnet18", k=3, seed=32, mode="he",
+             num_samples=synth.num_samples(3, 32), encrypt_indices=list(range(100, 2000))),
     ]
+
+
+def rl_weights(k, seed):
+    """An RL action: k positive float64 weights summing to ~1 (float.hex for the recipe)."""
+    rng = np.random.default_rng(1000 + seed)
+    w = rng.uniform(0.2, 1.0, k)
+    return [float(v).hex() for v in (w / w.sum())]
 
 
 def run_gan_case(case):
@@ -618,7 +809,8 @@ def main():
         if args.only and case["name"] != args.only:
             continue
         print("case", case["name"], flush=True)
-        out, _ = run_gan_case(case) if case.get("mode") == "gan" else run_case(case)
+        runner = {"gan": run_gan_case, "he": run_he_case}.get(case.get("mode"), run_case)
+        out, _ = runner(case)
         arrays = out.pop("_full", None)
         if arrays:
             for key, arr in arrays.items():

@@ -22,7 +22,13 @@ CANON_NAN = np.uint32(0x7FC00000)
 
 def load_cases():
     with open(os.path.join(GOLDEN, "fedavg_cases.json")) as f:
-        return json.load(f)["cases"]
+        cases = json.load(f)["cases"]
+    for c in cases:
+        # async simulated wall time: the update order is what the reference's
+        # _process_clients produced (heap pops + stale sweep); replay it
+        if c["recipe"].get("mode") == "async_wall":
+            c["recipe"] = dict(c["recipe"], order=c["expected"]["updates_order"])
+    return cases
 
 
 def load_full():
@@ -71,7 +77,7 @@ def weights_for(recipe, impl, similarities=None):
     ns = [recipe["num_samples"][c] for c in order]
     st = [recipe.get("staleness", [0] * recipe["k"])[c] for c in order]
     mode = recipe.get("mode", "fedavg")
-    if mode in ("fedavg", "polaris"):  # Polaris aggregates with plain FedAvg weights
+    if mode in ("fedavg", "polaris", "cross_silo", "async_wall"):  # plain FedAvg weights
         return impl.fedavg(ns), None
     if mode == "fedbuff":
         return impl.fedbuff(len(ns)), None
@@ -117,6 +123,8 @@ def case_size(recipe):
 
 # modes whose weights depend on reductions over the deltas (own tests)
 PER_ENTRY_MODES = ("fedatt", "fedadp")
+# modes with their own arithmetic (float64 weights / vectors): own tests
+OWN_TEST_MODES = ("rl", "rl_f32", "he")
 
 
 def host_state_dicts(recipe):

@@ -157,6 +157,11 @@ def _flat(layout, sd, region):
     ("port_resnet18_k16", "PortServerMixin"),
     ("pisces_resnet18_k8", "PiscesServerMixin"),
     ("lenet5_k7_edge_values", "DeltasAggregationMixin"),
+    # async simulated wall time: updates in the order the reference's _process_clients formed them
+    ("async_wall_resnet18_k12", "FusedAggregationMixin"),
+    # cross-silo (fedavg_cs._process_reports dispatches to the same hooks)
+    ("cross_silo_resnet18_k6", "FusedAggregationMixin"),
+    ("cross_silo_lenet5_k4_edges", "DeltasAggregationMixin"),
 ])
 def test_server_hooks_match_reference(name, mixin):
     """The product's Plato hooks, dispatched like _process_reports (servers/fedavg.py:171-196)."""
@@ -191,7 +196,7 @@ def test_server_hooks_match_reference(name, mixin):
     assert list(updated.keys()) == [e.name for e in layout.entries]
     assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
     assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
-    if recipe.get("mode") in ("fedavg", "port", "pisces", None):
+    if recipe.get("mode") in ("fedavg", "port", "pisces", "cross_silo", "async_wall", None):
         assert server.total_samples == sum(recipe["num_samples"])
 
 
@@ -469,3 +474,58 @@ def test_stage_on_arrival_then_adopt_matches_reference():
     assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
     assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
     assert len(eng._arrivals) == 0  # released after the round
+
+
+RL = [c for c in CASES if c["recipe"].get("mode") in ("rl", "rl_f32")]
+
+
+@pytest.mark.parametrize("case", RL, ids=[c["recipe"]["name"] for c in RL])
+def test_rl_smart_weighting_matches_reference(case):
+    """RLDeltasAggregationMixin == rl_server.RLServer.aggregate_deltas (float64 and float32 actions)."""
+    from plato_amd.servers.variants import RLDeltasAggregationMixin
+
+    recipe, exp = case["recipe"], case["expected"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    updates = _updates(recipe, payloads)
+    dtype = np.float64 if recipe["mode"] == "rl" else np.float32
+
+    class Agent:
+        num_samples = None
+
+        async def prep_agent_update(self):
+            return None
+
+    class Server(RLDeltasAggregationMixin):
+        aggregation_device = DEV
+        agent = Agent()
+
+        def update_state(self):
+            self.state_updated = True
+
+        async def update_action(self):
+            self.smart_weighting = np.array([[float.fromhex(h)] for h in recipe["action"]], dtype=dtype)
+
+    server = Server()
+    deltas = [{n: p[n] - baseline[n] for n in p} for p in [u.payload for u in updates]]
+    avg = asyncio.run(server.aggregate_deltas(updates, deltas))
+    assert server.state_updated and server.agent.num_samples == [u.report.num_samples for u in updates]
+    assert G.sha(G.canon(_flat(layout, avg, "f32"))) == exp["avg_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, avg, "i64"))) == exp["avg_i64f_sha256"]
+    updated = {n: baseline[n] + avg[n] for n in baseline}  # the reference's update_weights
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert server.total_samples == exp["total_samples"]
+
+
+HE = [c for c in CASES if c["recipe"].get("mode") == "he"]
+
+
+@pytest.mark.parametrize("case", HE, ids=[c["recipe"]["name"] for c in HE])
+def test_he_plaintext_half_matches_reference(engine, case):
+    """fedavg_he._fedavg_hybrid's unencrypted sum: float64 vectors, float64 accumulation, on the GPU."""
+    from tests.test_oracle import he_vectors
+
+    recipe, exp = case["recipe"], case["expected"]
+    vecs = he_vectors(recipe)
+    got = engine.weighted_sum(vecs, W.fedavg(recipe["num_samples"]))
+    assert got.dtype == torch.float64 and got.numel() == exp["n_unencrypted"]
+    assert G.sha(np.ascontiguousarray(got.numpy())) == exp["unencrypted_avg_sha256"]

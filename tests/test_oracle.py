@@ -98,7 +98,7 @@ def test_known_answer_reference_fedavg_tests():
 
 
 NON_ASYNC = [c for c in CASES
-             if c["recipe"].get("mode", "fedavg") not in ("fedasync", "gan") + G.PER_ENTRY_MODES]
+             if c["recipe"].get("mode", "fedavg") not in ("fedasync", "gan") + G.PER_ENTRY_MODES + G.OWN_TEST_MODES]
 
 
 @pytest.mark.parametrize("case", NON_ASYNC, ids=_ids(NON_ASYNC))
@@ -200,3 +200,63 @@ def test_oracle_cosine_similarity_matches_reference(name):
             continue
         d = np.concatenate([np.subtract(xs_f[i], bf, dtype=np.float32), (xs_i[i] - bi).astype(np.float32)])
         assert abs(ref.cosine_similarity_fp64(v, d) - float(s)) <= 1e-5
+
+
+RL = [c for c in CASES if c["recipe"].get("mode") in ("rl", "rl_f32")]
+
+
+@pytest.mark.parametrize("case", RL, ids=_ids(RL))
+def test_oracle_rl_smart_weighting(case):
+    """rl_server.py:66-71: float64 action -> float64 arithmetic on fp32 entries, fp32 on int64 entries."""
+    from plato_amd.servers.variants import rl_smart_weights
+
+    recipe, exp = case["recipe"], case["expected"]
+    layout, bf, bi, xs_f, xs_i = _inputs(recipe)
+    action = np.array([[float.fromhex(h)] for h in recipe["action"]],
+                      dtype=np.float64 if recipe["mode"] == "rl" else np.float32)
+    w, w_i, f64 = rl_smart_weights(action, recipe["k"], layout.n_i64 > 0)
+    assert f64 == (recipe["mode"] == "rl")
+    d_f = [np.subtract(x, bf, dtype=np.float32) for x in xs_f]
+    with np.errstate(over="ignore"):
+        d_i = [x - bi for x in xs_i]
+    if f64:
+        avg_f, avg_i = ref.w64_numpy(d_f, d_i, w, w_i)
+    else:
+        avg_f, avg_i = ref.deltas_numpy(d_f, d_i, w)
+    assert G.sha(G.canon(avg_f)) == exp["avg_f32_sha256"]
+    assert G.sha(G.canon(avg_i)) == exp["avg_i64f_sha256"]
+    new_f = np.add(bf, avg_f, dtype=np.float32)
+    new_i = np.add(bi.astype(np.float32), avg_i, dtype=np.float32)
+    assert G.sha(G.canon(new_f)) == exp["updated_f32_sha256"]
+    assert G.sha(ref.trunc_to_int64(new_i)) == exp["loaded_i64_sha256"]
+    assert exp["total_samples"] == sum(recipe["num_samples"])
+
+
+def he_vectors(recipe):
+    """The float64 plaintext vectors homo_enc.encrypt_weights builds (homo_enc.py:50-63)."""
+    layout = __import__("plato_amd.arena", fromlist=["ArenaLayout"]).ArenaLayout.from_shapes(
+        G.model_spec(recipe["model"]))
+    bf, bi = synth.baseline_arena(layout.n_f32, layout.n_i64, recipe["seed"])
+    vecs = []
+    for c in range(recipe["k"]):
+        xf, xi = synth.client_arena(bf, bi, recipe["seed"], c)
+        parts = [(xf if e.region == "f32" else xi)[e.offset:e.offset + e.numel].astype(np.float64)
+                 for e in layout.entries]
+        vecs.append(np.delete(np.concatenate(parts), recipe["encrypt_indices"]))
+    return vecs
+
+
+HE = [c for c in CASES if c["recipe"].get("mode") == "he"]
+
+
+@pytest.mark.parametrize("case", HE, ids=_ids(HE))
+def test_oracle_he_plaintext_is_a_float64_sum(case):
+    """fedavg_he.py:88-98: `fp32 zeros += float64 ndarray * w` falls back to numpy: a float64 sum."""
+    recipe, exp = case["recipe"], case["expected"]
+    vecs = he_vectors(recipe)
+    ws = ref.fedavg_weights(recipe["num_samples"])
+    acc = np.zeros(vecs[0].size, dtype=np.float64)
+    for v, w in zip(vecs, ws):
+        acc = acc + v * w
+    assert exp["dtype"] == "torch.float64" and exp["n_unencrypted"] == acc.size
+    assert G.sha(acc) == exp["unencrypted_avg_sha256"]

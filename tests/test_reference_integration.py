@@ -35,3 +35,7 @@ def test_hook_dispatch_in_reference_process_reports(tmp_path):
         assert ing["payload_matches"] and ing["arena_backed"], mode
         got, exp = ing["comm_overhead_bytes"]
         assert abs(got - exp) <= 2 * 2 * 122 + 64, mode  # storage-key digits only (see test_ingest.py)
+    # the other callers of the hooks, in the reference's own code paths:
+    # fedavg_cs._process_reports, RLServer.aggregate_deltas (mixin), HE _fedavg_hybrid (mixin),
+    # and _process_clients' async simulated-wall-time ordering -> the reference's fixtures
+    assert calls["more"] == {"cross_silo": True, "rl": True, "he": True, "async_order": True, "async_model": True}
