@@ -68,7 +68,7 @@ def _launch(engine, layout, base, slab, order, weights, scales, deltas=False):
 
 
 NON_ASYNC = [c for c in CASES
-             if c["recipe"].get("mode", "fedavg") not in ("fedasync", "gan") + G.PER_ENTRY_MODES
+             if c["recipe"].get("mode", "fedavg") not in ("fedasync", "gan") + G.PER_ENTRY_MODES + G.OWN_TEST_MODES
              and c["recipe"].get("codec") is None]
 BF16 = [c for c in CASES if c["recipe"].get("codec") == "bf16"]
 
@@ -116,7 +116,7 @@ def test_full_arrays_small_cases(engine):
     full = G.load_full()
     for case in CASES:
         recipe = case["recipe"]
-        if not recipe.get("full") or recipe.get("codec") or recipe.get("mode") in G.PER_ENTRY_MODES:
+        if not recipe.get("full") or recipe.get("codec") or recipe.get("mode") in G.PER_ENTRY_MODES + G.OWN_TEST_MODES:
             continue
         layout, base, slab = _device_inputs(recipe)
         weights, scales = G.weights_for(recipe, W, G.reference_similarities(case))
