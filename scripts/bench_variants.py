@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--qsgd-codes", default="qsgd", choices=["qsgd", "uniform"])
     ap.add_argument("--norm-variants", action="store_true", help="also time each entry_norms kernel variant")
     ap.add_argument("--qsgd-variants", action="store_true", help="also time each fedavg_qsgd kernel variant")
+    ap.add_argument("--qsgd-list", default=None, help="comma-separated fedavg_qsgd variants to time (instead of all)")
     ap.add_argument("--norm-order", default="longest", choices=["longest", "layout"],
                     help="entry order of the norms launch (longest first = the engine's)")
     args = ap.parse_args()
@@ -141,8 +142,10 @@ def main():
         "norms": (run_norms, (k + 1) * n_f * 4 + (k + 1) * n_i * 8),
         "fedavg": (run_fedavg, layout.algorithmic_bytes(k)),
     }
-    if args.qsgd_variants:  # tuning: every plato_agg_tune_fedavg_qsgd variant
-        for v in range(_lib.lib().plato_agg_tune_num_qsgd_variants()):
+    if args.qsgd_variants or args.qsgd_list:  # tuning: every (or the listed) plato_agg_tune_fedavg_qsgd variant
+        vlist = ([int(x) for x in args.qsgd_list.split(",")] if args.qsgd_list
+                 else range(_lib.lib().plato_agg_tune_num_qsgd_variants()))
+        for v in vlist:
             kernels[f"qsgd_v{v}"] = ((lambda v=v: run_qsgd(v)), kernels["qsgd"][1])
     if args.norm_variants:  # tuning: every plato_agg_tune_entry_norms variant
         for v in range(14):

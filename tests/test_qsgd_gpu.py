@@ -71,8 +71,8 @@ SPEC = [("a", (3,), "f32"), ("n0", (), "i64"), ("b", (17,), "f32"), ("c", (5, 7)
         ("e", (1000,), "f32"), ("g", (4099,), "f32"), ("h", (2,), "f32"), ("big", (3, 4097), "f32")]
 
 
-@pytest.mark.parametrize("variant", [None, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13])
-@pytest.mark.parametrize("cap,k,two", [(8, 3, False), (20, 9, True), (4096, 17, False), (1 << 20, 5, False)])
+@pytest.mark.parametrize("variant", [None, *range(1, 41), *range(44, 51)])
+@pytest.mark.parametrize("cap,k,two", [(8, 3, False), (20, 9, True), (4096, 17, False), (64, 16, True), (1 << 20, 5, False)])
 def test_qsgd_kernel_matches_oracle(engine, monkeypatch, cap, k, two, variant):
     """Chunk pieces of every alignment (caps 8/20: partial 16-byte groups everywhere;
     2^20: pieces longer than one pass), K not a multiple of the 8-client table batch,
