@@ -274,7 +274,7 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
  *   out = fp32(b + acc)     (int64 entries: fp32(b) + acc)
  * d_codes_* are K device pointers to byte arenas laid out like the fp32 /
  * int64 regions (element e <-> byte e), 16-byte aligned.  Chunk tables as
- * for plato_agg_fedavg_entrywise (pieces of <= 8192 elements run one pass).
+ * for plato_agg_fedavg_entrywise (pieces of <= 4096 elements run one pass).
  */
 int plato_agg_fedavg_qsgd(const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64, int K,
                           const float* d_max_v, int n_entries, float divisor,

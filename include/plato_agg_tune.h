@@ -85,12 +85,15 @@ int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const i
                                size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream);
 
 /* plato_agg_fedavg_qsgd kernel variants, workgroup size x clients per decode-table
- * batch x elements per lane: 0 = 1024x8x8 (plato_agg_fedavg_qsgd), 1 = 256x8x16,
+ * batch x elements per lane: 0 = 512x4x8 pipelined (plato_agg_fedavg_qsgd), 1 = 256x8x16,
  * 2 = 512x16x16, 3 = 256x4x16, 4 = 1024x8x16, 5 = 256x8x8, 6 = 512x8x8,
  * 7 = 128x8x16, 8 = 512x16x8, 9 = 512x8x4, 10 = 512x8x16 (the first default),
- * 11 = 256x16x8, 12 = 1024x16x8, 13 = 1024x4x8; 14-27 the pipelined form
+ * 11 = 256x16x8, 12 = 1024x16x8, 13 = 1024x4x8; 14-26 the pipelined form
  * (double-buffered tables, next batch's codes loaded before the current batch is
- * summed, one barrier per batch) in the shapes listed in qsgd.hip.  plato_agg_tune_qsgd_chunk gives
+ * summed, one barrier per batch), 27 = 1024x8x8 (the round-1 default), 28-35 hybrid
+ * arithmetic/table decode, 36-40 more pipelined shapes, 41-43 timing probes (NOT the
+ * FedAvg: no code loads / no table lookups / neither), 44-50 two-level batching, 51-57
+ * resident tables; shapes listed in qsgd.hip.  plato_agg_tune_qsgd_chunk gives
  * the chunk capacity (elements per workgroup pass) the variant is built for. */
 int plato_agg_tune_num_qsgd_variants(void);
 int plato_agg_tune_qsgd_chunk(int variant);

@@ -42,9 +42,10 @@ typedef __attribute__((address_space(1))) const u1 gu1;
 // Kernel shape (tuning space, plato_agg_tune_fedavg_qsgd): B threads per
 // workgroup share each batch's decode tables, U clients per table batch, G
 // elements per lane (one 16/8/4-byte code load per client).  The default
-// (variant 0) is B = 1024, U = 8, G = 8: 8,192-element chunks as before, but
-// half the per-lane work and twice the waves to cover each batch's code
-// loads, 0.43 -> 0.33 ms on C2-sized inputs.
+// (variant 0) is the pipelined form below at B = 512, U = 4, G = 8 (4,096-element
+// chunks); the round-1 default (B = 1024, U = 8, G = 8, not pipelined) is variant 27.
+// Every shape, pipelined, two-level or resident-table form measured lands within
+// 0.32-0.34 ms on C2-sized inputs; DESIGN.md §11 has the counters and probes.
 constexpr int kG = 16;      // elements per lane group (one 16-byte code load) of the default
 
 template <class T>
@@ -595,6 +596,111 @@ __global__ __launch_bounds__(kBlock) void fedavg_qsgd_tb_kernel(QArgs a) {
   }
 }
 
+// Resident tables: a workgroup decodes the tables of up to kKmax clients into LDS once per chunk (one
+// barrier), then streams every client's codes with no further barrier: no per-batch table build,
+// scalar loads of max_v or s_barrier inside the client loop.  K > kKmax runs in phases of kKmax
+// clients (a barrier and a table build per phase).
+template <int kUr, bool TWO, int kG2>
+__device__ __forceinline__ void rt_step(const QArgs& a, int i0, int iend, bool full, bool have, const Chunk& ch,
+                                        uint64_t e0, const CodeOf<kG2> (&cur)[kUr], CodeOf<kG2> (&nxt)[kUr],
+                                        const float (*tab)[256], const float (&b)[kG2], float (&acc)[kG2]) {
+  const int nu = iend - i0 < kUr ? iend - i0 : kUr;
+  float wu[kUr], su[kUr];
+  load_weights<kUr, TWO>(a, i0, wu, su);
+  if (full && i0 + kUr < iend) load_codes<kUr, kG2>(a, i0 + kUr, iend, e0, nxt);
+  if (full) {
+    sum_batch<kUr, kG2, TWO>(nu, cur, wu, su, tab, b, acc);
+  } else if (have) {
+    for (int u = 0; u < nu; ++u) {
+      const uint8_t* p = sld(a.cf, i0 + u);
+#pragma unroll
+      for (int q = 0; q < kG2; ++q) {
+        const uint64_t e = e0 + q;
+        if (e >= ch.begin && e < ch.end) acc[q] = acc[q] + term(tab[u][p[e]], b[q], wu[u], su[u], TWO);
+      }
+    }
+  }
+}
+
+template <int kBlock, int kUr, bool TWO, int kG2, int kKmax>
+__device__ void qsgd_f32_chunk_rt(const QArgs& a, uint32_t c, float (*lut)[256]) {
+  const Chunk ch = load_chunk(a.tf, c, a.n_f32);
+  const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
+  const uint64_t g0 = ch.begin / kG2, g1 = (uint64_t(ch.end) + kG2 - 1) / kG2;
+  const int K = a.K;
+  for (uint64_t gp = g0; gp < g1; gp += kBlock) {  // one pass for chunks <= kBlock * kG2 elements
+    const uint64_t g = gp + threadIdx.x;
+    const bool have = g < g1;
+    const uint64_t e0 = g * kG2;
+    const bool full = have && e0 >= ch.begin && e0 + kG2 <= ch.end;
+    float b[kG2], acc[kG2];
+#pragma unroll
+    for (int q = 0; q < kG2; ++q) {
+      acc[q] = 0.f;
+      b[q] = 0.f;
+    }
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < kG2 / 4; ++q) {
+        const f4 v = *((gf4*)(a.base_f + e0) + q);
+        b[4 * q] = v.x;
+        b[4 * q + 1] = v.y;
+        b[4 * q + 2] = v.z;
+        b[4 * q + 3] = v.w;
+      }
+    } else if (have) {
+#pragma unroll
+      for (int q = 0; q < kG2; ++q) {
+        const uint64_t e = e0 + q;
+        if (e >= ch.begin && e < ch.end) b[q] = a.base_f[e];
+      }
+    }
+    for (int p0 = 0; p0 < K; p0 += kKmax) {
+      const int pend = K - p0 < kKmax ? K : p0 + kKmax;
+      CodeOf<kG2> ca[kUr], cb[kUr];
+      if (full) load_codes<kUr, kG2>(a, p0, pend, e0, ca);  // in flight during the table build
+      if (gp != g0 || p0) __syncthreads();                 // the previous phase's lookups are done
+      for (int t = threadIdx.x; t < (pend - p0) * 128; t += kBlock) {
+        const int u = __builtin_amdgcn_readfirstlane(t >> 7), z = t & 127;
+        const float v = decode(uint32_t(z), sld(mrow, p0 + u), a.divisor);
+        lut[u][z] = v;
+        lut[u][z + 128] = z ? -v : v;
+      }
+      __syncthreads();
+      for (int i0 = p0; i0 < pend; i0 += 2 * kUr) {
+        rt_step<kUr, TWO, kG2>(a, i0, pend, full, have, ch, e0, ca, cb, &lut[i0 - p0], b, acc);
+        if (i0 + kUr < pend)
+          rt_step<kUr, TWO, kG2>(a, i0 + kUr, pend, full, have, ch, e0, cb, ca, &lut[i0 + kUr - p0], b, acc);
+      }
+    }
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < kG2 / 4; ++q) {
+        const f4 v = f4{b[4 * q] + acc[4 * q], b[4 * q + 1] + acc[4 * q + 1], b[4 * q + 2] + acc[4 * q + 2],
+                        b[4 * q + 3] + acc[4 * q + 3]};
+        __builtin_nontemporal_store(v, (gf4w*)(a.out_f + e0) + q);
+      }
+    } else if (have) {
+#pragma unroll
+      for (int q = 0; q < kG2; ++q) {
+        const uint64_t e = e0 + q;
+        if (e >= ch.begin && e < ch.end) a.out_f[e] = b[q] + acc[q];
+      }
+    }
+  }
+}
+
+template <int kBlock, int kUr, bool TWO, int kGE, int kKmax>
+__global__ __launch_bounds__(kBlock) void fedavg_qsgd_rt_kernel(QArgs a) {
+  __shared__ float lut[kKmax][256];
+  const uint32_t c = blockIdx.x;
+  if (c < a.ncf) {
+    qsgd_f32_chunk_rt<kBlock, kUr, TWO, kGE, kKmax>(a, c, lut);
+  } else {
+    qsgd_i64_chunk<kBlock, TWO>(a, c - a.ncf);
+  }
+}
+
 template <int kBlock, int kU, bool TWO, int kGE, int kWaves, int kA>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(kWaves, 8))) void fedavg_qsgd_pipe_kernel(
     QArgs a) {
@@ -624,6 +730,10 @@ template <int B, int U, bool TWO, int G = kG>
 void launch_q(const QArgs& a, hipStream_t st, uint32_t nc) {
   hipLaunchKernelGGL((fedavg_qsgd_kernel<B, U, TWO, G>), dim3(nc), dim3(B), 0, st, a);
 }
+template <int B, int UR, bool TWO, int G, int KMAX>
+void launch_qr(const QArgs& a, hipStream_t st, uint32_t nc) {
+  hipLaunchKernelGGL((fedavg_qsgd_rt_kernel<B, UR, TWO, G, KMAX>), dim3(nc), dim3(B), 0, st, a);
+}
 template <int B, int UT, int UR, bool TWO, int G>
 void launch_qt(const QArgs& a, hipStream_t st, uint32_t nc) {
   hipLaunchKernelGGL((fedavg_qsgd_tb_kernel<B, UT, UR, TWO, G>), dim3(nc), dim3(B), 0, st, a);
@@ -637,7 +747,7 @@ struct QVariant {
   QFn fn[2];        // [TWO]
 };
 const QVariant kQVariants[] = {
-    {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},  // 0 (default)
+    {512, 4, 8, {&launch_qp<512, 4, false, 8>, &launch_qp<512, 4, true, 8>}},  // 0 (default): pipelined
     {256, 8, 16, {&launch_q<256, 8, false>, &launch_q<256, 8, true>}},      // 1
     {512, 16, 16, {&launch_q<512, 16, false>, &launch_q<512, 16, true>}},   // 2
     {256, 4, 16, {&launch_q<256, 4, false>, &launch_q<256, 4, true>}},      // 3
@@ -666,7 +776,7 @@ const QVariant kQVariants[] = {
     {1024, 8, 4, {&launch_qp<1024, 8, false, 4>, &launch_qp<1024, 8, true, 4>}},          // 24
     {512, 8, 4, {&launch_qp<512, 8, false, 4>, &launch_qp<512, 8, true, 4>}},             // 25
     {1024, 4, 8, {&launch_qp<1024, 4, false, 8>, &launch_qp<1024, 4, true, 8>}},          // 26
-    {512, 4, 8, {&launch_qp<512, 4, false, 8>, &launch_qp<512, 4, true, 8>}},             // 27
+    {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},            // 27 (round-1 default)
     // hybrid decode: last field = elements per lane decoded arithmetically (the rest via the tables)
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 1, 4>, &launch_qp<512, 4, true, 8, 1, 4>}},       // 28
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 1, 2>, &launch_qp<512, 4, true, 8, 1, 2>}},       // 29
@@ -681,7 +791,7 @@ const QVariant kQVariants[] = {
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 7>, &launch_qp<512, 4, true, 8, 7>}},             // 38
     {512, 4, 4, {&launch_qp<512, 4, false, 4>, &launch_qp<512, 4, true, 4>}},                   // 39
     {128, 4, 8, {&launch_qp<128, 4, false, 8>, &launch_qp<128, 4, true, 8>}},                   // 40
-    // timing probes of variant 27 (results are NOT the FedAvg; never a default, not parity-tested):
+    // timing probes of variant 0 (results are NOT the FedAvg; never a default, not parity-tested):
     // 41 without the code loads, 42 without the table lookups, 43 without either
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 1, -1>, &launch_qp<512, 4, true, 8, 1, -1>}},     // 41
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 1, -2>, &launch_qp<512, 4, true, 8, 1, -2>}},     // 42
@@ -694,6 +804,14 @@ const QVariant kQVariants[] = {
     {256, 16, 8, {&launch_qt<256, 16, 4, false, 8>, &launch_qt<256, 16, 4, true, 8>}},          // 48
     {512, 16, 16, {&launch_qt<512, 16, 2, false, 16>, &launch_qt<512, 16, 2, true, 16>}},       // 49
     {512, 32, 8, {&launch_qt<512, 32, 8, false, 8>, &launch_qt<512, 32, 8, true, 8>}},          // 50
+    // resident tables (u = clients per LDS phase), register sub-batches of 4 (55: 8)
+    {1024, 128, 8, {&launch_qr<1024, 4, false, 8, 128>, &launch_qr<1024, 4, true, 8, 128>}},    // 51
+    {1024, 64, 8, {&launch_qr<1024, 4, false, 8, 64>, &launch_qr<1024, 4, true, 8, 64>}},       // 52
+    {1024, 128, 16, {&launch_qr<1024, 4, false, 16, 128>, &launch_qr<1024, 4, true, 16, 128>}}, // 53
+    {512, 32, 8, {&launch_qr<512, 4, false, 8, 32>, &launch_qr<512, 4, true, 8, 32>}},          // 54
+    {1024, 128, 8, {&launch_qr<1024, 8, false, 8, 128>, &launch_qr<1024, 8, true, 8, 128>}},    // 55
+    {512, 64, 8, {&launch_qr<512, 4, false, 8, 64>, &launch_qr<512, 4, true, 8, 64>}},          // 56
+    {256, 32, 8, {&launch_qr<256, 4, false, 8, 32>, &launch_qr<256, 4, true, 8, 32>}},          // 57
 };
 constexpr int kNumQVariants = sizeof(kQVariants) / sizeof(kQVariants[0]);
 
