@@ -57,6 +57,9 @@ def parse():
                    help="also time arrival staging and the trigger-to-result latency (C4, examples/async)")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                    help="strong: one job bucket-sharded over the ranks (+ all-gather); weak: a job per rank")
+    p.add_argument("--pieces", type=int, default=4,
+                   help="strong scaling, N>1: each rank's bucket in this many pieces, the all-gather of "
+                        "piece p running on RCCL's stream while the kernels of the later pieces run")
     p.add_argument("--engine-devices", type=int, default=0,
                    help="single-process multi-GPU engine (plato_amd.multi) over this many devices: host-inclusive "
                         "and device-resident timings of the server's own path (repeats cuda:0 on a 1-GPU box)")
@@ -226,14 +229,18 @@ def main():
     k = args.clients or k_default
     full_layout = ArenaLayout.from_shapes(model_spec(model))
     plan = None
+    pieces = 1
     if scaling == "strong" and world > 1:
-        # one model, parameter-bucket sharded: this rank holds bucket `rank`
-        from plato_amd.distributed import BucketPlan
+        # one model, parameter-bucket sharded and cut into `pieces` round-robin pieces: piece
+        # j = p * world + r belongs to rank r, so the p-th pieces of all ranks are contiguous in
+        # the model and one all-gather per p assembles them in place
+        from plato_amd.distributed import PiecePlan
 
-        plan = BucketPlan.for_layout(full_layout, world)
-        lo, hi = plan.f32_range(rank)
-        a, b = plan.i64_range(rank)
-        layout = ArenaLayout([], hi - lo, b - a)
+        pieces = max(1, args.pieces)
+        plan = PiecePlan.for_layout(full_layout, world, pieces)
+        piece_n = [plan.piece_elements(rank, p) for p in range(pieces)]
+        n_i64_loc = full_layout.n_i64 if rank == 0 else 0
+        layout = ArenaLayout([], pieces * plan.length, n_i64_loc)
         job_bytes = full_layout.algorithmic_bytes(k)
     else:
         layout = full_layout
@@ -267,17 +274,28 @@ def main():
     tf = torch.from_numpy(pf).to(dev)
     ti = torch.from_numpy(pi).to(dev)
     if plan is not None:
-        # the all-gather send buffer holds this rank's result bucket followed by
-        # the int64 entries' results (meaningful on rank 0): one collective
+        # send buffer: [piece 0 | int64 results (meaningful on rank 0) | piece 1 | ... ]; the
+        # all-gather of piece p lands in gathered[goff[p]:], ranks in model order
+        L = plan.length
         ipad = -(-max(full_layout.n_i64, 1) // 64) * 64
-        send = torch.zeros(plan.per + ipad, dtype=torch.float32, device=dev)
-        out_f, out_i = send[: plan.per], send[plan.per:]
-        gathered = torch.empty(world * (plan.per + ipad), dtype=torch.float32, device=dev)
+        send = torch.zeros(pieces * L + ipad, dtype=torch.float32, device=dev)
+        soff = [0] + [L + ipad + (p - 1) * L for p in range(1, pieces)]
+        slen = [L + ipad] + [L] * (pieces - 1)
+        goff = [0] + [world * (L + ipad) + (p - 1) * world * L for p in range(1, pieces)]
+        gathered = torch.empty(world * (pieces * L + ipad), dtype=torch.float32, device=dev)
+        out_i = send[L: L + ipad]
+        # per piece: client-row pointers offset to the piece (rows are pieces * L long)
+        piece_tf = [torch.from_numpy(pf + p * L * 4).to(dev) for p in range(pieces)]
+        piece_lay = [ArenaLayout([], piece_n[p], layout.n_i64 if p == 0 else 0) for p in range(pieces)]
+        out_f = send  # (unused for N>1 beyond the slices below)
     else:
         out_f = torch.empty(layout.row_f32, dtype=torch.float32, device=dev)
         out_i = torch.empty(layout.row_i64, dtype=torch.float32, device=dev)
     stream = torch.cuda.current_stream(dev)
     torch.cuda.synchronize(dev)
+
+    if args.codec == "bf16" and plan is not None:
+        raise SystemExit("--codec bf16 is timed per GPU only (--scaling weak) for --gpus N>1")
 
     def kernel(variant=None):
         if args.codec == "bf16":
@@ -287,26 +305,46 @@ def main():
                       layout.n_f32, layout.n_i64, stream.cuda_stream)
             return
         engine.variant = args.variant if variant is None else variant
-        engine.launch_fedavg(layout, tf, ti, w, None, k, base.f32, base.i64, out_f, out_i, stream)
+        if plan is None:
+            engine.launch_fedavg(layout, tf, ti, w, None, k, base.f32, base.i64, out_f, out_i, stream)
+            return
+        for p in range(pieces):
+            kernel_piece(p)
+            start_gather(p)
 
     rehearsal = world > 1 and os.environ.get("PLATO_BENCH_BACKEND", "nccl") == "gloo"
+    pending = []
+
+    def kernel_piece(p):
+        lay = piece_lay[p]
+        if lay.n_f32 or lay.n_i64:
+            engine.launch_fedavg(lay, piece_tf[p], ti, w, None, k, base.f32[p * L:], base.i64,
+                                 send[soff[p]:], out_i, stream)
+
+    def start_gather(p):
+        """All-gather of piece p: on RCCL's own stream, ordered after the kernels enqueued so far
+        and concurrent with the later pieces' kernels (async_op; waited for in assemble())."""
+        import torch.distributed as dist
+
+        src = send[soff[p]: soff[p] + slen[p]]
+        dst = gathered[goff[p]: goff[p] + world * slen[p]]
+        if rehearsal:  # gloo moves host tensors (ranks sharing one GPU)
+            host = torch.empty(dst.numel(), dtype=torch.float32)
+            dist.all_gather_into_tensor(host, src.cpu())
+            dst.copy_(host)
+        else:  # RCCL over xGMI
+            pending.append(dist.all_gather_into_tensor(dst, src, async_op=True))
 
     def assemble():
-        if plan is not None:
-            import torch.distributed as dist
-
-            if rehearsal:  # gloo moves host tensors (ranks sharing one GPU)
-                host = torch.empty(gathered.numel(), dtype=torch.float32)
-                dist.all_gather_into_tensor(host, send.cpu())
-                gathered.copy_(host)
-            else:  # RCCL over xGMI
-                dist.all_gather_into_tensor(gathered, send)
+        while pending:
+            pending.pop(0).wait()  # the launch stream waits for RCCL's stream
 
     def step(variant=None):
         kernel(variant)
         assemble()
 
-    alg_bytes = layout.algorithmic_bytes(k)
+    alg_bytes = (layout.algorithmic_bytes(k) if plan is None
+                 else sum(lay.algorithmic_bytes(k) for lay in piece_lay))  # this rank's pieces, no padding
     if args.codec == "bf16":  # K bf16 client arenas + fp32 baseline and result
         alg_bytes = k * 2 * (layout.n_f32 + layout.n_i64) + 2 * (layout.n_f32 * 4 + layout.n_i64 * 8)
         job_bytes = (alg_bytes * world if plan is None else
@@ -442,14 +480,15 @@ def main():
                         "(deltas -> weighted sum -> update), inputs resident in HBM; "
                         + ("each rank aggregates its own model-sized job" if scaling == "weak" and world > 1
                            else f"one job bucket-sharded over {world} GPU(s)"
-                           + (", RCCL all-gather of the result buckets inside the timed region" if world > 1
-                              else "")),
+                           + (f", {pieces} pieces per rank, RCCL all-gather of each piece overlapping the "
+                              "later pieces' kernels, all inside the timed region" if world > 1 else "")),
             "clients": k,
             "params_f32_per_gpu": layout.n_f32,
             "params_i64_per_gpu": layout.n_i64,
             "algorithmic_bytes_per_step_per_gpu": alg_bytes,
             "algorithmic_bytes_per_step_job": job_bytes,
             "parallelism": f"bucket{world}",
+            "pieces_per_rank": pieces,
             "kernel_variant": variant,
             "payload_codec": args.codec,
             "kernel_ms_max_over_ranks": round(kernel_ms_max, 4),

@@ -69,6 +69,57 @@ class BucketPlan:
         return (k + 2) * ((hi - lo) * 4 + (b - a) * 8)
 
 
+@dataclass(frozen=True)
+class PiecePlan:
+    """Bucket sharding in round-robin pieces, for an assembly that overlaps the kernels.
+
+    The arena is cut into ``world * pieces`` equal 256-byte-aligned pieces
+    (:class:`BucketPlan` over that many virtual buckets); piece ``j`` belongs to
+    rank ``j % world``.  Rank r keeps its pieces back to back in a local arena
+    (piece p at ``p * length``).  The p-th pieces of all ranks are contiguous
+    in the model, so one all-gather per p lands them in place, and the
+    all-gather of piece p can run while the kernels of pieces p+1.. run.  The
+    int64 entries ride with piece 0 of rank 0.
+    """
+
+    buckets: BucketPlan
+    world: int
+    pieces: int
+
+    @classmethod
+    def make(cls, n_f32: int, n_i64: int, world: int, pieces: int) -> "PiecePlan":
+        if pieces < 1:
+            raise ValueError("pieces must be >= 1")
+        return cls(BucketPlan.make(n_f32, n_i64, world * pieces), world, pieces)
+
+    @classmethod
+    def for_layout(cls, layout: ArenaLayout, world: int, pieces: int) -> "PiecePlan":
+        return cls.make(layout.n_f32, layout.n_i64, world, pieces)
+
+    @property
+    def length(self) -> int:
+        """Padded piece length (elements)."""
+        return self.buckets.per
+
+    def piece_range(self, rank: int, p: int) -> tuple[int, int]:
+        """Model element range of rank's piece p (may be short or empty at the end)."""
+        return self.buckets.f32_range(p * self.world + rank)
+
+    def piece_elements(self, rank: int, p: int) -> int:
+        lo, hi = self.piece_range(rank, p)
+        return hi - lo
+
+    def gather_offset(self, p: int) -> int:
+        """Where the all-gather of the p-th pieces starts in the assembled arena."""
+        return p * self.world * self.length
+
+    def gather_piece(self, p: int, piece: torch.Tensor, full: torch.Tensor, group=None, async_op: bool = False):
+        """All-gather rank pieces p (``length`` elements each) into ``full`` (``world*pieces*length``)."""
+        n = self.world * self.length
+        dst = full[self.gather_offset(p): self.gather_offset(p) + n]
+        return dist.all_gather_into_tensor(dst, piece[: self.length], group=group, async_op=async_op)
+
+
 def gather_buckets(plan: BucketPlan, bucket_f32: torch.Tensor, bucket_i64f: torch.Tensor | None,
                    group=None) -> tuple[torch.Tensor, torch.Tensor]:
     """Assemble the full result on every rank: all-gather of equal padded buckets.

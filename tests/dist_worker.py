@@ -5,6 +5,9 @@ Modes:
                compute (the sequential-K kernel is elementwise, so each
                bucket's result is the oracle on that slice); gathered model
                must equal the single-process oracle bit for bit.
+  cpu-pieces   gloo, CPU: bucket sharding in round-robin pieces (PiecePlan, the
+               strong-scaling bench's layout), one all-gather per piece; the
+               assembled model must equal the single-process oracle bit for bit.
   cpu-client   gloo, CPU: client sharding + reduce_scatter + all_gather;
                max|new - new_seq| / max|new_seq| <= 1e-6.
   gpu-bucket   gloo, every rank on cuda:0: BucketAggregator (HIP kernel) per
@@ -29,7 +32,7 @@ from oracle import fedavg_oracle as ref  # noqa: E402
 from oracle import synth  # noqa: E402
 from plato_amd import workloads  # noqa: E402
 from plato_amd.arena import ArenaLayout  # noqa: E402
-from plato_amd.distributed import (BucketPlan, client_shard, gather_buckets,  # noqa: E402
+from plato_amd.distributed import (BucketPlan, PiecePlan, client_shard, gather_buckets,  # noqa: E402
                                    reduce_scatter_partials)
 
 
@@ -38,6 +41,24 @@ def inputs(spec, k, seed):
     bf, bi = synth.baseline_arena(layout.n_f32, layout.n_i64, seed)
     xs = [synth.client_arena(bf, bi, seed, c) for c in range(k)]
     return layout, bf, bi, [x[0] for x in xs], [x[1] for x in xs]
+
+
+def cpu_pieces(rank, world, out):
+    layout, bf, bi, xs_f, xs_i = inputs(workloads.lenet5(), 6, 23)
+    w = ref.fedavg_weights(synth.num_samples(6, 23))
+    plan = PiecePlan.make(layout.n_f32, layout.n_i64, world, 3)
+    L = plan.length
+    local = torch.zeros(plan.pieces * L, dtype=torch.float32)
+    for p in range(plan.pieces):
+        lo, hi = plan.piece_range(rank, p)
+        got, _ = ref.fedavg_numpy(bf[lo:hi], bi[:0], [x[lo:hi] for x in xs_f], [x[:0] for x in xs_i], w)
+        local[p * L: p * L + (hi - lo)] = torch.from_numpy(got)
+    full = torch.empty(world * plan.pieces * L, dtype=torch.float32)
+    for p in range(plan.pieces):
+        plan.gather_piece(p, local[p * L:], full)
+    exp, _ = ref.fedavg_numpy(bf, bi, xs_f, xs_i, w)
+    out["bit_exact"] = full[: layout.n_f32].numpy().tobytes() == exp.tobytes()
+    out["pieces"], out["length"] = plan.pieces, L
 
 
 def cpu_bucket(rank, world, out):
@@ -132,7 +153,7 @@ def main():
         dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     out = {"rank": rank, "world": world}
-    {"cpu-bucket": cpu_bucket, "cpu-client": cpu_client, "gpu-bucket": gpu_bucket,
+    {"cpu-bucket": cpu_bucket, "cpu-pieces": cpu_pieces, "cpu-client": cpu_client, "gpu-bucket": gpu_bucket,
      "gpu-rccl": gpu_rccl}[mode](rank, world, out)
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
         json.dump(out, f)

@@ -55,6 +55,38 @@ def test_gloo_bucket_sharding_bit_exact(tmp_path):
     assert all(o["bit_exact"] for o in outs)
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_piece_sharding_bit_exact(tmp_path, world):
+    """The strong-scaling bench's layout: round-robin pieces, one all-gather per piece."""
+    outs = _run("cpu-pieces", world, tmp_path)
+    assert all(o["bit_exact"] for o in outs)
+
+
+@pytest.mark.parametrize("n_f32,world,pieces", [(61706, 2, 4), (11183562, 8, 4), (100, 8, 3), (0, 2, 2)])
+def test_piece_plan_covers_arena_once(n_f32, world, pieces):
+    from plato_amd.distributed import PiecePlan
+
+    plan = PiecePlan.make(n_f32, 20, world, pieces)
+    L = plan.length
+    assert L % 64 == 0
+    covered = []
+    for p in range(pieces):
+        for r in range(world):
+            lo, hi = plan.piece_range(r, p)
+            assert hi - lo <= L
+            # in the assembled arena the piece sits where the all-gather of group p puts rank r
+            if hi > lo:
+                assert plan.gather_offset(p) + r * L == lo
+            covered.append((lo, hi))
+    covered.sort()
+    pos = 0
+    for lo, hi in covered:
+        if hi > lo:
+            assert lo == pos
+            pos = hi
+    assert pos == n_f32
+
+
 def test_gloo_client_sharding_normwise(tmp_path):
     outs = _run("cpu-client", 2, tmp_path)
     for o in outs:
