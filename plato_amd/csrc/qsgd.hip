@@ -812,6 +812,9 @@ const QVariant kQVariants[] = {
     {1024, 128, 8, {&launch_qr<1024, 8, false, 8, 128>, &launch_qr<1024, 8, true, 8, 128>}},    // 55
     {512, 64, 8, {&launch_qr<512, 4, false, 8, 64>, &launch_qr<512, 4, true, 8, 64>}},          // 56
     {256, 32, 8, {&launch_qr<256, 4, false, 8, 32>, &launch_qr<256, 4, true, 8, 32>}},          // 57
+    {512, 32, 8, {&launch_qr<512, 8, false, 8, 32>, &launch_qr<512, 8, true, 8, 32>}},          // 58
+    {512, 32, 4, {&launch_qr<512, 16, false, 4, 32>, &launch_qr<512, 16, true, 4, 32>}},        // 59
+    {512, 32, 4, {&launch_qr<512, 8, false, 4, 32>, &launch_qr<512, 8, true, 4, 32>}},          // 60
 };
 constexpr int kNumQVariants = sizeof(kQVariants) / sizeof(kQVariants[0]);
 
