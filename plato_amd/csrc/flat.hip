@@ -72,45 +72,85 @@ __device__ __forceinline__ uint32_t find_segment(const plato_agg_segment* segs, 
 
 constexpr int kFlatPer = 8;  // positions per thread
 
+// One element of a segment (the segment's region / flags and the mode are workgroup-uniform).
+template <int MODE, bool I64, bool NEG>
+__device__ __forceinline__ float flat_value(const FlatArgs& a, const void* xf, const void* xi, uint64_t e) {
+  float v;
+  if (!I64) {
+    const float x = __builtin_nontemporal_load(static_cast<const float*>(xf) + e);
+    v = MODE == PLATO_AGG_FLAT_RAW ? x : x - a.base_f[e];
+    if (NEG) v = (-v) / a.lr;
+  } else if (MODE == PLATO_AGG_FLAT_RAW) {
+    v = static_cast<const float*>(xi)[e];
+    if (NEG) v = (-v) / a.lr;
+  } else if (MODE == PLATO_AGG_FLAT_CAST_DIFF) {
+    // torch.cat casts each int64 entry to fp32 before the subtraction
+    v = float(static_cast<const int64_t*>(xi)[e]) - float(a.base_i[e]);
+    if (NEG) v = (-v) / a.lr;
+  } else {
+    // int64 delta, exact (wrapping) in int64; -delta too, then the cast
+    uint64_t d = uint64_t(static_cast<const int64_t*>(xi)[e]) - uint64_t(a.base_i[e]);
+    v = NEG ? float(int64_t(uint64_t(0) - d)) / a.lr : float(int64_t(d));
+  }
+  return v;
+}
+
+template <int MODE, bool I64, bool NEG>
+__device__ __forceinline__ void flat_range(const FlatArgs& a, const void* xf, const void* xi, float* out,
+                                           uint64_t lo, uint64_t hi, uint64_t shift) {
+  // positions lo..hi-1 of one segment, consecutive positions on consecutive lanes (coalesced),
+  // kFlatPer positions per lane loaded before any is stored (loads in flight, not one at a time)
+  for (uint64_t p0 = lo; p0 < hi; p0 += 256 * kFlatPer) {
+    float v[kFlatPer];
+#pragma unroll
+    for (int u = 0; u < kFlatPer; ++u) {
+      const uint64_t p = p0 + uint64_t(u) * 256 + threadIdx.x;
+      v[u] = p < hi ? flat_value<MODE, I64, NEG>(a, xf, xi, p - shift) : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < kFlatPer; ++u) {
+      const uint64_t p = p0 + uint64_t(u) * 256 + threadIdx.x;
+      if (p < hi) __builtin_nontemporal_store(v[u], out + p);
+    }
+  }
+}
+
+template <int MODE>
+__device__ __forceinline__ void flat_block(const FlatArgs& a, const void* xf, const void* xi, float* out,
+                                           uint64_t b0, uint64_t b1) {
+  // the segments overlapping [b0, b1), one after the other; every branch is workgroup-uniform
+  for (uint32_t s = find_segment(a.segs, a.n_segs, b0); s < a.n_segs; ++s) {
+    const uint64_t fo = a.segs[s].flat_offset;
+    if (fo >= b1) break;
+    const uint64_t so = a.segs[s].src_offset, n = a.segs[s].numel;
+    const uint32_t region = a.segs[s].region, flags = a.segs[s].flags;
+    const uint64_t lo = fo > b0 ? fo : b0, hi = fo + n < b1 ? fo + n : b1;
+    if (lo >= hi) continue;
+    const uint64_t shift = fo - so;  // position p reads source element p - shift (mod 2^64)
+    const bool neg = flags & PLATO_AGG_SEG_NEG_DIV;
+    if (region == 0) {
+      if (neg) flat_range<MODE, false, true>(a, xf, xi, out, lo, hi, shift);
+      else flat_range<MODE, false, false>(a, xf, xi, out, lo, hi, shift);
+    } else {
+      if (neg) flat_range<MODE, true, true>(a, xf, xi, out, lo, hi, shift);
+      else flat_range<MODE, true, false>(a, xf, xi, out, lo, hi, shift);
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void flatten_kernel(FlatArgs a) {
   const int k = blockIdx.y;
   const void* xf = sld(a.src_f, k);
   const void* xi = sld(a.src_i, k);
   float* out = sld(a.out, k);
-  const uint64_t p0 = uint64_t(blockIdx.x) * (256 * kFlatPer) + threadIdx.x;
-  uint32_t s = 0;
-  for (int j = 0; j < kFlatPer; ++j) {
-    const uint64_t p = p0 + uint64_t(j) * 256;
-    if (p >= a.n_flat) return;
-    if (j == 0) {
-      s = find_segment(a.segs, a.n_segs, p);
-    } else {
-      while (s + 1 < a.n_segs && a.segs[s + 1].flat_offset <= p) ++s;
-    }
-    const plato_agg_segment g = a.segs[s];
-    const uint64_t e = g.src_offset + (p - g.flat_offset);
-    float v;
-    if (g.region == 0) {
-      const float x = static_cast<const float*>(xf)[e];
-      v = a.mode == PLATO_AGG_FLAT_RAW ? x : x - a.base_f[e];
-      if (g.flags & PLATO_AGG_SEG_NEG_DIV) v = (-v) / a.lr;
-    } else if (a.mode == PLATO_AGG_FLAT_RAW) {
-      v = static_cast<const float*>(xi)[e];
-      if (g.flags & PLATO_AGG_SEG_NEG_DIV) v = (-v) / a.lr;
-    } else if (a.mode == PLATO_AGG_FLAT_CAST_DIFF) {
-      // torch.cat casts each int64 entry to fp32 before the subtraction
-      v = float(static_cast<const int64_t*>(xi)[e]) - float(a.base_i[e]);
-      if (g.flags & PLATO_AGG_SEG_NEG_DIV) v = (-v) / a.lr;
-    } else {
-      // int64 delta, exact (wrapping) in int64; -delta too, then the cast
-      uint64_t d = uint64_t(static_cast<const int64_t*>(xi)[e]) - uint64_t(a.base_i[e]);
-      if (g.flags & PLATO_AGG_SEG_NEG_DIV) {
-        v = float(int64_t(uint64_t(0) - d)) / a.lr;
-      } else {
-        v = float(int64_t(d));
-      }
-    }
-    out[p] = v;
+  const uint64_t b0 = uint64_t(blockIdx.x) * (256 * kFlatPer);
+  const uint64_t b1 = b0 + 256 * kFlatPer < a.n_flat ? b0 + 256 * kFlatPer : a.n_flat;
+  if (a.mode == PLATO_AGG_FLAT_RAW) {
+    flat_block<PLATO_AGG_FLAT_RAW>(a, xf, xi, out, b0, b1);
+  } else if (a.mode == PLATO_AGG_FLAT_CAST_DIFF) {
+    flat_block<PLATO_AGG_FLAT_CAST_DIFF>(a, xf, xi, out, b0, b1);
+  } else {
+    flat_block<PLATO_AGG_FLAT_DELTA>(a, xf, xi, out, b0, b1);
   }
 }
 
@@ -424,16 +464,8 @@ __global__ void cosine_combine_kernel(CosArgs a, int K) {
 // ((r4+r5)+(r6+r7)), then the rest; else split at n2 = n/2 - (n/2)%8.
 constexpr int kPW = 128;
 
-struct SqSrc {
-  const float* x;
-  const float* b;
-  __device__ __forceinline__ float operator()(uint64_t i) const {
-    const float d = x[i] - b[i];
-    return d * d;
-  }
-};
-
-__device__ float pw_leaf(const SqSrc& v, uint64_t off, uint64_t n) {
+template <class V>
+__device__ float pw_leaf(const V& v, uint64_t off, uint64_t n) {
   if (n < 8) {
     float res = 0.f;
     for (uint64_t i = 0; i < n; ++i) res += v(off + i);
@@ -449,11 +481,22 @@ __device__ float pw_leaf(const SqSrc& v, uint64_t off, uint64_t n) {
   return res;
 }
 
-// The recursion, post-order, on an explicit stack (depth <= 7 for 8192 elements).
-__device__ float pw_sum(const SqSrc& v, uint64_t off, uint64_t n) {
-  uint64_t so[16], sn[16];
-  float sl[16];
-  int stage[16];
+// The recursion, post-order, on an explicit stack (depth <= 7 for 8192 elements);
+// leaf(off, n) gives the value of a leaf (<= kPW elements), visited left to right.
+// The stack lives wherever the caller puts it (registers, or LDS for a single lane).
+struct PwStack {
+  uint32_t* so;
+  uint32_t* sn;
+  float* sl;
+  uint32_t* stage;
+};
+
+template <class Leaf>
+__device__ float pw_walk(const Leaf& leaf, uint32_t off, uint32_t n, PwStack st) {
+  uint32_t* so = st.so;
+  uint32_t* sn = st.sn;
+  float* sl = st.sl;
+  uint32_t* stage = st.stage;
   int sp = 0;
   so[0] = off;
   sn[0] = n;
@@ -462,12 +505,12 @@ __device__ float pw_sum(const SqSrc& v, uint64_t off, uint64_t n) {
   bool have = false;  // `ret` holds the value of the node just finished
   for (;;) {
     if (!have) {
-      if (sn[sp] <= kPW) {
-        ret = pw_leaf(v, so[sp], sn[sp]);
+      if (sn[sp] <= uint32_t(kPW)) {
+        ret = leaf(so[sp], sn[sp]);
         have = true;
         --sp;
       } else {  // descend into the left half
-        uint64_t n2 = sn[sp] / 2;
+        uint32_t n2 = sn[sp] / 2;
         n2 -= n2 % 8;
         so[sp + 1] = so[sp];
         sn[sp + 1] = n2;
@@ -479,7 +522,7 @@ __device__ float pw_sum(const SqSrc& v, uint64_t off, uint64_t n) {
     }
     if (sp < 0) return ret;
     if (stage[sp] == 1) {  // left done: remember it, descend right
-      uint64_t n2 = sn[sp] / 2;
+      uint32_t n2 = sn[sp] / 2;
       n2 -= n2 % 8;
       sl[sp] = ret;
       stage[sp] = 2;
@@ -509,10 +552,17 @@ struct SumsqArgs {
   float* out;                     // [K][n_pieces]
 };
 
-__global__ __launch_bounds__(256) void np_sumsq_chunks_kernel(SumsqArgs a) {
-  const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (t >= uint64_t(a.n_chunks) * uint64_t(a.K)) return;
-  const uint32_t k = uint32_t(t / a.n_chunks), c = uint32_t(t % a.n_chunks);
+// One workgroup per (client, 8192-chunk): the chunk's squared deltas are staged in LDS with
+// coalesced loads (one pad float per 128, so that leaves starting 128 apart sit in different
+// banks).  A full 8192-element chunk is numpy's balanced case: 64 leaves of 128, summed one per
+// lane of wave 0, then combined pairwise by a 6-level xor butterfly (a + b == b + a, so every
+// level adds exactly the tree's left and right halves).  A shorter chunk (the last one of an
+// entry) is walked serially by one lane over the staged values.
+__device__ __forceinline__ uint32_t np_pad(uint64_t e) { return uint32_t(e + e / kPW); }
+
+__global__ __launch_bounds__(256) void np_sumsq_chunks_lds_kernel(SumsqArgs a) {
+  __shared__ float sq[kNpBuf + kNpBuf / kPW];
+  const uint32_t k = blockIdx.x / a.n_chunks, c = blockIdx.x % a.n_chunks;
   uint32_t lo = 0, hi = a.n_pieces;  // the piece holding chunk c
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -521,8 +571,39 @@ __global__ __launch_bounds__(256) void np_sumsq_chunks_kernel(SumsqArgs a) {
   const plato_agg_chunk p = a.pieces[lo];
   const uint64_t begin = uint64_t(p.begin) + uint64_t(c - a.first_chunk[lo]) * kNpBuf;
   const uint64_t end = begin + kNpBuf < uint64_t(p.end) ? begin + kNpBuf : uint64_t(p.end);
-  SqSrc v{a.x[k], a.base};
-  a.chunk_sums[uint64_t(k) * a.n_chunks + c] = pw_sum(v, begin, end - begin);
+  const uint32_t n = uint32_t(end - begin);
+  const float* x = a.x[k] + begin;
+  const float* b = a.base + begin;
+  for (uint32_t i0 = 0; i0 < n; i0 += 256 * 8) {  // 16 loads in flight per lane
+    float xv[8], bv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t i = i0 + u * 256 + threadIdx.x;
+      xv[u] = i < n ? __builtin_nontemporal_load(x + i) : 0.f;
+      bv[u] = i < n ? b[i] : 0.f;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t i = i0 + u * 256 + threadIdx.x;
+      const float d = xv[u] - bv[u];
+      if (i < n) sq[np_pad(i)] = d * d;
+    }
+  }
+  __syncthreads();
+  const auto v = [&](uint64_t e) { return sq[np_pad(e)]; };
+  float* dst = a.chunk_sums + uint64_t(k) * a.n_chunks + c;
+  if (n == kNpBuf) {
+    if (threadIdx.x < 64) {
+      float s = pw_leaf(v, uint64_t(threadIdx.x) * kPW, kPW);
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) s = s + __shfl_xor(s, m);
+      if (threadIdx.x == 0) *dst = s;
+    }
+  } else if (threadIdx.x == 0) {
+    uint32_t so[16], sn[16], stage[16];
+    float sl[16];
+    *dst = pw_walk([&](uint32_t o, uint32_t m) { return pw_leaf(v, o, m); }, 0, n, PwStack{so, sn, sl, stage});
+  }
 }
 
 __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
@@ -563,7 +644,8 @@ int plato_agg_np_sumsq(const float* const* d_x, int K, const float* d_base, cons
   a.out = d_out;
   const uint64_t t1 = uint64_t(n_chunks) * uint64_t(K), t2 = uint64_t(n_pieces) * uint64_t(K);
   if (t1) {
-    hipLaunchKernelGGL(np_sumsq_chunks_kernel, dim3(uint32_t((t1 + 255) / 256)), dim3(256), 0, stream, a);
+    if (t1 > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "too many chunks");
+    hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, dim3(uint32_t(t1)), dim3(256), 0, stream, a);
     if (int rc = check_launch("np_sumsq chunks launch")) return rc;
   }
   hipLaunchKernelGGL(np_sumsq_pieces_kernel, dim3(uint32_t((t2 + 255) / 256)), dim3(256), 0, stream, a);

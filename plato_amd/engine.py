@@ -853,7 +853,7 @@ class AggregationRound:
         return out, stride
 
     def fedadp_dots(self, grads: tuple[torch.Tensor, torch.Tensor], slots: Sequence[int], lr: float,
-                    batch_bytes: float = 4e9):
+                    batch_bytes: float = 32e9):
         """FedAdp's float32 reductions of process_grad's flattened vectors, bit-exact.
 
         ``grads`` is the device global gradient (fp32 arena, fp32 values of the
@@ -879,30 +879,33 @@ class AggregationRound:
         g_flat, stride = self._flatten(_lib.PLATO_AGG_FLAT_RAW, segs, len(order), n_flat, [grads[0].data_ptr()],
                                        [grads[1].data_ptr()], None, lr, stream)
         k = len(slots)
-        inner = torch.empty(k, dtype=torch.float32, device=eng.device)
-        l_sq = torch.empty(k, dtype=torch.float32, device=eng.device)
-        g_sq = torch.empty(1, dtype=torch.float32, device=eng.device)
-        gp = torch.tensor([g_flat.data_ptr()], dtype=torch.int64, device=eng.device)
-        _lib.call("plato_agg_sdot_pairs", gp.data_ptr(), gp.data_ptr(), 1, n_flat, g_sq.data_ptr(), None,
-                  _stream_handle(stream))
+        # row 0: g.g (the global gradient's squared norm), rows 1..k: g.loc_k and loc_k.loc_k.
+        # g.g rides as one more pair of the first batch's launch: each pair is one workgroup
+        # streaming both vectors, so a launch of its own would cost as much as the whole batch.
+        xy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
+        yy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         per = max(1, int(batch_bytes // (stride * 4)))
         base = (_ptr(eng._base.f32), _ptr(eng._base.i64))
-        keep = [gp]
+        keep = []
         for s0 in range(0, k, per):
             part = slots[s0:s0 + per]
             locs, _ = self._flatten(_lib.PLATO_AGG_FLAT_DELTA, segs, len(order), n_flat,
                                     [self._pf[i] for i in part], [self._pi[i] for i in part], base, lr, stream)
-            xs = torch.from_numpy(np.full(len(part), g_flat.data_ptr(), dtype=np.int64)).to(eng.device)
-            ys = torch.from_numpy(np.asarray([locs.data_ptr() + r * stride * 4 for r in range(len(part))],
-                                             dtype=np.int64)).to(eng.device)
-            _lib.call("plato_agg_sdot_pairs", xs.data_ptr(), ys.data_ptr(), len(part), n_flat,
-                      inner.data_ptr() + 4 * s0, l_sq.data_ptr() + 4 * s0, _stream_handle(stream))
+            first = s0 == 0
+            ys_h = ([g_flat.data_ptr()] if first else []) + [locs.data_ptr() + r * stride * 4 for r in range(len(part))]
+            xs = torch.from_numpy(np.full(len(ys_h), g_flat.data_ptr(), dtype=np.int64)).to(eng.device)
+            ys = torch.from_numpy(np.asarray(ys_h, dtype=np.int64)).to(eng.device)
+            row = 0 if first else s0 + 1
+            _lib.call("plato_agg_sdot_pairs", xs.data_ptr(), ys.data_ptr(), len(ys_h), n_flat,
+                      xy.data_ptr() + 4 * row, yy.data_ptr() + 4 * row, _stream_handle(stream))
             keep.append((locs, xs, ys))
             if s0 + per < k:
                 stream.synchronize()  # bound the flat buffers to one batch
-                keep = [gp]
+                keep = []
         stream.synchronize()
-        return inner.cpu().numpy(), g_sq.cpu().numpy()[0], l_sq.cpu().numpy()
+        xy_h, yy_h = xy.cpu().numpy(), yy.cpu().numpy()
+        inner, g_sq, l_sq = xy_h[1:], xy_h[0], yy_h[1:]
+        return inner, g_sq, l_sq
 
     def np_sumsq(self, slots: Sequence[int]) -> np.ndarray:
         """numpy's float32 ``np.sum(np.square(x - b))`` of every fp32 entry, per client, bit-exact.

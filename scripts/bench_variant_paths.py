@@ -1,0 +1,104 @@
+"""Timing of the variant servers' whole-model reductions on C2-sized inputs (K ResNet-18 clients in HBM).
+
+Each path is what the mixin calls, end to end on the device, host sync included:
+
+* port      AggregationRound.model_similarities: flatten (current - previous, K deltas) ->
+            torch-order vector norms (8 serial fma chains over the whole flattened model) ->
+            torch-order cascade cosine sums (examples/async/port/port_server.py:24-52)
+* fedadp    launch_entrywise (global gradient, device) + fedadp_dots: flatten in name order ->
+            OpenBLAS-order sdot pairs (fedadp_server.py:91-99)
+* polaris   np_sumsq: numpy pairwise-order squared deltas per fp32 entry (polaris_server.py:78-81)
+* fedatt    entry_norms: torch-order per-entry norms of every client delta (fedatt_algorithm.py:34-39)
+
+One JSON line per path: median wall ms over --reps after one warm-up, the bytes the path
+reads/writes at minimum, and the serial-chain length that bounds it (the reference's own
+float32 evaluation order).
+
+Usage: python scripts/bench_variant_paths.py [--clients 128] [--reps 5]
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=128)
+    ap.add_argument("--reps", type=int, default=5)
+    args = ap.parse_args()
+
+    from plato_amd import workloads
+    from plato_amd.arena import ArenaLayout
+    from plato_amd.engine import DeviceArena, FedAvgEngine
+    from plato_amd.synthetic import fill_baseline, fill_clients
+
+    dev = torch.device("cuda", 0)
+    k = args.clients
+    layout = ArenaLayout.from_shapes(workloads.resnet(18, 10))
+    engine = FedAvgEngine(dev)
+    base = DeviceArena(layout, dev)
+    fill_baseline(base, 0)
+    n_f, n_i = layout.n_f32, layout.n_i64
+    baseline = layout.unpack(base.f32[:n_f].cpu(), base.i64[:n_i].cpu())
+    prev = DeviceArena(layout, dev)
+    fill_baseline(prev, 1)
+    previous = layout.unpack(prev.f32[:n_f].cpu(), prev.i64[:n_i].cpu())
+    del prev
+    rnd = engine.begin(baseline, k)
+    rnd.put_baseline(baseline)
+    fill_clients(rnd.slab, base, 0, k)  # the round's own slab, filled on the device
+    for s in range(k):
+        pf, pi = rnd.slab.row_pointers([s])
+        rnd._pf[s], rnd._pi[s] = int(pf[0]), int(pi[0])
+        rnd.staged[s] = True
+    torch.cuda.synchronize(dev)
+    slots = list(range(k))
+    n_e = len(layout.entries)
+    longest = max(e.numel for e in layout.entries)
+    client_bytes = k * (n_f * 4 + n_i * 8)
+
+    def fedadp():
+        w = np.full((n_e, k), 1.0 / k)
+        grads = rnd.launch_entrywise(w, add_base=False, device=True)
+        rnd.fedadp_dots(grads, slots, 0.01)
+
+    paths = {
+        "port": (lambda: rnd.model_similarities(previous, slots),
+                 client_bytes + 3 * n_f * 4, (n_f + n_i) // 8,
+                 "flatten + vector_norm (8 fma chains over the flattened model) + cascade cosine sums"),
+        "fedadp": (fedadp, 2 * client_bytes, (n_f + n_i) // 64,
+                   "global gradient + flatten + sdot (64 fma chains over the flattened model)"),
+        "polaris": (lambda: rnd.np_sumsq(slots), client_bytes, 0,
+                    "numpy pairwise sums per entry (8-way unrolled blocks of 128)"),
+        "fedatt": (lambda: rnd.entry_norms(slots), client_bytes, longest // 8,
+                   "per-entry torch norms: 8 fma chains per (entry, client)"),
+    }
+    for name, (fn, nbytes, chain, what) in paths.items():
+        fn()
+        torch.cuda.synchronize(dev)
+        ts = []
+        for _ in range(args.reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        med = statistics.median(ts) * 1e3
+        print(json.dumps({"path": name, "clients": k, "ms_median": round(med, 3), "ms_min": round(min(ts) * 1e3, 3),
+                          "min_bytes": int(nbytes), "GBps_of_min_bytes": round(nbytes / (med * 1e-3) / 1e9, 1),
+                          "serial_chain_steps": int(chain), "what": what}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -94,7 +94,8 @@ def test_np_sumsq_equals_numpy_order():
     from plato_amd.engine import FedAvgEngine
 
     spec = [("conv.a", (7,), "f32"), ("conv.b", (129,), "f32"), ("n", (2,), "i64"), ("conv.c", (8192,), "f32"),
-            ("conv.d", (8193,), "f32"), ("fc", (100003,), "f32"), ("conv.e", (512, 256, 3, 3), "f32")]
+            ("conv.d", (8193,), "f32"), ("fc", (100003,), "f32"), ("conv.e", (512, 256, 3, 3), "f32"),
+            ("s64", (64,), "f32"), ("s1000", (1000,), "f32"), ("s16377", (16377,), "f32"), ("s8191", (8191,), "f32")]
     layout = ArenaLayout.from_shapes(spec)
     rng = np.random.default_rng(4)
     bf = rng.standard_normal(layout.n_f32).astype(np.float32)

@@ -243,6 +243,14 @@ def test_fedadp_server_matches_reference(engine, name):
     g_f, g_i = rnd.launch_entrywise(w1, add_base=False, device=True)
     assert G.sha(G.canon(g_f[: layout.n_f32].cpu().numpy())) == exp["global_grads_f32_sha256"]
     assert G.sha(G.canon(g_i[: layout.n_i64].cpu().numpy())) == exp["global_grads_i64f_sha256"]
+    # the dots in one launch and in batches of 1 and 3 clients (g.g rides with the first batch)
+    whole = rnd.fedadp_dots((g_f, g_i), range(recipe["k"]), 0.01)
+    stride_bytes = -(-(layout.n_f32 + layout.n_i64) // 64) * 64 * 4
+    for per in (1, 3):
+        parts = rnd.fedadp_dots((g_f, g_i), range(recipe["k"]), 0.01, batch_bytes=per * stride_bytes)
+        assert np.asarray(parts[0]).tobytes() == np.asarray(whole[0]).tobytes()
+        assert np.float32(parts[1]).tobytes() == np.float32(whole[1]).tobytes()
+        assert np.asarray(parts[2]).tobytes() == np.asarray(whole[2]).tobytes()
     rnd.launch(ref_w)
     again = rnd.result()
     assert G.sha(G.canon(_flat(layout, again, "f32"))) == exp["updated_f32_sha256"]
