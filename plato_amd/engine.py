@@ -993,8 +993,10 @@ class AggregationRound:
         chunk = torch.from_numpy(np.asarray([[0, 0, n_flat, 0]], dtype=np.uint32).view(np.int32)).to(eng.device)
         norms = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         h = _stream_handle(stream)
+        # the rows are `stride` long (the padding past n_flat is read, never summed): declaring that length keeps the
+        # one n_flat-long piece off the kernel's partial-last-float4 fallback (a per-wave path ~1.5x slower)
         _lib.call("plato_agg_entry_norms_f32", tab.data_ptr(), None, k + 1, None, None, chunk.data_ptr(), 1, None,
-                  0, 1, n_flat, 0, norms.data_ptr(), h)
+                  0, 1, stride, 0, norms.data_ptr(), h)
         ws = torch.empty(max(1, eng.lib.plato_agg_torch_cosine_workspace(k, threads) // 4), dtype=torch.float32,
                          device=eng.device)
         out = torch.empty(k, dtype=torch.float32, device=eng.device)
