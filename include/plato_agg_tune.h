@@ -84,6 +84,15 @@ int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const i
                                const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
                                size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream);
 
+/* plato_agg_sdot_shared kernel variants (pairs per workgroup x chains per
+ * workgroup x 64-element blocks per stage x ring stages x producer waves):
+ * 0 = 4x16x64x6x4, 1 = 2x32x32x8x3, 2 = 8x8x128x4x4,
+ * 3 = 4x16x32x8x5, 4 = 4x16x64x4x2; 5-7 = variants 0-2 with the chain groups of a
+ * pair group on one XCD (one L2); 5 is plato_agg_sdot_shared.  Bitwise identical results. */
+int plato_agg_tune_num_sdot_shared_variants(void);
+int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n,
+                               float* d_workspace, float* d_out_xy, float* d_out_yy, hipStream_t stream);
+
 /* plato_agg_fedavg_qsgd kernel variants, workgroup size x clients per decode-table
  * batch x elements per lane: 0 = 512x4x8 pipelined (plato_agg_fedavg_qsgd), 1 = 256x8x16,
  * 2 = 512x16x16, 3 = 256x4x16, 4 = 1024x8x16, 5 = 256x8x8, 6 = 512x8x8,

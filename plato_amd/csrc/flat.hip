@@ -263,6 +263,267 @@ __global__ __launch_bounds__(kSdotThreads) void sdot_skx_kernel(SdotArgs a) {
   if (a.out_yy) a.out_yy[pair] = float(tyy + kyy);
 }
 
+// ------------------------------------------- sdot, shared x, chains split
+// FedAdp's dots all share one vector (x = the flattened global gradient,
+// fedadp_server.py:95-99): np.inner(g, loc_k) and loc_k . loc_k for every
+// client, g . g once.  sdot_skx_kernel above gives each pair one workgroup,
+// and its tile stream keeps ~32 KiB in flight per CU, so 129 pairs of 45 MB
+// vectors ran at ~21 GB/s per CU (4.2 ms for 128 ResNet-18 clients).
+// Here the 64 chains of sdot_k_SKYLAKEX (chain j sums positions j mod 64,
+// serially over the 64-element blocks) are split over 64 / kC workgroups, and
+// each workgroup runs kC chains for kP pairs that share x: its chain wave holds
+// kP x kC chains (every lane useful), x is read once per workgroup instead of
+// once per pair, and kW producer waves keep kPS - 1 stages of kS blocks in
+// flight by LDS-DMA (global_load_lds_dwordx4, no VGPRs) — ~100 KiB per CU.
+// Measured: 129 pairs of ResNet-18-sized vectors 4.23 -> 2.10 ms; the
+// default keeps a pair group's chain groups on one XCD, since with the groups on
+// different XCDs every 128-byte line was fetched twice (PMC: 12.2 vs 6.2 GB).
+// The chains' partial sums go to a workspace; sdot_finish_kernel applies the
+// fold, the 32-element block, the horizontal sum and the float64 tail exactly
+// as sdot_skx_kernel does, so results are bitwise identical to it.
+typedef __attribute__((address_space(1))) void gvoid;
+typedef __attribute__((address_space(3))) void lvoid;
+
+template <int N>
+__device__ __forceinline__ void sd_wait_vmcnt() {  // s_waitcnt vmcnt(N) only (gfx9 encoding)
+  static_assert(N >= 0 && N < 64, "vmcnt range");
+  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
+}
+
+// One v_fma_f32 (the same instruction __builtin_fmaf selects).  Opaque to the
+// SLP vectorizer, which otherwise packs the x.y and y.y chains into a
+// v_pk_fma_f32 fed by two v_mov per step (~30 cycles per step measured).
+__device__ __forceinline__ float chain_fma(float a, float b, float c) {
+  asm("v_fma_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+  return c;
+}
+
+struct SdotSArgs {
+  const float* x;
+  const float* const* y;
+  uint64_t nsteps;  // whole 64-element blocks
+  float* ws;        // [n_pairs][128]: chain partials of x.y, then of y.y
+  int n_pairs;
+};
+
+template <int kP, int kC, int kS>
+struct SdotShape {
+  static constexpr int kV = 1 + kP;                // vectors per stage: x, y_0 .. y_{kP-1}
+  static constexpr int kRegion = kS * kC + kC;     // floats per vector region; the pad puts
+                                                   // y_p's lanes in distinct banks
+  static constexpr int kStage = kV * kRegion;
+  static constexpr int kStepsPerLd = 256 / kC;     // blocks per 1 KiB LDS-DMA (64 lanes x 16 B)
+  static constexpr int kLdPerVec = kS / kStepsPerLd;
+  static constexpr int kLd = kV * kLdPerVec;       // LDS-DMAs per stage
+  static_assert(kP * kC == 64, "one chain wave: kP pairs x kC chains");
+  static_assert(kS % kStepsPerLd == 0 && kS % 16 == 0, "stage shape");
+};
+
+template <int kP, int kC, int kS, int kPS, int kW, bool kXcd = false>
+__global__ __launch_bounds__(64 * (1 + kW)) void sdot_shared_kernel(SdotSArgs a) {
+  using Sh = SdotShape<kP, kC, kS>;
+  constexpr int kPer = Sh::kLd / kW;  // LDS-DMAs per producer wave per stage
+  static_assert(Sh::kLd % kW == 0, "stage must split evenly over the producer waves");
+  static_assert((kPS - 2) * kPer < 64, "vmcnt range");
+  __shared__ __attribute__((aligned(16))) float ring[kPS * Sh::kStage];
+  constexpr int kGroups = 64 / kC;
+  // kXcd: workgroups are dealt to the 8 XCDs round-robin by blockIdx, so the kGroups chain
+  // groups of a pair group get ids that agree mod 8 — one XCD, one L2 — and each 128-byte
+  // line of y (and x) is fetched from HBM once for all of them, not once per XCD
+  int pg, cg;
+  if (kXcd) {
+    const int b = int(blockIdx.x), lo = b & 7, hi = b / (8 * kGroups);
+    cg = (b / 8) % kGroups;
+    pg = hi * 8 + lo;
+    if (pg * kP >= a.n_pairs) return;  // padding workgroup (before any barrier)
+  } else {
+    pg = int(blockIdx.x) / kGroups;
+    cg = int(blockIdx.x) % kGroups;
+  }
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  const uint64_t nsteps = a.nsteps;
+  const uint64_t nst = (nsteps + kS - 1) / kS;
+  if (wave > 0) {  // producer
+    const int w = wave - 1;
+    const float* src[kPer];
+#pragma unroll
+    for (int r = 0; r < kPer; ++r) {
+      const int v = (w + kW * r) / Sh::kLdPerVec;
+      const int pair = pg * kP + v - 1;
+      src[r] = v == 0 ? a.x : sld(a.y, pair < a.n_pairs ? pair : a.n_pairs - 1);
+    }
+    const uint32_t lofs = uint32_t(cg * kC + (lane % (kC / 4)) * 4);  // float offset inside a block
+    const int lstep = lane / (kC / 4);
+    auto issue = [&](uint64_t st, int slot) {
+#pragma unroll
+      for (int r = 0; r < kPer; ++r) {
+        const int q = w + kW * r;
+        const int v = q / Sh::kLdPerVec, j = q % Sh::kLdPerVec;
+        uint64_t step = st * kS + uint64_t(j * Sh::kStepsPerLd + lstep);
+        step = step < nsteps ? step : nsteps - 1;  // a ragged last stage re-reads a valid block
+        float* dst = ring + slot * Sh::kStage + v * Sh::kRegion + j * Sh::kStepsPerLd * kC;
+        __builtin_amdgcn_global_load_lds((gvoid*)(src[r] + step * 64 + lofs), (lvoid*)dst, 16, 0, 0);
+      }
+    };
+#pragma unroll
+    for (int p = 0; p < kPS - 1; ++p)
+      if (uint64_t(p) < nst) issue(uint64_t(p), p);
+    int slot = 0;  // t mod kPS
+    for (uint64_t t = 0; t < nst; ++t, slot = slot + 1 == kPS ? 0 : slot + 1) {
+      if (t + kPS - 2 < nst) sd_wait_vmcnt<(kPS - 2) * kPer>();  // stage t landed
+      else sd_wait_vmcnt<0>();
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __builtin_amdgcn_s_barrier();  // stage t published; the chain wave is done with stage t - 1
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      if (t + kPS - 1 < nst) issue(t + kPS - 1, slot == 0 ? kPS - 1 : slot - 1);  // into stage t - 1's slot
+    }
+    sd_wait_vmcnt<0>();
+    return;
+  }
+  // chain wave: lane = (pair p of the group, chain c of the workgroup's kC)
+  __builtin_amdgcn_s_setprio(3);
+  const int p = lane / kC, c = lane % kC;
+  float axy = 0.f, ayy = 0.f;
+  int slot = 0;
+  for (uint64_t t = 0; t < nst; ++t, slot = slot + 1 == kPS ? 0 : slot + 1) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const float* X = ring + slot * Sh::kStage + c;
+    const float* Y = ring + slot * Sh::kStage + (1 + p) * Sh::kRegion + c;
+    const uint64_t left = nsteps - t * kS;
+    if (left >= uint64_t(kS)) {
+      // blocks of 16 steps, the next block's reads in flight
+      float xv[16], yv[16], xn[16], yn[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        xv[q] = X[q * kC];
+        yv[q] = Y[q * kC];
+      }
+#pragma unroll
+      for (int blk = 0; blk < kS / 16; ++blk) {
+        if (blk + 1 < kS / 16) {
+#pragma unroll
+          for (int q = 0; q < 16; ++q) {
+            xn[q] = X[(16 * (blk + 1) + q) * kC];
+            yn[q] = Y[(16 * (blk + 1) + q) * kC];
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          axy = chain_fma(xv[q], yv[q], axy);
+          ayy = chain_fma(yv[q], yv[q], ayy);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          xv[q] = xn[q];
+          yv[q] = yn[q];
+        }
+      }
+    } else {
+      for (int s = 0; s < int(left); ++s) {
+        const float xs = X[s * kC], ys = Y[s * kC];
+        axy = chain_fma(xs, ys, axy);
+        ayy = chain_fma(ys, ys, ayy);
+      }
+    }
+  }
+  const int pair = pg * kP + p, chain = cg * kC + c;
+  if (pair < a.n_pairs) {
+    a.ws[uint64_t(pair) * 128 + chain] = axy;
+    a.ws[uint64_t(pair) * 128 + 64 + chain] = ayy;
+  }
+}
+
+// The rest of sdot_k_SKYLAKEX per pair from the 64 chain sums (sdot_skx_kernel's epilogue).
+__global__ __launch_bounds__(64) void sdot_finish_kernel(const float* x, const float* const* ys, uint64_t n,
+                                                         const float* ws, float* out_xy, float* out_yy) {
+  const int pair = blockIdx.x, lane = threadIdx.x & 63;
+  const float* y = sld(ys, pair);
+  const uint64_t n1 = n & ~uint64_t(31);
+  const uint64_t n64 = n1 & ~uint64_t(63);
+  const float axy = ws[uint64_t(pair) * 128 + lane];
+  const float ayy = ws[uint64_t(pair) * 128 + 64 + lane];
+  const float hxy = __shfl(axy, (lane + 8) & 63, 64);
+  const float hyy = __shfl(ayy, (lane + 8) & 63, 64);
+  const int r = lane >> 4, l = lane & 15;
+  float bxy = 0.f, byy = 0.f;
+  if (l < 8) {
+    bxy = axy + hxy;
+    byy = ayy + hyy;
+    if (n1 > n64) {
+      const float xv = x[n64 + 8 * r + l];
+      const float yv = y[n64 + 8 * r + l];
+      bxy = __builtin_fmaf(xv, yv, bxy);
+      byy = __builtin_fmaf(yv, yv, byy);
+    }
+  }
+  const float xy1 = __shfl(bxy, 16 + l, 64), xy2 = __shfl(bxy, 32 + l, 64), xy3 = __shfl(bxy, 48 + l, 64);
+  const float yy1 = __shfl(byy, 16 + l, 64), yy2 = __shfl(byy, 32 + l, 64), yy3 = __shfl(byy, 48 + l, 64);
+  const float sxy = ((bxy + xy1) + xy2) + xy3;
+  const float syy = ((byy + yy1) + yy2) + yy3;
+  const float sxy4 = __shfl(sxy, (lane + 4) & 63, 64);
+  const float syy4 = __shfl(syy, (lane + 4) & 63, 64);
+  const float hx = sxy + sxy4, hy = syy + syy4;
+  const float hx1 = __shfl(hx, 1, 64), hx2 = __shfl(hx, 2, 64), hx3 = __shfl(hx, 3, 64);
+  const float hy1 = __shfl(hy, 1, 64), hy2 = __shfl(hy, 2, 64), hy3 = __shfl(hy, 3, 64);
+  if (lane != 0) return;
+  double kxy = 0.0, kyy = 0.0;
+  if (n1) {
+    kxy = double((hx + hx1) + (hx2 + hx3));
+    kyy = double((hy + hy1) + (hy2 + hy3));
+  }
+  double txy = 0.0, tyy = 0.0;
+  for (uint64_t i = n1; i < n; ++i) {
+    const float xv = x[i], yv = y[i];
+    txy += double(yv * xv);
+    tyy += double(yv * yv);
+  }
+  out_xy[pair] = float(txy + kxy);
+  if (out_yy) out_yy[pair] = float(tyy + kyy);
+}
+
+using SdotSFn = void (*)(const SdotSArgs&, hipStream_t);
+template <int kP, int kC, int kS, int kPS, int kW, bool kXcd = false>
+void launch_sdot_shared(const SdotSArgs& a, hipStream_t st) {
+  uint32_t pgs = uint32_t((a.n_pairs + kP - 1) / kP);
+  if (kXcd) pgs = (pgs + 7) / 8 * 8;
+  const uint32_t groups = pgs * uint32_t(64 / kC);
+  hipLaunchKernelGGL((sdot_shared_kernel<kP, kC, kS, kPS, kW, kXcd>), dim3(groups), dim3(64 * (1 + kW)), 0, st, a);
+}
+// pairs per workgroup x chains per workgroup x blocks per stage x stages x producer waves
+const SdotSFn kSdotSVariants[] = {
+    &launch_sdot_shared<4, 16, 64, 6, 4>,   // 0: 64 B of each block per vector
+    &launch_sdot_shared<2, 32, 32, 8, 3>,   // 1: 128 B per block, x shared by 2 pairs
+    &launch_sdot_shared<8, 8, 128, 4, 4>,   // 2: 32 B per block, x shared by 8 pairs
+    &launch_sdot_shared<4, 16, 32, 8, 5>,   // 3: shorter stages, deeper ring
+    &launch_sdot_shared<4, 16, 64, 4, 2>,   // 4: shallower ring, 2 producers (2 workgroups / CU)
+    &launch_sdot_shared<4, 16, 64, 6, 4, true>,   // 5 (default): variant 0, a pair group's chain groups on one XCD
+    &launch_sdot_shared<2, 32, 32, 8, 3, true>,   // 6: variant 1, likewise
+    &launch_sdot_shared<8, 8, 128, 4, 4, true>,   // 7: variant 2, likewise
+};
+constexpr int kNumSdotSVariants = sizeof(kSdotSVariants) / sizeof(kSdotSVariants[0]);
+
+int run_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n, float* d_ws,
+                    float* d_out_xy, float* d_out_yy, hipStream_t stream) {
+  if (variant < 0 || variant >= kNumSdotSVariants) return set_error(PLATO_AGG_EINVAL, "bad sdot_shared variant");
+  if (n_pairs <= 0) return set_error(PLATO_AGG_EINVAL, "no pairs");
+  if (!d_x || !d_y || !d_out_xy || !d_ws) return set_error(PLATO_AGG_EINVAL, "null pointer");
+  if (reinterpret_cast<uintptr_t>(d_x) & 15u) return set_error(PLATO_AGG_EINVAL, "x must be 16-byte aligned");
+  const uint64_t nsteps = (uint64_t(n) & ~uint64_t(31)) / 64;
+  if (nsteps) {
+    SdotSArgs a{d_x, d_y, nsteps, d_ws, n_pairs};
+    kSdotSVariants[variant](a, stream);
+  } else {
+    (void)hipMemsetAsync(d_ws, 0, size_t(n_pairs) * 128 * sizeof(float), stream);
+  }
+  hipLaunchKernelGGL(sdot_finish_kernel, dim3(uint32_t(n_pairs)), dim3(64), 0, stream, d_x, d_y, uint64_t(n), d_ws,
+                     d_out_xy, d_out_yy);
+  return check_launch("sdot_shared launch");
+}
+
 // ------------------------------------------------- torch cascade sum (cos)
 constexpr int kSumThreads = 256;
 
@@ -687,6 +948,22 @@ int plato_agg_sdot_pairs(const float* const* d_x, const float* const* d_y, int n
   SdotArgs a{d_x, d_y, uint64_t(n), d_out_xy, d_out_yy};
   hipLaunchKernelGGL(sdot_skx_kernel, dim3(uint32_t(n_pairs)), dim3(kSdotThreads), 0, stream, a);
   return check_launch("sdot launch");
+}
+
+size_t plato_agg_sdot_shared_workspace(int n_pairs) {
+  return size_t(n_pairs > 0 ? n_pairs : 0) * 128 * sizeof(float);
+}
+
+int plato_agg_sdot_shared(const float* d_x, const float* const* d_y, int n_pairs, size_t n, float* d_workspace,
+                          float* d_out_xy, float* d_out_yy, hipStream_t stream) {
+  return run_sdot_shared(5, d_x, d_y, n_pairs, n, d_workspace, d_out_xy, d_out_yy, stream);
+}
+
+int plato_agg_tune_num_sdot_shared_variants(void) { return kNumSdotSVariants; }
+
+int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n,
+                               float* d_workspace, float* d_out_xy, float* d_out_yy, hipStream_t stream) {
+  return run_sdot_shared(variant, d_x, d_y, n_pairs, n, d_workspace, d_out_xy, d_out_yy, stream);
 }
 
 size_t plato_agg_torch_cosine_workspace(int K, int threads) {

@@ -861,7 +861,7 @@ class AggregationRound:
         Returns ``(inner[K], g_sq, l_sq[K])`` as numpy float32: ``np.inner(g,
         loc_k)``, ``g.dot(g)``, ``loc_k.dot(loc_k)`` exactly as numpy's OpenBLAS
         forms them (examples/server_aggregation/fedadp/fedadp_server.py:91-99,
-        ``plato_agg_flatten`` + ``plato_agg_sdot_pairs``).
+        ``plato_agg_flatten`` + ``plato_agg_sdot_shared``: every pair shares x = g).
         """
         slots = self._check_slots(slots)
         if not self.has_baseline:
@@ -880,11 +880,13 @@ class AggregationRound:
                                        [grads[1].data_ptr()], None, lr, stream)
         k = len(slots)
         # row 0: g.g (the global gradient's squared norm), rows 1..k: g.loc_k and loc_k.loc_k.
-        # g.g rides as one more pair of the first batch's launch: each pair is one workgroup
-        # streaming both vectors, so a launch of its own would cost as much as the whole batch.
+        # g.g rides as one more pair (g, g) of the first batch's launch: a launch is as long as
+        # its serial chains, so a launch of its own would cost as much as the whole batch.
         xy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         yy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         per = max(1, int(batch_bytes // (stride * 4)))
+        ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(min(k, per) + 1) // 4, dtype=torch.float32,
+                         device=eng.device)
         base = (_ptr(eng._base.f32), _ptr(eng._base.i64))
         keep = []
         for s0 in range(0, k, per):
@@ -893,12 +895,11 @@ class AggregationRound:
                                     [self._pf[i] for i in part], [self._pi[i] for i in part], base, lr, stream)
             first = s0 == 0
             ys_h = ([g_flat.data_ptr()] if first else []) + [locs.data_ptr() + r * stride * 4 for r in range(len(part))]
-            xs = torch.from_numpy(np.full(len(ys_h), g_flat.data_ptr(), dtype=np.int64)).to(eng.device)
             ys = torch.from_numpy(np.asarray(ys_h, dtype=np.int64)).to(eng.device)
             row = 0 if first else s0 + 1
-            _lib.call("plato_agg_sdot_pairs", xs.data_ptr(), ys.data_ptr(), len(ys_h), n_flat,
+            _lib.call("plato_agg_sdot_shared", g_flat.data_ptr(), ys.data_ptr(), len(ys_h), n_flat, ws.data_ptr(),
                       xy.data_ptr() + 4 * row, yy.data_ptr() + 4 * row, _stream_handle(stream))
-            keep.append((locs, xs, ys))
+            keep.append((locs, ys))
             if s0 + per < k:
                 stream.synchronize()  # bound the flat buffers to one batch
                 keep = []

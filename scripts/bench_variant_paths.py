@@ -37,7 +37,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--clients", type=int, default=128)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--sdot", action="store_true",
+                    help="also time the sdot kernels alone on K+1 flat ResNet-18-sized pairs sharing x")
+    ap.add_argument("--sdot-only", action="store_true", help="only the sdot kernels (for PMC passes)")
     args = ap.parse_args()
+    args.sdot = args.sdot or args.sdot_only
 
     from plato_amd import workloads
     from plato_amd.arena import ArenaLayout
@@ -86,6 +90,8 @@ def main():
                    "per-entry torch norms: 8 fma chains per (entry, client)"),
     }
     for name, (fn, nbytes, chain, what) in paths.items():
+        if args.sdot_only:
+            break
         fn()
         torch.cuda.synchronize(dev)
         ts = []
@@ -98,6 +104,49 @@ def main():
         print(json.dumps({"path": name, "clients": k, "ms_median": round(med, 3), "ms_min": round(min(ts) * 1e3, 3),
                           "min_bytes": int(nbytes), "GBps_of_min_bytes": round(nbytes / (med * 1e-3) / 1e9, 1),
                           "serial_chain_steps": int(chain), "what": what}), flush=True)
+    if args.sdot:
+        sdot_kernels(dev, k, n_f + n_i, args.reps)
+
+
+def sdot_kernels(dev, k, n, reps):
+    """plato_agg_sdot_pairs (one workgroup per pair) vs every plato_agg_sdot_shared variant, bitwise compared."""
+    from plato_amd import _lib
+
+    stride = -(-n // 64) * 64
+    x = torch.randn(stride, device=dev)
+    ys = torch.randn((k + 1, stride), device=dev) * 1e-2
+    ys[0] = x
+    py = torch.tensor([ys.data_ptr() + r * stride * 4 for r in range(k + 1)], dtype=torch.int64, device=dev)
+    px = torch.full((k + 1,), x.data_ptr(), dtype=torch.int64, device=dev)
+    ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(k + 1) // 4, device=dev)
+    h = torch.cuda.current_stream(dev).cuda_stream
+    runs = {"pairs": lambda o1, o2: _lib.call("plato_agg_sdot_pairs", px.data_ptr(), py.data_ptr(), k + 1, n,
+                                              o1.data_ptr(), o2.data_ptr(), h)}
+    for v in range(_lib.lib().plato_agg_tune_num_sdot_shared_variants()):
+        runs[f"shared_v{v}"] = (lambda o1, o2, v=v: _lib.call("plato_agg_tune_sdot_shared", v, x.data_ptr(),
+                                                               py.data_ptr(), k + 1, n, ws.data_ptr(), o1.data_ptr(),
+                                                               o2.data_ptr(), h))
+    ref = None
+    for name, fn in runs.items():
+        o1 = torch.empty(k + 1, device=dev)
+        o2 = torch.empty(k + 1, device=dev)
+        fn(o1, o2)
+        torch.cuda.synchronize(dev)
+        got = (o1.cpu().numpy().tobytes(), o2.cpu().numpy().tobytes())
+        ref = ref or got
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn(o1, o2)
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        med = statistics.median(ts)
+        uniq = (k + 1) * n * 4 + n * 4  # every y once + x once
+        print(json.dumps({"sdot": name, "pairs": k + 1, "n": n, "ms_median": round(med, 4),
+                          "ms_min": round(min(ts), 4), "GBps_unique_bytes": round(uniq / (med * 1e-3) / 1e9, 1),
+                          "bitwise_equal_to_pairs": got == ref}), flush=True)
 
 
 if __name__ == "__main__":

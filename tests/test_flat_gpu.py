@@ -47,6 +47,35 @@ def test_sdot_pairs_equal_openblas_order(n):
         assert got_yy[j].tobytes() == R.sdot(ys[j], ys[j]).tobytes(), (n, j)
 
 
+@pytest.mark.parametrize("n", SIZES + [(1 << 20) + 37])
+def test_sdot_shared_equals_openblas_order(n):
+    """The split-chain shared-x kernel (every variant) == OpenBLAS order, 9 pairs (ragged pair groups),
+    one pair being (x, x) as FedAdp's g.g is."""
+    rng = np.random.default_rng(n + 7)
+    x = rng.standard_normal(n).astype(np.float32)
+    ys = [x] + [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(8)]
+    bx, _ = _rows([x])
+    by, py = _rows(ys)
+    k = len(ys)
+    ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(k) // 4, dtype=torch.float32, device=DEV)
+    h = torch.cuda.current_stream().cuda_stream
+    want_xy = [R.sdot(x, y).tobytes() for y in ys]
+    want_yy = [R.sdot(y, y).tobytes() for y in ys]
+    for variant in [None] + list(range(_lib.lib().plato_agg_tune_num_sdot_shared_variants())):
+        out_xy = torch.full((k,), float("nan"), device=DEV)
+        out_yy = torch.full((k,), float("nan"), device=DEV)
+        if variant is None:
+            _lib.call("plato_agg_sdot_shared", bx.data_ptr(), py.data_ptr(), k, n, ws.data_ptr(), out_xy.data_ptr(),
+                      out_yy.data_ptr(), h)
+        else:
+            _lib.call("plato_agg_tune_sdot_shared", variant, bx.data_ptr(), py.data_ptr(), k, n, ws.data_ptr(),
+                      out_xy.data_ptr(), out_yy.data_ptr(), h)
+        got_xy, got_yy = out_xy.cpu().numpy(), out_yy.cpu().numpy()
+        for j in range(k):
+            assert got_xy[j].tobytes() == want_xy[j], (n, variant, j)
+            assert got_yy[j].tobytes() == want_yy[j], (n, variant, j)
+
+
 @pytest.mark.parametrize("n", SIZES + [1 << 20, (1 << 20) + 3])
 def test_norms_and_cosine_sum_equal_torch_order(n):
     rng = np.random.default_rng(n + 1)
