@@ -88,7 +88,9 @@ int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const i
  * workgroup x 64-element blocks per stage x ring stages x producer waves):
  * 0 = 4x16x64x6x4, 1 = 2x32x32x8x3, 2 = 8x8x128x4x4,
  * 3 = 4x16x32x8x5, 4 = 4x16x64x4x2; 5-7 = variants 0-2 with the chain groups of a
- * pair group on one XCD (one L2); 5 is plato_agg_sdot_shared.  Bitwise identical results. */
+ * pair group on one XCD (one L2); 8-11 = 2x16x64x6x4, 1x32x32x8x2, 2x16x64x4x3,
+ * 1x16x64x4x2 on one XCD per pair group (32 / 16 chain lanes per workgroup: more
+ * workgroups); 5 is plato_agg_sdot_shared.  Bitwise identical results. */
 int plato_agg_tune_num_sdot_shared_variants(void);
 int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n,
                                float* d_workspace, float* d_out_xy, float* d_out_yy, hipStream_t stream);
