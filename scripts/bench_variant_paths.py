@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--sdot", action="store_true",
                     help="also time the sdot kernels alone on K+1 flat ResNet-18-sized pairs sharing x")
     ap.add_argument("--sdot-only", action="store_true", help="only the sdot kernels (for PMC passes)")
+    ap.add_argument("--port-norms", action="store_true",
+                    help="time the entry_norms variants on Port's K+1 flattened vectors (one entry each)")
     args = ap.parse_args()
     args.sdot = args.sdot or args.sdot_only
 
@@ -106,6 +108,43 @@ def main():
                           "serial_chain_steps": int(chain), "what": what}), flush=True)
     if args.sdot:
         sdot_kernels(dev, k, n_f + n_i, args.reps)
+    if args.port_norms:
+        port_norms(dev, k, n_f + n_i, args.reps)
+
+
+def port_norms(dev, k, n, reps):
+    """The vector norms of Port's similarity (8 torch-order fma chains over each whole flattened
+    vector) through every producer/consumer entry_norms variant, bitwise compared."""
+    from plato_amd import _lib
+
+    stride = -(-n // 64) * 64
+    rows = torch.randn((k + 1, stride), device=dev) * 1e-2
+    tab = torch.tensor([rows.data_ptr() + r * stride * 4 for r in range(k + 1)], dtype=torch.int64, device=dev)
+    chunk = torch.from_numpy(np.asarray([[0, 0, stride, 0]], dtype=np.uint32).view(np.int32)).to(dev)
+    h = torch.cuda.current_stream(dev).cuda_stream
+    ref = None
+    for v in (12, 9, 10, 11, 13, 0, 6, 7):
+        out = torch.empty(k + 1, device=dev)
+
+        def fn():
+            _lib.call("plato_agg_tune_entry_norms", v, tab.data_ptr(), None, k + 1, None, None, chunk.data_ptr(), 1,
+                      None, 0, 1, stride, 0, out.data_ptr(), h)
+        fn()
+        torch.cuda.synchronize(dev)
+        got = out.cpu().numpy().tobytes()
+        ref = ref or got
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        med = statistics.median(ts)
+        print(json.dumps({"port_norms_variant": v, "vectors": k + 1, "n": stride, "ms_median": round(med, 4),
+                          "cycles_per_step_at_2.4GHz": round(med * 1e-3 * 2.4e9 / (stride // 8), 2),
+                          "bitwise_equal_to_v12": got == ref}), flush=True)
 
 
 def sdot_kernels(dev, k, n, reps):
