@@ -773,9 +773,10 @@ def cpu_baseline(layout, base, slab, k, weights, out_f, out_i, reps, config):
     # time the reference sequence with the host's CPUs as well as torch's
     # default pool; the CPUs this process may use (nproc counts the whole machine)
     avail = cpus_available() or default_threads
+    nproc = os.cpu_count() or avail  # the whole machine (report it too, even past the quota)
     by_threads = {}
     upd = None
-    for threads in sorted({default_threads, avail}):
+    for threads in sorted({default_threads, avail, nproc}):
         progress(f"cpu baseline: {k_s} clients on {threads} threads")
         torch.set_num_threads(threads)
         times = []
@@ -830,6 +831,7 @@ def cpu_baseline(layout, base, slab, k, weights, out_f, out_i, reps, config):
         "cores": threads,
         "by_threads": {str(t): round(layout.algorithmic_bytes(k_s) / v / 1e9, 3) for t, v in by_threads.items()},
         "cpus_available": avail,
+        "nproc": nproc,
         "kind": "port",
         "one_thread": {"value": round(layout.algorithmic_bytes(k1) / statistics.median(t1) / 1e9, 3),
                        "unit": "GB/s", "sample": f"first {k1} clients, median of 2 after 1 warm-up"},
