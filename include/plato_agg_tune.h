@@ -75,9 +75,13 @@ int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n,
  *       512- / 1024-element tiles
  *   11 = variant 9 with the chain wave at s_setprio 3
  *   12 = variant 9 with the chain waves of the entries at least half as long as
- *        the table's first at s_setprio 3, the others at 1 (the default; the
- *        engine passes the table longest first)
- *   13 = variant 12 with those long entries' producer waves at s_setprio 2 */
+ *        the table's first at s_setprio 3, the others at 1 (the engine passes the
+ *        table longest first; the default until round 2)
+ *   13 = variant 12 with those long entries' producer waves at s_setprio 2
+ *   14, 15 = variant 12 with 1,024-element tiles, 4 / 5 stages (15 is the default for
+ *        grids of more than 512 (entry, client) pairs)
+ *   16 = variant 12 with 2,048-element tiles, 3 stages (the default for grids of at most
+ *        512 pairs, e.g. Port's flattened vectors) */
 int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
                                const float* d_base_f32, const int64_t* d_base_i64,
                                const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,

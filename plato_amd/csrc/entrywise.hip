@@ -1123,7 +1123,7 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
               const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_chunk* d_entries_f32,
               uint32_t n_entries_f32, const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  if (variant < 0 || variant > 13) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
+  if (variant < 0 || variant > 16) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (n_entries <= 0 || !d_out) return set_error(PLATO_AGG_EINVAL, "null output / no entries");
   if (n_entries_f32 && (!d_x_f32 || !d_entries_f32)) return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
@@ -1148,15 +1148,16 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
   a.nei = n_entries_i64;
   a.n_entries = uint32_t(n_entries);
   a.K = K;
-  // Variants (include/plato_agg_tune.h): 12 (the default) producer/consumer with
-  // transposed 512-element tiles and the long chains' waves at raised priority,
-  // the fastest on MI355X; 9, 11 the same without / with a flat
+  // Variants (include/plato_agg_tune.h): 15 / 16 (the defaults, by grid size) are
+  // variant 12 with 1,024- / 2,048-element tiles; 12 producer/consumer with
+  // transposed 512-element tiles and the long chains' waves at raised priority
+  // (the round-1 default); 9, 11 the same without / with a flat
   // raised priority; 0 natural tiles; 1 per-wave; 2, 3, 8 LDS-DMA
   // ring with 4 / 1 / 2 clients per workgroup; 4 / 5 variant 8 without the
   // chains / without the loads (timing probes, wrong results); 6, 7
   // producer/consumer with 1024- / 256-element tiles; 9, 10 producer/consumer
   // with transposed d tiles (512 / 1,024 elements).
-  static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2, 0, 0, 0, 0, 0};
+  static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2, 0, 0, 0, 0, 0, 0, 0, 0};
   const int G = kGroup[variant];
   a.probe = variant == 4 ? 1u : variant == 5 ? 2u : 0u;
   if (variant == 0 || variant == 6 || variant == 7 || variant >= 9) {
@@ -1178,6 +1179,17 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
     } else if (variant == 13) {
       if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true, -2>), grid, dim3(128), 0, stream, a);
       else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true, -2>), grid, dim3(128), 0, stream, a);
+    } else if (variant >= 14) {  // 1,024 / 2,048-element transposed tiles at variant 12's priorities
+      if (variant == 14) {
+        if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 4, true, true, -1>), grid, dim3(128), 0, stream, a);
+        else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 4, false, true, -1>), grid, dim3(128), 0, stream, a);
+      } else if (variant == 15) {
+        if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 5, true, true, -1>), grid, dim3(128), 0, stream, a);
+        else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 5, false, true, -1>), grid, dim3(128), 0, stream, a);
+      } else {
+        if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<2048, 3, true, true, -1>), grid, dim3(128), 0, stream, a);
+        else hipLaunchKernelGGL((entry_norms_pc_kernel<2048, 3, false, true, -1>), grid, dim3(128), 0, stream, a);
+      }
     } else if (variant == 10) {
       if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, true, true>), grid, dim3(128), 0, stream, a);
       else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, false, true>), grid, dim3(128), 0, stream, a);
@@ -1223,8 +1235,14 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
                               const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
                               const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
                               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  return run_norms(12, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32, d_entries_i64,
-                   n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
+  // Longer tiles halve the chain wave's barriers and exposed LDS latency per step but take more LDS
+  // per workgroup: 2,048-element tiles (3 stages, 2 workgroups per CU) win when every (entry, client)
+  // workgroup can be resident at once (Port's K + 1 flattened vectors: 4.33 vs 5.22 ms; FedAtt at
+  // K = 4: 0.96 vs 1.12 ms), 1,024-element tiles (5 stages, 3 per CU) on large grids (FedAtt at
+  // K = 128: 1.23 vs 1.37 ms).  DESIGN.md §11.
+  const uint64_t pairs = (uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K > 0 ? K : 0);
+  return run_norms(pairs <= 512 ? 16 : 15, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32,
+                   d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
 }
 
 int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,

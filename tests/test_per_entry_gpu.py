@@ -141,7 +141,7 @@ def test_entry_norm_kernels_agree_bitwise(engine, k, deltas):
         ef, ei = engine._norm_tables(layout)
         n_e = len(layout.entries)
         outs = []
-        for variant in (0, 1, 2, 3, 6, 7, 8, 9, 10, 11, 12, 13):
+        for variant in (0, 1, 2, 3, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16):
             out = torch.full((k * n_e,), float("nan"), device=dev)
             _lib.call("plato_agg_tune_entry_norms", variant, tf.data_ptr(), ti.data_ptr(), k,
                       None if deltas else b_f.data_ptr(), None if deltas else b_i.data_ptr(), ef.data_ptr(),
