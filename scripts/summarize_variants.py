@@ -14,7 +14,7 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = {"qsgd": "fedavg_qsgd_kernel", "entrywise": "fedavg_entrywise_kernel",
+KERNELS = {"qsgd": "fedavg_qsgd_", "entrywise": "fedavg_entrywise_kernel",
            "stats": "entry_stats_partial", "norms": "entry_norms", "fedavg": "fedavg_kernel"}
 
 
