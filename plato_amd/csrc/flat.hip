@@ -59,6 +59,7 @@ struct FlatArgs {
   float lr;
   float* const* out;
   int mode;
+  int K;
 };
 
 __device__ __forceinline__ uint32_t find_segment(const plato_agg_segment* segs, uint32_t n, uint64_t p) {
@@ -71,53 +72,82 @@ __device__ __forceinline__ uint32_t find_segment(const plato_agg_segment* segs, 
 }
 
 constexpr int kFlatPer = 8;  // positions per thread
+constexpr int kFlatK = 8;    // clients per workgroup: the baseline is read once for all of them
+
+// The baseline element of a position (what the delta modes subtract), read once per workgroup.
+struct FlatBase {
+  float f;
+  int64_t i;
+};
+
+template <int MODE, bool I64>
+__device__ __forceinline__ FlatBase flat_base(const FlatArgs& a, uint64_t e) {
+  FlatBase b{0.f, 0};
+  if (MODE != PLATO_AGG_FLAT_RAW) {
+    if (!I64) b.f = a.base_f[e];
+    else b.i = a.base_i[e];
+  }
+  return b;
+}
 
 // One element of a segment (the segment's region / flags and the mode are workgroup-uniform).
 template <int MODE, bool I64, bool NEG>
-__device__ __forceinline__ float flat_value(const FlatArgs& a, const void* xf, const void* xi, uint64_t e) {
+__device__ __forceinline__ float flat_value(const FlatArgs& a, const void* xf, const void* xi, uint64_t e,
+                                            FlatBase b) {
   float v;
   if (!I64) {
     const float x = __builtin_nontemporal_load(static_cast<const float*>(xf) + e);
-    v = MODE == PLATO_AGG_FLAT_RAW ? x : x - a.base_f[e];
+    v = MODE == PLATO_AGG_FLAT_RAW ? x : x - b.f;
     if (NEG) v = (-v) / a.lr;
   } else if (MODE == PLATO_AGG_FLAT_RAW) {
     v = static_cast<const float*>(xi)[e];
     if (NEG) v = (-v) / a.lr;
   } else if (MODE == PLATO_AGG_FLAT_CAST_DIFF) {
     // torch.cat casts each int64 entry to fp32 before the subtraction
-    v = float(static_cast<const int64_t*>(xi)[e]) - float(a.base_i[e]);
+    v = float(static_cast<const int64_t*>(xi)[e]) - float(b.i);
     if (NEG) v = (-v) / a.lr;
   } else {
     // int64 delta, exact (wrapping) in int64; -delta too, then the cast
-    uint64_t d = uint64_t(static_cast<const int64_t*>(xi)[e]) - uint64_t(a.base_i[e]);
+    uint64_t d = uint64_t(static_cast<const int64_t*>(xi)[e]) - uint64_t(b.i);
     v = NEG ? float(int64_t(uint64_t(0) - d)) / a.lr : float(int64_t(d));
   }
   return v;
 }
 
 template <int MODE, bool I64, bool NEG>
-__device__ __forceinline__ void flat_range(const FlatArgs& a, const void* xf, const void* xi, float* out,
-                                           uint64_t lo, uint64_t hi, uint64_t shift) {
+__device__ __forceinline__ void flat_range(const FlatArgs& a, int k0, int nk, uint64_t lo, uint64_t hi,
+                                           uint64_t shift) {
   // positions lo..hi-1 of one segment, consecutive positions on consecutive lanes (coalesced),
-  // kFlatPer positions per lane loaded before any is stored (loads in flight, not one at a time)
+  // kFlatPer positions per lane loaded before any is stored (loads in flight, not one at a time);
+  // the baseline values once, then each of the workgroup's nk clients
   for (uint64_t p0 = lo; p0 < hi; p0 += 256 * kFlatPer) {
-    float v[kFlatPer];
+    FlatBase b[kFlatPer];
 #pragma unroll
     for (int u = 0; u < kFlatPer; ++u) {
       const uint64_t p = p0 + uint64_t(u) * 256 + threadIdx.x;
-      v[u] = p < hi ? flat_value<MODE, I64, NEG>(a, xf, xi, p - shift) : 0.f;
+      b[u] = p < hi ? flat_base<MODE, I64>(a, p - shift) : FlatBase{0.f, 0};
     }
+    for (int kk = 0; kk < nk; ++kk) {
+      const void* xf = sld(a.src_f, k0 + kk);
+      const void* xi = sld(a.src_i, k0 + kk);
+      float* out = sld(a.out, k0 + kk);
+      float v[kFlatPer];
 #pragma unroll
-    for (int u = 0; u < kFlatPer; ++u) {
-      const uint64_t p = p0 + uint64_t(u) * 256 + threadIdx.x;
-      if (p < hi) __builtin_nontemporal_store(v[u], out + p);
+      for (int u = 0; u < kFlatPer; ++u) {
+        const uint64_t p = p0 + uint64_t(u) * 256 + threadIdx.x;
+        v[u] = p < hi ? flat_value<MODE, I64, NEG>(a, xf, xi, p - shift, b[u]) : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < kFlatPer; ++u) {
+        const uint64_t p = p0 + uint64_t(u) * 256 + threadIdx.x;
+        if (p < hi) __builtin_nontemporal_store(v[u], out + p);
+      }
     }
   }
 }
 
 template <int MODE>
-__device__ __forceinline__ void flat_block(const FlatArgs& a, const void* xf, const void* xi, float* out,
-                                           uint64_t b0, uint64_t b1) {
+__device__ __forceinline__ void flat_block(const FlatArgs& a, int k0, int nk, uint64_t b0, uint64_t b1) {
   // the segments overlapping [b0, b1), one after the other; every branch is workgroup-uniform
   for (uint32_t s = find_segment(a.segs, a.n_segs, b0); s < a.n_segs; ++s) {
     const uint64_t fo = a.segs[s].flat_offset;
@@ -129,28 +159,26 @@ __device__ __forceinline__ void flat_block(const FlatArgs& a, const void* xf, co
     const uint64_t shift = fo - so;  // position p reads source element p - shift (mod 2^64)
     const bool neg = flags & PLATO_AGG_SEG_NEG_DIV;
     if (region == 0) {
-      if (neg) flat_range<MODE, false, true>(a, xf, xi, out, lo, hi, shift);
-      else flat_range<MODE, false, false>(a, xf, xi, out, lo, hi, shift);
+      if (neg) flat_range<MODE, false, true>(a, k0, nk, lo, hi, shift);
+      else flat_range<MODE, false, false>(a, k0, nk, lo, hi, shift);
     } else {
-      if (neg) flat_range<MODE, true, true>(a, xf, xi, out, lo, hi, shift);
-      else flat_range<MODE, true, false>(a, xf, xi, out, lo, hi, shift);
+      if (neg) flat_range<MODE, true, true>(a, k0, nk, lo, hi, shift);
+      else flat_range<MODE, true, false>(a, k0, nk, lo, hi, shift);
     }
   }
 }
 
 __global__ __launch_bounds__(256) void flatten_kernel(FlatArgs a) {
-  const int k = blockIdx.y;
-  const void* xf = sld(a.src_f, k);
-  const void* xi = sld(a.src_i, k);
-  float* out = sld(a.out, k);
+  const int k0 = int(blockIdx.y) * kFlatK;
+  const int nk = a.K - k0 < kFlatK ? a.K - k0 : kFlatK;
   const uint64_t b0 = uint64_t(blockIdx.x) * (256 * kFlatPer);
   const uint64_t b1 = b0 + 256 * kFlatPer < a.n_flat ? b0 + 256 * kFlatPer : a.n_flat;
   if (a.mode == PLATO_AGG_FLAT_RAW) {
-    flat_block<PLATO_AGG_FLAT_RAW>(a, xf, xi, out, b0, b1);
+    flat_block<PLATO_AGG_FLAT_RAW>(a, k0, nk, b0, b1);
   } else if (a.mode == PLATO_AGG_FLAT_CAST_DIFF) {
-    flat_block<PLATO_AGG_FLAT_CAST_DIFF>(a, xf, xi, out, b0, b1);
+    flat_block<PLATO_AGG_FLAT_CAST_DIFF>(a, k0, nk, b0, b1);
   } else {
-    flat_block<PLATO_AGG_FLAT_DELTA>(a, xf, xi, out, b0, b1);
+    flat_block<PLATO_AGG_FLAT_DELTA>(a, k0, nk, b0, b1);
   }
 }
 
@@ -943,9 +971,11 @@ int plato_agg_flatten(int mode, const void* const* d_src_f32, const void* const*
   a.lr = lr;
   a.out = d_out;
   a.mode = mode;
+  a.K = K;
   const uint64_t blocks = (uint64_t(n_flat) + 256 * kFlatPer - 1) / (256 * kFlatPer);
   if (blocks > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "vector too long");
-  hipLaunchKernelGGL(flatten_kernel, dim3(uint32_t(blocks), uint32_t(K)), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(flatten_kernel, dim3(uint32_t(blocks), uint32_t((K + kFlatK - 1) / kFlatK)), dim3(256), 0,
+                     stream, a);
   return check_launch("flatten launch");
 }
 

@@ -144,3 +144,67 @@ def test_np_sumsq_equals_numpy_order():
             d = np.subtract(xf[e.offset:e.offset + e.numel], bf[e.offset:e.offset + e.numel], dtype=np.float32)
             assert got[c, e_i].tobytes() == np.sum(np.square(d.reshape(e.shape))).tobytes(), (c, e.name)
             assert got[c, e_i].tobytes() == R.np_sum(np.square(d)).tobytes()
+
+
+@pytest.mark.parametrize("mode", [_lib.PLATO_AGG_FLAT_DELTA, _lib.PLATO_AGG_FLAT_CAST_DIFF, _lib.PLATO_AGG_FLAT_RAW])
+@pytest.mark.parametrize("k", [1, 8, 11])
+def test_flatten_modes_match_numpy(mode, k):
+    """plato_agg_flatten: segments in a permuted order (fp32 and int64 entries, ragged sizes, every
+    source/flat alignment), -1/lr on some segments, client groups of 8 with a ragged last group
+    (the baseline is read once per group): equal to the numpy restatement of torch.cat / FedAdp's
+    process_grad element by element."""
+    rng = np.random.default_rng(100 * mode + k)
+    sizes = [("a", 5, "f32"), ("n0", 1, "i64"), ("b", 4099, "f32"), ("c", 37, "f32"), ("n1", 3, "i64"),
+             ("d", 70001, "f32"), ("e", 2, "f32")]
+    off = {"f32": 0, "i64": 0}
+    ents = []
+    for name, n, reg in sizes:
+        ents.append((name, n, reg, off[reg]))
+        off[reg] += n
+    n_f, n_i = off["f32"], off["i64"]
+    lr = np.float32(0.0137)
+    bf = rng.standard_normal(n_f).astype(np.float32)
+    bi = rng.integers(-2**40, 2**40, n_i)
+    xf = [bf + rng.standard_normal(n_f).astype(np.float32) * 0.1 for _ in range(k)]
+    xi = [bi + rng.integers(-5, 5, n_i) for _ in range(k)]
+    xi_raw = [rng.standard_normal(n_i).astype(np.float32) for _ in range(k)]  # RAW: fp32 values
+    order = list(rng.permutation(len(ents)))
+    rows, flat, want = [], 0, [[] for _ in range(k)]
+    for j, idx in enumerate(order):
+        name, n, reg, so = ents[idx]
+        neg = j % 2 == 1
+        rows.append([flat, so, n, (0 if reg == "f32" else 1) | ((1 if neg else 0) << 32)])
+        flat += n
+        for c in range(k):
+            if reg == "f32":
+                x = xf[c][so:so + n]
+                v = x if mode == _lib.PLATO_AGG_FLAT_RAW else np.subtract(x, bf[so:so + n], dtype=np.float32)
+                if neg:
+                    v = np.divide(-v, lr, dtype=np.float32)
+            elif mode == _lib.PLATO_AGG_FLAT_RAW:
+                v = xi_raw[c][so:so + n]
+                if neg:
+                    v = np.divide(-v, lr, dtype=np.float32)
+            elif mode == _lib.PLATO_AGG_FLAT_CAST_DIFF:
+                v = np.subtract(xi[c][so:so + n].astype(np.float32), bi[so:so + n].astype(np.float32),
+                                dtype=np.float32)
+                if neg:
+                    v = np.divide(-v, lr, dtype=np.float32)
+            else:
+                d = (xi[c][so:so + n] - bi[so:so + n]).astype(np.int64)
+                v = np.divide((-d).astype(np.float32), lr, dtype=np.float32) if neg else d.astype(np.float32)
+            want[c].append(np.asarray(v, dtype=np.float32))
+    segs = torch.from_numpy(np.asarray(rows, dtype=np.uint64).view(np.int64)).to(DEV)
+    stride = -(-flat // 64) * 64
+    out = torch.full((k, stride), float("nan"), device=DEV)
+    src_f = [torch.from_numpy(v).to(DEV) for v in xf]
+    src_i = [torch.from_numpy(v).to(DEV) for v in (xi_raw if mode == _lib.PLATO_AGG_FLAT_RAW else xi)]
+    ptrs = torch.tensor([t.data_ptr() for t in src_f] + [t.data_ptr() for t in src_i] +
+                        [out.data_ptr() + r * stride * 4 for r in range(k)], dtype=torch.int64, device=DEV)
+    b_f, b_i = torch.from_numpy(bf).to(DEV), torch.from_numpy(bi).to(DEV)
+    _lib.call("plato_agg_flatten", mode, ptrs.data_ptr(), ptrs.data_ptr() + 8 * k, k, b_f.data_ptr(), b_i.data_ptr(),
+              segs.data_ptr(), len(rows), flat, float(lr), ptrs.data_ptr() + 16 * k,
+              torch.cuda.current_stream().cuda_stream)
+    got = out.cpu().numpy()[:, :flat]
+    for c in range(k):
+        assert got[c].tobytes() == np.concatenate(want[c]).tobytes(), c
