@@ -55,7 +55,7 @@ def test_gloo_bucket_sharding_bit_exact(tmp_path):
     assert all(o["bit_exact"] for o in outs)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_piece_sharding_bit_exact(tmp_path, world):
     """The strong-scaling bench's layout: round-robin pieces, one all-gather per piece."""
     outs = _run("cpu-pieces", world, tmp_path)
