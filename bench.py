@@ -773,10 +773,12 @@ def cpu_baseline(layout, base, slab, k, weights, out_f, out_i, reps, config):
     # time the reference sequence with the host's CPUs as well as torch's
     # default pool; the CPUs this process may use (nproc counts the whole machine)
     avail = cpus_available() or default_threads
-    nproc = os.cpu_count() or avail  # the whole machine (report it too, even past the quota)
+    # nproc counts the whole machine; a pool that size under the job's CPU quota oversubscribes it
+    # (a 256-thread pass on a 16-CPU quota ran for minutes), so it is reported, not timed
+    nproc = os.cpu_count() or avail
     by_threads = {}
     upd = None
-    for threads in sorted({default_threads, avail, nproc}):
+    for threads in sorted({default_threads, avail}):
         progress(f"cpu baseline: {k_s} clients on {threads} threads")
         torch.set_num_threads(threads)
         times = []
