@@ -377,14 +377,15 @@ int plato_agg_sdot_pairs(const float* const* d_x, const float* const* d_y, int n
 /*
  * The same sdot_k_SKYLAKEX results (bitwise equal to plato_agg_sdot_pairs) for
  * pairs that share x: FedAdp's np.inner(g, loc_k) and loc_k . loc_k for every
- * client, and g . g as a pair (g, g) (fedadp_server.py:91-99).  The 64 chains
- * are split over workgroups and each workgroup reads x once for several pairs;
- * d_workspace holds plato_agg_sdot_shared_workspace(n_pairs) bytes of chain
- * partials.  x 16-byte aligned; y rows any float alignment.
+ * client (fedadp_server.py:91-99); with with_xx = 1 also g . g, written to
+ * d_out_xy[n_pairs] and d_out_yy[n_pairs].  The 64 chains are split over
+ * workgroups and each workgroup reads x once for its pairs; d_workspace holds
+ * plato_agg_sdot_shared_workspace(n_pairs, with_xx) bytes of chain partials.
+ * x 16-byte aligned; y rows any float alignment.
  */
-size_t plato_agg_sdot_shared_workspace(int n_pairs);
-int plato_agg_sdot_shared(const float* d_x, const float* const* d_y, int n_pairs, size_t n, float* d_workspace,
-                          float* d_out_xy, float* d_out_yy, hipStream_t stream);
+size_t plato_agg_sdot_shared_workspace(int n_pairs, int with_xx);
+int plato_agg_sdot_shared(const float* d_x, const float* const* d_y, int n_pairs, size_t n, int with_xx,
+                          float* d_workspace, float* d_out_xy, float* d_out_yy, hipStream_t stream);
 
 /*
  * The sum in Port's F.cosine_similarity(a, b_k, dim=0) (port_server.py:50),

@@ -94,10 +94,12 @@ int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const i
  * 3 = 4x16x32x8x5, 4 = 4x16x64x4x2; 5-7 = variants 0-2 with the chain groups of a
  * pair group on one XCD (one L2); 8-11 = 2x16x64x6x4, 1x32x32x8x2, 2x16x64x4x3,
  * 1x16x64x4x2 on one XCD per pair group (32 / 16 chain lanes per workgroup: more
- * workgroups); 5 is plato_agg_sdot_shared.  Bitwise identical results. */
+ * workgroups).  plato_agg_sdot_shared runs 8 (with_xx, <= 128 pairs), 11 (with_xx,
+ * <= 64 pairs) or 5.  Bitwise identical results. */
 int plato_agg_tune_num_sdot_shared_variants(void);
 int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n,
-                               float* d_workspace, float* d_out_xy, float* d_out_yy, hipStream_t stream);
+                               int with_xx, float* d_workspace, float* d_out_xy, float* d_out_yy,
+                               hipStream_t stream);
 
 /* plato_agg_fedavg_qsgd kernel variants, workgroup size x clients per decode-table
  * batch x elements per lane: 0 = 512x4x8 pipelined (plato_agg_fedavg_qsgd), 1 = 256x8x16,

@@ -115,9 +115,9 @@ SIGNATURES = {
          _c_float, _c_void_p, _c_void_p],
     ),
     "plato_agg_sdot_pairs": (_c_int, [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p, _c_void_p, _c_void_p]),
-    "plato_agg_sdot_shared_workspace": (_c_size_t, [_c_int]),
+    "plato_agg_sdot_shared_workspace": (_c_size_t, [_c_int, _c_int]),
     "plato_agg_sdot_shared": (
-        _c_int, [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+        _c_int, [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "plato_agg_torch_cosine_workspace": (_c_size_t, [_c_int, _c_int]),
     "plato_agg_torch_cosine_sum": (
         _c_int,
@@ -160,7 +160,8 @@ SIGNATURES = {
     ),
     "plato_agg_tune_num_sdot_shared_variants": (_c_int, []),
     "plato_agg_tune_sdot_shared": (
-        _c_int, [_c_int, _c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+        _c_int, [_c_int, _c_void_p, _c_void_p, _c_int, _c_size_t, _c_int, _c_void_p, _c_void_p, _c_void_p,
+                 _c_void_p]),
     "plato_agg_tune_entry_norms": (
         _c_int,
         [_c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_void_p,

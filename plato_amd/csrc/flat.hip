@@ -330,8 +330,9 @@ struct SdotSArgs {
   const float* x;
   const float* const* y;
   uint64_t nsteps;  // whole 64-element blocks
-  float* ws;        // [n_pairs][128]: chain partials of x.y, then of y.y
+  float* ws;        // [n_pairs + with_xx][128]: chain partials of x.y, then of y.y
   int n_pairs;
+  int with_xx;      // also x.x, as a virtual pair (x, x) after the last pair
 };
 
 template <int kP, int kC, int kS>
@@ -348,7 +349,7 @@ struct SdotShape {
   static_assert(kS % kStepsPerLd == 0 && kS % 16 == 0, "stage shape");
 };
 
-template <int kP, int kC, int kS, int kPS, int kW, bool kXcd = false>
+template <int kP, int kC, int kS, int kPS, int kW, bool kXcd = false, bool kXX = false>
 __global__ __launch_bounds__(64 * (1 + kW)) void sdot_shared_kernel(SdotSArgs a) {
   using Sh = SdotShape<kP, kC, kS>;
   constexpr int kPer = Sh::kLd / kW;  // LDS-DMAs per producer wave per stage
@@ -414,7 +415,7 @@ __global__ __launch_bounds__(64 * (1 + kW)) void sdot_shared_kernel(SdotSArgs a)
   // a CU's LDS-DMA stream tops out near 12 B/clk, MI355X_MICROARCH.md)
   __builtin_amdgcn_s_setprio(3);
   const int p = (lane % Sh::kL) / kC, c = lane % kC;
-  float axy = 0.f, ayy = 0.f;
+  float axy = 0.f, ayy = 0.f, axx = 0.f;  // kXX: every chain wave also runs x.x (x is in LDS anyway)
   int slot = 0;
   for (uint64_t t = 0; t < nst; ++t, slot = slot + 1 == kPS ? 0 : slot + 1) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
@@ -445,6 +446,7 @@ __global__ __launch_bounds__(64 * (1 + kW)) void sdot_shared_kernel(SdotSArgs a)
         for (int q = 0; q < 16; ++q) {
           axy = chain_fma(xv[q], yv[q], axy);
           ayy = chain_fma(yv[q], yv[q], ayy);
+          if (kXX) axx = chain_fma(xv[q], xv[q], axx);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -458,6 +460,7 @@ __global__ __launch_bounds__(64 * (1 + kW)) void sdot_shared_kernel(SdotSArgs a)
         const float xs = X[s * kC], ys = Y[s * kC];
         axy = chain_fma(xs, ys, axy);
         ayy = chain_fma(ys, ys, ayy);
+        if (kXX) axx = chain_fma(xs, xs, axx);
       }
     }
   }
@@ -466,13 +469,17 @@ __global__ __launch_bounds__(64 * (1 + kW)) void sdot_shared_kernel(SdotSArgs a)
     a.ws[uint64_t(pair) * 128 + chain] = axy;
     a.ws[uint64_t(pair) * 128 + 64 + chain] = ayy;
   }
+  if (kXX && pg == 0 && lane < kC) {  // the virtual pair (x, x): its x.y and y.y chains are both x.x
+    a.ws[uint64_t(a.n_pairs) * 128 + chain] = axx;
+    a.ws[uint64_t(a.n_pairs) * 128 + 64 + chain] = axx;
+  }
 }
 
 // The rest of sdot_k_SKYLAKEX per pair from the 64 chain sums (sdot_skx_kernel's epilogue).
-__global__ __launch_bounds__(64) void sdot_finish_kernel(const float* x, const float* const* ys, uint64_t n,
-                                                         const float* ws, float* out_xy, float* out_yy) {
+__global__ __launch_bounds__(64) void sdot_finish_kernel(const float* x, const float* const* ys, int n_pairs,
+                                                         uint64_t n, const float* ws, float* out_xy, float* out_yy) {
   const int pair = blockIdx.x, lane = threadIdx.x & 63;
-  const float* y = sld(ys, pair);
+  const float* y = pair < n_pairs ? sld(ys, pair) : x;  // pair n_pairs: the virtual (x, x)
   const uint64_t n1 = n & ~uint64_t(31);
   const uint64_t n64 = n1 & ~uint64_t(63);
   const float axy = ws[uint64_t(pair) * 128 + lane];
@@ -522,7 +529,12 @@ void launch_sdot_shared(const SdotSArgs& a, hipStream_t st) {
   uint32_t pgs = uint32_t((a.n_pairs + kP - 1) / kP);
   if (kXcd) pgs = (pgs + 7) / 8 * 8;
   const uint32_t groups = pgs * uint32_t(64 / kC);
-  hipLaunchKernelGGL((sdot_shared_kernel<kP, kC, kS, kPS, kW, kXcd>), dim3(groups), dim3(64 * (1 + kW)), 0, st, a);
+  if (a.with_xx)
+    hipLaunchKernelGGL((sdot_shared_kernel<kP, kC, kS, kPS, kW, kXcd, true>), dim3(groups), dim3(64 * (1 + kW)), 0,
+                       st, a);
+  else
+    hipLaunchKernelGGL((sdot_shared_kernel<kP, kC, kS, kPS, kW, kXcd, false>), dim3(groups), dim3(64 * (1 + kW)), 0,
+                       st, a);
 }
 // pairs per workgroup x chains per workgroup x blocks per stage x stages x producer waves
 const SdotSFn kSdotSVariants[] = {
@@ -531,10 +543,11 @@ const SdotSFn kSdotSVariants[] = {
     &launch_sdot_shared<8, 8, 128, 4, 4>,   // 2: 32 B per block, x shared by 8 pairs
     &launch_sdot_shared<4, 16, 32, 8, 5>,   // 3: shorter stages, deeper ring
     &launch_sdot_shared<4, 16, 64, 4, 2>,   // 4: shallower ring, 2 producers (2 workgroups / CU)
-    &launch_sdot_shared<4, 16, 64, 6, 4, true>,   // 5 (default): variant 0, a pair group's chain groups on one XCD
+    &launch_sdot_shared<4, 16, 64, 6, 4, true>,   // 5: variant 0, a pair group's chain groups on one XCD
     &launch_sdot_shared<2, 32, 32, 8, 3, true>,   // 6: variant 1, likewise
     &launch_sdot_shared<8, 8, 128, 4, 4, true>,   // 7: variant 2, likewise
     // half / quarter chain waves: twice / four times the workgroups, all 256 CUs streaming
+    // (default_sdot_variant picks 8 / 11 when x.x rides along and the workgroups fit the CUs)
     &launch_sdot_shared<2, 16, 64, 6, 4, true>,   // 8
     &launch_sdot_shared<1, 32, 32, 8, 2, true>,   // 9
     &launch_sdot_shared<2, 16, 64, 4, 3, true>,   // 10
@@ -542,21 +555,32 @@ const SdotSFn kSdotSVariants[] = {
 };
 constexpr int kNumSdotSVariants = sizeof(kSdotSVariants) / sizeof(kSdotSVariants[0]);
 
-int run_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n, float* d_ws,
-                    float* d_out_xy, float* d_out_yy, hipStream_t stream) {
-  if (variant < 0 || variant >= kNumSdotSVariants) return set_error(PLATO_AGG_EINVAL, "bad sdot_shared variant");
+// The default by size: with x.x folded in, as many workgroups as CUs when the pairs allow it (a CU's
+// stream, ~24 GB/s, is what bounds a workgroup): 128 pairs -> 2 pairs x 16 chains per workgroup,
+// 64 x 4 = 256 workgroups; otherwise variant 5.
+int default_sdot_variant(int n_pairs, int with_xx) {
+  if (with_xx && n_pairs <= 64) return 11;
+  if (with_xx && n_pairs <= 128) return 8;
+  return 5;
+}
+
+int run_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n, int with_xx,
+                    float* d_ws, float* d_out_xy, float* d_out_yy, hipStream_t stream) {
+  if (variant < 0) variant = default_sdot_variant(n_pairs, with_xx);
+  if (variant >= kNumSdotSVariants) return set_error(PLATO_AGG_EINVAL, "bad sdot_shared variant");
   if (n_pairs <= 0) return set_error(PLATO_AGG_EINVAL, "no pairs");
+  if (with_xx != 0 && with_xx != 1) return set_error(PLATO_AGG_EINVAL, "with_xx must be 0 or 1");
   if (!d_x || !d_y || !d_out_xy || !d_ws) return set_error(PLATO_AGG_EINVAL, "null pointer");
   if (reinterpret_cast<uintptr_t>(d_x) & 15u) return set_error(PLATO_AGG_EINVAL, "x must be 16-byte aligned");
   const uint64_t nsteps = (uint64_t(n) & ~uint64_t(31)) / 64;
   if (nsteps) {
-    SdotSArgs a{d_x, d_y, nsteps, d_ws, n_pairs};
+    SdotSArgs a{d_x, d_y, nsteps, d_ws, n_pairs, with_xx};
     kSdotSVariants[variant](a, stream);
   } else {
-    (void)hipMemsetAsync(d_ws, 0, size_t(n_pairs) * 128 * sizeof(float), stream);
+    (void)hipMemsetAsync(d_ws, 0, size_t(n_pairs + with_xx) * 128 * sizeof(float), stream);
   }
-  hipLaunchKernelGGL(sdot_finish_kernel, dim3(uint32_t(n_pairs)), dim3(64), 0, stream, d_x, d_y, uint64_t(n), d_ws,
-                     d_out_xy, d_out_yy);
+  hipLaunchKernelGGL(sdot_finish_kernel, dim3(uint32_t(n_pairs + with_xx)), dim3(64), 0, stream, d_x, d_y, n_pairs,
+                     uint64_t(n), d_ws, d_out_xy, d_out_yy);
   return check_launch("sdot_shared launch");
 }
 
@@ -988,20 +1012,22 @@ int plato_agg_sdot_pairs(const float* const* d_x, const float* const* d_y, int n
   return check_launch("sdot launch");
 }
 
-size_t plato_agg_sdot_shared_workspace(int n_pairs) {
-  return size_t(n_pairs > 0 ? n_pairs : 0) * 128 * sizeof(float);
+size_t plato_agg_sdot_shared_workspace(int n_pairs, int with_xx) {
+  return size_t(n_pairs > 0 ? n_pairs : 0) * 128 * sizeof(float) + (with_xx ? 128 * sizeof(float) : 0);
 }
 
-int plato_agg_sdot_shared(const float* d_x, const float* const* d_y, int n_pairs, size_t n, float* d_workspace,
-                          float* d_out_xy, float* d_out_yy, hipStream_t stream) {
-  return run_sdot_shared(5, d_x, d_y, n_pairs, n, d_workspace, d_out_xy, d_out_yy, stream);
+int plato_agg_sdot_shared(const float* d_x, const float* const* d_y, int n_pairs, size_t n, int with_xx,
+                          float* d_workspace, float* d_out_xy, float* d_out_yy, hipStream_t stream) {
+  return run_sdot_shared(-1, d_x, d_y, n_pairs, n, with_xx, d_workspace, d_out_xy, d_out_yy, stream);
 }
 
 int plato_agg_tune_num_sdot_shared_variants(void) { return kNumSdotSVariants; }
 
 int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n,
-                               float* d_workspace, float* d_out_xy, float* d_out_yy, hipStream_t stream) {
-  return run_sdot_shared(variant, d_x, d_y, n_pairs, n, d_workspace, d_out_xy, d_out_yy, stream);
+                               int with_xx, float* d_workspace, float* d_out_xy, float* d_out_yy,
+                               hipStream_t stream) {
+  if (variant < 0) return set_error(PLATO_AGG_EINVAL, "bad sdot_shared variant");
+  return run_sdot_shared(variant, d_x, d_y, n_pairs, n, with_xx, d_workspace, d_out_xy, d_out_yy, stream);
 }
 
 size_t plato_agg_torch_cosine_workspace(int K, int threads) {

@@ -879,13 +879,13 @@ class AggregationRound:
         g_flat, stride = self._flatten(_lib.PLATO_AGG_FLAT_RAW, segs, len(order), n_flat, [grads[0].data_ptr()],
                                        [grads[1].data_ptr()], None, lr, stream)
         k = len(slots)
-        # row 0: g.g (the global gradient's squared norm), rows 1..k: g.loc_k and loc_k.loc_k.
-        # g.g rides as one more pair (g, g) of the first batch's launch: a launch is as long as
-        # its serial chains, so a launch of its own would cost as much as the whole batch.
+        # rows 0..k-1: g.loc_k and loc_k.loc_k; row k: g.g (the global gradient's squared norm),
+        # which the last batch's launch forms alongside (with_xx): a launch is as long as its
+        # serial chains, so a launch of its own would cost as much as the whole batch.
         xy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         yy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         per = max(1, int(batch_bytes // (stride * 4)))
-        ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(min(k, per) + 1) // 4, dtype=torch.float32,
+        ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(min(k, per), 1) // 4, dtype=torch.float32,
                          device=eng.device)
         base = (_ptr(eng._base.f32), _ptr(eng._base.i64))
         keep = []
@@ -893,19 +893,18 @@ class AggregationRound:
             part = slots[s0:s0 + per]
             locs, _ = self._flatten(_lib.PLATO_AGG_FLAT_DELTA, segs, len(order), n_flat,
                                     [self._pf[i] for i in part], [self._pi[i] for i in part], base, lr, stream)
-            first = s0 == 0
-            ys_h = ([g_flat.data_ptr()] if first else []) + [locs.data_ptr() + r * stride * 4 for r in range(len(part))]
+            last = s0 + per >= k
+            ys_h = [locs.data_ptr() + r * stride * 4 for r in range(len(part))]
             ys = torch.from_numpy(np.asarray(ys_h, dtype=np.int64)).to(eng.device)
-            row = 0 if first else s0 + 1
-            _lib.call("plato_agg_sdot_shared", g_flat.data_ptr(), ys.data_ptr(), len(ys_h), n_flat, ws.data_ptr(),
-                      xy.data_ptr() + 4 * row, yy.data_ptr() + 4 * row, _stream_handle(stream))
+            _lib.call("plato_agg_sdot_shared", g_flat.data_ptr(), ys.data_ptr(), len(ys_h), n_flat, int(last),
+                      ws.data_ptr(), xy.data_ptr() + 4 * s0, yy.data_ptr() + 4 * s0, _stream_handle(stream))
             keep.append((locs, ys))
             if s0 + per < k:
                 stream.synchronize()  # bound the flat buffers to one batch
                 keep = []
         stream.synchronize()
         xy_h, yy_h = xy.cpu().numpy(), yy.cpu().numpy()
-        inner, g_sq, l_sq = xy_h[1:], xy_h[0], yy_h[1:]
+        inner, g_sq, l_sq = xy_h[:k], xy_h[k], yy_h[:k]
         return inner, g_sq, l_sq
 
     def np_sumsq(self, slots: Sequence[int]) -> np.ndarray:

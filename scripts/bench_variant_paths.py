@@ -154,16 +154,18 @@ def sdot_kernels(dev, k, n, reps):
     stride = -(-n // 64) * 64
     x = torch.randn(stride, device=dev)
     ys = torch.randn((k + 1, stride), device=dev) * 1e-2
-    ys[0] = x
+    ys[k] = x  # the per-pair kernel gets g.g as a pair (x, x) after the clients
     py = torch.tensor([ys.data_ptr() + r * stride * 4 for r in range(k + 1)], dtype=torch.int64, device=dev)
     px = torch.full((k + 1,), x.data_ptr(), dtype=torch.int64, device=dev)
-    ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(k + 1) // 4, device=dev)
+    ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(k, 1) // 4, device=dev)
     h = torch.cuda.current_stream(dev).cuda_stream
     runs = {"pairs": lambda o1, o2: _lib.call("plato_agg_sdot_pairs", px.data_ptr(), py.data_ptr(), k + 1, n,
-                                              o1.data_ptr(), o2.data_ptr(), h)}
+                                              o1.data_ptr(), o2.data_ptr(), h),
+            "shared_default": lambda o1, o2: _lib.call("plato_agg_sdot_shared", x.data_ptr(), py.data_ptr(), k, n, 1,
+                                                       ws.data_ptr(), o1.data_ptr(), o2.data_ptr(), h)}
     for v in range(_lib.lib().plato_agg_tune_num_sdot_shared_variants()):
         runs[f"shared_v{v}"] = (lambda o1, o2, v=v: _lib.call("plato_agg_tune_sdot_shared", v, x.data_ptr(),
-                                                               py.data_ptr(), k + 1, n, ws.data_ptr(), o1.data_ptr(),
+                                                               py.data_ptr(), k, n, 1, ws.data_ptr(), o1.data_ptr(),
                                                                o2.data_ptr(), h))
     ref = None
     for name, fn in runs.items():

@@ -48,32 +48,39 @@ def test_sdot_pairs_equal_openblas_order(n):
 
 
 @pytest.mark.parametrize("n", SIZES + [(1 << 20) + 37])
-def test_sdot_shared_equals_openblas_order(n):
-    """The split-chain shared-x kernel (every variant) == OpenBLAS order, 9 pairs (ragged pair groups),
-    one pair being (x, x) as FedAdp's g.g is."""
+@pytest.mark.parametrize("npairs", [9, 128])
+def test_sdot_shared_equals_openblas_order(n, npairs):
+    """The split-chain shared-x kernel (every variant, the size-picked default) == OpenBLAS order: 9 pairs
+    (ragged pair groups) and 128 (FedAdp's ResNet-18 round), with and without x.x as the virtual pair
+    (x, x) after the last one (FedAdp's g.g)."""
+    if npairs == 128 and n > 100003:
+        pytest.skip("size covered at 9 pairs")
     rng = np.random.default_rng(n + 7)
     x = rng.standard_normal(n).astype(np.float32)
-    ys = [x] + [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(8)]
+    ys = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(npairs)]
     bx, _ = _rows([x])
     by, py = _rows(ys)
     k = len(ys)
-    ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(k) // 4, dtype=torch.float32, device=DEV)
+    ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(k, 1) // 4, dtype=torch.float32, device=DEV)
     h = torch.cuda.current_stream().cuda_stream
-    want_xy = [R.sdot(x, y).tobytes() for y in ys]
-    want_yy = [R.sdot(y, y).tobytes() for y in ys]
+    want_xy = [R.sdot(x, y).tobytes() for y in ys] + [R.sdot(x, x).tobytes()]
+    want_yy = [R.sdot(y, y).tobytes() for y in ys] + [R.sdot(x, x).tobytes()]
     for variant in [None] + list(range(_lib.lib().plato_agg_tune_num_sdot_shared_variants())):
-        out_xy = torch.full((k,), float("nan"), device=DEV)
-        out_yy = torch.full((k,), float("nan"), device=DEV)
-        if variant is None:
-            _lib.call("plato_agg_sdot_shared", bx.data_ptr(), py.data_ptr(), k, n, ws.data_ptr(), out_xy.data_ptr(),
-                      out_yy.data_ptr(), h)
-        else:
-            _lib.call("plato_agg_tune_sdot_shared", variant, bx.data_ptr(), py.data_ptr(), k, n, ws.data_ptr(),
-                      out_xy.data_ptr(), out_yy.data_ptr(), h)
-        got_xy, got_yy = out_xy.cpu().numpy(), out_yy.cpu().numpy()
-        for j in range(k):
-            assert got_xy[j].tobytes() == want_xy[j], (n, variant, j)
-            assert got_yy[j].tobytes() == want_yy[j], (n, variant, j)
+        for with_xx in (0, 1):
+            out_xy = torch.full((k + 1,), float("nan"), device=DEV)
+            out_yy = torch.full((k + 1,), float("nan"), device=DEV)
+            if variant is None:
+                _lib.call("plato_agg_sdot_shared", bx.data_ptr(), py.data_ptr(), k, n, with_xx, ws.data_ptr(),
+                          out_xy.data_ptr(), out_yy.data_ptr(), h)
+            else:
+                _lib.call("plato_agg_tune_sdot_shared", variant, bx.data_ptr(), py.data_ptr(), k, n, with_xx,
+                          ws.data_ptr(), out_xy.data_ptr(), out_yy.data_ptr(), h)
+            got_xy, got_yy = out_xy.cpu().numpy(), out_yy.cpu().numpy()
+            for j in range(k + with_xx):
+                assert got_xy[j].tobytes() == want_xy[j], (n, variant, with_xx, j)
+                assert got_yy[j].tobytes() == want_yy[j], (n, variant, with_xx, j)
+            if not with_xx:
+                assert np.isnan(got_xy[k]) and np.isnan(got_yy[k])
 
 
 @pytest.mark.parametrize("n", SIZES + [1 << 20, (1 << 20) + 3])
