@@ -47,14 +47,12 @@ def test_sdot_pairs_equal_openblas_order(n):
         assert got_yy[j].tobytes() == R.sdot(ys[j], ys[j]).tobytes(), (n, j)
 
 
-@pytest.mark.parametrize("n", SIZES + [(1 << 20) + 37])
-@pytest.mark.parametrize("npairs", [9, 128])
+@pytest.mark.parametrize("n,npairs", [(n, 9) for n in SIZES + [(1 << 20) + 37]] +
+                         [(n, 128) for n in SIZES if n <= 100003])
 def test_sdot_shared_equals_openblas_order(n, npairs):
     """The split-chain shared-x kernel (every variant, the size-picked default) == OpenBLAS order: 9 pairs
     (ragged pair groups) and 128 (FedAdp's ResNet-18 round), with and without x.x as the virtual pair
     (x, x) after the last one (FedAdp's g.g)."""
-    if npairs == 128 and n > 100003:
-        pytest.skip("size covered at 9 pairs")
     rng = np.random.default_rng(n + 7)
     x = rng.standard_normal(n).astype(np.float32)
     ys = [(rng.standard_normal(n) * 1e-2).astype(np.float32) for _ in range(npairs)]
