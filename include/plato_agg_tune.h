@@ -79,9 +79,9 @@ int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n,
  *        table longest first; the default until round 2)
  *   13 = variant 12 with those long entries' producer waves at s_setprio 2
  *   14, 15 = variant 12 with 1,024-element tiles, 4 / 5 stages (15 is the default for
- *        grids of more than 512 (entry, client) pairs)
+ *        grids of more than 6,144 (entry, client) pairs)
  *   16 = variant 12 with 2,048-element tiles, 3 stages (the default for grids of at most
- *        512 pairs, e.g. Port's flattened vectors) */
+ *        6,144 pairs, e.g. Port's flattened vectors, FedAtt on ResNet-18 up to K = 64) */
 int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
                                const float* d_base_f32, const int64_t* d_base_i64,
                                const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,

@@ -1236,13 +1236,13 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
                               const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
                               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
   // Longer tiles halve the chain wave's barriers and exposed LDS latency per step but take more LDS
-  // per workgroup: 2,048-element tiles (3 stages, 2 workgroups per CU) win when every (entry, client)
-  // workgroup can be resident at once (Port's K + 1 flattened vectors: 4.33 vs 5.22 ms; FedAtt at
-  // K = 4: 0.96 vs 1.12 ms), 1,024-element tiles (5 stages, 3 per CU) on large grids (FedAtt at
-  // K = 128: 1.23 vs 1.37 ms).  DESIGN.md §11.
+  // per workgroup: 2,048-element tiles (3 stages, 2 workgroups per CU) win on small and medium grids
+  // (Port's K + 1 flattened vectors: 4.33 vs 5.22 ms; FedAtt on ResNet-18, 82 entries, K = 4-64:
+  // 4-6 % ahead of 1,024-element tiles), 1,024-element tiles (5 stages, 3 per CU) on large ones
+  // (FedAtt at K = 128, 10,496 pairs: 1.22 vs 1.48 ms).  DESIGN.md §11.
   const uint64_t pairs = (uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K > 0 ? K : 0);
-  return run_norms(pairs <= 512 ? 16 : 15, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32,
-                   d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
+  return run_norms(pairs <= 6144 ? 16 : 15, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32,
+                   n_entries_f32, d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
 }
 
 int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
