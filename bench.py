@@ -148,19 +148,30 @@ def kernel_signature(variant: int) -> str:
             f"{b(f & 4)}, {b(f & 8)}, {(f >> 4) & 255}, {b(f & (1 << 12))}>, true, false>")
 
 
+def source_stamp() -> str:
+    """sha256[:16] of the hot kernel's source: a profile summary records it, so a stale one shows."""
+    import hashlib
+
+    with open(os.path.join(ROOT, "plato_amd", "csrc", "fedavg_agg.hip"), "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
 def pmc_traffic(alg_bytes: int, kernel: str):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload and kernel.
+    """The committed rocprofv3 summary of this workload and kernel (PMC traffic + kernel-trace timing).
 
     PMC counters cannot be read from inside a timed run; scripts/profile.sh
-    collects FETCH_SIZE / WRITE_SIZE in their own passes of this same command
-    and scripts/summarize_profile.py writes profiles/<tag>_summary.json.  A
-    summary counts only if it profiled the same algorithmic bytes AND the same
-    kernel instantiation (a summary of another variant is ignored), and it
-    carries the source's build stamp so a stale one can be spotted.
+    runs this bench once unprofiled and then under rocprofv3 (kernel trace,
+    FETCH_SIZE and WRITE_SIZE in their own passes) in the same GPU lease, and
+    scripts/summarize_profile.py writes profiles/<tag>_summary.json with the
+    unprofiled run's ms_per_step / kernel_ms beside the profile's durations.
+    A summary counts only if it profiled the same algorithmic bytes AND the
+    same kernel instantiation; among those the newest tag wins, and one built
+    from the current kernel source is preferred.
     """
     import glob
 
-    best = None
+    stamp = source_stamp()
+    found = []
     for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json"))):
         try:
             with open(path) as f:
@@ -168,11 +179,34 @@ def pmc_traffic(alg_bytes: int, kernel: str):
         except (OSError, ValueError):
             continue
         if summ.get("algorithmic_bytes") == alg_bytes and kernel in summ.get("kernel", ""):
-            best = (path, summ)
-    if best is None:
-        return None, None, None
-    path, summ = best
-    return summ["pmc"]["hbm_bytes"], os.path.relpath(path, ROOT), summ.get("avg_duration_ms")
+            found.append((summ.get("source_sha16") == stamp, path, summ))
+    if not found:
+        return None
+    current, path, summ = max(found, key=lambda x: (x[0], x[1]))
+    summ = dict(summ, path=os.path.relpath(path, ROOT), current_source=current)
+    return summ
+
+
+def profile_roofline(summ, alg_bytes: int, kernel_ms: float, ms_per_step: float):
+    """Roofline fields taken from the committed profile, and how they compare with this run."""
+    if summ is None:
+        return {"traffic": None, "traffic_source": None}
+    avg = summ.get("avg_duration_ms")
+    timed = summ.get("timed_avg_ms") or avg
+    out = {
+        "traffic": summ["pmc"]["hbm_bytes"],
+        "traffic_source": summ["path"],
+        "traffic_source_current": summ["current_source"],
+        "traffic_profile_avg_ms": avg,
+        # the profile's own roofline: algorithmic bytes / the rocprofv3 kernel-trace duration
+        "frac_profile": round(alg_bytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if avg else None,
+        "frac_profile_timed": round(alg_bytes / (timed * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if timed else None,
+        "profile_over_this_run_kernel_ms": round(timed / kernel_ms, 4) if timed else None,
+        # a profile slower than this run's whole step was measured on another box / clock
+        "profile_avg_exceeds_ms_per_step": bool(avg and avg > ms_per_step),
+        "profile_lease_bench": summ.get("bench_same_lease"),
+    }
+    return out
 
 
 def cpus_available() -> int:
@@ -458,9 +492,9 @@ def main():
 
     value_gbs = job_bytes * args.steps / wall / 1e9
     variant = args.variant if args.variant is not None else 0
-    traffic, traffic_src, prof_ms = (pmc_traffic(alg_bytes, kernel_signature(variant)) if args.codec == "native"
-                                     else (None, None, None))
+    summ = pmc_traffic(alg_bytes, kernel_signature(variant)) if args.codec == "native" else None
     achieved = alg_bytes / (kernel_ms_max * 1e-3) / 1e9
+    prof = profile_roofline(summ, alg_bytes, kernel_ms_max, wall / args.steps * 1e3)
 
     result = {
         "metric": BASELINE_METRIC,
@@ -500,12 +534,12 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": traffic,
+            "traffic": prof["traffic"],
             "traffic_unit": "bytes/launch (HBM, rocprofv3 PMC)",
-            "traffic_source": traffic_src,
-            "traffic_profile_avg_ms": prof_ms,
+            **{k2: v2 for k2, v2 in prof.items() if k2 != "traffic"},
             "kernel_ms": round(kernel_ms, 4),
             "kernel_ms_max_over_ranks": round(kernel_ms_max, 4),
+            "kernel_source_sha16": source_stamp(),
         },
     }
 

@@ -33,6 +33,17 @@ class _AlgorithmEngine:
             self._plato_amd_engine = eng
         return eng
 
+    async def _off_loop(self, fn, *args):
+        """Run ``fn`` on the algorithm's one aggregation worker thread (device work off the event loop)."""
+        import asyncio
+        import concurrent.futures
+
+        ex = getattr(self, "_plato_amd_executor", None)
+        if ex is None:
+            ex = concurrent.futures.ThreadPoolExecutor(1, thread_name_prefix="plato-amd-alg")
+            self._plato_amd_executor = ex
+        return await asyncio.get_running_loop().run_in_executor(ex, fn, *args)
+
 
 class FedAvgAlgorithmMixin(_AlgorithmEngine):
     def compute_weight_deltas(self, baseline_weights, weights_received):
@@ -45,7 +56,8 @@ class FedAvgAlgorithmMixin(_AlgorithmEngine):
 
 class FedAsyncAlgorithmMixin(FedAvgAlgorithmMixin):
     async def aggregate_weights(self, baseline_weights, weights_received, mixing=0.9, **kwargs):
-        return self.aggregation_engine().mix_weights(baseline_weights, weights_received[0], mixing)
+        return await self._off_loop(self.aggregation_engine().mix_weights, baseline_weights, weights_received[0],
+                                    mixing)
 
 
 class FedAttAlgorithmMixin(_AlgorithmEngine):
@@ -84,7 +96,6 @@ class FedAttAlgorithmMixin(_AlgorithmEngine):
             return default
 
     async def aggregate_weights(self, baseline_weights, weights_received, **kwargs):
-        import asyncio
         from collections import OrderedDict
 
         import torch
@@ -92,21 +103,27 @@ class FedAttAlgorithmMixin(_AlgorithmEngine):
         from .. import weights as W
 
         engine = self.aggregation_engine()
-        rnd = engine.begin(baseline_weights, len(weights_received))
-        rnd.put_baseline(baseline_weights)
-        for slot, payload in enumerate(weights_received):
-            if not rnd.adopt(slot, payload):
-                rnd.put_client(slot, payload)
-            await asyncio.sleep(0)
-        # the reference's fp32 norms bit for bit (torch's CPU reduction order), then its softmax
-        atts = W.fedatt_attention(rnd.entry_norms(range(len(weights_received))))
-        epsilon = self._fedatt_param("epsilon", 1.2)
-        magnitude = self._fedatt_param("magnitude", 0.001)
-        noise = OrderedDict((name, torch.randn(weight.shape)) for name, weight in baseline_weights.items())
-        rnd.launch_entrywise(-atts.astype(np.float64), scale=-epsilon, noise=noise,
-                             noise_scale=magnitude, add_base=True)
-        while not rnd.ready():
-            await asyncio.sleep(0)
-        result = rnd.result()
-        engine.release_arrivals()
-        return result
+        try:
+            rnd = engine.begin(baseline_weights, len(weights_received))
+
+            def stage_and_norms():
+                rnd.put_baseline(baseline_weights)
+                for slot, payload in enumerate(weights_received):
+                    if not rnd.adopt(slot, payload):
+                        rnd.put_client(slot, payload)
+                # the reference's fp32 norms bit for bit (torch's CPU reduction order)
+                return rnd.entry_norms(range(len(weights_received)))
+
+            # pack + H2D + the norms launch and its sync run on the worker thread, not the event loop
+            norms = await self._off_loop(stage_and_norms)
+            atts = W.fedatt_attention(norms)  # the reference's softmax
+            epsilon = self._fedatt_param("epsilon", 1.2)
+            magnitude = self._fedatt_param("magnitude", 0.001)
+            # the reference's RNG stream: torch.randn per key in baseline order, on this thread
+            noise = OrderedDict((name, torch.randn(weight.shape)) for name, weight in baseline_weights.items())
+            await self._off_loop(lambda: rnd.launch_entrywise(-atts.astype(np.float64), scale=-epsilon, noise=noise,
+                                                              noise_scale=magnitude, add_base=True))
+            await self._off_loop(rnd.wait)  # a HIP event wait on the worker thread
+            return rnd.result()
+        finally:
+            engine.release_arrivals()

@@ -30,7 +30,7 @@ import torch
 
 from . import _lib
 from .arena import CODECS, F32, I64, ArenaLayout, payload_codec
-from .staging import HostPacker, PinnedRing, ResultPool, arena_source
+from .staging import HostPacker, PinnedRing, ResultPool, arena_source, payload_fingerprint
 
 
 def fp32_weights(values: Sequence[float]) -> np.ndarray:
@@ -136,17 +136,18 @@ class _Stager:
                 if n_i:
                     dst_i64[:n_i].copy_(arena_i[:n_i], non_blocking=True)
             return
-        j = self.ring.acquire()
-        hf, hi = self.ring.slots[j]
-        self.packer.pack(state_dict, hf, hi)
-        with torch.cuda.stream(self.stream):
-            if n_f:
-                dst_f32[:n_f].copy_(hf[:n_f], non_blocking=True)
-            if n_i:
-                dst_i64[:n_i].copy_(hi[:n_i], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(self.stream)
-        self.ring.fence(j, [ev])
+        with self.ring.lock:  # acquire -> pack -> copy -> fence as one step (executor vs event loop)
+            j = self.ring.acquire()
+            hf, hi = self.ring.slots[j]
+            self.packer.pack(state_dict, hf, hi)
+            with torch.cuda.stream(self.stream):
+                if n_f:
+                    dst_f32[:n_f].copy_(hf[:n_f], non_blocking=True)
+                if n_i:
+                    dst_i64[:n_i].copy_(hi[:n_i], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.stream)
+            self.ring.fence(j, [ev])
 
     def fence(self, stream: torch.cuda.Stream) -> None:
         """Make ``stream`` wait for every copy issued so far."""
@@ -297,19 +298,22 @@ class FedAvgEngine:
         slab, row = free.pop()
         self._stagers[codec].put(payload, slab.f32[row], slab.i64[row])
         pf, pi = slab.row_pointers([row])
-        # keep the dict alive: its id() is the key
-        self._arrivals[id(payload)] = (payload, codec, self._layout.signature, int(pf[0]), int(pi[0]), slab, row)
+        # keep the dict alive: its id() is the key; the fingerprint detects later edits
+        self._arrivals[id(payload)] = (payload, codec, self._layout.signature, int(pf[0]), int(pi[0]), slab, row,
+                                       payload_fingerprint(payload))
         return True
 
     def _arrival_rows(self, payload, layout: ArenaLayout, codec: str):
         hit = self._arrivals.get(id(payload))
         if hit is None or hit[0] is not payload or hit[1] != codec or hit[2] != layout.signature:
             return None
+        if hit[7] != payload_fingerprint(payload):
+            return None  # an entry was replaced or written after arrival: stage the current tensors
         return hit[3], hit[4]
 
     def release_arrivals(self) -> None:
-        """Return every arrival slot (after the round that used them has completed)."""
-        for payload, codec, _, _, _, slab, row in self._arrivals.values():
+        """Return every arrival slot (after the round that used them has completed, or failed)."""
+        for payload, codec, _, _, _, slab, row, _ in self._arrivals.values():
             self._arrival_free.setdefault(codec, []).append((slab, row))
         self._arrivals = {}
 

@@ -39,7 +39,7 @@ from . import _lib
 from .arena import CODECS, ArenaLayout, payload_codec
 from .distributed import BucketPlan
 from .engine import FedAvgEngine, fp32_weights, require_device
-from .staging import HostPacker, PinnedRing, ResultPool, arena_source
+from .staging import HostPacker, PinnedRing, ResultPool, arena_source, payload_fingerprint
 
 MULTI_CODECS = ("native", "bf16")
 
@@ -151,16 +151,17 @@ class MultiDeviceEngine:
                 shard.copy_in(src[0], src[1], df, di)
             return
         ring, packer = self._ring(codec)
-        j = ring.acquire()
-        hf, hi = ring.slots[j]
-        packer.pack(payload, hf, hi)
-        events = []
-        for shard, (df, di) in zip(self._shards, rows):
-            shard.copy_in(hf, hi, df, di)
-            ev = torch.cuda.Event()
-            ev.record(shard.copy_stream)
-            events.append(ev)
-        ring.fence(j, events)
+        with ring.lock:  # acquire -> pack -> copies -> fence as one step (executor vs event loop)
+            j = ring.acquire()
+            hf, hi = ring.slots[j]
+            packer.pack(payload, hf, hi)
+            events = []
+            for shard, (df, di) in zip(self._shards, rows):
+                shard.copy_in(hf, hi, df, di)
+                ev = torch.cuda.Event()
+                ev.record(shard.copy_stream)
+                events.append(ev)
+            ring.fence(j, events)
 
     # ------------------------------------------------------------ rounds
     def begin(self, template, capacity: int, codec: str = "native") -> "MultiRound":
@@ -192,17 +193,20 @@ class MultiDeviceEngine:
         slabs, row = free.pop()
         self._stage(payload, codec, [(f[row], i[row]) for f, i in slabs])
         ptrs = [(_row_ptr(f, row), _row_ptr(i, row)) for f, i in slabs]
-        self._arrivals[id(payload)] = (payload, codec, self._layout.signature, ptrs, slabs, row)
+        self._arrivals[id(payload)] = (payload, codec, self._layout.signature, ptrs, slabs, row,
+                                       payload_fingerprint(payload))
         return True
 
     def _arrival_rows(self, payload, layout: ArenaLayout, codec: str):
         hit = self._arrivals.get(id(payload))
         if hit is None or hit[0] is not payload or hit[1] != codec or hit[2] != layout.signature:
             return None
+        if hit[6] != payload_fingerprint(payload):
+            return None  # edited after arrival: the round stages its current tensors
         return hit[3]
 
     def release_arrivals(self) -> None:
-        for _, codec, _, _, slabs, row in self._arrivals.values():
+        for _, codec, _, _, slabs, row, _ in self._arrivals.values():
             self._arrival_free.setdefault(codec, []).append((slabs, row))
         self._arrivals = {}
         self.primary.release_arrivals()

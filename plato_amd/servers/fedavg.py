@@ -43,6 +43,9 @@ class _EngineHolder:
     #: weights computed from the staged payloads (Port, FedAdp, Polaris): such
     #: rounds run on one GPU (the multi-GPU engine's first device)
     needs_staged_round = False
+    #: FedAdp / Port: before the first round, check that this host's numpy / torch
+    #: reduction order is the one the device reproduces (plato_amd.hostorder)
+    host_order_check = True
 
     def aggregation_engine(self):
         eng = getattr(self, "_plato_amd_engine", None)
@@ -125,32 +128,39 @@ class FusedAggregationMixin(_EngineHolder):
         # bf16 payloads (model_quantize on the clients) stay bf16 on the device
         codec = payload_codec(weights_received[0])
         engine = self.round_engine(codec)
-        rnd = engine.begin(baseline_weights, len(weights_received), codec)
+        try:
+            rnd = engine.begin(baseline_weights, len(weights_received), codec)
 
-        def stage():
-            with tracing.range("plato_amd.stage"):
-                rnd.put_baseline(baseline_weights)
-                for slot, payload in enumerate(weights_received):
-                    # payloads staged at arrival (WireIngestMixin.stage_on_arrival) are adopted in place
-                    if not rnd.adopt(slot, payload):
-                        rnd.put_client(slot, payload)
+            def stage():
+                with tracing.range("plato_amd.stage"):
+                    rnd.put_baseline(baseline_weights)
+                    for slot, payload in enumerate(weights_received):
+                        # payloads staged at arrival (WireIngestMixin.stage_on_arrival) are adopted in place
+                        if not rnd.adopt(slot, payload):
+                            rnd.put_client(slot, payload)
 
-        # Pack + H2D run on a worker thread: the event loop keeps serving the
-        # clients meanwhile (the reference yields per client, servers/fedavg.py:157).
-        await self._off_loop(stage)
-        # weights may need the staged arenas (Port's similarity reduction); the
-        # hook runs on the event loop thread like the reference's
+            # Pack + H2D run on a worker thread: the event loop keeps serving the
+            # clients meanwhile (the reference yields per client, servers/fedavg.py:157).
+            await self._off_loop(stage)
+            # The weights may need the staged arenas (Port's similarity, FedAdp's dots,
+            # Polaris' sums): those device reductions and their host syncs run on the
+            # same worker thread, so the event loop is never blocked on the GPU.
+            weights, scales = await self._off_loop(self._weights_on_round, rnd, updates)
+            with tracing.range("plato_amd.launch"):
+                rnd.launch(weights, scales)
+            with tracing.range("plato_amd.fetch"):
+                return await self._finish(rnd)
+        finally:
+            # also when a hook, a weight computation or a launch raised: the arrival slots and
+            # the payload references they hold must not leak into the next round
+            engine.release_arrivals()
+
+    def _weights_on_round(self, rnd, updates):
         self._plato_amd_round = rnd
         try:
-            weights, scales = self.aggregation_weights(updates)
+            return self.aggregation_weights(updates)
         finally:
             self._plato_amd_round = None
-        with tracing.range("plato_amd.launch"):
-            rnd.launch(weights, scales)
-        with tracing.range("plato_amd.fetch"):
-            result = await self._finish(rnd)
-        engine.release_arrivals()
-        return result
 
 
 class DeltasAggregationMixin(_EngineHolder):

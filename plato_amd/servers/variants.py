@@ -13,6 +13,7 @@ import os
 
 import numpy as np
 
+from .. import hostorder
 from .. import weights as W
 from .fedavg import FusedAggregationMixin, _EngineHolder
 
@@ -70,7 +71,10 @@ class PortWeights(_EngineHolder):
         import torch
 
         previous = torch.load(path, map_location="cpu", weights_only=True)
-        sims = rnd.model_similarities(previous, need, threads=self.port_threads)
+        threads = torch.get_num_threads() if self.port_threads is None else int(self.port_threads)
+        if self.host_order_check:
+            hostorder.check_port(rnd.engine.device, threads)  # this host's F.cosine_similarity order
+        sims = rnd.model_similarities(previous, need, threads=threads)
         out = [1.0] * len(updates)
         for i, sim in zip(need, sims):
             out[i] = sim
@@ -139,7 +143,9 @@ class FedAsyncMixing(_EngineHolder):
                     getattr(fn, "a", 1), getattr(fn, "b", 0))
         engine = self.aggregation_engine()
         engine = getattr(engine, "primary", engine)  # one model-sized elementwise pass: one GPU
-        return engine.mix_weights(baseline_weights, weights_received[0], self.mixing_hyperparam)
+        # pack + H2D + kernel + D2H on the aggregation worker thread, not the event loop
+        return await self._off_loop(engine.mix_weights, baseline_weights, weights_received[0],
+                                    self.mixing_hyperparam)
 
 
 class GanDeltasAggregationMixin(_EngineHolder):
@@ -237,6 +243,8 @@ class FedAdpWeights(_EngineHolder):
             if lr is None:
                 raise ValueError("FedAdp needs parameters.optimizer.lr (or set fedadp_lr)")
         alpha = self.fedadp_alpha if self.fedadp_alpha is not None else _config_attr("algorithm", "alpha", 5)
+        if self.host_order_check:
+            hostorder.check_fedadp(rnd.engine.device)  # this host's numpy sdot order
         inner, g_sq, l_sq = rnd.fedadp_dots(grads, range(k), lr)
         angles = W.fedadp_angles_from_dots(inner, g_sq, l_sq)
         contribs = W.fedadp_contributions(angles, self.selected_clients, self.local_angles,
@@ -366,11 +374,27 @@ class HEHybridMixin(_EngineHolder):
 
     The CKKS half (tenseal vectors) stays the reference's; the unencrypted
     float64 vectors are summed by :meth:`FedAvgEngine.weighted_sum` with the
-    reference's float64 promotion.  Compose as
-    ``class Server(HEHybridMixin, fedavg_he.Server)``.
+    reference's float64 promotion.  The reference's ``aggregate_weights``
+    (``fedavg_he.py:50-64``) calls ``_fedavg_hybrid`` synchronously on the event
+    loop; here the hybrid sum is formed first on the aggregation worker thread
+    and the reference's method then picks it up, so its decrypt / serialize
+    steps run unchanged.  Compose as ``class Server(HEHybridMixin, fedavg_he.Server)``.
     """
 
+    async def aggregate_weights(self, updates, baseline_weights, weights_received):
+        self._plato_amd_hybrid = await self._off_loop(self._fedavg_hybrid_device, updates)
+        try:
+            return await super().aggregate_weights(updates, baseline_weights, weights_received)
+        finally:
+            self._plato_amd_hybrid = None
+
     def _fedavg_hybrid(self, updates):
+        done = getattr(self, "_plato_amd_hybrid", None)
+        if done is not None:
+            return done
+        return self._fedavg_hybrid_device(updates)
+
+    def _fedavg_hybrid_device(self, updates):
         from plato.utils import homo_enc
 
         weights_received = [homo_enc.deserialize_weights(update.payload, self.context) for update in updates]

@@ -17,6 +17,7 @@ the caller kept).
 
 from __future__ import annotations
 
+import threading
 from typing import Mapping
 
 import numpy as np
@@ -68,6 +69,18 @@ class HostPacker:
                 raise ingest.IngestError(f"pack failed ({rc}): {lib.plato_ingest_last_error().decode()}")
 
 
+def payload_fingerprint(state_dict) -> tuple:
+    """Identity + in-place version of every tensor of a payload (and its arena, if ingested).
+
+    A payload prestaged on arrival is adopted only if this is unchanged: a
+    processor or hook that replaced an entry (new tensor object) or wrote one
+    in place (torch bumps the tensor's version counter) after the copy was
+    taken makes the round stage the payload again from its current tensors.
+    """
+    return (getattr(state_dict, "layout_signature", None),
+            tuple((name, id(t), getattr(t, "_version", 0)) for name, t in state_dict.items()))
+
+
 def arena_source(state_dict, layout: ArenaLayout, codec: str):
     """The pinned arena regions of an ingested payload, or None if it must be packed."""
     arena_f = getattr(state_dict, "arena_f32", None)
@@ -78,7 +91,13 @@ def arena_source(state_dict, layout: ArenaLayout, codec: str):
 
 
 class PinnedRing:
-    """``depth`` pinned full-arena slots; a slot is reused once its copies have completed."""
+    """``depth`` pinned full-arena slots; a slot is reused once its copies have completed.
+
+    Staging runs on the aggregation executor while arrivals may be prestaged
+    from the event loop: a caller holds :attr:`lock` from :meth:`acquire`
+    through the pack, the copies and :meth:`fence`, so two threads never pack
+    into one slot or reuse a slot whose DMA is still unfenced.
+    """
 
     def __init__(self, layout: ArenaLayout, codec: str = "native", depth: int = 4):
         dt_f, dt_i = CODECS[codec]
@@ -86,6 +105,7 @@ class PinnedRing:
                        torch.empty(layout.row_i64, dtype=dt_i, pin_memory=True)) for _ in range(depth)]
         self.events: list[list] = [[] for _ in range(depth)]
         self.next = 0
+        self.lock = threading.RLock()
 
     def acquire(self) -> int:
         j = self.next

@@ -25,7 +25,16 @@ def counter(path, name):
     return statistics.median(vals), len(vals)
 
 
-def main(tag, alg_bytes, label):
+def last_json(path):
+    """The bench's one JSON result line in a log (None if the run printed none)."""
+    try:
+        lines = [ln for ln in open(path) if ln.startswith("{")]
+    except OSError:
+        return None
+    return json.loads(lines[-1]) if lines else None
+
+
+def main(tag, alg_bytes, label, steps=20):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -37,6 +46,16 @@ def main(tag, alg_bytes, label):
     read_bytes = fetch_kib * 1024 * 2
     write_bytes = write_kib * 1024
     avg_ns = float(row["AverageNs"])
+    # the timed region's dispatches only (the bench's last `steps` launches; warm-up excluded)
+    trace = [r for r in csv.DictReader(open(os.path.join(src, "kt", "kt_kernel_trace.csv")))
+             if r["Kernel_Name"] == row["Name"]]
+    trace.sort(key=lambda r: int(r["Start_Timestamp"]))
+    durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace]
+    timed = durs[-steps:]
+    run = last_json(os.path.join(src, "bench.json"))
+    prof_run = last_json(os.path.join(src, "kt.log"))
+    sys.path.insert(0, ROOT)
+    import bench  # noqa: E402  (source stamp of the profiled kernel)
     out = {
         "tag": tag,
         "workload": label,
@@ -44,6 +63,16 @@ def main(tag, alg_bytes, label):
         "calls": int(row["Calls"]),
         "avg_duration_ms": avg_ns / 1e6,
         "min_duration_ms": float(row["MinNs"]) / 1e6,
+        "timed_avg_ms": statistics.fmean(timed),
+        "timed_median_ms": statistics.median(timed),
+        "timed_dispatches": len(timed),
+        "source_sha16": bench.source_stamp(),
+        # the same bench command unprofiled, in the same GPU lease (scripts/profile.sh step 0)
+        "bench_same_lease": None if run is None else {
+            "ms_per_step": run["ms_per_step"], "kernel_ms": run["roofline"]["kernel_ms"],
+            "value": run["value"], "frac": run["roofline"]["frac"]},
+        "bench_under_kernel_trace": None if prof_run is None else {
+            "ms_per_step": prof_run["ms_per_step"], "kernel_ms": prof_run["roofline"]["kernel_ms"]},
         "algorithmic_bytes": alg_bytes,
         "achieved_GBps_rocprof_avg": alg_bytes / avg_ns,
         "pmc": {
