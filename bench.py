@@ -141,7 +141,7 @@ def kernel_signature(variant: int) -> str:
     from plato_amd import _lib
 
     bs, v, u, fl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-    _lib.call("plato_agg_tune_describe", variant, ctypes.byref(bs), ctypes.byref(v), ctypes.byref(u), ctypes.byref(fl))
+    _lib.tune_call("plato_agg_tune_describe", variant, ctypes.byref(bs), ctypes.byref(v), ctypes.byref(u), ctypes.byref(fl))
     f = fl.value
     b = lambda x: "true" if x else "false"  # noqa: E731
     return (f"fedavg_kernel<(anonymous namespace)::Cfg<{bs.value}, {v.value}, {u.value}, {b(f & 1)}, {b(f & 2)}, "
@@ -334,7 +334,7 @@ def main():
     def kernel(variant=None):
         if args.codec == "bf16":
             v = (args.variant or 0) if variant is None else variant
-            _lib.call("plato_agg_tune_fedavg_bf16", v, tf.data_ptr(), ti.data_ptr(), w.data_ptr(), None, k,
+            _lib.tune_call("plato_agg_tune_fedavg_bf16", v, tf.data_ptr(), ti.data_ptr(), w.data_ptr(), None, k,
                       base.f32.data_ptr(), base.i64.data_ptr(), out_f.data_ptr(), out_i.data_ptr(),
                       layout.n_f32, layout.n_i64, stream.cuda_stream)
             return
@@ -385,7 +385,7 @@ def main():
                      k * 2 * (full_layout.n_f32 + full_layout.n_i64) + 2 * (full_layout.n_f32 * 4 + full_layout.n_i64 * 8))
 
     if args.sweep and args.codec == "bf16":
-        nv = _lib.lib().plato_agg_tune_num_bf16_variants()
+        nv = _lib.tune().plato_agg_tune_num_bf16_variants()
         times = {v: [] for v in range(nv)}
         for v in range(nv):
             kernel(v)
@@ -408,7 +408,7 @@ def main():
         return
 
     if args.sweep:
-        nv = _lib.lib().plato_agg_tune_num_variants()
+        nv = _lib.tune().plato_agg_tune_num_variants()
         times = {v: [] for v in range(nv)}
         for v in range(nv):
             for _ in range(3):
@@ -433,7 +433,7 @@ def main():
         for mode, name, nbytes in ((1, "read", n_probe * 4), (0, "copy", (n_probe // 2) * 8)):
             for blocks in (1024, 2048, 4096, 8192):
                 n_el = n_probe if mode == 1 else n_probe // 2
-                _lib.call("plato_agg_tune_stream", mode, src.data_ptr(), dst.data_ptr(), n_el, blocks,
+                _lib.tune_call("plato_agg_tune_stream", mode, src.data_ptr(), dst.data_ptr(), n_el, blocks,
                           stream.cuda_stream)
                 torch.cuda.synchronize(dev)
                 ts = []
@@ -441,7 +441,7 @@ def main():
                     e0 = torch.cuda.Event(enable_timing=True)
                     e1 = torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
-                    _lib.call("plato_agg_tune_stream", mode, src.data_ptr(), dst.data_ptr(), n_el, blocks,
+                    _lib.tune_call("plato_agg_tune_stream", mode, src.data_ptr(), dst.data_ptr(), n_el, blocks,
                               stream.cuda_stream)
                     e1.record(stream)
                     e1.synchronize()
@@ -455,7 +455,7 @@ def main():
 
             for v in range(nv):
                 bs, a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
-                _lib.lib().plato_agg_tune_describe(v, ctypes.byref(bs), ctypes.byref(a), ctypes.byref(b),
+                _lib.tune().plato_agg_tune_describe(v, ctypes.byref(bs), ctypes.byref(a), ctypes.byref(b),
                                                    ctypes.byref(c))
                 med = statistics.median(times[v])
                 print(json.dumps({"variant": v, "B": bs.value, "V": a.value, "U": b.value,

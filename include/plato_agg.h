@@ -388,6 +388,27 @@ int plato_agg_sdot_shared(const float* d_x, const float* const* d_y, int n_pairs
                           float* d_workspace, float* d_out_xy, float* d_out_yy, hipStream_t stream);
 
 /*
+ * FedAdp's dots straight from the staged arenas, bit-equal to plato_agg_flatten
+ * (PLATO_AGG_FLAT_DELTA with the segment map) followed by plato_agg_sdot_shared,
+ * without the flattened copies: process_grad(update) positions are gathered
+ * through d_segs (flat order: entries sorted by name.lower(), NEG_DIV on all but
+ * the first) from client k's arenas d_src_f32[k] / d_src_i64[k] and the baseline
+ * (loc = x - b, or -(x - b) / lr), and d_out_xy[k] = np.inner(x, loc_k),
+ * d_out_yy[k] = loc_k . loc_k in numpy's OpenBLAS sdot_k_SKYLAKEX order
+ * (examples/server_aggregation/fedadp/fedadp_server.py:91-99, 122-133).  d_x is
+ * the flattened global gradient (plato_agg_flatten RAW, 16-byte aligned, at
+ * least n_flat rounded up to 64 floats); with_xx = 1 also writes x . x to
+ * d_out_xy[n_pairs] and d_out_yy[n_pairs].  Segments: 1..2048, n_flat < 2^32;
+ * n_f32 / n_i64 = lengths of the arenas' fp32 (< 2^30) and int64 regions.
+ * d_workspace: plato_agg_fedadp_dots_workspace(n_pairs, with_xx, n_i64) bytes.
+ */
+size_t plato_agg_fedadp_dots_workspace(int n_pairs, int with_xx, size_t n_i64);
+int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
+                          const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
+                          uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
+                          float* d_out_xy, float* d_out_yy, hipStream_t stream);
+
+/*
  * The sum in Port's F.cosine_similarity(a, b_k, dim=0) (port_server.py:50),
  * as x86-64 PyTorch 2.10 forms it on `threads` CPU threads:
  *   q = (a / max(|a|, eps)) * (b_k / max(|b_k|, eps)),  out[k] = sum(q)

@@ -1,5 +1,10 @@
 /*
- * plato_agg_tune.h — benchmarking / tuning entry points of libplato_agg.so.
+ * plato_agg_tune.h — benchmarking / tuning entry points of libplato_agg_tune.so.
+ *
+ * libplato_agg_tune.so is built from the same sources as libplato_agg.so with
+ * -DPLATO_AGG_TUNE: it carries every kernel variant and these exports besides
+ * the plato_agg.h entry points.  The product library carries only the default
+ * variants and does not export these.
  *
  * Not part of the drop-in boundary (no reference interface behind them):
  * bench.py and the tuning sweep use them to time the kernel variants
@@ -120,6 +125,14 @@ int plato_agg_tune_fedavg_qsgd(int variant, const uint8_t* const* d_codes_f32, c
                                const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64, const float* d_base_f32,
                                const int64_t* d_base_i64, float* d_out_f32, float* d_out_i64f, size_t n_f32,
                                size_t n_i64, hipStream_t stream);
+
+/* plato_agg_fedadp_dots with an explicit tile shape (0 = the default; see csrc/fedadp.hip). */
+int plato_agg_tune_num_fedadp_variants(void);
+int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const* d_src_f32,
+                               const void* const* d_src_i64, int n_pairs, const float* d_base_f32,
+                               const int64_t* d_base_i64, const plato_agg_segment* d_segs, uint32_t n_segs,
+                               size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
+                               float* d_out_yy, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -13,6 +13,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libplato_agg.so")
+TUNE_LIB_PATH = os.path.join(_HERE, "libplato_agg_tune.so")
 ABI_VERSION = 2
 
 PLATO_AGG_OK = 0
@@ -31,8 +32,8 @@ _c_int = ctypes.c_int
 _c_float = ctypes.c_float
 _c_u64 = ctypes.c_uint64
 
-# name -> (restype, argtypes); must match include/plato_agg.h and
-# include/plato_agg_tune.h exactly (tests/test_abi.py checks the export list).
+# name -> (restype, argtypes); must match include/plato_agg.h exactly (tests/test_abi.py
+# checks the export list of libplato_agg.so against it).
 SIGNATURES = {
     "plato_agg_abi_version": (_c_int, []),
     "plato_agg_last_error": (ctypes.c_char_p, []),
@@ -118,6 +119,11 @@ SIGNATURES = {
     "plato_agg_sdot_shared_workspace": (_c_size_t, [_c_int, _c_int]),
     "plato_agg_sdot_shared": (
         _c_int, [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "plato_agg_fedadp_dots_workspace": (_c_size_t, [_c_int, _c_int, _c_size_t]),
+    "plato_agg_fedadp_dots": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,
+         _c_size_t, _c_size_t, _c_float, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "plato_agg_torch_cosine_workspace": (_c_size_t, [_c_int, _c_int]),
     "plato_agg_torch_cosine_sum": (
         _c_int,
@@ -135,7 +141,11 @@ SIGNATURES = {
     "plato_agg_comm_size": (_c_int, [_c_void_p]),
     "plato_agg_comm_allgather_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_void_p]),
     "plato_agg_comm_reduce_scatter_f32": (_c_int, [_c_void_p, _c_void_p, _c_void_p, _c_size_t, _c_void_p]),
-    # tuning / benchmarking (include/plato_agg_tune.h)
+}
+
+# include/plato_agg_tune.h: exported by libplato_agg_tune.so only (the same sources built with every
+# kernel variant; bench.py --sweep, scripts/ and the variant tests load it beside the product library)
+TUNE_SIGNATURES = {
     "plato_agg_tune_num_variants": (_c_int, []),
     "plato_agg_tune_set_launch_groups": (None, [_c_u64]),
     "plato_agg_tune_describe": (
@@ -162,6 +172,11 @@ SIGNATURES = {
     "plato_agg_tune_sdot_shared": (
         _c_int, [_c_int, _c_void_p, _c_void_p, _c_int, _c_size_t, _c_int, _c_void_p, _c_void_p, _c_void_p,
                  _c_void_p]),
+    "plato_agg_tune_num_fedadp_variants": (_c_int, []),
+    "plato_agg_tune_fedadp_dots": (
+        _c_int,
+        [_c_int, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,
+         _c_size_t, _c_size_t, _c_float, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "plato_agg_tune_entry_norms": (
         _c_int,
         [_c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_void_p,
@@ -176,6 +191,14 @@ SIGNATURES = {
 
 _lock = threading.Lock()
 _lib = None
+_tune = None
+
+
+def _bind(handle, signatures):
+    for name, (restype, argtypes) in signatures.items():
+        fn = getattr(handle, name)
+        fn.restype = restype
+        fn.argtypes = argtypes
 
 
 def lib() -> ctypes.CDLL:
@@ -195,10 +218,7 @@ def lib() -> ctypes.CDLL:
             handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         except OSError as exc:  # pragma: no cover - depends on the host
             raise RuntimeError(f"plato_amd: cannot load {LIB_PATH}: {exc}") from exc
-        for name, (restype, argtypes) in SIGNATURES.items():
-            fn = getattr(handle, name)
-            fn.restype = restype
-            fn.argtypes = argtypes
+        _bind(handle, SIGNATURES)
         version = handle.plato_agg_abi_version()
         if version != ABI_VERSION:
             raise RuntimeError(
@@ -206,6 +226,26 @@ def lib() -> ctypes.CDLL:
             )
         _lib = handle
         return _lib
+
+
+def tune() -> ctypes.CDLL:
+    """Load (once) the tuning library: every product entry point plus the plato_agg_tune_* variants."""
+    global _tune
+    if _tune is not None:
+        return _tune
+    lib()
+    with _lock:
+        if _tune is not None:
+            return _tune
+        if not os.path.exists(TUNE_LIB_PATH):
+            raise RuntimeError(f"plato_amd: {TUNE_LIB_PATH} is not built; run __graft_entry__.build()")
+        handle = ctypes.CDLL(TUNE_LIB_PATH)  # RTLD_LOCAL: its symbols never interpose the product's
+        _bind(handle, SIGNATURES)
+        _bind(handle, TUNE_SIGNATURES)
+        if handle.plato_agg_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"plato_amd: {TUNE_LIB_PATH} has another ABI version; rebuild it")
+        _tune = handle
+        return _tune
 
 
 def check(status: int, what: str) -> None:
@@ -221,3 +261,12 @@ def check(status: int, what: str) -> None:
 def call(name: str, *args) -> None:
     """Call a C-ABI entry point and raise on a non-zero status."""
     check(getattr(lib(), name)(*args), name)
+
+
+def tune_call(name: str, *args) -> None:
+    """Call an entry point of the tuning library (kernel variants) and raise on a non-zero status."""
+    h = tune()
+    status = getattr(h, name)(*args)
+    if status != PLATO_AGG_OK:
+        msg = h.plato_agg_last_error().decode(errors="replace")
+        raise (ValueError if status == PLATO_AGG_EINVAL else RuntimeError)(f"{name}: {msg} (status {status})")

@@ -1124,6 +1124,10 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
               uint32_t n_entries_f32, const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
   if (variant < 0 || variant > 16) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
+#ifndef PLATO_AGG_TUNE
+  // libplato_agg.so carries the two defaults of plato_agg_entry_norms_f32 only
+  if (variant != 15 && variant != 16) return set_error(PLATO_AGG_EINVAL, "entry_norms variant not in this build");
+#endif
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (n_entries <= 0 || !d_out) return set_error(PLATO_AGG_EINVAL, "null output / no entries");
   if (n_entries_f32 && (!d_x_f32 || !d_entries_f32)) return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
@@ -1157,13 +1161,24 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
   // chains / without the loads (timing probes, wrong results); 6, 7
   // producer/consumer with 1024- / 256-element tiles; 9, 10 producer/consumer
   // with transposed d tiles (512 / 1,024 elements).
+#ifdef PLATO_AGG_TUNE
   static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2, 0, 0, 0, 0, 0, 0, 0, 0};
   const int G = kGroup[variant];
+#endif
   a.probe = variant == 4 ? 1u : variant == 5 ? 2u : 0u;
   if (variant == 0 || variant == 6 || variant == 7 || variant >= 9) {
     // producer / consumer, one workgroup per (entry, client)
     const dim3 grid{uint32_t((uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K))};
     const bool hb = d_base_f32 != nullptr;
+#ifndef PLATO_AGG_TUNE
+    if (variant == 15) {
+      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 5, true, true, -1>), grid, dim3(128), 0, stream, a);
+      else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 5, false, true, -1>), grid, dim3(128), 0, stream, a);
+    } else {
+      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<2048, 3, true, true, -1>), grid, dim3(128), 0, stream, a);
+      else hipLaunchKernelGGL((entry_norms_pc_kernel<2048, 3, false, true, -1>), grid, dim3(128), 0, stream, a);
+    }
+#else
     if (variant == 0) {
       if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true>), grid, dim3(128), 0, stream, a);
       else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false>), grid, dim3(128), 0, stream, a);
@@ -1200,8 +1215,10 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
       if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<256, 12, true>), grid, dim3(128), 0, stream, a);
       else hipLaunchKernelGGL((entry_norms_pc_kernel<256, 12, false>), grid, dim3(128), 0, stream, a);
     }
+#endif
     return launch_error("entry_norms launch");
   }
+#ifdef PLATO_AGG_TUNE
   a.ngroups = uint32_t((K + (G ? G : 1) - 1) / (G ? G : 1));
   if (variant == 1) {  // per-wave chains (the first version)
     const dim3 grid{uint32_t((threads + kBlock - 1) / kBlock)};
@@ -1225,6 +1242,9 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
     else hipLaunchKernelGGL((entry_norms_ring_kernel<4, false>), grid, block, 0, stream, a);
   }
   return launch_error("entry_norms launch");
+#else
+  return launch_error("entry_norms launch");
+#endif
 }
 }  // namespace
 
@@ -1245,6 +1265,7 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
                    n_entries_f32, d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
 }
 
+#ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
 int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
                                const float* d_base_f32, const int64_t* d_base_i64,
                                const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
@@ -1253,5 +1274,6 @@ int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const i
   return run_norms(variant, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32,
                    d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
 }
+#endif  // PLATO_AGG_TUNE
 
 }  // extern "C"

@@ -1,0 +1,534 @@
+// fedadp.hip — FedAdp's float32 dots straight from the staged client arenas, for gfx950.
+// C ABI: include/plato_agg.h (plato_agg_fedadp_dots).  CPU restatement: oracle/reductions.c (sdot).
+//
+// The reference (examples/server_aggregation/fedadp/fedadp_server.py:91-99, 122-133) flattens
+// every client delta with process_grad — entries sorted by name.lower(), all but the first
+// divided by -lr — and takes numpy's float32 np.inner(g, loc_k) and np.linalg.norm(loc_k)
+// (sqrt of loc_k . loc_k), i.e. cblas_sdot of numpy's OpenBLAS: on AVX-512 hosts
+// sdot_k_SKYLAKEX, 64 fma chains (chain j sums positions = j mod 64, serially over the
+// 64-element blocks), a fold, one 32-element block, a fixed horizontal sum and a float64 tail.
+//
+// plato_agg_flatten + plato_agg_sdot_shared (flat.hip) materialise the K flattened deltas
+// (5.7 GB for 128 ResNet-18 clients written and read again).  Here the flattening is folded
+// into the dot kernel: producer waves gather positions from the staged arenas through the
+// segment map, form loc = (x - b) or -(x - b) / lr in registers and write them transposed
+// into an LDS tile; chain waves only run the fma chains out of LDS.
+//
+// Shape (one workgroup per CU for 128 clients):
+//   * 8 pairs (clients, all sharing g) x 4 of the 64 chains per workgroup; the 16 chain groups
+//     of a pair group run on one XCD, so every 128-byte line of an arena, of b and of g is
+//     fetched from HBM once and served to the other chain groups from that XCD's L2.
+//   * chain wave: lane = kind * 32 + chain * 8 + pair, kind 0 = g . loc, kind 1 = loc . loc:
+//     ONE dependent fma per step per lane (the dots are split over lanes, not interleaved),
+//     4 steps per ds_read_b128 of a transposed row; row pitch 260 floats and vector pitch
+//     4 rows make both reads of a step and the producers' ds_write_b32 conflict-free
+//     (2-way on the writes, which is free: MI355X_MICROARCH.md §LDS).
+//   * 8 producer waves, 2 gather iterations each per 256-block stage; their global loads run
+//     two stages ahead of the tile being written (two register sets, A and B), the tile ring
+//     has two slots, one s_barrier per stage.
+//   * g . g: an extra chain wave in the workgroups of pair group 0 (x . x over the same tile).
+// Compiled with -ffp-contract=off; the chain fma is an explicit v_fma_f32.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "common.h"
+#include "plato_agg.h"
+
+using plato_agg_internal::clear_error;
+using plato_agg_internal::set_error;
+
+namespace {
+
+int check_launch(const char* what) {
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(PLATO_AGG_EHIP, std::string(what) + ": " + hipGetErrorString(err));
+  return clear_error();
+}
+
+template <class T>
+__device__ __forceinline__ T sld(const T* p, int i) {
+  return ((__attribute__((address_space(4))) const T*)p)[i];
+}
+
+__device__ __forceinline__ float chain_fma(float a, float b, float c) {
+  asm("v_fma_f32 %0, %1, %2, %0" : "+v"(c) : "v"(a), "v"(b));
+  return c;
+}
+
+typedef __attribute__((address_space(1))) const float gfloat;
+
+// Segment map entry in LDS: positions [flat, end) read element src + (p - flat) of the region.
+struct AdpSeg {
+  uint32_t flat;
+  uint32_t end;
+  uint32_t src;
+  uint32_t info;  // bit 0: int64 region, bit 1: NEG_DIV
+};
+constexpr uint32_t kSegI64 = 1u, kSegNeg = 2u;
+constexpr int kMaxSegs = 2048;
+
+struct AdpArgs {
+  const float* x;                // flattened global gradient (process_grad(g)), >= nsteps * 64 floats
+  const float* const* xf;        // client fp32 arenas
+  const int64_t* const* xi;      // client int64 arenas
+  const float* base_f;
+  const int64_t* base_i;
+  const plato_agg_segment* segs;
+  uint32_t n_segs;
+  uint64_t n;                    // flat length
+  uint64_t nsteps;               // whole 64-element blocks before sdot's 32-block and tail
+  float lr;
+  float* ws;                     // [n_pairs + with_xx][128]: chain sums of x.y, then of y.y
+  float* y64;                    // [n_pairs][n_i64]: process_grad's value of every int64 element
+  uint64_t n_i64;
+  uint64_t n_f32;                // fp32 arena length (buffer bounds)
+  int n_pairs;
+  int with_xx;
+};
+
+// process_grad's value at one position, from the client's staged arena (flat.hip flat_value, DELTA)
+__device__ __forceinline__ float adp_f32(float x, float b, bool neg, float lr) {
+  float v = x - b;
+  if (neg) v = (-v) / lr;
+  return v;
+}
+__device__ __forceinline__ float adp_i64(int64_t x, int64_t b, bool neg, float lr) {
+  // int64 delta, exact (wrapping) in int64; -delta too, then the cast and the division
+  const uint64_t d = uint64_t(x) - uint64_t(b);
+  return neg ? float(int64_t(uint64_t(0) - d)) / lr : float(int64_t(d));
+}
+
+// The last segment with flat <= p, walking forward from `from` (segments are in flat order).
+__device__ __forceinline__ int seg_walk(const AdpSeg* S, int n_segs, uint32_t p, int from) {
+  int s = from;
+  while (s + 1 < n_segs && S[s + 1].flat <= p) ++s;
+  return s;
+}
+
+// kP pairs x kC chains per workgroup (kP * kC = 32: one chain wave of 2 kinds); kS steps per
+// stage; kW producer waves, kIt gather iterations of 64 positions each per stage; kVRpad floats
+// between vectors (chosen with the row pitch kS + 4 so that the chain wave's ds_read_b128 pairs
+// are conflict-free for the lane map kind * 32 + chain * kP + pair: DESIGN.md §12)
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad = 0>
+struct AdpShape {
+  static_assert(kP * kC == 32, "one chain wave: kind * 32 + chain * kP + pair");
+  static_assert(kS * kC == 64 * kW * kIt, "a stage is kW x kIt gather iterations of 64 positions");
+  static_assert(kS % 16 == 0, "the chain wave reads 16 steps per block");
+  static constexpr int kR = kS + 4;          // transposed row pitch (floats)
+  static constexpr int kVR = kC * kR + kVRpad;  // rows of one vector (x, loc_0 .. loc_{kP-1})
+  static constexpr int kSlot = (1 + kP) * kVR;
+  static constexpr int kBlkPerIt = 64 / kC;  // 64-blocks per gather iteration
+};
+
+// One producer wave's loads for one stage: x, b and the kP arenas at kIt positions per lane.
+template <int kP, int kIt>
+struct AdpRegs {
+  float x[kIt];
+  float b[kIt];
+  float y[kIt][kP];
+  uint32_t code[kIt];  // per lane: kSegNeg; kSegI64 (+ element << 8): an int64 position, fetched at write time
+  uint32_t fast;       // bit i: iteration i lies in one fp32 entry (wave-uniform)
+};
+
+// Buffer resources of a producer wave: raw buffer loads take a 32-bit byte offset per lane against
+// a descriptor in SGPRs, so a gathered load costs no 64-bit address arithmetic (and an offset past
+// num_records reads 0 instead of faulting).
+template <int kP>
+struct AdpSrc {
+  __amdgpu_buffer_rsrc_t x, b, y[kP];
+};
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t adp_rsrc(const void* base, uint64_t bytes) {
+  const uint64_t n = bytes < 0xffffffffull ? bytes : 0xffffffffull;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)uint32_t(n), 0x00020000);
+}
+
+__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
+}
+
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+__device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpSeg* S, int n_segs, int& cursor,
+                                          const AdpSrc<kP>& src, uint32_t t, int cg, int w, int lane,
+                                          AdpRegs<kP, kIt>& r) {
+  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad>;
+  const uint32_t last = uint32_t(a.nsteps - 1);
+  r.fast = 0;
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const int g = i * kW + w;
+    const uint32_t s0 = t * kS + uint32_t(g * Sh::kBlkPerIt);  // nsteps < 2^26: 32-bit block indices
+    const uint32_t s = min(s0 + uint32_t(lane / kC), last);     // a ragged last stage re-reads a valid block
+    const uint32_t p = s * 64 + uint32_t(cg * kC + lane % kC);
+    const uint32_t pf = min(s0, last) * 64 + uint32_t(cg * kC);
+    const uint32_t pl = min(s0 + uint32_t(Sh::kBlkPerIt - 1), last) * 64 + uint32_t(cg * kC + kC - 1);
+    cursor = __builtin_amdgcn_readfirstlane(seg_walk(S, n_segs, pf, cursor));
+    const AdpSeg cs = S[cursor];
+    uint32_t e, code;
+    // the loads below are the same on both paths (no branch around them): every trip issues
+    // kIt * (kP + 2) loads and the compiler's vmcnt bookkeeping covers exactly one stage
+    if (__builtin_amdgcn_readfirstlane(int(!(cs.info & kSegI64) && pl < cs.end))) {
+      r.fast |= 1u << i;  // the whole iteration inside one fp32 entry: one shift for every lane
+      e = p - cs.flat + cs.src;
+      code = cs.info;
+    } else {  // an entry boundary inside the iteration: per-lane entries
+      const AdpSeg ls = S[seg_walk(S, n_segs, p, cursor)];
+      const uint32_t el = p - ls.flat + ls.src;
+      const bool i64 = ls.info & kSegI64;
+      e = i64 ? 0u : el;
+      code = i64 ? (ls.info | (el << 8)) : ls.info;
+    }
+    r.code[i] = code;
+    r.x[i] = bload(src.x, p * 4u);
+    r.b[i] = bload(src.b, e * 4u);
+#pragma unroll
+    for (int k = 0; k < kP; ++k) r.y[i][k] = bload(src.y[k], e * 4u);
+  }
+}
+
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+__device__ __forceinline__ void adp_write(const AdpArgs& a, float* slot, int pair0, int w, int lane,
+                                          AdpRegs<kP, kIt>& r) {
+  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad>;
+  const float lr = a.lr;
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const int g = i * kW + w;
+    const int col = g * Sh::kBlkPerIt + lane / kC;  // step within the stage
+    float* dst = slot + (lane % kC) * Sh::kR + col;
+    dst[0] = r.x[i];
+    const uint32_t code = r.code[i];
+    if (r.fast & (1u << i)) {  // wave-uniform: one entry, one sign/divide mode
+      if (__builtin_amdgcn_readfirstlane(int(code)) & kSegNeg) {
+#pragma unroll
+        for (int k = 0; k < kP; ++k) dst[(1 + k) * Sh::kVR] = (-(r.y[i][k] - r.b[i])) / lr;
+      } else {
+#pragma unroll
+        for (int k = 0; k < kP; ++k) dst[(1 + k) * Sh::kVR] = r.y[i][k] - r.b[i];
+      }
+    } else {
+      const bool neg = code & kSegNeg;
+      if (code & kSegI64) {
+        // rare (one per int64 entry and chain group): the finished value from fedadp_i64_kernel's table
+#pragma unroll
+        for (int k = 0; k < kP; ++k) {
+          const int pair = pair0 + k < a.n_pairs ? pair0 + k : a.n_pairs - 1;
+          r.y[i][k] = a.y64[uint64_t(pair) * a.n_i64 + (code >> 8)];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < kP; ++k)
+        dst[(1 + k) * Sh::kVR] = (code & kSegI64) ? r.y[i][k] : adp_f32(r.y[i][k], r.b[i], neg, lr);
+    }
+  }
+}
+
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+__global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
+  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad>;
+  __shared__ __attribute__((aligned(16))) float ring[2 * Sh::kSlot];
+  __shared__ AdpSeg S[kMaxSegs];
+  constexpr int kGroups = 64 / kC;
+  // workgroups are dealt to the 8 XCDs round-robin: the kGroups chain groups of a pair group
+  // get ids that agree mod 8, so they share one XCD and its L2
+  const int b = int(blockIdx.x), lo = b & 7;
+  const int cg = (b / 8) % kGroups;
+  const int pg = (b / (8 * kGroups)) * 8 + lo;
+  if (pg * kP >= a.n_pairs) return;  // padding workgroup (before any barrier)
+  const int n_segs = int(a.n_segs);
+  for (int j = int(threadIdx.x); j < n_segs; j += int(blockDim.x)) {
+    const plato_agg_segment sg = a.segs[j];
+    S[j] = AdpSeg{uint32_t(sg.flat_offset), uint32_t(sg.flat_offset + sg.numel), uint32_t(sg.src_offset),
+                  (sg.region ? kSegI64 : 0u) | ((sg.flags & PLATO_AGG_SEG_NEG_DIV) ? kSegNeg : 0u)};
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = int(threadIdx.x & 63);
+  const uint64_t nsteps = a.nsteps;
+  const uint64_t nst = (nsteps + kS - 1) / kS;
+  const uint64_t nst2 = (nst + 1) & ~uint64_t(1);  // barriers: one per stage, in pairs
+  if (wave >= 2) {  // producer
+    const int w = wave - 2;
+    const int pair0 = pg * kP;
+    AdpSrc<kP> src;
+    src.x = adp_rsrc(a.x, a.nsteps * 256);
+    src.b = adp_rsrc(a.base_f, a.n_f32 * 4);
+#pragma unroll
+    for (int k = 0; k < kP; ++k)
+      src.y[k] = adp_rsrc(sld(a.xf, pair0 + k < a.n_pairs ? pair0 + k : a.n_pairs - 1), a.n_f32 * 4);
+    int cursor = 0;
+    AdpRegs<kP, kIt> ra, rb;
+    adp_issue<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, cursor, src, 0, cg, w, lane, ra);
+    adp_issue<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, cursor, src, 1, cg, w, lane, rb);
+    // whole pairs of stages (an odd count gets one idle trip): no branch inside the loop, so the
+    // compiler's vmcnt bookkeeping sees the same two stages in flight on every trip
+    for (uint32_t t = 0; t < uint32_t(nst2); t += 2) {
+      adp_write<kP, kC, kS, kW, kIt, kVRpad>(a, ring, pair0, w, lane, ra);
+      // past the last stage (t = nst) every position clamps to the last block: valid addresses,
+      // never consumed, and every trip issues the same loads
+      adp_issue<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, cursor, src, t + 2 < nst ? t + 2 : uint32_t(nst), cg, w,
+                                             lane, ra);
+      __builtin_amdgcn_s_barrier();  // stage t published in slot 0
+      adp_write<kP, kC, kS, kW, kIt, kVRpad>(a, ring + Sh::kSlot, pair0, w, lane, rb);
+      adp_issue<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, cursor, src, t + 3 < nst ? t + 3 : uint32_t(nst), cg, w,
+                                             lane, rb);
+      __builtin_amdgcn_s_barrier();  // stage t + 1 published in slot 1
+    }
+    return;
+  }
+  // chain waves: wave 0 the kP pairs' dots, wave 1 g . g (pair group 0 only; elsewhere it only
+  // keeps the barrier count)
+  __builtin_amdgcn_s_setprio(3);
+  const bool xx = wave == 1;
+  const bool active = !xx || (pg == 0 && a.with_xx);
+  const int kind = xx ? 0 : lane >> 5, c = xx ? lane % kC : (lane & 31) / kP, p = lane % kP;
+  const int arow = (xx || kind == 0 ? 0 : (1 + p) * Sh::kVR) + c * Sh::kR;
+  const int brow = (xx ? 0 : (1 + p) * Sh::kVR) + c * Sh::kR;
+  float acc = 0.f;
+  for (uint64_t t = 0; t < nst2; ++t) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (!active || t >= nst) continue;
+    const float* slot = ring + (t & 1) * Sh::kSlot;
+    const float* A = slot + arow;
+    const float* B = slot + brow;
+    const uint64_t left = nsteps - t * kS;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    if (left >= uint64_t(kS)) {
+      // 16 steps per block of 4 ds_read_b128 pairs, the next block's reads in flight
+      f4 av[4], bv[4], an[4], bn[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        av[q] = *reinterpret_cast<const f4*>(A + 4 * q);
+        bv[q] = *reinterpret_cast<const f4*>(B + 4 * q);
+      }
+#pragma unroll
+      for (int blk = 0; blk < kS / 16; ++blk) {
+        if (blk + 1 < kS / 16) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            an[q] = *reinterpret_cast<const f4*>(A + 16 * (blk + 1) + 4 * q);
+            bn[q] = *reinterpret_cast<const f4*>(B + 16 * (blk + 1) + 4 * q);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc = chain_fma(av[q].x, bv[q].x, acc);
+          acc = chain_fma(av[q].y, bv[q].y, acc);
+          acc = chain_fma(av[q].z, bv[q].z, acc);
+          acc = chain_fma(av[q].w, bv[q].w, acc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          av[q] = an[q];
+          bv[q] = bn[q];
+        }
+      }
+    } else {
+      for (int s = 0; s < int(left); ++s) acc = chain_fma(A[s], B[s], acc);
+    }
+  }
+  const int chain = cg * kC + c;
+  if (!xx) {
+    const int pair = pg * kP + p;
+    if (pair < a.n_pairs) a.ws[uint64_t(pair) * 128 + uint64_t(kind) * 64 + chain] = acc;
+  } else if (active && lane < kC) {  // the virtual pair (g, g): its x.y and y.y chains are both g.g
+    a.ws[uint64_t(a.n_pairs) * 128 + chain] = acc;
+    a.ws[uint64_t(a.n_pairs) * 128 + 64 + chain] = acc;
+  }
+}
+
+// process_grad's value of every int64 element (num_batches_tracked deltas), per pair: the gather
+// reads these finished values instead of doing int64 arithmetic in the stream
+__global__ __launch_bounds__(64) void fedadp_i64_kernel(AdpArgs a) {
+  const int pair = blockIdx.x;
+  const int64_t* xi = a.xi[pair];
+  for (uint32_t j = 0; j < a.n_segs; ++j) {
+    const plato_agg_segment sg = a.segs[j];
+    if (!sg.region) continue;
+    const bool neg = sg.flags & PLATO_AGG_SEG_NEG_DIV;
+    for (uint64_t q = threadIdx.x; q < sg.numel; q += 64) {
+      const uint64_t e = sg.src_offset + q;
+      a.y64[uint64_t(pair) * a.n_i64 + e] = adp_i64(xi[e], a.base_i[e], neg, a.lr);
+    }
+  }
+}
+
+// process_grad's value at any position (binary search of the segment map; the epilogue's few positions)
+__device__ float adp_y_at(const AdpArgs& a, int pair, uint64_t p) {
+  uint32_t lo = 0, hi = a.n_segs;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.segs[mid].flat_offset <= p) lo = mid; else hi = mid;
+  }
+  const plato_agg_segment sg = a.segs[lo];
+  const uint64_t e = sg.src_offset + (p - sg.flat_offset);
+  const bool neg = sg.flags & PLATO_AGG_SEG_NEG_DIV;
+  if (sg.region) return adp_i64(a.xi[pair][e], a.base_i[e], neg, a.lr);
+  return adp_f32(a.xf[pair][e], a.base_f[e], neg, a.lr);
+}
+
+// The rest of sdot_k_SKYLAKEX per pair from the 64 chain sums (flat.hip sdot_finish_kernel), with
+// the 32-element block and the float64 tail gathered from the arenas.
+__global__ __launch_bounds__(64) void fedadp_finish_kernel(AdpArgs a, float* out_xy, float* out_yy) {
+  const int pair = blockIdx.x, lane = threadIdx.x & 63;
+  const bool virt = pair >= a.n_pairs;  // (g, g)
+  const uint64_t n = a.n;
+  const uint64_t n1 = n & ~uint64_t(31);
+  const uint64_t n64 = n1 & ~uint64_t(63);
+  auto yv_at = [&](uint64_t p) { return virt ? a.x[p] : adp_y_at(a, pair, p); };
+  const float axy = a.ws[uint64_t(pair) * 128 + lane];
+  const float ayy = a.ws[uint64_t(pair) * 128 + 64 + lane];
+  const float hxy = __shfl(axy, (lane + 8) & 63, 64);
+  const float hyy = __shfl(ayy, (lane + 8) & 63, 64);
+  const int r = lane >> 4, l = lane & 15;
+  float bxy = 0.f, byy = 0.f;
+  if (l < 8) {
+    bxy = axy + hxy;
+    byy = ayy + hyy;
+    if (n1 > n64) {
+      const float xv = a.x[n64 + 8 * r + l];
+      const float yv = yv_at(n64 + 8 * r + l);
+      bxy = __builtin_fmaf(xv, yv, bxy);
+      byy = __builtin_fmaf(yv, yv, byy);
+    }
+  }
+  const float xy1 = __shfl(bxy, 16 + l, 64), xy2 = __shfl(bxy, 32 + l, 64), xy3 = __shfl(bxy, 48 + l, 64);
+  const float yy1 = __shfl(byy, 16 + l, 64), yy2 = __shfl(byy, 32 + l, 64), yy3 = __shfl(byy, 48 + l, 64);
+  const float sxy = ((bxy + xy1) + xy2) + xy3;
+  const float syy = ((byy + yy1) + yy2) + yy3;
+  const float sxy4 = __shfl(sxy, (lane + 4) & 63, 64);
+  const float syy4 = __shfl(syy, (lane + 4) & 63, 64);
+  const float hx = sxy + sxy4, hy = syy + syy4;
+  const float hx1 = __shfl(hx, 1, 64), hx2 = __shfl(hx, 2, 64), hx3 = __shfl(hx, 3, 64);
+  const float hy1 = __shfl(hy, 1, 64), hy2 = __shfl(hy, 2, 64), hy3 = __shfl(hy, 3, 64);
+  // the < 32 tail positions: gathered by one lane each, then summed by lane 0 in order
+  __shared__ float txy_s[32], tyy_s[32];
+  if (uint64_t(lane) < n - n1) {
+    const float xv = a.x[n1 + lane], yv = yv_at(n1 + lane);
+    txy_s[lane] = yv * xv;
+    tyy_s[lane] = yv * yv;
+  }
+  __syncthreads();
+  if (lane != 0) return;
+  double kxy = 0.0, kyy = 0.0;
+  if (n1) {
+    kxy = double((hx + hx1) + (hx2 + hx3));
+    kyy = double((hy + hy1) + (hy2 + hy3));
+  }
+  double txy = 0.0, tyy = 0.0;  // the scalar tail in float64, products rounded to fp32 first
+  for (int i = 0; i < int(n - n1); ++i) {
+    txy += double(txy_s[i]);
+    tyy += double(tyy_s[i]);
+  }
+  out_xy[pair] = float(txy + kxy);
+  out_yy[pair] = float(tyy + kyy);
+}
+
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+void launch_adp(const AdpArgs& a, hipStream_t st) {
+  constexpr int kGroups = 64 / kC;
+  uint32_t pgs = uint32_t((a.n_pairs + kP - 1) / kP);
+  pgs = (pgs + 7) / 8 * 8;  // whole XCD rounds (padding workgroups return at once)
+  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad>), dim3(pgs * kGroups), dim3(64 * (kW + 2)), 0,
+                     st, a);
+}
+using AdpFn = void (*)(const AdpArgs&, hipStream_t);
+// pairs x chains per workgroup, steps per stage, producer waves, iterations, vector pad
+const AdpFn kAdpVariants[] = {
+    &launch_adp<8, 4, 256, 8, 2, 0>,     // 0: 16 B per block per vector, x and b shared by 8 pairs
+    &launch_adp<4, 8, 256, 8, 4, 16>,    // 1: 32 B
+    &launch_adp<2, 16, 256, 8, 8, 32>,   // 2: 64 B
+    &launch_adp<1, 32, 128, 8, 8, 0>,    // 3: whole 128-byte lines, x and b per pair (from L2)
+};
+constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
+
+int run_fedadp(int variant, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
+               const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs, uint32_t n_segs,
+               size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
+               float* d_out_yy, hipStream_t stream);
+
+}  // namespace
+
+extern "C" {
+
+size_t plato_agg_fedadp_dots_workspace(int n_pairs, int with_xx, size_t n_i64) {
+  const size_t k = size_t(n_pairs > 0 ? n_pairs : 0);
+  return ((k + (with_xx ? 1 : 0)) * 128 + k * n_i64) * sizeof(float);
+}
+
+int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
+                          const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
+                          uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
+                          float* d_out_xy, float* d_out_yy, hipStream_t stream) {
+  return run_fedadp(0, d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32, d_base_i64, d_segs, n_segs, n_flat, n_f32,
+                    n_i64, lr, with_xx, d_workspace, d_out_xy, d_out_yy, stream);
+}
+
+#ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
+int plato_agg_tune_num_fedadp_variants(void) { return kNumAdpVariants; }
+
+int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const* d_src_f32,
+                               const void* const* d_src_i64, int n_pairs, const float* d_base_f32,
+                               const int64_t* d_base_i64, const plato_agg_segment* d_segs, uint32_t n_segs,
+                               size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
+                               float* d_out_yy, hipStream_t stream) {
+  return run_fedadp(variant, d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32, d_base_i64, d_segs, n_segs, n_flat,
+                    n_f32, n_i64, lr, with_xx, d_workspace, d_out_xy, d_out_yy, stream);
+}
+#endif  // PLATO_AGG_TUNE
+
+}  // extern "C"
+
+namespace {
+int run_fedadp(int variant, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
+               const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs, uint32_t n_segs,
+               size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
+               float* d_out_yy, hipStream_t stream) {
+  if (variant < 0 || variant >= kNumAdpVariants) return set_error(PLATO_AGG_EINVAL, "bad fedadp_dots variant");
+  if (n_pairs <= 0 || n_pairs > (1 << 20)) return set_error(PLATO_AGG_EINVAL, "n_pairs must be in [1, 2^20]");
+  if (with_xx != 0 && with_xx != 1) return set_error(PLATO_AGG_EINVAL, "with_xx must be 0 or 1");
+  if (!d_x || !d_src_f32 || !d_src_i64 || !d_base_f32 || !d_segs || !d_workspace || !d_out_xy || !d_out_yy ||
+      (n_i64 && !d_base_i64))
+    return set_error(PLATO_AGG_EINVAL, "null pointer");
+  if (reinterpret_cast<uintptr_t>(d_x) & 15u) return set_error(PLATO_AGG_EINVAL, "x must be 16-byte aligned");
+  if (n_segs == 0 || n_segs > uint32_t(kMaxSegs))
+    return set_error(PLATO_AGG_EINVAL, "segment count must be in [1, 2048]");
+  if (n_flat == 0 || n_flat >= (size_t(1) << 32)) return set_error(PLATO_AGG_EINVAL, "flat length must be in [1, 2^32)");
+  if (n_f32 >= (size_t(1) << 30)) return set_error(PLATO_AGG_EINVAL, "fp32 arena must be < 2^30 elements");
+  AdpArgs a{};
+  a.x = d_x;
+  a.xf = reinterpret_cast<const float* const*>(d_src_f32);
+  a.xi = reinterpret_cast<const int64_t* const*>(d_src_i64);
+  a.base_f = d_base_f32;
+  a.base_i = d_base_i64;
+  a.segs = d_segs;
+  a.n_segs = n_segs;
+  a.n = n_flat;
+  a.nsteps = (uint64_t(n_flat) & ~uint64_t(31)) / 64;
+  a.lr = lr;
+  a.ws = static_cast<float*>(d_workspace);
+  a.y64 = a.ws + (uint64_t(n_pairs) + (with_xx ? 1 : 0)) * 128;
+  a.n_i64 = n_i64;
+  a.n_f32 = n_f32;
+  a.n_pairs = n_pairs;
+  a.with_xx = with_xx;
+  if (n_i64) {
+    hipLaunchKernelGGL(fedadp_i64_kernel, dim3(uint32_t(n_pairs)), dim3(64), 0, stream, a);
+    if (int rc = check_launch("fedadp_i64 launch")) return rc;
+  }
+  if (a.nsteps) {
+    kAdpVariants[variant](a, stream);
+    if (int rc = check_launch("fedadp_dots launch")) return rc;
+  } else {
+    (void)hipMemsetAsync(d_workspace, 0, (size_t(n_pairs) + (with_xx ? 1 : 0)) * 128 * sizeof(float), stream);
+  }
+  hipLaunchKernelGGL(fedadp_finish_kernel, dim3(uint32_t(n_pairs + with_xx)), dim3(64), 0, stream, a, d_out_xy,
+                     d_out_yy);
+  return check_launch("fedadp_finish launch");
+}
+}  // namespace

@@ -379,6 +379,7 @@ constexpr Variant make_variant() {
 
 // Variant 0 is the default of the public entry points (fastest in the
 // interleaved sweep on MI355X).
+#ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so: every variant (bench.py --sweep, scripts/)
 const Variant kVariants[] = {
     make_variant<Cfg<256, 1, 8, true, true, false>>(),              // 0 (default): NT loads + NT stores
     make_variant<Cfg<256, 2, 8, false, false, false>>(),            // 1 first version
@@ -399,6 +400,11 @@ const Variant kVariants[] = {
     make_variant<Cfg<1024, 1, 8, true, true, false, false, 0, true>>(),  // 16 XCD, 1024 threads
     make_variant<Cfg<256, 1, 16, true, true, false, false, 0, true>>(),  // 17 XCD, U=16
 };
+#else  // libplato_agg.so: the default only
+const Variant kVariants[] = {
+    make_variant<Cfg<256, 1, 8, true, true, false>>(),              // 0 (default): NT loads + NT stores
+};
+#endif
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);
 
 // Tuning/test knob: f4 groups per launch (0 = the 4 GiB limit); lets tests
@@ -677,12 +683,18 @@ struct Bf16Variant {
   Bf16Fn fn[2];
 };
 // variant 0 is the default of plato_agg_fedavg_weights_bf16
+#ifdef PLATO_AGG_TUNE
 const Bf16Variant kBf16Variants[] = {
     {4, 8, {&launch_bf16<false, 4, 8>, &launch_bf16<true, 4, 8>}},
     {8, 8, {&launch_bf16<false, 8, 8>, &launch_bf16<true, 8, 8>}},
     {4, 16, {&launch_bf16<false, 4, 16>, &launch_bf16<true, 4, 16>}},
     {8, 4, {&launch_bf16<false, 8, 4>, &launch_bf16<true, 8, 4>}},
 };
+#else
+const Bf16Variant kBf16Variants[] = {
+    {4, 8, {&launch_bf16<false, 4, 8>, &launch_bf16<true, 4, 8>}},
+};
+#endif
 constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
 
 // ---------------------------------------------------------------------------
@@ -1117,6 +1129,7 @@ int plato_agg_fedavg_weights_bf16(const uint16_t* const* d_x_bf16, const uint16_
                   n_i64, stream);
 }
 
+#ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h: libplato_agg_tune.so only
 int plato_agg_tune_num_bf16_variants(void) { return kNumBf16Variants; }
 
 int plato_agg_tune_fedavg_bf16(int variant, const uint16_t* const* d_x_bf16, const uint16_t* const* d_x_i64_bf16,
@@ -1161,6 +1174,7 @@ int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n, 
   }
   return check_launch("stream probe launch");
 }
+#endif  // PLATO_AGG_TUNE
 
 int plato_agg_compute_deltas(const float* d_x_f32, const int64_t* d_x_i64, const float* d_base_f32,
                              const int64_t* d_base_i64, float* d_out_f32, int64_t* d_out_i64, size_t n_f32,

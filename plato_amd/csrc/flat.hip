@@ -537,6 +537,7 @@ void launch_sdot_shared(const SdotSArgs& a, hipStream_t st) {
                        st, a);
 }
 // pairs per workgroup x chains per workgroup x blocks per stage x stages x producer waves
+#ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so: every shape
 const SdotSFn kSdotSVariants[] = {
     &launch_sdot_shared<4, 16, 64, 6, 4>,   // 0: 64 B of each block per vector
     &launch_sdot_shared<2, 32, 32, 8, 3>,   // 1: 128 B per block, x shared by 2 pairs
@@ -553,15 +554,24 @@ const SdotSFn kSdotSVariants[] = {
     &launch_sdot_shared<2, 16, 64, 4, 3, true>,   // 10
     &launch_sdot_shared<1, 16, 64, 4, 2, true>,   // 11
 };
+constexpr int kSdotV5 = 5, kSdotV8 = 8, kSdotV11 = 11;
+#else  // libplato_agg.so: the three defaults of default_sdot_variant
+const SdotSFn kSdotSVariants[] = {
+    &launch_sdot_shared<4, 16, 64, 6, 4, true>,  // tune variant 5
+    &launch_sdot_shared<2, 16, 64, 6, 4, true>,  // tune variant 8
+    &launch_sdot_shared<1, 16, 64, 4, 2, true>,  // tune variant 11
+};
+constexpr int kSdotV5 = 0, kSdotV8 = 1, kSdotV11 = 2;
+#endif
 constexpr int kNumSdotSVariants = sizeof(kSdotSVariants) / sizeof(kSdotSVariants[0]);
 
 // The default by size: with x.x folded in, as many workgroups as CUs when the pairs allow it (a CU's
 // stream, ~24 GB/s, is what bounds a workgroup): 128 pairs -> 2 pairs x 16 chains per workgroup,
 // 64 x 4 = 256 workgroups; otherwise variant 5.
 int default_sdot_variant(int n_pairs, int with_xx) {
-  if (with_xx && n_pairs <= 64) return 11;
-  if (with_xx && n_pairs <= 128) return 8;
-  return 5;
+  if (with_xx && n_pairs <= 64) return kSdotV11;
+  if (with_xx && n_pairs <= 128) return kSdotV8;
+  return kSdotV5;
 }
 
 int run_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n, int with_xx,
@@ -1021,6 +1031,7 @@ int plato_agg_sdot_shared(const float* d_x, const float* const* d_y, int n_pairs
   return run_sdot_shared(-1, d_x, d_y, n_pairs, n, with_xx, d_workspace, d_out_xy, d_out_yy, stream);
 }
 
+#ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
 int plato_agg_tune_num_sdot_shared_variants(void) { return kNumSdotSVariants; }
 
 int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n,
@@ -1029,6 +1040,7 @@ int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const
   if (variant < 0) return set_error(PLATO_AGG_EINVAL, "bad sdot_shared variant");
   return run_sdot_shared(variant, d_x, d_y, n_pairs, n, with_xx, d_workspace, d_out_xy, d_out_yy, stream);
 }
+#endif  // PLATO_AGG_TUNE
 
 size_t plato_agg_torch_cosine_workspace(int K, int threads) {
   return size_t(K > 0 ? K : 0) * size_t(threads > 0 ? threads : 1) * sizeof(float);

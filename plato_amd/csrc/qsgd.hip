@@ -746,6 +746,7 @@ struct QVariant {
   int block, u, g;  // threads, clients per table batch, elements per lane
   QFn fn[2];        // [TWO]
 };
+#ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so: every shape (scripts/, tests/test_qsgd_gpu.py)
 const QVariant kQVariants[] = {
     {512, 4, 8, {&launch_qp<512, 4, false, 8>, &launch_qp<512, 4, true, 8>}},  // 0 (default): pipelined
     {256, 8, 16, {&launch_q<256, 8, false>, &launch_q<256, 8, true>}},      // 1
@@ -816,6 +817,11 @@ const QVariant kQVariants[] = {
     {512, 32, 4, {&launch_qr<512, 16, false, 4, 32>, &launch_qr<512, 16, true, 4, 32>}},        // 59
     {512, 32, 4, {&launch_qr<512, 8, false, 4, 32>, &launch_qr<512, 8, true, 4, 32>}},          // 60
 };
+#else  // libplato_agg.so: the default only
+const QVariant kQVariants[] = {
+    {512, 4, 8, {&launch_qp<512, 4, false, 8>, &launch_qp<512, 4, true, 8>}},  // 0 (default): pipelined
+};
+#endif
 constexpr int kNumQVariants = sizeof(kQVariants) / sizeof(kQVariants[0]);
 
 bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
@@ -880,6 +886,7 @@ int plato_agg_fedavg_qsgd(const uint8_t* const* d_codes_f32, const uint8_t* cons
                   d_chunks_i64, n_chunks_i64, d_base_f32, d_base_i64, d_out_f32, d_out_i64f, n_f32, n_i64, stream);
 }
 
+#ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
 int plato_agg_tune_num_qsgd_variants(void) { return kNumQVariants; }
 
 int plato_agg_tune_qsgd_chunk(int variant) {
@@ -897,5 +904,6 @@ int plato_agg_tune_fedavg_qsgd(int variant, const uint8_t* const* d_codes_f32, c
                   n_chunks_f32, d_chunks_i64, n_chunks_i64, d_base_f32, d_base_i64, d_out_f32, d_out_i64f, n_f32,
                   n_i64, stream);
 }
+#endif  // PLATO_AGG_TUNE
 
 }  // extern "C"

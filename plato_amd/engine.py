@@ -342,7 +342,7 @@ class FedAvgEngine:
                 _lib.call("plato_agg_fedavg_deltas", _ptr(ptr_f32), ptr_i, _ptr(w), _ptr(s), k,
                           _ptr(out_f32), _ptr(out_i64f) if n_i else None, *args_tail)
         else:
-            _lib.call("plato_agg_tune_fedavg", self.variant, int(base_f32 is not None), _ptr(ptr_f32),
+            _lib.tune_call("plato_agg_tune_fedavg", self.variant, int(base_f32 is not None), _ptr(ptr_f32),
                       ptr_i, _ptr(w), _ptr(s), k, _ptr(base_f32),
                       _ptr(base_i64) if n_i else None, _ptr(out_f32),
                       _ptr(out_i64f) if n_i else None, *args_tail)
@@ -629,7 +629,7 @@ class AggregationRound:
             if eng.qsgd_variant is None:
                 _lib.call("plato_agg_fedavg_qsgd", *args)
             else:  # tuning / tests
-                _lib.call("plato_agg_tune_fedavg_qsgd", eng.qsgd_variant, *args)
+                _lib.tune_call("plato_agg_tune_fedavg_qsgd", eng.qsgd_variant, *args)
             w = (w, mv)
         elif self.codec == "bf16":
             n_i = lay.n_i64
@@ -856,27 +856,67 @@ class AggregationRound:
         self._keep_flat = ptrs
         return out, stride
 
-    def fedadp_dots(self, grads: tuple[torch.Tensor, torch.Tensor], slots: Sequence[int], lr: float,
-                    batch_bytes: float = 32e9):
-        """FedAdp's float32 reductions of process_grad's flattened vectors, bit-exact.
-
-        ``grads`` is the device global gradient (fp32 arena, fp32 values of the
-        int64 entries), e.g. :meth:`launch_entrywise` with ``device=True``.
-        Returns ``(inner[K], g_sq, l_sq[K])`` as numpy float32: ``np.inner(g,
-        loc_k)``, ``g.dot(g)``, ``loc_k.dot(loc_k)`` exactly as numpy's OpenBLAS
-        forms them (examples/server_aggregation/fedadp/fedadp_server.py:91-99,
-        ``plato_agg_flatten`` + ``plato_agg_sdot_shared``: every pair shares x = g).
-        """
-        slots = self._check_slots(slots)
-        if not self.has_baseline:
-            raise ValueError("baseline not staged")
-        eng, lay = self.engine, self.layout
+    def _fedadp_order(self):
+        lay = self.layout
         names = lay.keys()
         order = sorted(range(len(names)), key=lambda i: names[i].lower())
         if order and lay.entries[order[0]].region != F32:
             raise ValueError("FedAdp: the first entry in name order is int64, so the reference flattens to "
                              "float64 (np.append) and takes float64 dots; the device path reproduces the "
                              "float32 case only")
+        return order
+
+    def fedadp_dots(self, grads: tuple[torch.Tensor, torch.Tensor], slots: Sequence[int], lr: float):
+        """FedAdp's float32 reductions of process_grad's flattened vectors, bit-exact.
+
+        ``grads`` is the device global gradient (fp32 arena, fp32 values of the
+        int64 entries), e.g. :meth:`launch_entrywise` with ``device=True``.
+        Returns ``(inner[K], g_sq, l_sq[K])`` as numpy float32: ``np.inner(g,
+        loc_k)``, ``g.dot(g)``, ``loc_k.dot(loc_k)`` exactly as numpy's OpenBLAS
+        forms them (examples/server_aggregation/fedadp/fedadp_server.py:91-99).
+        The global gradient is flattened once (``plato_agg_flatten``, RAW); the
+        clients' loc_k are gathered from their staged arenas inside
+        ``plato_agg_fedadp_dots``, which runs the sdot chains with no flattened
+        copies of the K deltas.
+        """
+        slots = self._check_slots(slots)
+        if not self.has_baseline:
+            raise ValueError("baseline not staged")
+        eng, lay = self.engine, self.layout
+        order = self._fedadp_order()
+        segs, n_flat = self._flat_segments(order, True)
+        stream = torch.cuda.current_stream(eng.device)
+        self.stager.fence(stream)
+        g_flat, _ = self._flatten(_lib.PLATO_AGG_FLAT_RAW, segs, len(order), n_flat, [grads[0].data_ptr()],
+                                  [grads[1].data_ptr()], None, lr, stream)
+        k = len(slots)
+        ptrs = torch.from_numpy(np.asarray([self._pf[i] for i in slots] + [self._pi[i] for i in slots],
+                                           dtype=np.int64)).to(eng.device)
+        xy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
+        yy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
+        ws = torch.empty(-(-_lib.lib().plato_agg_fedadp_dots_workspace(k, 1, lay.n_i64) // 4), dtype=torch.float32,
+                         device=eng.device)
+        n_i = lay.n_i64
+        _lib.call("plato_agg_fedadp_dots", g_flat.data_ptr(), ptrs.data_ptr(), ptrs.data_ptr() + 8 * k, k,
+                  _ptr(eng._base.f32), _ptr(eng._base.i64) if n_i else None, segs.data_ptr(), len(order), n_flat,
+                  lay.n_f32, n_i, float(lr), 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(), _stream_handle(stream))
+        xy_h, yy_h = xy.cpu().numpy(), yy.cpu().numpy()  # stream-ordered D2H (syncs this stream)
+        self._keep_flat = (g_flat, ptrs, ws)
+        return xy_h[:k], xy_h[k], yy_h[:k]
+
+    def fedadp_dots_flat(self, grads: tuple[torch.Tensor, torch.Tensor], slots: Sequence[int], lr: float,
+                         batch_bytes: float = 32e9):
+        """The same dots through materialised flat vectors (``plato_agg_flatten`` + ``plato_agg_sdot_shared``).
+
+        The round-2 path, kept as an independent device cross-check of
+        :meth:`fedadp_dots` (tests) and for the before/after timing
+        (scripts/bench_variant_paths.py).
+        """
+        slots = self._check_slots(slots)
+        if not self.has_baseline:
+            raise ValueError("baseline not staged")
+        eng, lay = self.engine, self.layout
+        order = self._fedadp_order()
         segs, n_flat = self._flat_segments(order, True)
         stream = torch.cuda.current_stream(eng.device)
         self.stager.fence(stream)
@@ -884,8 +924,7 @@ class AggregationRound:
                                        [grads[1].data_ptr()], None, lr, stream)
         k = len(slots)
         # rows 0..k-1: g.loc_k and loc_k.loc_k; row k: g.g (the global gradient's squared norm),
-        # which the last batch's launch forms alongside (with_xx): a launch is as long as its
-        # serial chains, so a launch of its own would cost as much as the whole batch.
+        # which the last batch's launch forms alongside (with_xx)
         xy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         yy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         per = max(1, int(batch_bytes // (stride * 4)))

@@ -362,7 +362,7 @@ class MultiRound:
                               _ptr(sc), k, _ptr(s.base_f), _ptr(s.base_i) if n_i else None, _ptr(out_f),
                               _ptr(out_i) if n_i else None, s.n, n_i, h)
                 elif eng.variant is not None:
-                    _lib.call("plato_agg_tune_fedavg", eng.variant, int(not deltas), _ptr(tf),
+                    _lib.tune_call("plato_agg_tune_fedavg", eng.variant, int(not deltas), _ptr(tf),
                               _ptr(ti) if n_i else None, _ptr(w), _ptr(sc), k,
                               None if deltas else _ptr(s.base_f), None if (deltas or not n_i) else _ptr(s.base_i),
                               _ptr(out_f), _ptr(out_i) if n_i else None, s.n, n_i, h)

@@ -5,8 +5,10 @@ Each path is what the mixin calls, end to end on the device, host sync included:
 * port      AggregationRound.model_similarities: flatten (current - previous, K deltas) ->
             torch-order vector norms (8 serial fma chains over the whole flattened model) ->
             torch-order cascade cosine sums (examples/async/port/port_server.py:24-52)
-* fedadp    launch_entrywise (global gradient, device) + fedadp_dots: flatten in name order ->
-            OpenBLAS-order sdot pairs (fedadp_server.py:91-99)
+* fedadp    launch_entrywise (global gradient, device) + fedadp_dots: g flattened in name order,
+            the K client deltas gathered from their arenas inside the OpenBLAS-order sdot kernel
+            (plato_agg_fedadp_dots; fedadp_server.py:91-99)
+* fedadp_flat  the round-2 path: the K deltas flattened into HBM, then plato_agg_sdot_shared
 * polaris   np_sumsq: numpy pairwise-order squared deltas per fp32 entry (polaris_server.py:78-81)
 * fedatt    entry_norms: torch-order per-entry norms of every client delta (fedatt_algorithm.py:34-39)
 
@@ -40,10 +42,14 @@ def main():
     ap.add_argument("--sdot", action="store_true",
                     help="also time the sdot kernels alone on K+1 flat ResNet-18-sized pairs sharing x")
     ap.add_argument("--sdot-only", action="store_true", help="only the sdot kernels (for PMC passes)")
+    ap.add_argument("--fedadp-kernel", action="store_true",
+                    help="HIP-event time of plato_agg_fedadp_dots alone (+ bitwise check against the flat path)")
+    ap.add_argument("--fedadp-only", action="store_true", help="only the fedadp kernel timing (for PMC passes)")
     ap.add_argument("--port-norms", action="store_true",
                     help="time the entry_norms variants on Port's K+1 flattened vectors (one entry each)")
     args = ap.parse_args()
     args.sdot = args.sdot or args.sdot_only
+    args.fedadp_kernel = args.fedadp_kernel or args.fedadp_only
 
     from plato_amd import workloads
     from plato_amd.arena import ArenaLayout
@@ -80,19 +86,26 @@ def main():
         grads = rnd.launch_entrywise(w, add_base=False, device=True)
         rnd.fedadp_dots(grads, slots, 0.01)
 
+    def fedadp_flat():
+        w = np.full((n_e, k), 1.0 / k)
+        grads = rnd.launch_entrywise(w, add_base=False, device=True)
+        rnd.fedadp_dots_flat(grads, slots, 0.01)
+
     paths = {
         "port": (lambda: rnd.model_similarities(previous, slots),
                  client_bytes + 3 * n_f * 4, (n_f + n_i) // 8,
                  "flatten + vector_norm (8 fma chains over the flattened model) + cascade cosine sums"),
         "fedadp": (fedadp, 2 * client_bytes, (n_f + n_i) // 64,
-                   "global gradient + flatten + sdot (64 fma chains over the flattened model)"),
+                   "global gradient + g flatten + fused gather/sdot (64 fma chains over the flattened model)"),
+        "fedadp_flat": (fedadp_flat, 2 * client_bytes, (n_f + n_i) // 64,
+                        "global gradient + flatten of g and the K deltas + sdot_shared (round 2)"),
         "polaris": (lambda: rnd.np_sumsq(slots), client_bytes, 0,
                     "numpy pairwise sums per entry (8-way unrolled blocks of 128)"),
         "fedatt": (lambda: rnd.entry_norms(slots), client_bytes, longest // 8,
                    "per-entry torch norms: 8 fma chains per (entry, client)"),
     }
     for name, (fn, nbytes, chain, what) in paths.items():
-        if args.sdot_only:
+        if args.sdot_only or args.fedadp_only:
             break
         fn()
         torch.cuda.synchronize(dev)
@@ -106,10 +119,61 @@ def main():
         print(json.dumps({"path": name, "clients": k, "ms_median": round(med, 3), "ms_min": round(min(ts) * 1e3, 3),
                           "min_bytes": int(nbytes), "GBps_of_min_bytes": round(nbytes / (med * 1e-3) / 1e9, 1),
                           "serial_chain_steps": int(chain), "what": what}), flush=True)
+    if args.fedadp_kernel:
+        fedadp_kernel(dev, rnd, slots, layout, args.reps)
     if args.sdot:
         sdot_kernels(dev, k, n_f + n_i, args.reps)
     if args.port_norms:
         port_norms(dev, k, n_f + n_i, args.reps)
+
+
+def fedadp_kernel(dev, rnd, slots, layout, reps):
+    """plato_agg_fedadp_dots alone (HIP events on the launch stream), against the flatten + sdot_shared path."""
+    from plato_amd import _lib
+
+    k, n_e = len(slots), len(layout.entries)
+    grads = rnd.launch_entrywise(np.full((n_e, k), 1.0 / k), add_base=False, device=True)
+    want = rnd.fedadp_dots_flat(grads, slots, 0.01)
+    got = rnd.fedadp_dots(grads, slots, 0.01)
+    same = all(np.asarray(a).tobytes() == np.asarray(b).tobytes() for a, b in zip(got, want))
+    g_flat, ptrs, ws = rnd._keep_flat
+    eng = rnd.engine
+    order = rnd._fedadp_order()
+    segs, n_flat = rnd._flat_segments(order, True)
+    xy = torch.empty(k + 1, device=dev)
+    yy = torch.empty(k + 1, device=dev)
+    h = torch.cuda.current_stream(dev).cuda_stream
+
+    runs = {"default": lambda: _lib.call("plato_agg_fedadp_dots", g_flat.data_ptr(), ptrs.data_ptr(),
+                                         ptrs.data_ptr() + 8 * k, k, eng._base.f32.data_ptr(),
+                                         eng._base.i64.data_ptr(), segs.data_ptr(), len(order), n_flat,
+                                         layout.n_f32, layout.n_i64, 0.01, 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(), h)}
+    for v in range(_lib.tune().plato_agg_tune_num_fedadp_variants()):
+        runs[f"v{v}"] = (lambda v=v: _lib.tune_call("plato_agg_tune_fedadp_dots", v, g_flat.data_ptr(), ptrs.data_ptr(),
+                                                    ptrs.data_ptr() + 8 * k, k, eng._base.f32.data_ptr(),
+                                                    eng._base.i64.data_ptr(), segs.data_ptr(), len(order), n_flat,
+                                                    layout.n_f32, layout.n_i64, 0.01, 1, ws.data_ptr(), xy.data_ptr(),
+                                                    yy.data_ptr(), h))
+    # unique bytes: each client's fp32 arena + int64 counters once, the baseline and g_flat once
+    uniq = k * (layout.n_f32 * 4 + layout.n_i64 * 8) + 2 * layout.n_f32 * 4 + n_flat * 4
+    for name, fn in runs.items():
+        fn()
+        torch.cuda.synchronize(dev)
+        ok = (xy.cpu().numpy()[:k].tobytes() == np.asarray(want[0]).tobytes()
+              and xy.cpu().numpy()[k:].tobytes() == np.float32(want[1]).tobytes()
+              and yy.cpu().numpy()[:k].tobytes() == np.asarray(want[2]).tobytes())
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        med = statistics.median(ts)
+        print(json.dumps({"fedadp_dots": name, "pairs": k + 1, "n_flat": n_flat, "ms_median": round(med, 4),
+                          "ms_min": round(min(ts), 4), "GBps_unique_bytes": round(uniq / (med * 1e-3) / 1e9, 1),
+                          "unique_bytes": uniq, "bitwise_equal_to_flat_path": ok and same}), flush=True)
 
 
 def port_norms(dev, k, n, reps):
@@ -127,7 +191,7 @@ def port_norms(dev, k, n, reps):
         out = torch.empty(k + 1, device=dev)
 
         def fn():
-            _lib.call("plato_agg_tune_entry_norms", v, tab.data_ptr(), None, k + 1, None, None, chunk.data_ptr(), 1,
+            _lib.tune_call("plato_agg_tune_entry_norms", v, tab.data_ptr(), None, k + 1, None, None, chunk.data_ptr(), 1,
                       None, 0, 1, stride, 0, out.data_ptr(), h)
         fn()
         torch.cuda.synchronize(dev)
@@ -163,8 +227,8 @@ def sdot_kernels(dev, k, n, reps):
                                               o1.data_ptr(), o2.data_ptr(), h),
             "shared_default": lambda o1, o2: _lib.call("plato_agg_sdot_shared", x.data_ptr(), py.data_ptr(), k, n, 1,
                                                        ws.data_ptr(), o1.data_ptr(), o2.data_ptr(), h)}
-    for v in range(_lib.lib().plato_agg_tune_num_sdot_shared_variants()):
-        runs[f"shared_v{v}"] = (lambda o1, o2, v=v: _lib.call("plato_agg_tune_sdot_shared", v, x.data_ptr(),
+    for v in range(_lib.tune().plato_agg_tune_num_sdot_shared_variants()):
+        runs[f"shared_v{v}"] = (lambda o1, o2, v=v: _lib.tune_call("plato_agg_tune_sdot_shared", v, x.data_ptr(),
                                                                py.data_ptr(), k, n, 1, ws.data_ptr(), o1.data_ptr(),
                                                                o2.data_ptr(), h))
     ref = None

@@ -106,8 +106,8 @@ def main():
                       _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(out_f),
                       _ptr(out_i), n_f, n_i, h)
             return
-        cf, ci = chunks(_lib.lib().plato_agg_tune_qsgd_chunk(variant))
-        _lib.call("plato_agg_tune_fedavg_qsgd", variant, _ptr(qtf), _ptr(qti), k, _ptr(max_v), n_e, 63.0, _ptr(w),
+        cf, ci = chunks(_lib.tune().plato_agg_tune_qsgd_chunk(variant))
+        _lib.tune_call("plato_agg_tune_fedavg_qsgd", variant, _ptr(qtf), _ptr(qti), k, _ptr(max_v), n_e, 63.0, _ptr(w),
                   None, _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(out_f),
                   _ptr(out_i), n_f, n_i, h)
 
@@ -129,7 +129,7 @@ def main():
             _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64), _ptr(ef),
                       ef.shape[0], _ptr(ei), ei.shape[0], n_e, n_f, n_i, _ptr(norms_out), h)
         else:
-            _lib.call("plato_agg_tune_entry_norms", variant, _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64),
+            _lib.tune_call("plato_agg_tune_entry_norms", variant, _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64),
                       _ptr(ef), ef.shape[0], _ptr(ei), ei.shape[0], n_e, n_f, n_i, _ptr(norms_out), h)
 
     def run_fedavg():
@@ -144,7 +144,7 @@ def main():
     }
     if args.qsgd_variants or args.qsgd_list:  # tuning: every (or the listed) plato_agg_tune_fedavg_qsgd variant
         vlist = ([int(x) for x in args.qsgd_list.split(",")] if args.qsgd_list
-                 else range(_lib.lib().plato_agg_tune_num_qsgd_variants()))
+                 else range(_lib.tune().plato_agg_tune_num_qsgd_variants()))
         for v in vlist:
             kernels[f"qsgd_v{v}"] = ((lambda v=v: run_qsgd(v)), kernels["qsgd"][1])
     if args.norm_variants:  # tuning: every plato_agg_tune_entry_norms variant

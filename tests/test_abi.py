@@ -12,7 +12,7 @@ from plato_amd import _lib
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols(pattern="plato_agg*.h"):
+def declared_symbols(pattern="plato_agg.h"):
     names = set()
     for header in glob.glob(os.path.join(ROOT, "include", pattern)):
         text = open(header).read()
@@ -37,6 +37,19 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(handle, name), name
     # and the Python binding knows the signature of each
     assert declared_symbols() == set(_lib.SIGNATURES)
+    # the tuning entry points are not part of the product library
+    for name in declared_symbols("plato_agg_tune.h"):
+        assert not hasattr(handle, name), name
+
+
+def test_tuning_library_exports_both_headers():
+    if not os.path.exists(_lib.TUNE_LIB_PATH):
+        pytest.skip("tuning library not built (run __graft_entry__.build())")
+    handle = ctypes.CDLL(_lib.TUNE_LIB_PATH)
+    tune = declared_symbols("plato_agg_tune.h")
+    assert tune == set(_lib.TUNE_SIGNATURES)
+    for name in declared_symbols() | tune:
+        assert hasattr(handle, name), name
 
 
 def test_ingest_library_exports_its_header():
@@ -59,7 +72,7 @@ def test_binding_loads_and_reports_abi():
         pytest.skip("library not built")
     lib = _lib.lib()
     assert lib.plato_agg_abi_version() == _lib.ABI_VERSION
-    assert lib.plato_agg_tune_num_variants() >= 1
+    assert _lib.tune().plato_agg_tune_num_variants() >= 1
 
 
 def test_argument_errors_are_raised_without_gpu_work():

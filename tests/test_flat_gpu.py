@@ -63,7 +63,7 @@ def test_sdot_shared_equals_openblas_order(n, npairs):
     h = torch.cuda.current_stream().cuda_stream
     want_xy = [R.sdot(x, y).tobytes() for y in ys] + [R.sdot(x, x).tobytes()]
     want_yy = [R.sdot(y, y).tobytes() for y in ys] + [R.sdot(x, x).tobytes()]
-    for variant in [None] + list(range(_lib.lib().plato_agg_tune_num_sdot_shared_variants())):
+    for variant in [None] + list(range(_lib.tune().plato_agg_tune_num_sdot_shared_variants())):
         for with_xx in (0, 1):
             out_xy = torch.full((k + 1,), float("nan"), device=DEV)
             out_yy = torch.full((k + 1,), float("nan"), device=DEV)
@@ -71,7 +71,7 @@ def test_sdot_shared_equals_openblas_order(n, npairs):
                 _lib.call("plato_agg_sdot_shared", bx.data_ptr(), py.data_ptr(), k, n, with_xx, ws.data_ptr(),
                           out_xy.data_ptr(), out_yy.data_ptr(), h)
             else:
-                _lib.call("plato_agg_tune_sdot_shared", variant, bx.data_ptr(), py.data_ptr(), k, n, with_xx,
+                _lib.tune_call("plato_agg_tune_sdot_shared", variant, bx.data_ptr(), py.data_ptr(), k, n, with_xx,
                           ws.data_ptr(), out_xy.data_ptr(), out_yy.data_ptr(), h)
             got_xy, got_yy = out_xy.cpu().numpy(), out_yy.cpu().numpy()
             for j in range(k + with_xx):

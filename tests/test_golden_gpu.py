@@ -358,9 +358,9 @@ def test_bf16_codec_device_resident_matches_reference(engine, case):
     out_f = torch.empty(layout.row_f32, device=DEV)
     out_i = torch.empty(layout.row_i64, device=DEV)
     n_i = layout.n_i64
-    for v in range(_lib.lib().plato_agg_tune_num_bf16_variants()):  # every variant, bit for bit
+    for v in range(_lib.tune().plato_agg_tune_num_bf16_variants()):  # every variant, bit for bit
         out_f.fill_(float("nan"))
-        _lib.call("plato_agg_tune_fedavg_bf16", v, tf.data_ptr(), ti.data_ptr() if n_i else None, w.data_ptr(),
+        _lib.tune_call("plato_agg_tune_fedavg_bf16", v, tf.data_ptr(), ti.data_ptr() if n_i else None, w.data_ptr(),
                   None, len(order), base.f32.data_ptr(), base.i64.data_ptr() if n_i else None, out_f.data_ptr(),
                   out_i.data_ptr() if n_i else None, layout.n_f32, n_i, torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()

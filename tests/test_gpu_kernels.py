@@ -88,7 +88,7 @@ def test_all_variants_identical(engine):
     weights = ref.fedavg_weights(synth.num_samples(k, seed))
     bf, bi, xs_f, xs_i = host_inputs(layout.n_f32, layout.n_i64, seed, k)
     exp_f, exp_i = ref.fedavg_numpy(bf, bi, xs_f, xs_i, weights)
-    for v in range(_lib.lib().plato_agg_tune_num_variants()):
+    for v in range(_lib.tune().plato_agg_tune_num_variants()):
         got_f, got_i = _run(engine, layout, base, slab, k, weights, variant=v)
         assert bits_equal(got_f, exp_f), (v, first_mismatch(got_f, exp_f))
         assert bits_equal(got_i, exp_i), v
@@ -170,10 +170,10 @@ def test_split_launch_ranges_bit_exact(engine, groups):
     weights = ref.fedavg_weights(synth.num_samples(k, seed))
     scales = [1.0 / (1 + 0.11 * i) for i in range(k)]
     bf, bi, xs_f, xs_i = host_inputs(layout.n_f32, layout.n_i64, seed, k)
-    lib = _lib.lib()
+    lib = _lib.tune()
     lib.plato_agg_tune_set_launch_groups(groups)
     try:
-        for v in (None, 14, 10):
+        for v in (0, 14, 10):  # variant 0 = the default kernel, from the tuning library whose split is lowered
             got_f, got_i = _run(engine, layout, base, slab, k, weights, scales=scales, variant=v)
             exp_f, exp_i = ref.fedavg_numpy(bf, bi, xs_f, xs_i, weights, scales)
             assert bits_equal(got_f, exp_f), (v, first_mismatch(got_f, exp_f))
@@ -188,8 +188,8 @@ def test_split_launch_ranges_bit_exact(engine, groups):
         w = torch.from_numpy(ref.fp32(weights)).to(dev)
         out_f = torch.full((layout.row_f32,), float("nan"), device=dev)
         out_i = torch.full((layout.row_i64,), float("nan"), device=dev)
-        _lib.call("plato_agg_fedavg_weights_bf16", tf.data_ptr(), ti.data_ptr(), w.data_ptr(), None, k,
-                  base.f32.data_ptr(), base.i64.data_ptr(), out_f.data_ptr(), out_i.data_ptr(),
+        _lib.tune_call("plato_agg_fedavg_weights_bf16", tf.data_ptr(), ti.data_ptr(), w.data_ptr(), None, k,
+                       base.f32.data_ptr(), base.i64.data_ptr(), out_f.data_ptr(), out_i.data_ptr(),
                   layout.n_f32, layout.n_i64, torch.cuda.current_stream().cuda_stream)
         lib.plato_agg_tune_set_launch_groups(0)
         ref_f = torch.full_like(out_f, float("nan"))

@@ -143,7 +143,7 @@ def test_entry_norm_kernels_agree_bitwise(engine, k, deltas):
         outs = []
         for variant in (0, 1, 2, 3, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16):
             out = torch.full((k * n_e,), float("nan"), device=dev)
-            _lib.call("plato_agg_tune_entry_norms", variant, tf.data_ptr(), ti.data_ptr(), k,
+            _lib.tune_call("plato_agg_tune_entry_norms", variant, tf.data_ptr(), ti.data_ptr(), k,
                       None if deltas else b_f.data_ptr(), None if deltas else b_i.data_ptr(), ef.data_ptr(),
                       ef.shape[0], ei.data_ptr(), ei.shape[0], n_e, layout.n_f32, layout.n_i64, out.data_ptr(),
                       torch.cuda.current_stream().cuda_stream)
@@ -243,14 +243,19 @@ def test_fedadp_server_matches_reference(engine, name):
     g_f, g_i = rnd.launch_entrywise(w1, add_base=False, device=True)
     assert G.sha(G.canon(g_f[: layout.n_f32].cpu().numpy())) == exp["global_grads_f32_sha256"]
     assert G.sha(G.canon(g_i[: layout.n_i64].cpu().numpy())) == exp["global_grads_i64f_sha256"]
-    # the dots in one launch and in batches of 1 and 3 clients (g.g rides with the first batch)
+    # the fused gather kernel against the materialised-flatten path, whole and in batches of 1 and 3
+    # clients (g.g rides with the last batch), and on client subsets and orders
     whole = rnd.fedadp_dots((g_f, g_i), range(recipe["k"]), 0.01)
     stride_bytes = -(-(layout.n_f32 + layout.n_i64) // 64) * 64 * 4
-    for per in (1, 3):
-        parts = rnd.fedadp_dots((g_f, g_i), range(recipe["k"]), 0.01, batch_bytes=per * stride_bytes)
+    for per in (1e12, 1, 3):
+        parts = rnd.fedadp_dots_flat((g_f, g_i), range(recipe["k"]), 0.01, batch_bytes=per * stride_bytes)
         assert np.asarray(parts[0]).tobytes() == np.asarray(whole[0]).tobytes()
         assert np.float32(parts[1]).tobytes() == np.float32(whole[1]).tobytes()
         assert np.asarray(parts[2]).tobytes() == np.asarray(whole[2]).tobytes()
+    sub = [recipe["k"] - 1, 0, 2]
+    part = rnd.fedadp_dots((g_f, g_i), sub, 0.01)
+    assert np.asarray(part[0]).tobytes() == np.asarray(whole[0])[sub].tobytes()
+    assert np.asarray(part[2]).tobytes() == np.asarray(whole[2])[sub].tobytes()
     rnd.launch(ref_w)
     again = rnd.result()
     assert G.sha(G.canon(_flat(layout, again, "f32"))) == exp["updated_f32_sha256"]
@@ -281,3 +286,36 @@ def test_polaris_server_matches_reference(engine):
     # numpy's float32 pairwise sums on the device: the reference's bits, expected fill included
     assert {c: v.hex() for c, v in got.items()} == {c: v.hex() for c, v in want.items()}
     assert sorted(set(range(1024)) - set(server.unexplored_clients)) == sorted(c for c in G.order_of(recipe))
+
+
+@pytest.mark.parametrize("name", ["fedadp_lenet5_k6", "fedadp_resnet18_k8"])
+def test_fedadp_dots_tile_shapes_agree_bitwise(engine, name):
+    """Every tile shape of the fused gather + sdot kernel (tuning library) equals the flatten + sdot path."""
+    from plato_amd import _lib
+
+    recipe = CASES[name]["recipe"]
+    layout, base, pays, _, updates = _host(recipe)
+    k = recipe["k"]
+    rnd = engine.begin(base, k)
+    rnd.put_baseline(base)
+    for i, p in enumerate(pays):
+        rnd.put_client(i, p)
+    w1 = np.tile(np.full(k, 1.0 / k), (len(layout.entries), 1))
+    grads = rnd.launch_entrywise(w1, add_base=False, device=True)
+    want = rnd.fedadp_dots_flat(grads, range(k), 0.01)
+    rnd.fedadp_dots(grads, range(k), 0.01)
+    g_flat, ptrs, ws = rnd._keep_flat
+    order = rnd._fedadp_order()
+    segs, n_flat = rnd._flat_segments(order, True)
+    dev = torch.device(DEV)
+    for v in range(_lib.tune().plato_agg_tune_num_fedadp_variants()):
+        xy = torch.full((k + 1,), float("nan"), device=dev)
+        yy = torch.full((k + 1,), float("nan"), device=dev)
+        _lib.tune_call("plato_agg_tune_fedadp_dots", v, g_flat.data_ptr(), ptrs.data_ptr(), ptrs.data_ptr() + 8 * k, k,
+                       engine._base.f32.data_ptr(), engine._base.i64.data_ptr(), segs.data_ptr(), len(order), n_flat,
+                       layout.n_f32, layout.n_i64, 0.01, 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(),
+                       torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert xy.cpu().numpy()[:k].tobytes() == np.asarray(want[0]).tobytes(), v
+        assert xy.cpu().numpy()[k:].tobytes() == np.float32(want[1]).tobytes(), v
+        assert yy.cpu().numpy()[:k].tobytes() == np.asarray(want[2]).tobytes(), v
