@@ -438,6 +438,27 @@ int plato_agg_np_sumsq(const float* const* d_x, int K, const float* d_base, cons
                        float* d_out, hipStream_t stream);
 
 /*
+ * Coded client payloads (or the baseline) as fp32 rows of the "promoted"
+ * layout, for the variant servers' per-entry reductions: what the reference's
+ * inbound dequantizers hand the server (plato/processors/model_dequantize.py:
+ * 15-18, model_dequantize_qsgd.py:34-60), every entry float32 — the int64
+ * counters included, so a counter's delta is float32(x) - float32(b).
+ *   PLATO_AGG_DECODE_NATIVE  fp32 copied, int64 cast to fp32 (RNE)
+ *   PLATO_AGG_DECODE_BF16    bf16 widened (exact), both regions
+ *   PLATO_AGG_DECODE_QSGD    fp32(fp32(fp32(zeta) * max_v[entry][k]) / divisor)
+ * Element e of the fp32 region lands at d_dst[k][e], element e of the int64
+ * region at d_dst[k][i64_dst_offset + e]; pieces from d_chunks_* (entry, begin,
+ * end); d_max_v: [n_entries][K] (QSGD only).
+ */
+#define PLATO_AGG_DECODE_NATIVE 0
+#define PLATO_AGG_DECODE_BF16 1
+#define PLATO_AGG_DECODE_QSGD 2
+int plato_agg_decode_rows(int codec, const void* const* d_src_f32, const void* const* d_src_i64, int K,
+                          const float* d_max_v, float divisor, const plato_agg_chunk* d_chunks_f32,
+                          uint32_t n_chunks_f32, const plato_agg_chunk* d_chunks_i64, uint32_t n_chunks_i64,
+                          size_t i64_dst_offset, float* const* d_dst, hipStream_t stream);
+
+/*
  * Single-process RCCL communicator over the GPUs one Plato server drives.
  * The reference has no collectives (aggregation runs on one CPU
  * process); these serve the multi-GPU engine behind the same

@@ -25,6 +25,7 @@ PLATO_AGG_FLAT_DELTA = 0
 PLATO_AGG_FLAT_CAST_DIFF = 1
 PLATO_AGG_FLAT_RAW = 2
 PLATO_AGG_SEG_NEG_DIV = 1
+PLATO_AGG_DECODE = {"native": 0, "bf16": 1, "qsgd": 2}
 
 _c_void_p = ctypes.c_void_p
 _c_size_t = ctypes.c_size_t
@@ -136,6 +137,10 @@ SIGNATURES = {
         [_c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, ctypes.c_uint32, _c_void_p,
          _c_void_p, _c_void_p],
     ),
+    "plato_agg_decode_rows": (
+        _c_int,
+        [_c_int, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_float, _c_void_p, ctypes.c_uint32, _c_void_p,
+         ctypes.c_uint32, _c_size_t, _c_void_p, _c_void_p]),
     "plato_agg_comm_create": (_c_int, [_c_int, _c_void_p, ctypes.POINTER(_c_void_p)]),
     "plato_agg_comm_destroy": (_c_int, [_c_void_p]),
     "plato_agg_comm_size": (_c_int, [_c_void_p]),

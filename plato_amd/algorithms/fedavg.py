@@ -102,28 +102,33 @@ class FedAttAlgorithmMixin(_AlgorithmEngine):
 
         from .. import weights as W
 
+        from ..arena import payload_codec
+
         engine = self.aggregation_engine()
         try:
-            rnd = engine.begin(baseline_weights, len(weights_received))
+            rnd = engine.begin(baseline_weights, len(weights_received), payload_codec(weights_received[0]))
 
             def stage_and_norms():
                 rnd.put_baseline(baseline_weights)
                 for slot, payload in enumerate(weights_received):
                     if not rnd.adopt(slot, payload):
                         rnd.put_client(slot, payload)
+                # coded payloads (bf16 / QSGD): the dequantized rows, every entry float32 as the
+                # reference's inbound processor hands them over; native: the round itself
+                work = rnd.decoded()
                 # the reference's fp32 norms bit for bit (torch's CPU reduction order)
-                return rnd.entry_norms(range(len(weights_received)))
+                return work, work.entry_norms(range(len(weights_received)))
 
             # pack + H2D + the norms launch and its sync run on the worker thread, not the event loop
-            norms = await self._off_loop(stage_and_norms)
+            work, norms = await self._off_loop(stage_and_norms)
             atts = W.fedatt_attention(norms)  # the reference's softmax
             epsilon = self._fedatt_param("epsilon", 1.2)
             magnitude = self._fedatt_param("magnitude", 0.001)
             # the reference's RNG stream: torch.randn per key in baseline order, on this thread
             noise = OrderedDict((name, torch.randn(weight.shape)) for name, weight in baseline_weights.items())
-            await self._off_loop(lambda: rnd.launch_entrywise(-atts.astype(np.float64), scale=-epsilon, noise=noise,
-                                                              noise_scale=magnitude, add_base=True))
-            await self._off_loop(rnd.wait)  # a HIP event wait on the worker thread
-            return rnd.result()
+            await self._off_loop(lambda: work.launch_entrywise(-atts.astype(np.float64), scale=-epsilon, noise=noise,
+                                                               noise_scale=magnitude, add_base=True))
+            await self._off_loop(work.wait)  # a HIP event wait on the worker thread
+            return work.result()
         finally:
             engine.release_arrivals()

@@ -179,6 +179,23 @@ class ArenaLayout:
         self._cache[key] = out
         return out
 
+    def promoted(self) -> "ArenaLayout":
+        """The same entries, all fp32: the int64 counters as fp32 entries after the fp32 region.
+
+        What a dequantized payload is in the reference (every entry float32 after
+        model_dequantize / model_dequantize_qsgd), so the per-entry reductions
+        of the variant servers run on it with float32(x) - float32(b) for a
+        counter (plato_agg_decode_rows builds the rows).  Entry order, names and
+        shapes are unchanged; a counter's offset is ``row_f32 + its int64 offset``.
+        """
+        hit = self._cache.get("promoted")
+        if hit is None:
+            entries = [e if e.region == F32 else Entry(e.name, F32, self.row_f32 + e.offset, e.numel, e.shape)
+                       for e in self.entries]
+            hit = ArenaLayout(entries, self.row_f32 + self.n_i64 if self.n_i64 else self.n_f32, 0)
+            self._cache["promoted"] = hit
+        return hit
+
     # ---------------------------------------------------------- pack / unpack
     def pack(self, state_dict: Mapping[str, torch.Tensor], out_f32: torch.Tensor,
              out_i64: torch.Tensor | None) -> None:

@@ -149,7 +149,7 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_o
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe>
 __device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpSeg* S, int n_segs, int& cursor,
                                           const AdpSrc<kP>& src, uint32_t t, int cg, int w, int lane,
                                           AdpRegs<kP, kIt>& r) {
@@ -181,6 +181,13 @@ __device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpSeg* S, int
       code = i64 ? (ls.info | (el << 8)) : ls.info;
     }
     r.code[i] = code;
+    if (kProbe == 3) {  // timing probe: no loads (wrong results)
+      r.x[i] = float(p);
+      r.b[i] = float(e);
+#pragma unroll
+      for (int k = 0; k < kP; ++k) r.y[i][k] = float(e + k);
+      continue;
+    }
     r.x[i] = bload(src.x, p * 4u);
     r.b[i] = bload(src.b, e * 4u);
 #pragma unroll
@@ -188,7 +195,7 @@ __device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpSeg* S, int
   }
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe>
 __device__ __forceinline__ void adp_write(const AdpArgs& a, float* slot, int pair0, int w, int lane,
                                           AdpRegs<kP, kIt>& r) {
   using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad>;
@@ -201,7 +208,7 @@ __device__ __forceinline__ void adp_write(const AdpArgs& a, float* slot, int pai
     dst[0] = r.x[i];
     const uint32_t code = r.code[i];
     if (r.fast & (1u << i)) {  // wave-uniform: one entry, one sign/divide mode
-      if (__builtin_amdgcn_readfirstlane(int(code)) & kSegNeg) {
+      if (kProbe != 1 && (__builtin_amdgcn_readfirstlane(int(code)) & kSegNeg)) {  // probe 1: no division
 #pragma unroll
         for (int k = 0; k < kP; ++k) dst[(1 + k) * Sh::kVR] = (-(r.y[i][k] - r.b[i])) / lr;
       } else {
@@ -225,7 +232,7 @@ __device__ __forceinline__ void adp_write(const AdpArgs& a, float* slot, int pai
   }
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0>
 __global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
   using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad>;
   __shared__ __attribute__((aligned(16))) float ring[2 * Sh::kSlot];
@@ -250,6 +257,10 @@ __global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
   const uint64_t nst2 = (nst + 1) & ~uint64_t(1);  // barriers: one per stage, in pairs
   if (wave >= 2) {  // producer
     const int w = wave - 2;
+    if (kProbe == 4) {  // timing probe: the chains alone (producers only keep the barrier count)
+      for (uint64_t t = 0; t < nst2; ++t) __builtin_amdgcn_s_barrier();
+      return;
+    }
     const int pair0 = pg * kP;
     AdpSrc<kP> src;
     src.x = adp_rsrc(a.x, a.nsteps * 256);
@@ -259,19 +270,19 @@ __global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
       src.y[k] = adp_rsrc(sld(a.xf, pair0 + k < a.n_pairs ? pair0 + k : a.n_pairs - 1), a.n_f32 * 4);
     int cursor = 0;
     AdpRegs<kP, kIt> ra, rb;
-    adp_issue<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, cursor, src, 0, cg, w, lane, ra);
-    adp_issue<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, cursor, src, 1, cg, w, lane, rb);
+    adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cursor, src, 0, cg, w, lane, ra);
+    adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cursor, src, 1, cg, w, lane, rb);
     // whole pairs of stages (an odd count gets one idle trip): no branch inside the loop, so the
     // compiler's vmcnt bookkeeping sees the same two stages in flight on every trip
     for (uint32_t t = 0; t < uint32_t(nst2); t += 2) {
-      adp_write<kP, kC, kS, kW, kIt, kVRpad>(a, ring, pair0, w, lane, ra);
+      adp_write<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, ring, pair0, w, lane, ra);
       // past the last stage (t = nst) every position clamps to the last block: valid addresses,
       // never consumed, and every trip issues the same loads
-      adp_issue<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, cursor, src, t + 2 < nst ? t + 2 : uint32_t(nst), cg, w,
+      adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cursor, src, t + 2 < nst ? t + 2 : uint32_t(nst), cg, w,
                                              lane, ra);
       __builtin_amdgcn_s_barrier();  // stage t published in slot 0
-      adp_write<kP, kC, kS, kW, kIt, kVRpad>(a, ring + Sh::kSlot, pair0, w, lane, rb);
-      adp_issue<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, cursor, src, t + 3 < nst ? t + 3 : uint32_t(nst), cg, w,
+      adp_write<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, ring + Sh::kSlot, pair0, w, lane, rb);
+      adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cursor, src, t + 3 < nst ? t + 3 : uint32_t(nst), cg, w,
                                              lane, rb);
       __builtin_amdgcn_s_barrier();  // stage t + 1 published in slot 1
     }
@@ -290,7 +301,7 @@ __global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_s_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (!active || t >= nst) continue;
+    if (!active || t >= nst || kProbe == 2) continue;  // probe 2: no chains
     const float* slot = ring + (t & 1) * Sh::kSlot;
     const float* A = slot + arow;
     const float* B = slot + brow;
@@ -306,7 +317,7 @@ __global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
       }
 #pragma unroll
       for (int blk = 0; blk < kS / 16; ++blk) {
-        if (blk + 1 < kS / 16) {
+        if (kProbe != 5 && blk + 1 < kS / 16) {  // probe 5: no LDS reads after the first block
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
             an[q] = *reinterpret_cast<const f4*>(A + 16 * (blk + 1) + 4 * q);
@@ -324,8 +335,10 @@ __global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          av[q] = an[q];
-          bv[q] = bn[q];
+          if (kProbe != 5) {
+            av[q] = an[q];
+            bv[q] = bn[q];
+          }
         }
       }
     } else {
@@ -429,13 +442,13 @@ __global__ __launch_bounds__(64) void fedadp_finish_kernel(AdpArgs a, float* out
   out_yy[pair] = float(tyy + kyy);
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0>
 void launch_adp(const AdpArgs& a, hipStream_t st) {
   constexpr int kGroups = 64 / kC;
   uint32_t pgs = uint32_t((a.n_pairs + kP - 1) / kP);
   pgs = (pgs + 7) / 8 * 8;  // whole XCD rounds (padding workgroups return at once)
-  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad>), dim3(pgs * kGroups), dim3(64 * (kW + 2)), 0,
-                     st, a);
+  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe>), dim3(pgs * kGroups),
+                     dim3(64 * (kW + 2)), 0, st, a);
 }
 using AdpFn = void (*)(const AdpArgs&, hipStream_t);
 // pairs x chains per workgroup, steps per stage, producer waves, iterations, vector pad
@@ -444,6 +457,15 @@ const AdpFn kAdpVariants[] = {
     &launch_adp<4, 8, 256, 8, 4, 16>,    // 1: 32 B
     &launch_adp<2, 16, 256, 8, 8, 32>,   // 2: 64 B
     &launch_adp<1, 32, 128, 8, 8, 0>,    // 3: whole 128-byte lines, x and b per pair (from L2)
+#ifdef PLATO_AGG_TUNE
+    &launch_adp<2, 16, 192, 12, 4, 32>,  // 4: variant 2 with 12 producer waves
+    &launch_adp<2, 16, 128, 8, 4, 32>,   // 5: variant 2, half stages
+    &launch_adp<2, 16, 256, 8, 8, 32, 1>,  // 6: probe of 2 without the division (wrong results)
+    &launch_adp<2, 16, 256, 8, 8, 32, 2>,  // 7: probe of 2 without the chains (wrong results)
+    &launch_adp<2, 16, 256, 8, 8, 32, 3>,  // 8: probe of 2 without the loads (wrong results)
+    &launch_adp<2, 16, 256, 8, 8, 32, 4>,  // 9: probe of 2: the chains alone (wrong results)
+    &launch_adp<2, 16, 256, 8, 8, 32, 5>,  // 10: probe of 2: chains without LDS reads (wrong results)
+#endif
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 

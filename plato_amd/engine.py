@@ -259,11 +259,18 @@ class FedAvgEngine:
             pool = layout._cache["result_pool"] = ResultPool(layout)
         return pool
 
-    def _f32_stager(self) -> "_Stager":
-        st = self._stagers.get("f32")
+    def _f32_stager(self, layout: ArenaLayout | None = None) -> "_Stager":
+        """All-fp32 arrays over the model's keys (FedAtt's noise), packed in ``layout`` (default: the engine's)."""
+        if layout is None or layout is self._layout:
+            st = self._stagers.get("f32")
+            if st is None:
+                st = _Stager(self._layout, self.device, codec="f32", stream=self._copy_stream)
+                self._stagers["f32"] = st
+            return st
+        st = layout._cache.get(("f32_stager", str(self.device)))
         if st is None:
-            st = _Stager(self._layout, self.device, codec="f32", stream=self._copy_stream)
-            self._stagers["f32"] = st
+            st = layout._cache[("f32_stager", str(self.device))] = _Stager(layout, self.device, codec="f32",
+                                                                           stream=self._copy_stream)
         return st
 
     # ---------------------------------------------------- arrival staging
@@ -547,12 +554,19 @@ class AggregationRound:
         self._kernel_events = None
         self.timings: dict = {}
         self._k = 0
+        self._decoded = None
+
+    @property
+    def _base(self) -> DeviceArena:
+        """The baseline arena this round's kernels read (the engine's; a decoded round has its own)."""
+        return self.engine._base
 
     def put_baseline(self, baseline: Mapping[str, torch.Tensor]) -> None:
         self.layout.check_compatible(baseline, "baseline_weights")
         eng = self.engine
         eng._stager.put(baseline, eng._base.f32, eng._base.i64)
         self.has_baseline = True
+        self._decoded = None
 
     def put_client(self, slot: int, payload: Mapping[str, torch.Tensor],
                    what: str = "weights_received") -> None:
@@ -624,7 +638,7 @@ class AggregationRound:
             ncf, nci = int(cf.shape[0]), int(ci.shape[0])
             args = (_ptr(tf), _ptr(ti) if n_i else None, len(order), _ptr(mv), len(lay.entries),
                     float(self._level - 1), _ptr(w), _ptr(s), _ptr(cf), ncf, _ptr(ci) if nci else None, nci,
-                    _ptr(eng._base.f32), _ptr(eng._base.i64) if n_i else None, _ptr(out_f),
+                    _ptr(self._base.f32), _ptr(self._base.i64) if n_i else None, _ptr(out_f),
                     _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
             if eng.qsgd_variant is None:
                 _lib.call("plato_agg_fedavg_qsgd", *args)
@@ -634,11 +648,11 @@ class AggregationRound:
         elif self.codec == "bf16":
             n_i = lay.n_i64
             _lib.call("plato_agg_fedavg_weights_bf16", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w), _ptr(s),
-                      len(order), _ptr(eng._base.f32), _ptr(eng._base.i64) if n_i else None, _ptr(out_f),
+                      len(order), _ptr(self._base.f32), _ptr(self._base.i64) if n_i else None, _ptr(out_f),
                       _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
         else:
-            eng.launch_fedavg(lay, tf, ti, w, s, len(order), None if deltas else eng._base.f32,
-                              None if deltas else eng._base.i64, out_f, out_i, stream)
+            eng.launch_fedavg(lay, tf, ti, w, s, len(order), None if deltas else self._base.f32,
+                              None if deltas else self._base.i64, out_f, out_i, stream)
         e1.record(stream)
         self._kernel_events = (e0, e1)
         self._fetch(stream, out_f, out_i, (tf, ti, w, s))
@@ -677,7 +691,7 @@ class AggregationRound:
         e0.record(stream)
         n_i = lay.n_i64
         _lib.call("plato_agg_fedavg_w64", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w64), _ptr(wi), len(order),
-                  None if deltas else _ptr(eng._base.f32), None if (deltas or not n_i) else _ptr(eng._base.i64),
+                  None if deltas else _ptr(self._base.f32), None if (deltas or not n_i) else _ptr(self._base.i64),
                   _ptr(out_f), _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
         e1.record(stream)
         self._kernel_events = (e0, e1)
@@ -702,8 +716,70 @@ class AggregationRound:
         if not slots:
             raise ValueError("no client slots")
         if self.codec != "native":
-            raise NotImplementedError("per-entry kernels take native (fp32/int64) payloads")
+            raise ValueError("per-entry kernels take fp32 rows: run them on rnd.decoded() for coded payloads")
         return slots
+
+    def _stage_model(self, state_dict, what: str, stream) -> DeviceArena:
+        """A native model (e.g. Port's stored global model) as a device arena of this round's layout."""
+        self.layout.check_compatible(state_dict, what)
+        eng = self.engine
+        arena = DeviceArena(self.layout, eng.device)
+        eng._stager.put(state_dict, arena.f32, arena.i64)
+        eng._stager.fence(stream)
+        return arena
+
+    def decoded(self) -> "AggregationRound":
+        """This round as the reference's server sees coded payloads: every entry float32.
+
+        The reference dequantizes in its inbound processor (plato/processors/
+        model_dequantize.py:15-18, model_dequantize_qsgd.py:34-60) before any
+        server code runs, so FedAtt / FedAdp / Polaris / Port reduce float32
+        state_dicts whose num_batches_tracked counters are float32 too.  The
+        staged slots (bf16 or QSGD codes in HBM) and the baseline are decoded
+        once by ``plato_agg_decode_rows`` into fp32 rows of ``layout.promoted()``
+        (the counters become fp32 entries, the baseline's cast with RNE), and
+        the returned round runs the per-entry kernels on them.  Slots are the
+        same; the plain FedAvg launch stays on this round (decode in registers).
+        A native round returns itself.
+        """
+        if self.codec == "native":
+            return self
+        if self._decoded is not None:
+            return self._decoded
+        if not self.has_baseline:
+            raise ValueError("baseline not staged")
+        eng, lay = self.engine, self.layout
+        slots = [i for i in range(self.capacity) if self.staged[i]]
+        if not slots:
+            raise ValueError("no client slots staged")
+        play = lay.promoted()
+        rnd = _DecodedRound(self, play, slots)
+        stream = torch.cuda.current_stream(eng.device)
+        self.stager.fence(stream)
+        eng._stager.fence(stream)
+        cf, ci = eng._chunks(lay, 4096)
+        ncf, nci = int(cf.shape[0]), int(ci.shape[0])
+        dst_off = lay.row_f32
+        h = _stream_handle(stream)
+
+        def decode(codec, src_f, src_i, dsts, mv=None, divisor=0.0):
+            k = len(dsts)
+            tab = torch.from_numpy(np.asarray(list(src_f) + list(src_i) + list(dsts), dtype=np.int64)).to(eng.device)
+            _lib.call("plato_agg_decode_rows", _lib.PLATO_AGG_DECODE[codec], tab.data_ptr(), tab.data_ptr() + 8 * k, k,
+                      _ptr(mv), float(divisor), _ptr(cf), ncf, _ptr(ci) if nci else None, nci, dst_off,
+                      tab.data_ptr() + 16 * k, h)
+            return tab
+
+        keep = [decode("native", [_ptr(eng._base.f32)], [_ptr(eng._base.i64)], [_ptr(rnd._own_base.f32)])]
+        rows = rnd.slab.row_pointers(range(len(slots)))[0]
+        mv = None
+        if self.codec == "qsgd":
+            mv = torch.from_numpy(np.ascontiguousarray(np.stack([self._mv[i] for i in slots], axis=1))).to(eng.device)
+        keep.append(decode(self.codec, [self._pf[i] for i in slots], [self._pi[i] for i in slots], list(rows), mv,
+                           0.0 if self._level is None else float(self._level - 1)))
+        rnd._keep_decode = (keep, mv)
+        self._decoded = rnd
+        return rnd
 
     def entry_stats(self, slots: Sequence[int], v: tuple | None = None, deltas: bool = False):
         """Per (client, entry) fp64 sums over the staged slots (``plato_agg_entry_stats``).
@@ -732,7 +808,7 @@ class AggregationRound:
         vf, vi = (None, None) if v is None else v
         n_i = lay.n_i64
         _lib.call("plato_agg_entry_stats", _ptr(tf), _ptr(ti) if n_i else None, k,
-                  None if deltas else _ptr(eng._base.f32), None if (deltas or not n_i) else _ptr(eng._base.i64),
+                  None if deltas else _ptr(self._base.f32), None if (deltas or not n_i) else _ptr(self._base.i64),
                   _ptr(vf), _ptr(vi) if (vf is not None and n_i) else None,
                   _ptr(cf), ncf, _ptr(ci) if nci else None, nci, n_e, lay.n_f32, n_i, _ptr(ws), _ptr(out),
                   _stream_handle(stream))
@@ -762,8 +838,8 @@ class AggregationRound:
         out = torch.zeros(k * n_e, dtype=torch.float32, device=eng.device)
         n_i = lay.n_i64
         nef, nei = int(ef.shape[0]), int(ei.shape[0])
-        _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti) if n_i else None, k, _ptr(eng._base.f32),
-                  _ptr(eng._base.i64) if n_i else None, _ptr(ef), nef, _ptr(ei) if nei else None, nei, n_e,
+        _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti) if n_i else None, k, _ptr(self._base.f32),
+                  _ptr(self._base.i64) if n_i else None, _ptr(ef), nef, _ptr(ei) if nei else None, nei, n_e,
                   lay.n_f32, n_i, _ptr(out), _stream_handle(stream))
         return np.ascontiguousarray(out.cpu().numpy().reshape(k, n_e).T)
 
@@ -795,21 +871,23 @@ class AggregationRound:
         tf, ti = eng._pointer_tables(pf, pi)
         dw = torch.from_numpy(w).to(eng.device)
         nz = None
+        nst = None
         if noise is not None:
             nz = DeviceArena(lay, eng.device, i64_dtype=torch.float32)
             lay.check_compatible(noise, "noise", "f32")
-            eng._f32_stager().put(noise, nz.f32, nz.i64)
+            nst = eng._f32_stager(lay)
+            nst.put(noise, nz.f32, nz.i64)
         stream = torch.cuda.current_stream(eng.device)
         self.stager.fence(stream)
-        if nz is not None:
-            eng._f32_stager().fence(stream)
+        if nst is not None:
+            nst.fence(stream)
         out_f = torch.empty(lay.row_f32, dtype=torch.float32, device=eng.device)
         out_i = torch.empty(lay.row_i64, dtype=torch.float32, device=eng.device)
         n_i = lay.n_i64
         ncf, nci = int(cf.shape[0]), int(ci.shape[0])
         _lib.call("plato_agg_fedavg_entrywise", _ptr(tf), _ptr(ti) if n_i else None, k, _ptr(dw), n_e,
                   _ptr(cf), ncf, _ptr(ci) if nci else None, nci,
-                  None if deltas else _ptr(eng._base.f32), None if (deltas or not n_i) else _ptr(eng._base.i64),
+                  None if deltas else _ptr(self._base.f32), None if (deltas or not n_i) else _ptr(self._base.i64),
                   None if nz is None else _ptr(nz.f32), None if (nz is None or not n_i) else _ptr(nz.i64),
                   float(scale), float(noise_scale), _lib.PLATO_AGG_ADD_BASE if add_base else 0,
                   _ptr(out_f), _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
@@ -898,7 +976,7 @@ class AggregationRound:
                          device=eng.device)
         n_i = lay.n_i64
         _lib.call("plato_agg_fedadp_dots", g_flat.data_ptr(), ptrs.data_ptr(), ptrs.data_ptr() + 8 * k, k,
-                  _ptr(eng._base.f32), _ptr(eng._base.i64) if n_i else None, segs.data_ptr(), len(order), n_flat,
+                  _ptr(self._base.f32), _ptr(self._base.i64) if n_i else None, segs.data_ptr(), len(order), n_flat,
                   lay.n_f32, n_i, float(lr), 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(), _stream_handle(stream))
         xy_h, yy_h = xy.cpu().numpy(), yy.cpu().numpy()  # stream-ordered D2H (syncs this stream)
         self._keep_flat = (g_flat, ptrs, ws)
@@ -930,7 +1008,7 @@ class AggregationRound:
         per = max(1, int(batch_bytes // (stride * 4)))
         ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(min(k, per), 1) // 4, dtype=torch.float32,
                          device=eng.device)
-        base = (_ptr(eng._base.f32), _ptr(eng._base.i64))
+        base = (_ptr(self._base.f32), _ptr(self._base.i64))
         keep = []
         for s0 in range(0, k, per):
             part = slots[s0:s0 + per]
@@ -986,7 +1064,7 @@ class AggregationRound:
         ws = torch.empty(max(1, eng.lib.plato_agg_np_sumsq_workspace(k, n_chunks) // 4), dtype=torch.float32,
                          device=eng.device)
         dev_out = torch.empty((k, n_p), dtype=torch.float32, device=eng.device)
-        _lib.call("plato_agg_np_sumsq", tf.data_ptr(), k, _ptr(eng._base.f32), pieces.data_ptr(), first.data_ptr(),
+        _lib.call("plato_agg_np_sumsq", tf.data_ptr(), k, _ptr(self._base.f32), pieces.data_ptr(), first.data_ptr(),
                   n_p, n_chunks, ws.data_ptr(), dev_out.data_ptr(), _stream_handle(stream))
         out[:, entry_of] = dev_out.cpu().numpy()
         return out
@@ -1016,20 +1094,17 @@ class AggregationRound:
         threads = torch.get_num_threads() if threads is None else int(threads)
         eng = self.engine
         lay = self.layout
-        lay.check_compatible(reference, "reference model")
         stream = torch.cuda.current_stream(eng.device)
-        prev = DeviceArena(lay, eng.device)
-        eng._stager.put(reference, prev.f32, prev.i64)
-        eng._stager.fence(stream)
+        prev = self._stage_model(reference, "reference model", stream)
         self.stager.fence(stream)
         segs, n_flat = self._flat_segments(list(range(len(lay.entries))), False)
         n_segs = len(lay.entries)
         # current - previous, then each client's delta, as torch.cat lays them out
-        cur, stride = self._flatten(_lib.PLATO_AGG_FLAT_CAST_DIFF, segs, n_segs, n_flat, [_ptr(eng._base.f32)],
-                                    [_ptr(eng._base.i64)], (_ptr(prev.f32), _ptr(prev.i64)), 0.0, stream)
+        cur, stride = self._flatten(_lib.PLATO_AGG_FLAT_CAST_DIFF, segs, n_segs, n_flat, [_ptr(self._base.f32)],
+                                    [_ptr(self._base.i64)], (_ptr(prev.f32), _ptr(prev.i64)), 0.0, stream)
         k = len(slots)
         deltas, _ = self._flatten(_lib.PLATO_AGG_FLAT_DELTA, segs, n_segs, n_flat, [self._pf[i] for i in slots],
-                                  [self._pi[i] for i in slots], (_ptr(eng._base.f32), _ptr(eng._base.i64)), 0.0,
+                                  [self._pi[i] for i in slots], (_ptr(self._base.f32), _ptr(self._base.i64)), 0.0,
                                   stream)
         rows = [cur.data_ptr()] + [deltas.data_ptr() + r * stride * 4 for r in range(k)]
         tab = torch.from_numpy(np.asarray(rows, dtype=np.int64)).to(eng.device)
@@ -1074,6 +1149,60 @@ class AggregationRound:
         host_f, host_i = self._out[0], self._out[1]
         self._out = None
         return self.layout.unpack(host_f, host_i)
+
+
+class _DecodedRound(AggregationRound):
+    """A coded round's slots and baseline as fp32 rows of the promoted layout (AggregationRound.decoded)."""
+
+    def __init__(self, parent: AggregationRound, layout: ArenaLayout, slots: Sequence[int]):
+        eng = parent.engine
+        self._parent = parent
+        self.engine = eng
+        self.layout = layout
+        self.capacity = parent.capacity
+        self.codec = "native"
+        self.slab = ClientSlab(layout, len(slots), eng.device)
+        self.stager = parent.stager
+        self.staged = [False] * parent.capacity
+        self._pf = [0] * parent.capacity
+        self._pi = [0] * parent.capacity
+        rows = self.slab.row_pointers(range(len(slots)))
+        for r, slot in enumerate(slots):
+            self._pf[slot], self._pi[slot] = int(rows[0][r]), int(rows[1][r])
+            self.staged[slot] = True
+        self._mv = [None] * parent.capacity
+        self._level = None
+        self.has_baseline = True
+        self.event = None
+        self._out = None
+        self._t0 = parent._t0
+        self._kernel_events = None
+        self.timings = {}
+        self._k = 0
+        self._decoded = None
+        self._own_base = DeviceArena(layout, eng.device)
+
+    @property
+    def _base(self) -> DeviceArena:
+        return self._own_base
+
+    def decoded(self) -> "AggregationRound":
+        return self
+
+    def _stage_model(self, state_dict, what: str, stream) -> DeviceArena:
+        # staged in the model's own layout, then promoted like the baseline (counters cast to fp32)
+        native = AggregationRound._stage_model(self._parent, state_dict, what, stream)
+        out = DeviceArena(self.layout, self.engine.device)
+        lay = self._parent.layout
+        cf, ci = self.engine._chunks(lay, 4096)
+        ncf, nci = int(cf.shape[0]), int(ci.shape[0])
+        tab = torch.tensor([native.f32.data_ptr(), native.i64.data_ptr(), out.f32.data_ptr()], dtype=torch.int64,
+                           device=self.engine.device)
+        _lib.call("plato_agg_decode_rows", _lib.PLATO_AGG_DECODE["native"], tab.data_ptr(), tab.data_ptr() + 8, 1,
+                  None, 0.0, _ptr(cf), ncf, _ptr(ci) if nci else None, nci, lay.row_f32, tab.data_ptr() + 16,
+                  _stream_handle(stream))
+        self._keep_model = (native, tab)
+        return out
 
 
 def cast_to_int64(src_f32: torch.Tensor, stream: torch.cuda.Stream | None = None) -> torch.Tensor:

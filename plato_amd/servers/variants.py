@@ -74,7 +74,8 @@ class PortWeights(_EngineHolder):
         threads = torch.get_num_threads() if self.port_threads is None else int(self.port_threads)
         if self.host_order_check:
             hostorder.check_port(rnd.engine.device, threads)  # this host's F.cosine_similarity order
-        sims = rnd.model_similarities(previous, need, threads=threads)
+        # coded payloads: the per-entry reductions run on the dequantized rows (model_dequantize semantics)
+        sims = rnd.decoded().model_similarities(previous, need, threads=threads)
         out = [1.0] * len(updates)
         for i, sim in zip(need, sims):
             out[i] = sim
@@ -227,7 +228,9 @@ class FedAdpWeights(_EngineHolder):
     fedadp_lr = None
 
     def aggregation_weights(self, updates):
-        rnd = _staged_round(self, "FedAdp")
+        # coded payloads: global gradient and dots on the dequantized rows (every entry float32,
+        # as model_dequantize hands them to the reference); the final FedAvg stays on the codes
+        rnd = _staged_round(self, "FedAdp").decoded()
         if getattr(self, "local_angles", None) is None:
             self.local_angles = {}
         num_samples = [u.report.num_samples for u in updates]
@@ -270,7 +273,8 @@ class PolarisWeights(_EngineHolder):
     def aggregation_weights(self, updates):
         weights, scales = super().aggregation_weights(updates)  # FedAvg n_i/N, sets total_samples
         rnd = _staged_round(self, "Polaris")
-        sums = rnd.np_sumsq(range(len(updates)))  # numpy's float32 np.sum(np.square(delta)) per layer
+        # numpy's float32 np.sum(np.square(delta)) per layer (coded payloads: on the dequantized rows)
+        sums = rnd.decoded().np_sumsq(range(len(updates)))
         norms = W.polaris_delta_norms(sums, rnd.layout.keys())
         self.squared_deltas_current_round = np.zeros(self.number_of_client)
         sum_deltas_current_round = 0

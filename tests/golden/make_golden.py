@@ -688,6 +688,21 @@ def cases():
              num_samples=synth.num_samples(5, 29), action=rl_weights(5, 29), full=True),
         dict(name="rl_float32_resnet18_k4", model="resnet18", k=4, seed=30, mode="rl_f32",
              num_samples=synth.num_samples(4, 30), action=rl_weights(4, 30)),
+        # coded payloads reaching the variant servers: the reference dequantizes them in its inbound
+        # processor (model_dequantize / model_dequantize_qsgd) before FedAtt / FedAdp / Polaris / Port run
+        dict(name="fedatt_bf16_lenet5_k5", model="lenet5", k=5, seed=34, mode="fedatt", codec="bf16", noise_seed=5,
+             num_samples=synth.num_samples(5, 34), full=True),
+        dict(name="fedatt_qsgd_resnet18_k3", model="resnet18", k=3, seed=35, mode="fedatt", codec="qsgd",
+             noise_seed=9, num_samples=synth.num_samples(3, 35)),
+        dict(name="fedadp_bf16_resnet18_k4", model="resnet18", k=4, seed=36, mode="fedadp", codec="bf16",
+             current_round=2, num_samples=synth.num_samples(4, 36), order=[1, 3, 0, 2]),
+        dict(name="fedadp_qsgd_lenet5_k5", model="lenet5", k=5, seed=37, mode="fedadp", codec="qsgd",
+             current_round=1, num_samples=synth.num_samples(5, 37)),
+        dict(name="polaris_bf16_resnet18_k4", model="resnet18", k=4, seed=38, mode="polaris", codec="bf16",
+             num_samples=synth.num_samples(4, 38), order=[2, 0, 3, 1]),
+        dict(name="port_similarity_qsgd_lenet5_k6", model="lenet5", k=6, seed=39, mode="port", codec="qsgd",
+             num_samples=synth.num_samples(6, 39), staleness=[0, 3, 2, 5, 1, 4],
+             current_round=6, previous={"stream": 997, "scale": -26}),
         dict(name="he_plain_lenet5_k5", model="lenet5", k=5, seed=31, mode="he",
              num_samples=synth.num_samples(5, 31), encrypt_indices=list(range(0, 61706, 97)), full=True),
         dict(name="he_plain_resnet18_k3", model="resnet18", k=3, seed=32, mode="he",

@@ -83,14 +83,19 @@ def test_fedatt_kernel_contract_with_reference_attention_is_bit_exact(name):
     """entrywise_numpy (the kernel's contract) + the reference's atts + its noise stream."""
     case = CASES[name]
     recipe, exp = case["recipe"], case["expected"]
-    layout, base, pays, (bf, bi, xs_f, xs_i) = G.host_state_dicts(recipe)
+    layout, base, pays, arenas = G.host_state_dicts(recipe)
+    entries, bf, bi, xs_f, xs_i, split = G.oracle_arenas(recipe, layout, *arenas)
     torch.manual_seed(recipe["noise_seed"])
     noise = {n: torch.randn(t.shape) for n, t in base.items()}
-    nf = torch.cat([noise[e.name].reshape(-1) for e in layout.entries if e.region == "f32"]).numpy()
-    ni = np.array([noise[e.name].item() for e in layout.entries if e.region == "i64"], dtype=np.float32)
+    nf = np.zeros(max([e.offset + e.numel for e in entries if e.region == "f32"] + [0]), dtype=np.float32)
+    for e in entries:
+        if e.region == "f32":
+            nf[e.offset:e.offset + e.numel] = noise[e.name].reshape(-1).numpy()
+    ni = np.array([noise[e.name].item() for e in entries if e.region == "i64"], dtype=np.float32)
     atts = _hex_matrix(exp["fedatt_atts"])
-    new_f, new_i = ref.entrywise_numpy(layout.entries, bf, bi, xs_f, xs_i, -atts.astype(np.float64),
+    new_f, new_i = ref.entrywise_numpy(entries, bf, bi, xs_f, xs_i, -atts.astype(np.float64),
                                        scale=-1.2, noise_f=nf, noise_i=ni, noise_scale=0.001)
+    new_f, new_i = split(new_f, new_i)
     assert G.sha(G.canon(new_f)) == exp["updated_f32_sha256"]
     assert G.sha(G.canon(new_i)) == exp["updated_i64f_sha256"]
     assert G.sha(ref.trunc_to_int64(new_i)) == exp["loaded_i64_sha256"]
@@ -102,9 +107,10 @@ def test_fedatt_torch_order_norms_are_bit_exact(name):
     gives the reference's fp32 norms bit for bit, and weights.fedatt_attention its softmax."""
     case = CASES[name]
     recipe, exp = case["recipe"], case["expected"]
-    layout, _, _, (bf, bi, xs_f, xs_i) = G.host_state_dicts(recipe)
-    norms = np.zeros((len(layout.entries), recipe["k"]), dtype=np.float32)
-    for e_i, e in enumerate(layout.entries):
+    layout, _, _, arenas = G.host_state_dicts(recipe)
+    entries, bf, bi, xs_f, xs_i, _ = G.oracle_arenas(recipe, layout, *arenas)
+    norms = np.zeros((len(entries), recipe["k"]), dtype=np.float32)
+    for e_i, e in enumerate(entries):
         if e.region == "f32":
             rows = np.stack([np.subtract(x[e.offset:e.offset + e.numel], bf[e.offset:e.offset + e.numel],
                                          dtype=np.float32) for x in xs_f])
@@ -141,11 +147,12 @@ def _fedadp_inputs(recipe):
 def test_fedadp_oracle_reproduces_reference(name):
     case = CASES[name]
     recipe, exp = case["recipe"], case["expected"]
-    layout, base, pays, (bf, bi, xs_f, xs_i), ns, deltas = _fedadp_inputs(recipe)
+    layout, base, pays, arenas, ns, deltas = _fedadp_inputs(recipe)
+    _, bf, bi, xs_f, xs_i, split = G.oracle_arenas(recipe, layout, *arenas)
     w1 = ref.fedavg_weights(ns)
     d_f = [np.subtract(x, bf, dtype=np.float32) for x in xs_f]
     d_i = [x - bi for x in xs_i]
-    g_f, g_i = ref.deltas_numpy(d_f, d_i, w1)
+    g_f, g_i = split(*ref.deltas_numpy(d_f, d_i, w1))
     assert G.sha(G.canon(g_f)) == exp["global_grads_f32_sha256"]
     assert G.sha(G.canon(g_i)) == exp["global_grads_i64f_sha256"]
     grads = layout.unpack(torch.from_numpy(g_f), torch.from_numpy(g_i))
@@ -156,7 +163,7 @@ def test_fedadp_oracle_reproduces_reference(name):
     assert {str(c): "%08x" % np.float32(a).view(np.uint32) for c, a in local.items()} == exp["local_angles"]
     aw = W.fedadp_weighting(contribs, ns)
     assert [float(x).hex() for x in aw] == exp["adaptive_weighting"]
-    new_f, new_i = ref.fedavg_numpy(bf, bi, xs_f, xs_i, aw)
+    new_f, new_i = split(*ref.fedavg_numpy(bf, bi, xs_f, xs_i, aw))
     assert G.sha(G.canon(new_f)) == exp["updated_f32_sha256"]
     assert G.sha(ref.trunc_to_int64(new_i)) == exp["loaded_i64_sha256"]
 
@@ -173,7 +180,8 @@ def test_polaris_norms(name):
     ids = [c for c in G.order_of(recipe)]  # client_id - 1
     exact = ref.polaris_norms_numpy(deltas)
     assert [float(v).hex() for v in exact] == [float(want[c]).hex() for c in ids]
-    _, dd, _ = ref.entry_stats_fp64(layout.entries, bf, bi, xs_f, xs_i)
+    entries, bf, bi, xs_f, xs_i, _ = G.oracle_arenas(recipe, layout, bf, bi, xs_f, xs_i)
+    _, dd, _ = ref.entry_stats_fp64(entries, bf, bi, xs_f, xs_i)
     approx = W.polaris_delta_norms(dd, layout.keys())
     np.testing.assert_allclose(np.array(approx, dtype=np.float64), [want[c] for c in ids], rtol=1e-5)
     # the unexplored clients (all others below 200) get alpha * mean

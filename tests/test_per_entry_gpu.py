@@ -308,7 +308,10 @@ def test_fedadp_dots_tile_shapes_agree_bitwise(engine, name):
     order = rnd._fedadp_order()
     segs, n_flat = rnd._flat_segments(order, True)
     dev = torch.device(DEV)
+    probes = {6, 7, 8, 9, 10}  # timing probes of csrc/fedadp.hip (wrong results by design)
     for v in range(_lib.tune().plato_agg_tune_num_fedadp_variants()):
+        if v in probes:
+            continue
         xy = torch.full((k + 1,), float("nan"), device=dev)
         yy = torch.full((k + 1,), float("nan"), device=dev)
         _lib.tune_call("plato_agg_tune_fedadp_dots", v, g_flat.data_ptr(), ptrs.data_ptr(), ptrs.data_ptr() + 8 * k, k,
@@ -319,3 +322,130 @@ def test_fedadp_dots_tile_shapes_agree_bitwise(engine, name):
         assert xy.cpu().numpy()[:k].tobytes() == np.asarray(want[0]).tobytes(), v
         assert xy.cpu().numpy()[k:].tobytes() == np.float32(want[1]).tobytes(), v
         assert yy.cpu().numpy()[:k].tobytes() == np.asarray(want[2]).tobytes(), v
+
+
+# ------------------------------------------------------- coded payloads reaching the variants
+# The reference dequantizes bf16 / QSGD payloads in its inbound processor before FedAtt, FedAdp,
+# Polaris or Port run (plato/processors/model_dequantize.py:15-18, model_dequantize_qsgd.py:34-60);
+# the engine keeps the codes in HBM and runs those reductions on rows decoded once per round
+# (AggregationRound.decoded).  Fixtures: the reference's own servers on the dequantized payloads.
+def _coded(recipe):
+    layout, base, _, _ = G.host_state_dicts(recipe)
+    pays = G.coded_payloads(recipe)
+    st = recipe.get("staleness", [0] * recipe["k"])
+    updates = [types.SimpleNamespace(client_id=c + 1, report=types.SimpleNamespace(num_samples=recipe["num_samples"][c]),
+                                     payload=p, staleness=st[c]) for c, p in zip(G.order_of(recipe), pays)]
+    return layout, base, pays, updates
+
+
+@pytest.mark.parametrize("name", ["fedatt_bf16_lenet5_k5", "fedatt_qsgd_resnet18_k3"])
+def test_fedatt_coded_payloads_match_reference(engine, name):
+    from plato_amd.algorithms.fedavg import FedAttAlgorithmMixin
+
+    recipe, exp = CASES[name]["recipe"], CASES[name]["expected"]
+    layout, base, pays, _ = _coded(recipe)
+
+    class Algorithm(FedAttAlgorithmMixin):
+        aggregation_device = DEV
+
+    alg = Algorithm()
+    alg._plato_amd_engine = engine
+    rnd = engine.begin(base, recipe["k"], recipe["codec"])
+    rnd.put_baseline(base)
+    for i, p in enumerate(pays):
+        rnd.put_client(i, p)
+    norms = rnd.decoded().entry_norms(range(recipe["k"]))
+    assert norms.view(np.uint32).tolist() == _hex_matrix(exp["fedatt_norms"]).view(np.uint32).tolist()
+    torch.manual_seed(recipe["noise_seed"])
+    updated = asyncio.run(alg.aggregate_weights(base, pays))
+    assert list(updated) == layout.keys()
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+    assert G.sha(ref.trunc_to_int64(_flat(layout, updated, "i64"))) == exp["loaded_i64_sha256"]
+
+
+@pytest.mark.parametrize("name", ["fedadp_bf16_resnet18_k4", "fedadp_qsgd_lenet5_k5"])
+def test_fedadp_coded_payloads_match_reference(engine, name):
+    from plato_amd.servers.variants import FedAdpServerMixin
+
+    recipe, exp = CASES[name]["recipe"], CASES[name]["expected"]
+    layout, base, pays, updates = _coded(recipe)
+
+    class Server(FedAdpServerMixin):
+        aggregation_device = DEV
+        fedadp_lr = 0.01
+
+    server = Server()
+    server._plato_amd_engine = engine
+    server.current_round = recipe["current_round"]
+    server.selected_clients = [c + 1 for c in G.order_of(recipe)]
+    server.local_angles = {int(c): np.float32(float.fromhex(a)) for c, a in recipe.get("local_angles", {}).items()}
+    updated = asyncio.run(server.aggregate_weights(updates, base, pays))
+    assert [float(x).hex() for x in server.adaptive_weighting] == exp["adaptive_weighting"]
+    assert {str(c): "%08x" % np.float32(a).view(np.uint32) for c, a in server.local_angles.items()} == \
+        exp["local_angles"]
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(ref.trunc_to_int64(_flat(layout, updated, "i64"))) == exp["loaded_i64_sha256"]
+    # the global gradient on the decoded rows: the reference's digests
+    rnd = engine.begin(base, recipe["k"], recipe["codec"])
+    rnd.put_baseline(base)
+    for i, p in enumerate(pays):
+        rnd.put_client(i, p)
+    work = rnd.decoded()
+    w1 = np.tile(np.asarray([u.report.num_samples for u in updates], dtype=np.float64)
+                 / sum(u.report.num_samples for u in updates), (len(layout.entries), 1))
+    g_f, _ = work.launch_entrywise(w1, add_base=False, device=True)
+    g = g_f.cpu().numpy()
+    assert G.sha(G.canon(g[: layout.n_f32])) == exp["global_grads_f32_sha256"]
+    assert G.sha(G.canon(g[layout.row_f32: layout.row_f32 + layout.n_i64])) == exp["global_grads_i64f_sha256"]
+
+
+def test_polaris_coded_payloads_match_reference(engine):
+    from plato_amd.servers.variants import PolarisServerMixin
+
+    recipe, exp = CASES["polaris_bf16_resnet18_k4"]["recipe"], CASES["polaris_bf16_resnet18_k4"]["expected"]
+    layout, base, pays, updates = _coded(recipe)
+
+    class Server(PolarisServerMixin):
+        aggregation_device = DEV
+
+    server = Server()
+    server._plato_amd_engine = engine
+    server.number_of_client = 1024
+    server.unexplored_clients = list(range(1024))
+    server.alpha = 10
+    updated = asyncio.run(server.aggregate_weights(updates, base, pays))
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(ref.trunc_to_int64(_flat(layout, updated, "i64"))) == exp["loaded_i64_sha256"]
+    want = {int(c): float.fromhex(v) for c, v in exp["squared_deltas"].items()}
+    got = {i: float(v) for i, v in enumerate(server.squared_deltas_current_round) if v != 0}
+    assert {c: v.hex() for c, v in got.items()} == {c: v.hex() for c, v in want.items()}
+
+
+def test_port_coded_payloads_with_stale_model_match_reference(tmp_path):
+    from oracle import synth
+    from plato_amd.servers.variants import PortServerMixin
+
+    case = CASES["port_similarity_qsgd_lenet5_k6"]
+    recipe = case["recipe"]
+    layout, base, pays, updates = _coded(recipe)
+    bf, bi = synth.baseline_arena(layout.n_f32, layout.n_i64, recipe["seed"])
+    pv = recipe["previous"]
+    prev = layout.unpack(torch.from_numpy(synth.synth_f32(layout.n_f32, recipe["seed"], pv["stream"], pv["scale"],
+                                                          add=bf)),
+                         torch.from_numpy(synth.synth_i64(layout.n_i64, recipe["seed"], pv["stream"], 3, add=bi)))
+    path = tmp_path / "model_prev.pth"
+    torch.save(prev, path)
+
+    class Server(PortServerMixin):
+        aggregation_device = DEV
+        staleness_weight = 3
+        current_round = recipe["current_round"]
+        port_threads = 8  # the fixture host's torch pool
+
+        def port_previous_model_path(self):
+            return str(path)
+
+    updated = asyncio.run(Server().aggregate_weights(updates, base, pays))
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == case["expected"]["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == case["expected"]["updated_i64f_sha256"]
