@@ -25,13 +25,31 @@ from ..engine import FedAvgEngine
 
 class _AlgorithmEngine:
     aggregation_device = None
+    #: several devices: FedAtt's round is sharded by whole entries over them
+    #: (plato_amd.multi.EntryShardedEngine); the other methods use the first
+    aggregation_devices = None
 
     def aggregation_engine(self) -> FedAvgEngine:
         eng = getattr(self, "_plato_amd_engine", None)
         if eng is None:
-            eng = FedAvgEngine(self.aggregation_device)
+            devices = self.aggregation_devices
+            device = devices[0] if devices else self.aggregation_device
+            eng = FedAvgEngine(f"cuda:{device}" if isinstance(device, int) else device)
             self._plato_amd_engine = eng
         return eng
+
+    def entry_engine(self):
+        """The engine of per-entry rounds: every device of ``aggregation_devices``, else the one engine."""
+        devices = self.aggregation_devices
+        if devices is None or len(devices) < 2:
+            return self.aggregation_engine()
+        multi = getattr(self, "_plato_amd_multi", None)
+        if multi is None:
+            from ..multi import MultiDeviceEngine
+
+            multi = MultiDeviceEngine([f"cuda:{d}" if isinstance(d, int) else d for d in devices])
+            self._plato_amd_multi = multi
+        return multi.entries
 
     async def _off_loop(self, fn, *args):
         """Run ``fn`` on the algorithm's one aggregation worker thread (device work off the event loop)."""
@@ -104,7 +122,8 @@ class FedAttAlgorithmMixin(_AlgorithmEngine):
 
         from ..arena import payload_codec
 
-        engine = self.aggregation_engine()
+        # per-(entry, client) norms and a per-entry weighted sum: whole entries shard over several GPUs
+        engine = self.entry_engine()
         try:
             rnd = engine.begin(baseline_weights, len(weights_received), payload_codec(weights_received[0]))
 

@@ -27,6 +27,7 @@ from __future__ import annotations
 from dataclasses import dataclass
 from typing import Sequence
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -67,6 +68,67 @@ class BucketPlan:
         lo, hi = self.f32_range(rank)
         a, b = self.i64_range(rank)
         return (k + 2) * ((hi - lo) * 4 + (b - a) * 8)
+
+
+@dataclass(frozen=True)
+class EntryPlan:
+    """Entry-aligned sharding: shard g holds whole entries ``[groups[g][0], groups[g][1])`` (layout order).
+
+    The per-entry reductions of the variant servers — FedAtt's per-(entry,
+    client) norms and attentive sum (fedatt_algorithm.py:23-69), Polaris'
+    per-layer squared sums (polaris_server.py:68-100), QSGD's per-entry scales
+    (model_dequantize_qsgd.py:34-60) — read one entry at a time, so cutting the
+    model between entries keeps every value on one GPU and bit-identical to
+    the one-GPU result.  Groups are contiguous and chosen to minimise the
+    largest group's element count (fp32 and int64 elements alike; a small
+    dynamic program over the entry boundaries); every shard holds at least one
+    entry unless there are more shards than entries.
+    """
+
+    groups: tuple  # ((lo, hi), ...) entry index ranges, one per shard
+
+    @classmethod
+    def make(cls, sizes: Sequence[int], world: int) -> "EntryPlan":
+        if world < 1:
+            raise ValueError("world must be >= 1")
+        n = len(sizes)
+        prefix = np.concatenate([[0], np.cumsum(np.asarray(sizes, dtype=np.float64))])
+        empty_ok = n < world  # more shards than entries: some stay empty
+        # dp[j]: the smallest possible largest shard when the first j entries fill g shards
+        inf = float("inf")
+        dp = np.full(n + 1, inf)
+        dp[0] = 0.0
+        back = []
+        for g in range(1, world + 1):
+            new = np.full(n + 1, inf)
+            arg = np.zeros(n + 1, dtype=np.int64)
+            for j in range(n + 1):
+                hi = j if empty_ok else j - 1  # the last shard takes entries [i, j)
+                if hi < 0:
+                    continue
+                cost = np.maximum(dp[: hi + 1], prefix[j] - prefix[: hi + 1])
+                i = int(np.argmin(cost))
+                new[j], arg[j] = cost[i], i
+            back.append(arg)
+            dp = new
+        cuts = [n]
+        for g in range(world - 1, 0, -1):
+            cuts.append(int(back[g][cuts[-1]]))
+        cuts.append(0)
+        cuts.reverse()
+        return cls(tuple((cuts[r], cuts[r + 1]) for r in range(world)))
+
+    @classmethod
+    def for_layout(cls, layout: ArenaLayout, world: int) -> "EntryPlan":
+        return cls.make([e.numel for e in layout.entries], world)
+
+    @property
+    def world(self) -> int:
+        return len(self.groups)
+
+    def names(self, layout: ArenaLayout, shard: int) -> list[str]:
+        lo, hi = self.groups[shard]
+        return [e.name for e in layout.entries[lo:hi]]
 
 
 @dataclass(frozen=True)

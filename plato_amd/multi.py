@@ -20,9 +20,15 @@ contract and drives every GPU of the node from the server process:
   by an RCCL all-gather over xGMI (``plato_agg_comm_allgather_f32``, one
   communicator per GPU from ``ncclCommInitAll``).
 
-Rounds whose weights need reductions over the whole staged model (Port's
-similarity, FedAdp, FedAtt, Polaris) or per-entry scales (QSGD payloads) run on
-the first device's single-GPU engine (:attr:`MultiDeviceEngine.primary`).
+Rounds that reduce per entry — FedAtt's norms and attentive sum, Polaris'
+per-layer squared sums, QSGD payloads with their per-entry scales — are
+sharded by whole entries instead (:attr:`MultiDeviceEngine.entries`,
+:class:`~plato_amd.distributed.EntryPlan`): GPU g runs the single-GPU engine
+on its contiguous group of entries, every value stays on one GPU and the
+per-entry results are concatenated in layout order.  Rounds whose weights need
+serial reductions over the whole flattened model (Port's cosine similarity,
+FedAdp's dots: one fma chain per vector in the reference's order) run on the
+first device's engine (:attr:`MultiDeviceEngine.primary`).
 """
 
 from __future__ import annotations
@@ -37,7 +43,7 @@ import torch
 
 from . import _lib
 from .arena import CODECS, ArenaLayout, payload_codec
-from .distributed import BucketPlan
+from .distributed import BucketPlan, EntryPlan
 from .engine import FedAvgEngine, fp32_weights, require_device
 from .staging import HostPacker, PinnedRing, ResultPool, arena_source, payload_fingerprint
 
@@ -120,10 +126,18 @@ class MultiDeviceEngine:
         self._arrivals: dict = {}
         self._arrival_free: dict = {}
         self._comm = None
+        self._entries: "EntryShardedEngine | None" = None
 
     @property
     def world(self) -> int:
         return len(self.devices)
+
+    @property
+    def entries(self) -> "EntryShardedEngine":
+        """The same devices sharded by whole entries (per-entry variant rounds, QSGD payloads)."""
+        if self._entries is None:
+            self._entries = EntryShardedEngine(self)
+        return self._entries
 
     # ------------------------------------------------------------ layout
     def _prepare(self, template: Mapping[str, torch.Tensor] | ArenaLayout) -> ArenaLayout:
@@ -210,6 +224,8 @@ class MultiDeviceEngine:
             self._arrival_free.setdefault(codec, []).append((slabs, row))
         self._arrivals = {}
         self.primary.release_arrivals()
+        if self._entries is not None:
+            self._entries._release()
 
     def comm(self):
         """The RCCL communicator over the engine's devices (distinct GPUs only)."""
@@ -446,3 +462,269 @@ class MultiRound:
         self._out = None
         self._keep = None
         return self.layout.unpack(host_f, host_i)
+
+
+# --------------------------------------------------------------- entry-aligned shards
+def _sub_payload(payload, names: Sequence[str]):
+    """The entries ``names`` of a payload (same tensors, no copy); QSGD payloads keep their scales."""
+    from .processors.qsgd import QsgdPayload
+
+    if getattr(payload, "plato_codec", None) == "qsgd":
+        return QsgdPayload(((n, payload[n]) for n in names), max_v={n: payload.max_v[n] for n in names},
+                           shapes={n: payload.shapes[n] for n in names}, level=payload.level)
+    return OrderedDict((n, payload[n]) for n in names)
+
+
+class EntryShardedEngine:
+    """The devices of a :class:`MultiDeviceEngine`, sharded by whole entries (:class:`EntryPlan`).
+
+    Shard g is a single-GPU :class:`~plato_amd.engine.FedAvgEngine` on device g
+    that sees only its contiguous group of the model's entries: payloads are
+    split by key (the tensors are not copied), each shard packs and copies its
+    entries on its own copy stream (N PCIe links), and every single-GPU round
+    operation — the FedAvg launches of every codec, the decode of coded slots,
+    ``entry_norms`` / ``entry_stats`` / ``np_sumsq`` / ``launch_entrywise`` —
+    runs per shard, concurrently, on one worker thread per shard.  Same
+    surface as an engine: ``begin`` / ``prestage`` / ``release_arrivals``.
+    """
+
+    def __init__(self, multi: MultiDeviceEngine):
+        self.multi = multi
+        self.devices = multi.devices
+        self.variant = multi.variant
+        self._engines = [FedAvgEngine(d, variant=multi.variant) for d in self.devices]
+        self._plans: dict = {}
+        self._arrivals: dict = {}
+        self._pool = None
+
+    @property
+    def world(self) -> int:
+        return len(self.devices)
+
+    @property
+    def device(self) -> torch.device:
+        return self.devices[0]
+
+    def plan(self, layout: ArenaLayout) -> tuple[EntryPlan, list]:
+        """(plan, [(shard, entry names)] of the non-empty shards) for ``layout`` (cached by signature)."""
+        hit = self._plans.get(layout.signature)
+        if hit is None:
+            plan = EntryPlan.for_layout(layout, self.world)
+            parts = [(g, plan.names(layout, g)) for g in range(self.world) if plan.groups[g][1] > plan.groups[g][0]]
+            hit = self._plans[layout.signature] = (plan, parts)
+        return hit
+
+    def each(self, fn, items):
+        """``[fn(item) ...]`` with one worker thread per shard (torch / HIP calls release the GIL)."""
+        items = list(items)
+        if len(items) <= 1:
+            return [fn(x) for x in items]
+        if self._pool is None:
+            import concurrent.futures
+
+            self._pool = concurrent.futures.ThreadPoolExecutor(self.world, thread_name_prefix="plato-amd-shard")
+        return list(self._pool.map(fn, items))
+
+    def begin(self, template, capacity: int, codec: str = "native") -> "EntryRound":
+        if capacity <= 0:
+            raise ValueError("no client payloads to aggregate")
+        if isinstance(template, ArenaLayout):
+            raise TypeError("begin() needs the baseline state_dict (its tensors define every shard's arena)")
+        layout = ArenaLayout.from_state_dict(template)
+        _, parts = self.plan(layout)
+
+        def start(part):
+            g, names = part
+            with torch.cuda.device(self.devices[g]):
+                return self._engines[g].begin(OrderedDict((n, template[n]) for n in names), capacity, codec)
+
+        return EntryRound(self, layout, [(g, names) for g, names in parts], self.each(start, parts), codec)
+
+    def prestage(self, payload, baseline_layout: ArenaLayout) -> bool:
+        """Copy each shard's entries of an arriving payload to its GPU now (adopted by the next round)."""
+        codec = payload_codec(payload)
+        try:
+            baseline_layout.check_compatible(payload, "arriving payload", codec)
+        except (KeyError, ValueError):
+            return False
+        _, parts = self.plan(baseline_layout)
+        subs = [_sub_payload(payload, names) for _, names in parts]
+        for (g, names), sub in zip(parts, subs):
+            lay = self._sub_layout(baseline_layout, names)
+            with torch.cuda.device(self.devices[g]):
+                if not self._engines[g].prestage(sub, lay):
+                    return False
+        self._arrivals[id(payload)] = (payload, payload_fingerprint(payload), subs)
+        return True
+
+    def _sub_layout(self, layout: ArenaLayout, names) -> ArenaLayout:
+        key = ("entry_sub_layout", tuple(names))
+        hit = layout._cache.get(key)
+        if hit is None:
+            hit = layout._cache[key] = ArenaLayout.from_shapes([(layout[n].name, layout[n].shape, layout[n].region)
+                                                                for n in names])
+        return hit
+
+    def _arrival_subs(self, payload):
+        hit = self._arrivals.get(id(payload))
+        if hit is None or hit[0] is not payload or hit[1] != payload_fingerprint(payload):
+            return None  # not prestaged here, or edited after arrival: the round stages its current tensors
+        return hit[2]
+
+    def _release(self) -> None:
+        self._arrivals = {}
+        for eng in self._engines:
+            eng.release_arrivals()
+
+    def release_arrivals(self) -> None:
+        self.multi.release_arrivals()
+
+
+class EntryRound:
+    """One entry-sharded round: a single-GPU round per shard over its entries, results in layout order.
+
+    Per-entry outputs are concatenated along the entry axis (``entry_norms``
+    [E, K], ``np_sumsq`` [K, E], ``entry_stats``); model results are merged
+    key by key in baseline order.  Whole-model flattened reductions (FedAdp's
+    dots, Port's similarity) are not entry-local and are not offered here.
+    """
+
+    def __init__(self, engine: EntryShardedEngine, layout: ArenaLayout, parts, rounds, codec: str):
+        self.engine = engine
+        self.layout = layout
+        self.codec = codec
+        self._parts = parts          # [(shard, entry names)]
+        self._rounds = rounds        # the shards' AggregationRounds (or their decoded views)
+        self.capacity = rounds[0].capacity
+        self.timings: dict = {}
+        self._t0 = time.perf_counter()
+        self._k = 0
+        self._decoded = None
+
+    def _each(self, fn):
+        eng = self.engine
+
+        def run(i):
+            g = self._parts[i][0]
+            with torch.cuda.device(eng.devices[g]):
+                return fn(i, self._rounds[i])
+
+        return eng.each(run, range(len(self._rounds)))
+
+    def _split(self, state_dict):
+        return [_sub_payload(state_dict, names) for _, names in self._parts]
+
+    @property
+    def has_baseline(self) -> bool:
+        return all(r.has_baseline for r in self._rounds)
+
+    @property
+    def staged(self) -> list:
+        return [all(r.staged[s] for r in self._rounds) for s in range(self.capacity)]
+
+    # ------------------------------------------------------------ staging
+    def put_baseline(self, baseline) -> None:
+        self.layout.check_compatible(baseline, "baseline_weights")
+        subs = self._split(baseline)
+        self._each(lambda i, r: r.put_baseline(subs[i]))
+        self._decoded = None
+
+    def put_client(self, slot: int, payload, what: str = "weights_received") -> None:
+        if not 0 <= slot < self.capacity:
+            raise IndexError(f"slot {slot} outside [0, {self.capacity})")
+        self.layout.check_compatible(payload, f"{what}[{slot}]", self.codec)
+        subs = self._split(payload)
+        self._each(lambda i, r: r.put_client(slot, subs[i], what))
+        self._decoded = None
+
+    def adopt(self, slot: int, payload) -> bool:
+        subs = self.engine._arrival_subs(payload)
+        if subs is None or len(subs) != len(self._rounds):
+            return False
+        if not all(self._each(lambda i, r: r.adopt(slot, subs[i]))):
+            return False  # some shard's copy is stale: the caller stages the payload whole
+        self._decoded = None
+        return True
+
+    def decoded(self) -> "EntryRound":
+        """Coded slots decoded per shard into fp32 rows (AggregationRound.decoded); native: this round."""
+        if self.codec == "native":
+            return self
+        if self._decoded is None:
+            rounds = self._each(lambda i, r: r.decoded())
+            self._decoded = EntryRound(self.engine, self.layout.promoted(), self._parts, rounds, "native")
+        return self._decoded
+
+    # ------------------------------------------------------ per-entry reductions
+    def entry_norms(self, slots: Sequence[int]) -> np.ndarray:
+        slots = list(slots)
+        return np.concatenate(self._each(lambda i, r: r.entry_norms(slots)), axis=0)
+
+    def np_sumsq(self, slots: Sequence[int]) -> np.ndarray:
+        slots = list(slots)
+        return np.concatenate(self._each(lambda i, r: r.np_sumsq(slots)), axis=1)
+
+    def entry_stats(self, slots: Sequence[int], v: tuple | None = None, deltas: bool = False):
+        if v is not None:
+            raise ValueError("entry_stats with a device vector runs on one GPU")
+        slots = list(slots)
+        outs = self._each(lambda i, r: r.entry_stats(slots, None, deltas))
+        return None, np.concatenate([o[1] for o in outs], axis=1), None
+
+    def _rows(self):
+        """Entry rows of each shard in the layout (a shard's entries are contiguous)."""
+        rows, lo = [], 0
+        for _, names in self._parts:
+            rows.append((lo, lo + len(names)))
+            lo += len(names)
+        return rows
+
+    def launch_entrywise(self, weights: np.ndarray, order: Sequence[int] | None = None, scale: float = 1.0,
+                         noise: Mapping[str, torch.Tensor] | None = None, noise_scale: float = 0.0,
+                         add_base: bool = True, deltas: bool = False, device: bool = False):
+        if device:
+            raise ValueError("device-resident entrywise results stay on one GPU (FedAdp runs on the primary)")
+        w = np.asarray(weights)
+        if w.shape[0] != len(self.layout.entries):
+            raise ValueError(f"weights must be [entries={len(self.layout.entries)}, clients], got {w.shape}")
+        rows = self._rows()
+        noises = None if noise is None else self._split(noise)
+        self._t0 = time.perf_counter()
+        self._each(lambda i, r: r.launch_entrywise(w[rows[i][0]:rows[i][1]], order, scale,
+                                                   None if noises is None else noises[i], noise_scale,
+                                                   add_base, deltas))
+        self._k = w.shape[1]
+
+    # --------------------------------------------------------- FedAvg launches
+    def launch(self, weights: Sequence[float], scales: Sequence[float] | None = None,
+               order: Sequence[int] | None = None, deltas: bool = False) -> None:
+        self._each(lambda i, r: r.launch(weights, scales, order, deltas))
+        self._k = len(weights)
+
+    def launch_w64(self, weights64: Sequence[float], weights_i64: Sequence[float] | None = None,
+                   order: Sequence[int] | None = None, deltas: bool = False) -> None:
+        self._each(lambda i, r: r.launch_w64(weights64, weights_i64, order, deltas))
+        self._k = len(weights64)
+
+    def ready(self) -> bool:
+        return all(r.ready() for r in self._rounds)
+
+    def wait(self) -> None:
+        for r in self._rounds:
+            r.wait()
+
+    def algorithmic_bytes(self) -> int:
+        return sum(r.layout.algorithmic_bytes(self._k) for r in self._rounds)
+
+    def result(self) -> "OrderedDict[str, torch.Tensor]":
+        parts = self._each(lambda i, r: r.result())
+        merged = {}
+        for p in parts:
+            merged.update(p)
+        self.timings = {
+            "stage_ms": max(r.timings.get("stage_ms", 0.0) for r in self._rounds),
+            "kernel_ms": max(r.timings.get("kernel_ms", 0.0) for r in self._rounds),
+            "d2h_ms": max(r.timings.get("d2h_ms", 0.0) for r in self._rounds),
+            "total_ms": (time.perf_counter() - self._t0) * 1e3,
+        }
+        return OrderedDict((n, merged[n]) for n in self.layout.keys())

@@ -41,8 +41,12 @@ class _EngineHolder:
     #: kernel variant override (tuning only; None = library default)
     aggregation_variant = None
     #: weights computed from the staged payloads (Port, FedAdp, Polaris): such
-    #: rounds run on one GPU (the multi-GPU engine's first device)
+    #: rounds run on one GPU (the multi-GPU engine's first device) unless every
+    #: reduction they need is per entry (``entry_local_weights``)
     needs_staged_round = False
+    #: the staged-round weights reduce entry by entry (Polaris' per-layer sums):
+    #: the round is sharded by whole entries over ``aggregation_devices``
+    entry_local_weights = False
     #: FedAdp / Port: before the first round, check that this host's numpy / torch
     #: reduction order is the one the device reproduces (plato_amd.hostorder)
     host_order_check = True
@@ -64,11 +68,22 @@ class _EngineHolder:
         return eng
 
     def round_engine(self, codec: str):
-        """The engine one round runs on (multi-GPU unless the round needs one device)."""
+        """The engine one round runs on.
+
+        One GPU: its engine.  Several: parameter buckets for plain rounds of
+        native / bf16 payloads; whole-entry shards (``MultiDeviceEngine.entries``)
+        for QSGD payloads (per-entry scales) and entry-local staged weights
+        (Polaris); the first GPU for weights that reduce the whole flattened
+        model serially (Port's similarity, FedAdp's dots).
+        """
         eng = self.aggregation_engine()
         primary = getattr(eng, "primary", None)
-        if primary is not None and (self.needs_staged_round or codec not in ("native", "bf16")):
+        if primary is None:
+            return eng
+        if self.needs_staged_round and not self.entry_local_weights:
             return primary
+        if self.needs_staged_round or codec not in ("native", "bf16"):
+            return eng.entries
         return eng
 
     def aggregation_executor(self) -> concurrent.futures.ThreadPoolExecutor:

@@ -269,6 +269,7 @@ class PolarisWeights(_EngineHolder):
     """
 
     needs_staged_round = True
+    entry_local_weights = True  # per-layer sums: sharded by whole entries over aggregation_devices
 
     def aggregation_weights(self, updates):
         weights, scales = super().aggregation_weights(updates)  # FedAvg n_i/N, sets total_samples

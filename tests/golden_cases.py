@@ -90,6 +90,12 @@ def weights_for(recipe, impl, similarities=None):
     raise ValueError(mode)
 
 
+def plain_fedavg_weights(recipe) -> bool:
+    """The case's expected model follows from weights_for() alone (no staged-round reduction:
+    FedAtt / FedAdp, or Port with a stale model on disk, have their own tests)."""
+    return recipe.get("mode", "fedavg") not in ("fedatt", "fedadp") and "previous" not in recipe
+
+
 def fedasync_mixing(recipe, impl):
     st = recipe.get("staleness", [0])[0]
     return impl.fedasync_mixing(0.9, st, "hinge", 10, 4)

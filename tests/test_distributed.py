@@ -8,7 +8,7 @@ import sys
 
 import pytest
 
-from plato_amd.distributed import BucketPlan, client_shard
+from plato_amd.distributed import BucketPlan, EntryPlan, client_shard
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -43,6 +43,31 @@ def test_bucket_plan_covers_arena_once(n_f32, world):
     assert seen == n_f32
     assert plan.i64_range(0) == (0, 20) and all(plan.i64_range(r) == (0, 0) for r in range(1, world))
     assert sum(plan.bucket_bytes(r, 5) for r in range(world)) == 7 * (n_f32 * 4 + 20 * 8)
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 8, 13])
+@pytest.mark.parametrize("model", ["lenet5", "resnet18", "tiny"])
+def test_entry_plan_partitions_whole_entries(model, world):
+    """Entry-aligned shards: contiguous, every entry once, in order, balanced by elements."""
+    from plato_amd.arena import ArenaLayout
+    from tests import golden_cases as G
+
+    spec = [("a", (3,), "f32"), ("n", (), "i64"), ("b", (5000,), "f32")] if model == "tiny" else G.model_spec(model)
+    layout = ArenaLayout.from_shapes(spec)
+    plan = EntryPlan.for_layout(layout, world)
+    assert plan.world == world
+    n = len(layout.entries)
+    assert plan.groups[0][0] == 0 and plan.groups[-1][1] == n
+    for (a, b), (c, d) in zip(plan.groups, plan.groups[1:]):
+        assert a <= b == c <= d
+    names = [x for g in range(world) for x in plan.names(layout, g)]
+    assert names == layout.keys()
+    if n >= world:
+        assert all(b > a for a, b in plan.groups)  # every shard holds at least one entry
+    sizes = [sum(e.numel for e in layout.entries[a:b]) for a, b in plan.groups]
+    biggest = max(e.numel for e in layout.entries)
+    # no shard exceeds its share by more than one entry (the cut is at the nearest entry boundary)
+    assert max(sizes) <= sum(sizes) / world + biggest
 
 
 def test_client_shard_partition():

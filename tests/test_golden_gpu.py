@@ -70,7 +70,8 @@ def _launch(engine, layout, base, slab, order, weights, scales, deltas=False):
 NON_ASYNC = [c for c in CASES
              if c["recipe"].get("mode", "fedavg") not in ("fedasync", "gan") + G.PER_ENTRY_MODES + G.OWN_TEST_MODES
              and c["recipe"].get("codec") is None]
-BF16 = [c for c in CASES if c["recipe"].get("codec") == "bf16"]
+BF16 = [c for c in CASES if c["recipe"].get("codec") == "bf16"
+        and G.plain_fedavg_weights(c["recipe"])]
 
 
 @pytest.mark.parametrize("case", NON_ASYNC, ids=[c["recipe"]["name"] for c in NON_ASYNC])

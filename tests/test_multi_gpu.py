@@ -10,6 +10,7 @@ and runs when the box has them.
 
 import asyncio
 import pickle
+import types
 
 import numpy as np
 import pytest
@@ -251,3 +252,125 @@ def test_result_buffers_are_not_recycled_under_a_kept_result():
         assert torch.equal(first[k], snapshot[k]), k
     ptrs = {eng.aggregate_weights(baseline, payloads, weights)[layout.entries[0].name].data_ptr() for _ in range(3)}
     assert len(ptrs) <= 2  # dropped results give their buffer back to the pool
+
+
+# ------------------------------------------------------------ entry-aligned shards
+# FedAtt, Polaris and QSGD payloads reduce entry by entry (fedatt_algorithm.py:23-69,
+# polaris_server.py:68-100, model_dequantize_qsgd.py:34-60): over several devices their rounds
+# are sharded by whole entries (MultiDeviceEngine.entries), each shard a single-GPU round over
+# its entries.  Same reference digests at every shard count, including more shards than some
+# models have large entries.
+def _entry_host(name):
+    from tests.test_per_entry_gpu import CASES as PE, _host
+
+    return PE[name], _host(PE[name]["recipe"])
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("name", ["fedatt_resnet18_k8", "fedatt_lenet5_k6", "fedatt_qsgd_resnet18_k3"])
+def test_entry_sharded_fedatt_matches_reference(name, n):
+    from plato_amd.algorithms.fedavg import FedAttAlgorithmMixin
+    from tests.test_per_entry_gpu import _coded, _hex_matrix
+
+    case, (layout, base, pays, _, _) = _entry_host(name)
+    recipe, exp = case["recipe"], case["expected"]
+    if recipe.get("codec"):
+        layout, base, pays, _ = _coded(recipe)
+
+    class Algorithm(FedAttAlgorithmMixin):
+        aggregation_devices = _devices(n)
+
+    alg = Algorithm()
+    eng = alg.entry_engine()
+    assert eng.world == n
+    rnd = eng.begin(base, recipe["k"], recipe.get("codec", "native"))
+    rnd.put_baseline(base)
+    for i, p in enumerate(pays):
+        rnd.put_client(i, p)
+    norms = rnd.decoded().entry_norms(range(recipe["k"]))
+    assert norms.view(np.uint32).tolist() == _hex_matrix(exp["fedatt_norms"]).view(np.uint32).tolist()
+    torch.manual_seed(recipe["noise_seed"])
+    updated = asyncio.run(alg.aggregate_weights(base, pays))
+    assert list(updated) == layout.keys()
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("name", ["polaris_resnet18_k8", "polaris_bf16_resnet18_k4"])
+def test_entry_sharded_polaris_matches_reference(name, n):
+    from plato_amd.servers.variants import PolarisServerMixin
+    from tests.test_per_entry_gpu import _coded
+
+    case, (layout, base, pays, _, updates) = _entry_host(name)
+    recipe, exp = case["recipe"], case["expected"]
+    if recipe.get("codec"):
+        layout, base, pays, updates = _coded(recipe)
+
+    class Server(PolarisServerMixin):
+        aggregation_devices = _devices(n)
+
+    server = Server()
+    server.number_of_client = 1024
+    server.unexplored_clients = list(range(1024))
+    server.alpha = 10
+    assert server.round_engine(recipe.get("codec", "native")) is server.aggregation_engine().entries
+    updated = asyncio.run(server.aggregate_weights(updates, base, pays))
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    want = {int(c): float.fromhex(v) for c, v in exp["squared_deltas"].items()}
+    got = {i: float(v) for i, v in enumerate(server.squared_deltas_current_round) if v != 0}
+    assert {c: v.hex() for c, v in got.items()} == {c: v.hex() for c, v in want.items()}
+    assert server.get_logged_items()["aggregation_gpus"] == n
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+def test_entry_sharded_qsgd_payloads_match_reference(n):
+    from oracle import qsgd as Q
+    from oracle import synth
+    from plato_amd.arena import ArenaLayout
+    from plato_amd.processors.qsgd import Processor
+    from plato_amd.servers import FusedAggregationMixin
+
+    cases = [c for c in G.load_cases() if c["recipe"].get("codec") == "qsgd" and c["recipe"]["name"].startswith("qsgd")]
+    assert cases
+    for case in cases:
+        recipe, exp = case["recipe"], case["expected"]
+        layout = ArenaLayout.from_shapes(G.model_spec(recipe["model"]))
+        k, seed = recipe["k"], recipe["seed"]
+        bf, bi = synth.baseline_arena(layout.n_f32, layout.n_i64, seed)
+        baseline = layout.unpack(torch.from_numpy(bf), torch.from_numpy(bi))
+        proc = Processor()
+        payloads = {c: proc.process(Q.client_wire(layout.entries, seed, c)[0]) for c in range(k)}
+        updates = [types.SimpleNamespace(client_id=c + 1, report=types.SimpleNamespace(num_samples=recipe["num_samples"][c]),
+                                         payload=payloads[c], staleness=0) for c in G.order_of(recipe)]
+
+        class Server(FusedAggregationMixin):
+            aggregation_devices = _devices(n)
+
+        server = Server()
+        assert server.round_engine("qsgd") is server.aggregation_engine().entries
+        # half of the payloads arrive early and are prestaged shard by shard, the rest staged at aggregation
+        eng = server.round_engine("qsgd")
+        for u in updates[::2]:
+            assert eng.prestage(u.payload, layout)
+        updated = asyncio.run(server.aggregate_weights(updates, baseline, [u.payload for u in updates]))
+        assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"], recipe["name"]
+        assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"], recipe["name"]
+        assert eng._arrivals == {}
+
+
+def test_entry_sharded_round_rejects_whole_model_reductions():
+    """Device-resident entrywise results (FedAdp's global gradient) stay on one GPU."""
+    from tests.test_per_entry_gpu import CASES as PE, _host
+    from plato_amd.multi import MultiDeviceEngine
+
+    recipe = PE["fedadp_lenet5_k6"]["recipe"]
+    layout, base, pays, _, _ = _host(recipe)
+    eng = MultiDeviceEngine(_devices(2)).entries
+    rnd = eng.begin(base, recipe["k"])
+    rnd.put_baseline(base)
+    for i, p in enumerate(pays):
+        rnd.put_client(i, p)
+    with pytest.raises(ValueError, match="one GPU"):
+        rnd.launch_entrywise(np.ones((len(layout.entries), recipe["k"])), add_base=False, device=True)
+    assert not hasattr(rnd, "fedadp_dots") and not hasattr(rnd, "model_similarities")

@@ -24,7 +24,8 @@ from tests import golden_cases as G
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
-QSGD = [c for c in G.load_cases() if c["recipe"].get("codec") == "qsgd"]
+QSGD = [c for c in G.load_cases() if c["recipe"].get("codec") == "qsgd"
+        and G.plain_fedavg_weights(c["recipe"])]
 
 
 @pytest.fixture(scope="module")
