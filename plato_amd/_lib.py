@@ -178,6 +178,7 @@ TUNE_SIGNATURES = {
         _c_int, [_c_int, _c_void_p, _c_void_p, _c_int, _c_size_t, _c_int, _c_void_p, _c_void_p, _c_void_p,
                  _c_void_p]),
     "plato_agg_tune_num_fedadp_variants": (_c_int, []),
+    "plato_agg_tune_fedadp_is_probe": (_c_int, [_c_int]),
     "plato_agg_tune_fedadp_dots": (
         _c_int,
         [_c_int, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,

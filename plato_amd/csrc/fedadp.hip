@@ -14,24 +14,26 @@
 // segment map, form loc = (x - b) or -(x - b) / lr in registers and write them transposed
 // into an LDS tile; chain waves only run the fma chains out of LDS.
 //
-// Shape (one workgroup per CU for 128 clients):
-//   * 8 pairs (clients, all sharing g) x 4 of the 64 chains per workgroup; the 16 chain groups
-//     of a pair group run on one XCD, so every 128-byte line of an arena, of b and of g is
-//     fetched from HBM once and served to the other chain groups from that XCD's L2.
-//   * chain wave: lane = kind * 32 + chain * 8 + pair, kind 0 = g . loc, kind 1 = loc . loc:
-//     ONE dependent fma per step per lane (the dots are split over lanes, not interleaved),
-//     4 steps per ds_read_b128 of a transposed row; row pitch 260 floats and vector pitch
-//     4 rows make both reads of a step and the producers' ds_write_b32 conflict-free
-//     (2-way on the writes, which is free: MI355X_MICROARCH.md §LDS).
-//   * 8 producer waves, 2 gather iterations each per 256-block stage; their global loads run
-//     two stages ahead of the tile being written (two register sets, A and B), the tile ring
-//     has two slots, one s_barrier per stage.
-//   * g . g: an extra chain wave in the workgroups of pair group 0 (x . x over the same tile).
+// Shape (the product default, kAdpDefault; one workgroup per CU for 128 clients):
+//   * 1 pair (client) x 32 of the 64 chains per workgroup: a gather iteration reads whole
+//     128-byte lines (16 bytes per lane, buffer_load_dwordx4) of the client arena, of b and of g;
+//     the two chain groups of a pair run on one XCD, so x and b are served from its L2.
+//   * chain wave: lane = kind * 32 + chain, kind 0 = g . loc, kind 1 = loc . loc: ONE dependent
+//     fma per step per lane (the dots are split over lanes, not interleaved), 4 steps per
+//     ds_read_b128 of a transposed row (row pitch kS + 4 floats: conflict-free reads and writes).
+//   * 8 producer waves, 2 gather iterations each per 128-block stage; their global loads run
+//     kD = 2 stages ahead of the tile being written (kD register sets), the tile ring has two
+//     slots, one s_barrier per stage.  A wave's current entry is cached in SGPRs: the segment
+//     map in LDS is read only at entry boundaries.
+//   * g . g: an extra chain wave in the workgroups of pair 0 (x . x over the same tile).
+// The other shapes (8 / 4 / 2 pairs per workgroup, 4-byte gathers, deeper pipelines, chain waves
+// isolated on a SIMD) and the timing probes are tuning variants (PLATO_AGG_TUNE); DESIGN.md §13.
 // Compiled with -ffp-contract=off; the chain fma is an explicit v_fma_f32.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <string>
+#include <type_traits>
 
 #include "common.h"
 #include "plato_agg.h"
@@ -58,6 +60,7 @@ __device__ __forceinline__ float chain_fma(float a, float b, float c) {
 }
 
 typedef __attribute__((address_space(1))) const float gfloat;
+typedef float f4v __attribute__((ext_vector_type(4)));
 
 // Segment map entry in LDS: positions [flat, end) read element src + (p - flat) of the region.
 struct AdpSeg {
@@ -111,15 +114,18 @@ __device__ __forceinline__ int seg_walk(const AdpSeg* S, int n_segs, uint32_t p,
 // stage; kW producer waves, kIt gather iterations of 64 positions each per stage; kVRpad floats
 // between vectors (chosen with the row pitch kS + 4 so that the chain wave's ds_read_b128 pairs
 // are conflict-free for the lane map kind * 32 + chain * kP + pair: DESIGN.md §12)
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad = 0>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad = 0, int kV = 1>
 struct AdpShape {
   static_assert(kP * kC == 32, "one chain wave: kind * 32 + chain * kP + pair");
-  static_assert(kS * kC == 64 * kW * kIt, "a stage is kW x kIt gather iterations of 64 positions");
+  static_assert(kV == 1 || kV == 4, "one or four consecutive positions per lane and gather iteration");
+  static_assert(kC % kV == 0, "a lane's positions lie in one 64-block");
+  static_assert(kS * kC == 64 * kV * kW * kIt, "a stage is kW x kIt gather iterations of 64 * kV positions");
   static_assert(kS % 16 == 0, "the chain wave reads 16 steps per block");
   static constexpr int kR = kS + 4;          // transposed row pitch (floats)
   static constexpr int kVR = kC * kR + kVRpad;  // rows of one vector (x, loc_0 .. loc_{kP-1})
   static constexpr int kSlot = (1 + kP) * kVR;
-  static constexpr int kBlkPerIt = 64 / kC;  // 64-blocks per gather iteration
+  static constexpr int kBlkPerIt = 64 * kV / kC;  // 64-blocks per gather iteration
+  static constexpr int kLpB = kC / kV;             // lanes per 64-block in a gather iteration
 };
 
 // One producer wave's loads for one stage: x, b and the kP arenas at kIt positions per lane.
@@ -149,8 +155,23 @@ __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_o
   return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
 }
 
+// A producer wave's current segment, wave-uniform (SGPRs): the positions a wave gathers only move
+// forward, so the segment map in LDS is read only when an iteration crosses into the next entry
+struct AdpCursor {
+  int idx;
+  uint32_t flat, end, src, info;
+};
+
+__device__ __forceinline__ void adp_cursor_load(const AdpSeg* S, int idx, AdpCursor& c) {
+  c.idx = idx;
+  c.flat = __builtin_amdgcn_readfirstlane(S[idx].flat);
+  c.end = __builtin_amdgcn_readfirstlane(S[idx].end);
+  c.src = __builtin_amdgcn_readfirstlane(S[idx].src);
+  c.info = __builtin_amdgcn_readfirstlane(S[idx].info);
+}
+
 template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe>
-__device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpSeg* S, int n_segs, int& cursor,
+__device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpSeg* S, int n_segs, AdpCursor& cur,
                                           const AdpSrc<kP>& src, uint32_t t, int cg, int w, int lane,
                                           AdpRegs<kP, kIt>& r) {
   using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad>;
@@ -164,17 +185,16 @@ __device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpSeg* S, int
     const uint32_t p = s * 64 + uint32_t(cg * kC + lane % kC);
     const uint32_t pf = min(s0, last) * 64 + uint32_t(cg * kC);
     const uint32_t pl = min(s0 + uint32_t(Sh::kBlkPerIt - 1), last) * 64 + uint32_t(cg * kC + kC - 1);
-    cursor = __builtin_amdgcn_readfirstlane(seg_walk(S, n_segs, pf, cursor));
-    const AdpSeg cs = S[cursor];
+    while (pf >= cur.end && cur.idx + 1 < n_segs) adp_cursor_load(S, cur.idx + 1, cur);  // rare: next entry
     uint32_t e, code;
     // the loads below are the same on both paths (no branch around them): every trip issues
     // kIt * (kP + 2) loads and the compiler's vmcnt bookkeeping covers exactly one stage
-    if (__builtin_amdgcn_readfirstlane(int(!(cs.info & kSegI64) && pl < cs.end))) {
+    if (!(cur.info & kSegI64) && pl < cur.end) {
       r.fast |= 1u << i;  // the whole iteration inside one fp32 entry: one shift for every lane
-      e = p - cs.flat + cs.src;
-      code = cs.info;
+      e = p - cur.flat + cur.src;
+      code = cur.info;
     } else {  // an entry boundary inside the iteration: per-lane entries
-      const AdpSeg ls = S[seg_walk(S, n_segs, p, cursor)];
+      const AdpSeg ls = S[seg_walk(S, n_segs, p, cur.idx)];
       const uint32_t el = p - ls.flat + ls.src;
       const bool i64 = ls.info & kSegI64;
       e = i64 ? 0u : el;
@@ -232,9 +252,136 @@ __device__ __forceinline__ void adp_write(const AdpArgs& a, float* slot, int pai
   }
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0>
-__global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
-  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad>;
+// Four consecutive positions per lane (kV = 4): a lane's x, b and loc_k come from one 16-byte
+// buffer load each (an arena position is 4-byte aligned only: dword-aligned dwordx4 loads are
+// legal, MI355X_MICROARCH.md), so a gather iteration of 256 positions costs kP + 2 load
+// instructions instead of 4 x (kP + 2).  An iteration that crosses an entry keeps the loads
+// (their values are unused) and its lanes fetch their four positions one by one at write time.
+template <int kP, int kIt>
+struct AdpRegs4 {
+  f4v x[kIt];
+  f4v b[kIt];
+  f4v y[kIt][kP];
+  uint32_t code[kIt];  // fast iterations: the entry's info; otherwise the segment index of pos[i]
+  uint32_t pos[kIt];   // first position of the lane
+  uint32_t fast;       // bit i: iteration i lies in one fp32 entry (wave-uniform)
+};
+
+__device__ __forceinline__ f4v bload4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+__device__ __forceinline__ void adp_issue4(const AdpArgs& a, const AdpSeg* S, int n_segs, AdpCursor& cur,
+                                           const AdpSrc<kP>& src, uint32_t t, int cg, int w, int lane,
+                                           AdpRegs4<kP, kIt>& r) {
+  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, 4>;
+  const uint32_t last = uint32_t(a.nsteps - 1);
+  r.fast = 0;
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const int g = i * kW + w;
+    const uint32_t s0 = t * kS + uint32_t(g * Sh::kBlkPerIt);
+    const uint32_t s = min(s0 + uint32_t(lane / Sh::kLpB), last);
+    const uint32_t p = s * 64 + uint32_t(cg * kC + (lane % Sh::kLpB) * 4);
+    const uint32_t pf = min(s0, last) * 64 + uint32_t(cg * kC);
+    const uint32_t pl = min(s0 + uint32_t(Sh::kBlkPerIt - 1), last) * 64 + uint32_t(cg * kC + kC - 1);
+    while (pf >= cur.end && cur.idx + 1 < n_segs) adp_cursor_load(S, cur.idx + 1, cur);  // rare: next entry
+    uint32_t e, code;
+    if (!(cur.info & kSegI64) && pl < cur.end) {
+      r.fast |= 1u << i;
+      e = p - cur.flat + cur.src;
+      code = cur.info;
+    } else {
+      const int idx = seg_walk(S, n_segs, p, cur.idx);
+      e = 0u;  // the loads still go out (same count on every path); the write fetches the values
+      code = uint32_t(idx);
+    }
+    r.code[i] = code;
+    r.pos[i] = p;
+    r.x[i] = bload4(src.x, p * 4u);
+    r.b[i] = bload4(src.b, e * 4u);
+#pragma unroll
+    for (int k = 0; k < kP; ++k) r.y[i][k] = bload4(src.y[k], e * 4u);
+  }
+}
+
+// process_grad's value at flat position p of pair `pair`, walking the segment map from `idx`
+// (the slow path of an iteration that crosses an entry)
+__device__ __forceinline__ float adp_value_at(const AdpArgs& a, const AdpSeg* S, int n_segs, int& idx, uint32_t p,
+                                              int pair) {
+  idx = seg_walk(S, n_segs, p, idx);
+  const AdpSeg sg = S[idx];
+  const uint32_t el = p - sg.flat + sg.src;
+  if (sg.info & kSegI64) return a.y64[uint64_t(pair) * a.n_i64 + el];
+  return adp_f32(a.xf[pair][el], a.base_f[el], sg.info & kSegNeg, a.lr);
+}
+
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+__device__ __forceinline__ void adp_write4(const AdpArgs& a, const AdpSeg* S, int n_segs, float* slot, int pair0,
+                                           int w, int lane, AdpRegs4<kP, kIt>& r) {
+  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, 4>;
+  const float lr = a.lr;
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const int g = i * kW + w;
+    const int col = g * Sh::kBlkPerIt + lane / Sh::kLpB;  // step within the stage
+    float* dst = slot + (lane % Sh::kLpB) * 4 * Sh::kR + col;  // chain c0 = 4 * (lane % kLpB), rows c0 .. c0 + 3
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[j * Sh::kR] = r.x[i][j];
+    if (r.fast & (1u << i)) {  // wave-uniform: one entry, one sign/divide mode
+      if (__builtin_amdgcn_readfirstlane(int(r.code[i])) & kSegNeg) {
+#pragma unroll
+        for (int k = 0; k < kP; ++k)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dst[(1 + k) * Sh::kVR + j * Sh::kR] = (-(r.y[i][k][j] - r.b[i][j])) / lr;
+      } else {
+#pragma unroll
+        for (int k = 0; k < kP; ++k)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dst[(1 + k) * Sh::kVR + j * Sh::kR] = r.y[i][k][j] - r.b[i][j];
+      }
+    } else {  // rare: an entry boundary (or an int64 entry) inside the iteration
+      for (int k = 0; k < kP; ++k) {
+        const int pair = pair0 + k < a.n_pairs ? pair0 + k : a.n_pairs - 1;
+        int idx = int(r.code[i]);
+        for (int j = 0; j < 4; ++j) dst[(1 + k) * Sh::kVR + j * Sh::kR] = adp_value_at(a, S, n_segs, idx, r.pos[i] + j, pair);
+      }
+    }
+  }
+}
+
+// Waves per workgroup: kW producers + 2 chain waves, or with kIso 12 waves placed so that the chain
+// waves share a SIMD with no producer (waves are dealt to the CU's 4 SIMDs round-robin, so waves 0, 4
+// and 8 share one: wave 0 runs the pairs' chains, wave 4 g . g, wave 8 idles; producers are the other 9
+// waves, the last of them idle when kW = 8).  A producer's VALU instruction (the division sequence, the
+// 64-bit address arithmetic) holds its SIMD for several cycles, and on a shared SIMD the serial fma
+// chain waits for it at every step (timing probes).
+template <int kW, int kIso>
+constexpr int adp_waves() { return kIso ? 12 : kW + 2; }
+
+template <int kP, int kIt, int kV>
+using AdpRegsV = std::conditional_t<kV == 4, AdpRegs4<kP, kIt>, AdpRegs<kP, kIt>>;
+
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe, int kV>
+__device__ __forceinline__ void adp_issue_v(const AdpArgs& a, const AdpSeg* S, int n_segs, AdpCursor& cur,
+                                            const AdpSrc<kP>& src, uint32_t t, int cg, int w, int lane,
+                                            AdpRegsV<kP, kIt, kV>& r) {
+  if constexpr (kV == 4) adp_issue4<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, cur, src, t, cg, w, lane, r);
+  else adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cur, src, t, cg, w, lane, r);
+}
+
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe, int kV>
+__device__ __forceinline__ void adp_write_v(const AdpArgs& a, const AdpSeg* S, int n_segs, float* slot, int pair0,
+                                            int w, int lane, AdpRegsV<kP, kIt, kV>& r) {
+  if constexpr (kV == 4) adp_write4<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, slot, pair0, w, lane, r);
+  else adp_write<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, slot, pair0, w, lane, r);
+}
+
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2>
+__global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kernel(AdpArgs a) {
+  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, kV>;
+  static_assert(!kIso || kW <= 9, "kIso: at most 9 producer waves");
   __shared__ __attribute__((aligned(16))) float ring[2 * Sh::kSlot];
   __shared__ AdpSeg S[kMaxSegs];
   constexpr int kGroups = 64 / kC;
@@ -254,9 +401,20 @@ __global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = int(threadIdx.x & 63);
   const uint64_t nsteps = a.nsteps;
   const uint64_t nst = (nsteps + kS - 1) / kS;
-  const uint64_t nst2 = (nst + 1) & ~uint64_t(1);  // barriers: one per stage, in pairs
-  if (wave >= 2) {  // producer
-    const int w = wave - 2;
+  static_assert(kD >= 2 && kD <= 4, "2-4 stages of loads in flight per producer wave");
+  const uint64_t nst2 = (nst + kD - 1) / kD * kD;  // barriers: one per stage, in whole trips of kD stages
+  // role: chain wave 0 (pairs) / 1 (g . g), or producer w; idle waves end here (a wave that has ended
+  // is no longer counted by s_barrier)
+  int chain_role = -1, w = -1;
+  if (kIso) {
+    if ((wave & 3) == 0) chain_role = wave >> 2;
+    else w = (wave >> 2) * 3 + (wave & 3) - 1;
+    if (chain_role > 1 || w >= kW) return;
+  } else {
+    if (wave >= 2) w = wave - 2;
+    else chain_role = wave;
+  }
+  if (w >= 0) {  // producer
     if (kProbe == 4) {  // timing probe: the chains alone (producers only keep the barrier count)
       for (uint64_t t = 0; t < nst2; ++t) __builtin_amdgcn_s_barrier();
       return;
@@ -268,39 +426,61 @@ __global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
 #pragma unroll
     for (int k = 0; k < kP; ++k)
       src.y[k] = adp_rsrc(sld(a.xf, pair0 + k < a.n_pairs ? pair0 + k : a.n_pairs - 1), a.n_f32 * 4);
-    int cursor = 0;
-    AdpRegs<kP, kIt> ra, rb;
-    adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cursor, src, 0, cg, w, lane, ra);
-    adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cursor, src, 1, cg, w, lane, rb);
-    // whole pairs of stages (an odd count gets one idle trip): no branch inside the loop, so the
-    // compiler's vmcnt bookkeeping sees the same two stages in flight on every trip
-    for (uint32_t t = 0; t < uint32_t(nst2); t += 2) {
-      adp_write<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, ring, pair0, w, lane, ra);
-      // past the last stage (t = nst) every position clamps to the last block: valid addresses,
-      // never consumed, and every trip issues the same loads
-      adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cursor, src, t + 2 < nst ? t + 2 : uint32_t(nst), cg, w,
-                                             lane, ra);
-      __builtin_amdgcn_s_barrier();  // stage t published in slot 0
-      adp_write<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, ring + Sh::kSlot, pair0, w, lane, rb);
-      adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cursor, src, t + 3 < nst ? t + 3 : uint32_t(nst), cg, w,
-                                             lane, rb);
-      __builtin_amdgcn_s_barrier();  // stage t + 1 published in slot 1
+    AdpCursor cursor;
+    adp_cursor_load(S, 0, cursor);
+    // kD register sets: the loads of stage t + kD go out right after stage t is written, so every
+    // producer wave keeps kD stages of loads in flight; the tile ring in LDS has two slots
+    AdpRegsV<kP, kIt, kV> regs[kD];
+#pragma unroll
+    for (int j = 0; j < kD; ++j)
+      adp_issue_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV>(a, S, n_segs, cursor, src, uint32_t(j), cg, w, lane, regs[j]);
+    uint64_t t_start = 0, t_wait = 0, t_write = 0, c0 = 0;  // probe 6: cycle counts
+    if (kProbe == 6) t_start = __builtin_readcyclecounter();
+    // whole trips of kD stages (the last trip may run idle stages): no branch inside the loop, so the
+    // compiler's vmcnt bookkeeping sees the same kD stages in flight on every trip
+    for (uint32_t t = 0; t < uint32_t(nst2); t += kD) {
+#pragma unroll
+      for (int j = 0; j < kD; ++j) {
+        if (kProbe == 6) c0 = __builtin_readcyclecounter();
+        adp_write_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV>(a, S, n_segs, ring + ((t + j) & 1) * Sh::kSlot, pair0, w,
+                                                             lane, regs[j]);
+        if (kProbe == 6) t_write += __builtin_readcyclecounter() - c0;
+        // past the last stage (t = nst) every position clamps to the last block: valid addresses,
+        // never consumed, and every trip issues the same loads
+        const uint32_t nxt = t + j + kD;
+        adp_issue_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV>(a, S, n_segs, cursor, src, nxt < nst ? nxt : uint32_t(nst),
+                                                             cg, w, lane, regs[j]);
+        if (kProbe == 6) c0 = __builtin_readcyclecounter();
+        __builtin_amdgcn_s_barrier();  // stage t + j published in slot (t + j) & 1
+        if (kProbe == 6) t_wait += __builtin_readcyclecounter() - c0;
+      }
+    }
+    if (kProbe == 6 && lane == 0) {  // probe 6: [total, barrier wait, write, HW_ID] of every producer
+      uint32_t* o = reinterpret_cast<uint32_t*>(a.ws) + blockIdx.x * 48 + 8 + 4 * w;
+      o[0] = uint32_t(__builtin_readcyclecounter() - t_start);
+      o[1] = uint32_t(t_wait);
+      o[2] = uint32_t(t_write);
+      o[3] = uint32_t(__builtin_amdgcn_s_getreg((31 << 11) | 4));  // hwreg(HW_REG_HW_ID): wave, SIMD, CU ...
     }
     return;
   }
   // chain waves: wave 0 the kP pairs' dots, wave 1 g . g (pair group 0 only; elsewhere it only
   // keeps the barrier count)
   __builtin_amdgcn_s_setprio(3);
-  const bool xx = wave == 1;
+  const bool xx = chain_role == 1;
   const bool active = !xx || (pg == 0 && a.with_xx);
   const int kind = xx ? 0 : lane >> 5, c = xx ? lane % kC : (lane & 31) / kP, p = lane % kP;
   const int arow = (xx || kind == 0 ? 0 : (1 + p) * Sh::kVR) + c * Sh::kR;
   const int brow = (xx ? 0 : (1 + p) * Sh::kVR) + c * Sh::kR;
   float acc = 0.f;
+  uint64_t t_start = 0, t_wait = 0, c0 = 0;  // probe 6: cycle counts
+  if (kProbe == 6) t_start = __builtin_readcyclecounter();
   for (uint64_t t = 0; t < nst2; ++t) {
+    if (kProbe == 6) c0 = __builtin_readcyclecounter();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_s_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (kProbe == 6) t_wait += __builtin_readcyclecounter() - c0;
     if (!active || t >= nst || kProbe == 2) continue;  // probe 2: no chains
     const float* slot = ring + (t & 1) * Sh::kSlot;
     const float* A = slot + arow;
@@ -346,6 +526,17 @@ __global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
     }
   }
   const int chain = cg * kC + c;
+  if (kProbe == 6) {  // probe 6: [total, barrier wait, HW_ID] of the pairs' chain wave, HW_ID of g . g (no results)
+    uint32_t* o = reinterpret_cast<uint32_t*>(a.ws) + blockIdx.x * 48;
+    if (!xx && lane == 0) {
+      o[0] = uint32_t(__builtin_readcyclecounter() - t_start);
+      o[1] = uint32_t(t_wait);
+      o[2] = uint32_t(__builtin_amdgcn_s_getreg((31 << 11) | 4));
+    }
+    if (xx && lane == 0) o[3] = uint32_t(__builtin_amdgcn_s_getreg((31 << 11) | 4));
+    if (acc == 12345.f) a.ws[blockIdx.x] = acc;  // keep the chains
+    return;
+  }
   if (!xx) {
     const int pair = pg * kP + p;
     if (pair < a.n_pairs) a.ws[uint64_t(pair) * 128 + uint64_t(kind) * 64 + chain] = acc;
@@ -442,22 +633,26 @@ __global__ __launch_bounds__(64) void fedadp_finish_kernel(AdpArgs a, float* out
   out_yy[pair] = float(tyy + kyy);
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2>
 void launch_adp(const AdpArgs& a, hipStream_t st) {
   constexpr int kGroups = 64 / kC;
   uint32_t pgs = uint32_t((a.n_pairs + kP - 1) / kP);
   pgs = (pgs + 7) / 8 * 8;  // whole XCD rounds (padding workgroups return at once)
-  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe>), dim3(pgs * kGroups),
-                     dim3(64 * (kW + 2)), 0, st, a);
+  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe, kIso, kV, kD>), dim3(pgs * kGroups),
+                     dim3((64 * adp_waves<kW, kIso>())), 0, st, a);
 }
 using AdpFn = void (*)(const AdpArgs&, hipStream_t);
 // pairs x chains per workgroup, steps per stage, producer waves, iterations, vector pad
+// The product's shape (tuning variant 23): one pair and 32 of its 64 chains per workgroup, so a
+// gather reads whole 128-byte lines, 16 bytes per lane (x and b come once per pair, from L2);
+// 1.94 ms for 128 ResNet-18 clients against 5.4 ms for variant 0 (profiles/r03i_fedadp.log)
+constexpr AdpFn kAdpDefault = &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4>;
+#ifdef PLATO_AGG_TUNE
 const AdpFn kAdpVariants[] = {
     &launch_adp<8, 4, 256, 8, 2, 0>,     // 0: 16 B per block per vector, x and b shared by 8 pairs
     &launch_adp<4, 8, 256, 8, 4, 16>,    // 1: 32 B
     &launch_adp<2, 16, 256, 8, 8, 32>,   // 2: 64 B
     &launch_adp<1, 32, 128, 8, 8, 0>,    // 3: whole 128-byte lines, x and b per pair (from L2)
-#ifdef PLATO_AGG_TUNE
     &launch_adp<2, 16, 192, 12, 4, 32>,  // 4: variant 2 with 12 producer waves
     &launch_adp<2, 16, 128, 8, 4, 32>,   // 5: variant 2, half stages
     &launch_adp<2, 16, 256, 8, 8, 32, 1>,  // 6: probe of 2 without the division (wrong results)
@@ -465,11 +660,34 @@ const AdpFn kAdpVariants[] = {
     &launch_adp<2, 16, 256, 8, 8, 32, 3>,  // 8: probe of 2 without the loads (wrong results)
     &launch_adp<2, 16, 256, 8, 8, 32, 4>,  // 9: probe of 2: the chains alone (wrong results)
     &launch_adp<2, 16, 256, 8, 8, 32, 5>,  // 10: probe of 2: chains without LDS reads (wrong results)
-#endif
+    &launch_adp<2, 16, 256, 8, 8, 32, 0, 1>,  // 11: variant 2, chain waves on a SIMD of their own
+    &launch_adp<2, 16, 128, 8, 4, 32, 0, 1>,  // 12: variant 5, chain waves on a SIMD of their own
+    &launch_adp<4, 8, 256, 8, 4, 16, 0, 1>,   // 13: variant 1, chain waves on a SIMD of their own
+    &launch_adp<1, 32, 128, 8, 8, 0, 0, 1>,   // 14: variant 3, chain waves on a SIMD of their own
+    &launch_adp<2, 16, 256, 8, 8, 32, 4, 1>,  // 15: probe of 11: the chains alone (wrong results)
+    &launch_adp<2, 16, 256, 8, 8, 32, 2, 1>,  // 16: probe of 11: no chains (wrong results)
+    &launch_adp<2, 16, 256, 8, 8, 32, 6>,     // 17: probe of 2: cycle counts per wave into the workspace
+    &launch_adp<2, 16, 128, 8, 4, 32, 6, 1>,  // 18: probe of 12: cycle counts per wave into the workspace
+    &launch_adp<2, 16, 256, 8, 2, 32, 0, 0, 4>,  // 19: variant 2, 16-byte gathers
+    &launch_adp<2, 16, 128, 8, 1, 32, 0, 0, 4>,  // 20: variant 5, 16-byte gathers
+    &launch_adp<2, 16, 256, 8, 2, 32, 0, 1, 4>,  // 21: variant 19, chain waves on a SIMD of their own
+    &launch_adp<4, 8, 256, 8, 1, 16, 0, 0, 4>,   // 22: variant 1, 16-byte gathers
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4>,   // 23: variant 3, 16-byte gathers
+    &launch_adp<8, 4, 256, 4, 1, 0, 0, 0, 4>,    // 24: variant 0, 16-byte gathers (4 producer waves)
+    &launch_adp<2, 16, 256, 8, 2, 32, 6, 0, 4>,  // 25: probe of 19: cycle counts per wave into the workspace
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 3>,   // 26: variant 23, 3 stages of loads in flight
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 4>,   // 27: variant 23, 4 stages of loads in flight
+    &launch_adp<2, 16, 128, 8, 1, 32, 0, 0, 4, 4>,  // 28: variant 20, 4 stages of loads in flight
+    &launch_adp<1, 32, 128, 8, 2, 0, 6, 0, 4, 3>,   // 29: probe of 26: cycle counts per wave into the workspace
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 1, 4, 3>,   // 30: variant 26, chain waves on a SIMD of their own
+    &launch_adp<1, 32, 128, 8, 8, 0, 0, 0, 1, 3>,   // 31: variant 3, 3 stages of loads in flight
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
+// timing probes of the table above: wrong results by design (tests skip them)
+constexpr int kAdpProbes[] = {6, 7, 8, 9, 10, 15, 16, 17, 18, 25, 29};
+#endif
 
-int run_fedadp(int variant, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
+int run_fedadp(AdpFn fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
                const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs, uint32_t n_segs,
                size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
                float* d_out_yy, hipStream_t stream);
@@ -487,19 +705,26 @@ int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const 
                           const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
                           uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
                           float* d_out_xy, float* d_out_yy, hipStream_t stream) {
-  return run_fedadp(0, d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32, d_base_i64, d_segs, n_segs, n_flat, n_f32,
+  return run_fedadp(kAdpDefault, d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32, d_base_i64, d_segs, n_segs, n_flat, n_f32,
                     n_i64, lr, with_xx, d_workspace, d_out_xy, d_out_yy, stream);
 }
 
 #ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
 int plato_agg_tune_num_fedadp_variants(void) { return kNumAdpVariants; }
 
+int plato_agg_tune_fedadp_is_probe(int variant) {
+  for (int v : kAdpProbes)
+    if (v == variant) return 1;
+  return 0;
+}
+
 int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const* d_src_f32,
                                const void* const* d_src_i64, int n_pairs, const float* d_base_f32,
                                const int64_t* d_base_i64, const plato_agg_segment* d_segs, uint32_t n_segs,
                                size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
                                float* d_out_yy, hipStream_t stream) {
-  return run_fedadp(variant, d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32, d_base_i64, d_segs, n_segs, n_flat,
+  if (variant < 0 || variant >= kNumAdpVariants) return set_error(PLATO_AGG_EINVAL, "bad fedadp_dots variant");
+  return run_fedadp(kAdpVariants[variant], d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32, d_base_i64, d_segs, n_segs, n_flat,
                     n_f32, n_i64, lr, with_xx, d_workspace, d_out_xy, d_out_yy, stream);
 }
 #endif  // PLATO_AGG_TUNE
@@ -507,11 +732,10 @@ int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const*
 }  // extern "C"
 
 namespace {
-int run_fedadp(int variant, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
+int run_fedadp(AdpFn fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
                const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs, uint32_t n_segs,
                size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
                float* d_out_yy, hipStream_t stream) {
-  if (variant < 0 || variant >= kNumAdpVariants) return set_error(PLATO_AGG_EINVAL, "bad fedadp_dots variant");
   if (n_pairs <= 0 || n_pairs > (1 << 20)) return set_error(PLATO_AGG_EINVAL, "n_pairs must be in [1, 2^20]");
   if (with_xx != 0 && with_xx != 1) return set_error(PLATO_AGG_EINVAL, "with_xx must be 0 or 1");
   if (!d_x || !d_src_f32 || !d_src_i64 || !d_base_f32 || !d_segs || !d_workspace || !d_out_xy || !d_out_yy ||
@@ -544,7 +768,7 @@ int run_fedadp(int variant, const float* d_x, const void* const* d_src_f32, cons
     if (int rc = check_launch("fedadp_i64 launch")) return rc;
   }
   if (a.nsteps) {
-    kAdpVariants[variant](a, stream);
+    fn(a, stream);
     if (int rc = check_launch("fedadp_dots launch")) return rc;
   } else {
     (void)hipMemsetAsync(d_workspace, 0, (size_t(n_pairs) + (with_xx ? 1 : 0)) * 128 * sizeof(float), stream);

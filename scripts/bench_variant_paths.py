@@ -45,11 +45,13 @@ def main():
     ap.add_argument("--fedadp-kernel", action="store_true",
                     help="HIP-event time of plato_agg_fedadp_dots alone (+ bitwise check against the flat path)")
     ap.add_argument("--fedadp-only", action="store_true", help="only the fedadp kernel timing (for PMC passes)")
+    ap.add_argument("--fedadp-cycles", type=int, default=None, metavar="VARIANT",
+                    help="run a cycle-count probe variant of plato_agg_tune_fedadp_dots and summarise its workspace")
     ap.add_argument("--port-norms", action="store_true",
                     help="time the entry_norms variants on Port's K+1 flattened vectors (one entry each)")
     args = ap.parse_args()
     args.sdot = args.sdot or args.sdot_only
-    args.fedadp_kernel = args.fedadp_kernel or args.fedadp_only
+    args.fedadp_kernel = args.fedadp_kernel or args.fedadp_only or args.fedadp_cycles is not None
 
     from plato_amd import workloads
     from plato_amd.arena import ArenaLayout
@@ -105,7 +107,7 @@ def main():
                    "per-entry torch norms: 8 fma chains per (entry, client)"),
     }
     for name, (fn, nbytes, chain, what) in paths.items():
-        if args.sdot_only or args.fedadp_only:
+        if args.sdot_only or args.fedadp_only or args.fedadp_cycles is not None:
             break
         fn()
         torch.cuda.synchronize(dev)
@@ -120,14 +122,14 @@ def main():
                           "min_bytes": int(nbytes), "GBps_of_min_bytes": round(nbytes / (med * 1e-3) / 1e9, 1),
                           "serial_chain_steps": int(chain), "what": what}), flush=True)
     if args.fedadp_kernel:
-        fedadp_kernel(dev, rnd, slots, layout, args.reps)
+        fedadp_kernel(dev, rnd, slots, layout, args.reps, args.fedadp_cycles)
     if args.sdot:
         sdot_kernels(dev, k, n_f + n_i, args.reps)
     if args.port_norms:
         port_norms(dev, k, n_f + n_i, args.reps)
 
 
-def fedadp_kernel(dev, rnd, slots, layout, reps):
+def fedadp_kernel(dev, rnd, slots, layout, reps, cycles_variant=None):
     """plato_agg_fedadp_dots alone (HIP events on the launch stream), against the flatten + sdot_shared path."""
     from plato_amd import _lib
 
@@ -154,6 +156,24 @@ def fedadp_kernel(dev, rnd, slots, layout, reps):
                                                     eng._base.i64.data_ptr(), segs.data_ptr(), len(order), n_flat,
                                                     layout.n_f32, layout.n_i64, 0.01, 1, ws.data_ptr(), xy.data_ptr(),
                                                     yy.data_ptr(), h))
+    if cycles_variant is not None:
+        ws.zero_()
+        runs[f"v{cycles_variant}"]()
+        torch.cuda.synchronize(dev)
+        c = ws[:256 * 48].view(torch.int32).cpu().numpy().astype(np.int64).reshape(256, 48)
+        simd = lambda hw: (hw >> 4) & 3  # HW_REG_HW_ID bits 5:4
+        out = {"fedadp_cycles_variant": cycles_variant, "chain_total": int(np.median(c[:, 0])),
+               "chain_barrier_wait": int(np.median(c[:, 1])), "chain_simd_of_wg0": int(simd(c[0, 2])),
+               "gg_simd_of_wg0": int(simd(c[0, 3]))}
+        for w in range(9):
+            blk = c[:, 8 + 4 * w: 12 + 4 * w]
+            if not blk[:, 0].any():
+                continue
+            out[f"p{w}"] = {"total": int(np.median(blk[:, 0])), "wait": int(np.median(blk[:, 1])),
+                            "write": int(np.median(blk[:, 2])), "simd_wg0": int(simd(blk[0, 3])),
+                            "same_simd_as_chain": float(np.mean(simd(blk[:, 3]) == simd(c[:, 2])))}
+        print(json.dumps(out), flush=True)
+        return
     # unique bytes: each client's fp32 arena + int64 counters once, the baseline and g_flat once
     uniq = k * (layout.n_f32 * 4 + layout.n_i64 * 8) + 2 * layout.n_f32 * 4 + n_flat * 4
     for name, fn in runs.items():

@@ -308,9 +308,8 @@ def test_fedadp_dots_tile_shapes_agree_bitwise(engine, name):
     order = rnd._fedadp_order()
     segs, n_flat = rnd._flat_segments(order, True)
     dev = torch.device(DEV)
-    probes = {6, 7, 8, 9, 10}  # timing probes of csrc/fedadp.hip (wrong results by design)
     for v in range(_lib.tune().plato_agg_tune_num_fedadp_variants()):
-        if v in probes:
+        if _lib.tune().plato_agg_tune_fedadp_is_probe(v):  # timing probes: wrong results by design
             continue
         xy = torch.full((k + 1,), float("nan"), device=dev)
         yy = torch.full((k + 1,), float("nan"), device=dev)
