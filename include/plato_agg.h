@@ -409,6 +409,26 @@ int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const 
                           float* d_out_xy, float* d_out_yy, hipStream_t stream);
 
 /*
+ * Port's vector norms gathered from the arenas (replaces the flatten + norm of
+ * examples/async/port/port_server.py:38-50: torch.cat in state_dict order, then
+ * the norms inside F.cosine_similarity).  Vector v is x_v - b_v flattened by
+ * the segment map (state_dict order; int64 entries cast to float32 as
+ * torch.cat does: the wrapped int64 difference cast once, or with
+ * PLATO_AGG_PORT_CAST_FIRST for vector 0, current - previous, the difference
+ * of the two casts); d_out[v] = torch.linalg.vector_norm of it in x86-64
+ * ATen's order (8 fma chains over n - n % 8 positions, the lanes added in
+ * order, the scalar tail).  d_x_f32 / d_x_i64 / d_b_f32 / d_b_i64: n_vectors
+ * device pointers each (arenas of n_f32 fp32 elements / the int64 counters).
+ * d_flat_out: null, or n_vectors 16-byte aligned rows of >= n_flat floats that
+ * receive the flattened vectors (what plato_agg_torch_cosine_sum then reads).
+ */
+#define PLATO_AGG_PORT_CAST_FIRST 1
+int plato_agg_port_norms(const void* const* d_x_f32, const void* const* d_x_i64, const void* const* d_b_f32,
+                         const void* const* d_b_i64, int n_vectors, const plato_agg_segment* d_segs, uint32_t n_segs,
+                         size_t n_flat, size_t n_f32, int flags, float* d_out, float* const* d_flat_out,
+                         hipStream_t stream);
+
+/*
  * The sum in Port's F.cosine_similarity(a, b_k, dim=0) (port_server.py:50),
  * as x86-64 PyTorch 2.10 forms it on `threads` CPU threads:
  *   q = (a / max(|a|, eps)) * (b_k / max(|b_k|, eps)),  out[k] = sum(q)

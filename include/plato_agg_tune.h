@@ -136,6 +136,13 @@ int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const*
                                size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
                                float* d_out_yy, hipStream_t stream);
 
+/* plato_agg_port_norms with an explicit shape (see csrc/port.hip). */
+int plato_agg_tune_num_port_norms_variants(void);
+int plato_agg_tune_port_norms(int variant, const void* const* d_x_f32, const void* const* d_x_i64,
+                              const void* const* d_b_f32, const void* const* d_b_i64, int n_vectors,
+                              const plato_agg_segment* d_segs, uint32_t n_segs, size_t n_flat, size_t n_f32, int flags,
+                              float* d_out, float* const* d_flat_out, hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

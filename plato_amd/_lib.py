@@ -24,6 +24,7 @@ PLATO_AGG_ADD_BASE = 1
 PLATO_AGG_FLAT_DELTA = 0
 PLATO_AGG_FLAT_CAST_DIFF = 1
 PLATO_AGG_FLAT_RAW = 2
+PLATO_AGG_PORT_CAST_FIRST = 1
 PLATO_AGG_SEG_NEG_DIV = 1
 PLATO_AGG_DECODE = {"native": 0, "bf16": 1, "qsgd": 2}
 
@@ -125,6 +126,10 @@ SIGNATURES = {
         _c_int,
         [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,
          _c_size_t, _c_size_t, _c_float, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "plato_agg_port_norms": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, ctypes.c_uint32, _c_size_t, _c_size_t, _c_int,
+         _c_void_p, _c_void_p, _c_void_p]),
     "plato_agg_torch_cosine_workspace": (_c_size_t, [_c_int, _c_int]),
     "plato_agg_torch_cosine_sum": (
         _c_int,
@@ -179,6 +184,11 @@ TUNE_SIGNATURES = {
                  _c_void_p]),
     "plato_agg_tune_num_fedadp_variants": (_c_int, []),
     "plato_agg_tune_fedadp_is_probe": (_c_int, [_c_int]),
+    "plato_agg_tune_num_port_norms_variants": (_c_int, []),
+    "plato_agg_tune_port_norms": (
+        _c_int,
+        [_c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, ctypes.c_uint32, _c_size_t, _c_size_t,
+         _c_int, _c_void_p, _c_void_p, _c_void_p]),
     "plato_agg_tune_fedadp_dots": (
         _c_int,
         [_c_int, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,

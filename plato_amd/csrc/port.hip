@@ -1,0 +1,336 @@
+// port.hip — Port's vector norms straight from the staged arenas, for gfx950.
+// C ABI: include/plato_agg.h (plato_agg_port_norms).  CPU restatement: oracle/reductions.c (torch norm).
+//
+// The reference (examples/async/port/port_server.py:38-50) flattens the current model minus the
+// previous one and every client delta with torch.cat in state_dict order (int64 entries cast to
+// float32 on the way) and takes F.cosine_similarity, whose vector norms are ATen's
+// linalg_vector_norm of a contiguous float32 vector: on x86-64, 8 fma chains (chain j sums the
+// squares of positions = j mod 8, serially), the 8 lanes added in order, then ATen's scalar tail.
+//
+// The round-2 path flattened the vectors (plato_agg_flatten: 5.7 GB read and written for 128
+// ResNet-18 clients, 2.4 ms) before plato_agg_entry_norms_f32 read them again.  Here the
+// flattening is folded into the norm kernel: producer waves gather four positions per lane from
+// the arenas through the state_dict-order segment map (the int64 counters interleaved where
+// state_dict puts them), form the delta in registers and write it transposed into an LDS tile —
+// chain j's steps contiguous in row j; the chain wave walks the 8 chains out of LDS with
+// ds_read_b128.  The producers also store the flattened vector (d_flat_out) for the cosine sums,
+// which need the norms first: the store rides in the shadow of the serial chain.
+//
+// Shape: one workgroup per vector (V = K + 1: vector 0 = current - previous, vectors 1..K the
+// client deltas), 1 chain wave + kWp producer waves, 2,048-position tiles (256 steps per chain),
+// a two-slot tile ring and one s_barrier per tile; each producer keeps kD tiles of loads in flight.
+// The launch is bound by the serial chain (n / 8 dependent fmas), not by HBM; DESIGN.md §13.
+// Compiled with -ffp-contract=off; the chain fma is an explicit fma (torch's vfmadd231ps).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <string>
+
+#include "common.h"
+#include "plato_agg.h"
+
+using plato_agg_internal::clear_error;
+using plato_agg_internal::set_error;
+
+namespace {
+
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+template <class T>
+__device__ __forceinline__ T sld(const T* p, int i) {
+  return ((__attribute__((address_space(4))) const T*)p)[i];
+}
+
+constexpr int kLanes = 8;                 // torch's 8-lane vectorised accumulation
+constexpr int kT = 2048;                  // positions per tile
+constexpr int kSteps = kT / kLanes;       // 256 steps per chain and tile
+constexpr int kR = kSteps + 8;            // row pitch: conflict-free writes (see pn_write) and reads
+constexpr int kSlot = kLanes * kR;        // one tile
+constexpr int kIts = kT / 256;            // gather iterations of 256 positions (4 per lane) per tile
+constexpr int kMaxSegs = 2048;
+constexpr uint32_t kSegI64 = 1u;
+
+struct PnSeg {
+  uint32_t flat, end, src, info;  // positions [flat, end) read element src + (p - flat) of the region
+};
+
+struct PnArgs {
+  const float* const* xf;    // [V] fp32 arenas: the minuends
+  const int64_t* const* xi;  // [V] int64 arenas
+  const float* const* bf;    // [V] fp32 arenas subtracted
+  const int64_t* const* bi;  // [V] int64 arenas subtracted
+  const plato_agg_segment* segs;
+  uint32_t n_segs;
+  uint32_t n;                // flat length
+  uint32_t m;                // n - n % 8: the vectorised part
+  uint64_t n_f32;
+  int cast_first;            // vector 0 subtracts its int64 entries as torch.cat(...) - torch.cat(...)
+  float* out;                // [V]
+  float* const* flat;        // [V] rows for the flattened vectors (16-byte aligned), or null
+};
+
+// ATen's scalar tail of the last-dim 2-norm as x86-64 PyTorch 2.10 compiled it (entrywise.hip,
+// torch_norm_tail_step): 4 or more remaining -> separately rounded product and add, else fused.
+__device__ __forceinline__ float pn_tail_step(float s, float v, uint32_t e, uint32_t m, uint32_t n) {
+  if (n - m >= 4 && e < m + 4) return s + v * v;
+  return __builtin_fmaf(v, v, s);
+}
+
+// The flattened delta at position p (the slow path: entry boundaries, int64 entries, the tail).
+// fp32: x - b.  int64: torch.cat casts each int64 entry to float32 — vector 0 (current - previous)
+// subtracts the casts, the deltas (compute_weight_deltas, algorithms/fedavg.py:23) are int64
+// differences (wrapping) cast once.
+__device__ __forceinline__ float pn_value(const PnArgs& a, const PnSeg* S, int& idx, uint32_t p, int v) {
+  while (idx + 1 < int(a.n_segs) && S[idx + 1].flat <= p) ++idx;
+  const PnSeg sg = S[idx];
+  const uint32_t e = p - sg.flat + sg.src;
+  if (!(sg.info & kSegI64)) return a.xf[v][e] - a.bf[v][e];
+  const int64_t x = a.xi[v][e], b = a.bi[v][e];
+  if (v == 0 && a.cast_first) return float(x) - float(b);
+  return float(int64_t(uint64_t(x) - uint64_t(b)));
+}
+
+struct PnCursor {  // a producer wave's current entry, wave-uniform (positions only move forward)
+  int idx;
+  uint32_t flat, end, src, info;
+};
+
+__device__ __forceinline__ void pn_cursor_load(const PnSeg* S, int idx, PnCursor& c) {
+  c.idx = idx;
+  c.flat = __builtin_amdgcn_readfirstlane(S[idx].flat);
+  c.end = __builtin_amdgcn_readfirstlane(S[idx].end);
+  c.src = __builtin_amdgcn_readfirstlane(S[idx].src);
+  c.info = __builtin_amdgcn_readfirstlane(S[idx].info);
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t pn_rsrc(const void* base, uint64_t bytes) {
+  const uint64_t n = bytes < 0xffffffffull ? bytes : 0xffffffffull;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)uint32_t(n), 0x00020000);
+}
+
+__device__ __forceinline__ f4 pn_load4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
+  // dword-aligned 16-byte loads (an entry's arena offset is 4-byte aligned only)
+  return __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+}
+
+template <int kIt>
+struct PnRegs {
+  f4 x[kIt], b[kIt];
+  int seg[kIt];   // the wave's entry at the iteration's first position (where a slow iteration's walk starts)
+  uint32_t fast;  // bit i: iteration i lies inside one fp32 entry and below m (wave-uniform)
+};
+
+template <int kWp, int kIt>
+__device__ __forceinline__ void pn_issue(const PnArgs& a, const PnSeg* S, PnCursor& cur, __amdgpu_buffer_rsrc_t rx,
+                                         __amdgpu_buffer_rsrc_t rb, uint32_t t, int w, int lane, PnRegs<kIt>& r) {
+  r.fast = 0;
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const uint32_t pf = t * kT + uint32_t(i * kWp + w) * 256;  // the iteration's first position
+    const uint32_t pl = pf + 255;
+    while (pf >= cur.end && cur.idx + 1 < int(a.n_segs)) pn_cursor_load(S, cur.idx + 1, cur);  // rare
+    uint32_t e = 0;  // slow iterations still issue their loads (same count on every path)
+    r.seg[i] = cur.idx;
+    if (!(cur.info & kSegI64) && pl < cur.end && pl < a.m) {
+      r.fast |= 1u << i;
+      e = pf + uint32_t(4 * lane) - cur.flat + cur.src;
+    }
+    r.x[i] = pn_load4(rx, e * 4u);
+    r.b[i] = pn_load4(rb, e * 4u);
+  }
+}
+
+// Lane L holds positions p .. p + 3 (p = pf + 4L): chains 4 (L & 1) .. + 3, step (p - tile) / 8.
+// Row pitch kR = 264 (= 8 mod 64 banks): for each of the four writes the 64 lanes hit 64 banks.
+template <int kWp, int kIt, bool kNT>
+__device__ __forceinline__ void pn_write(const PnArgs& a, const PnSeg* S, float* slot, float* flat, uint32_t t, int w,
+                                         int lane, int v, const PnRegs<kIt>& r) {
+#pragma unroll
+  for (int i = 0; i < kIt; ++i) {
+    const int q = i * kWp + w;
+    float* dst = slot + (4 * (lane & 1)) * kR + q * 32 + (lane >> 1);
+    const uint32_t p = t * kT + uint32_t(q) * 256 + uint32_t(4 * lane);
+    if (r.fast & (1u << i)) {
+      const f4 d = r.x[i] - r.b[i];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) dst[c * kR] = d[c];
+      if (flat) {  // the flattened vector for the cosine sums, as a by-product
+        if (kNT) __builtin_nontemporal_store(d, reinterpret_cast<f4*>(flat + p));
+        else *reinterpret_cast<f4*>(flat + p) = d;
+      }
+    } else {  // an entry boundary, an int64 entry or the end of the vectorised part inside the iteration
+      int idx = r.seg[i];
+      for (int c = 0; c < 4; ++c) {
+        const float d = p + c < a.m ? pn_value(a, S, idx, p + c, v) : 0.f;
+        dst[c * kR] = d;
+        if (flat && p + c < a.m) flat[p + c] = d;  // positions m .. n - 1: the tail loop
+      }
+    }
+  }
+}
+
+template <int kWp, int kD, bool kNT = false>
+__global__ __launch_bounds__(64 * (1 + kWp)) void port_norms_kernel(PnArgs a) {
+  constexpr int kIt = kIts / kWp;
+  static_assert(kIts % kWp == 0, "whole gather iterations per producer");
+  __shared__ __attribute__((aligned(16))) float ring[2 * kSlot];
+  __shared__ PnSeg S[kMaxSegs];
+  const int v = int(blockIdx.x);
+  for (int j = int(threadIdx.x); j < int(a.n_segs); j += int(blockDim.x)) {
+    const plato_agg_segment sg = a.segs[j];
+    S[j] = PnSeg{uint32_t(sg.flat_offset), uint32_t(sg.flat_offset + sg.numel), uint32_t(sg.src_offset),
+                 sg.region ? kSegI64 : 0u};
+  }
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = int(threadIdx.x & 63);
+  const uint32_t ntiles = (a.m + kT - 1) / kT;
+  const uint32_t nbar = (ntiles + kD - 1) / kD * kD;  // barriers: whole trips of kD tiles
+  if (wave > 0) {  // producer
+    const int w = wave - 1;
+    const __amdgpu_buffer_rsrc_t rx = pn_rsrc(sld(a.xf, v), a.n_f32 * 4), rb = pn_rsrc(sld(a.bf, v), a.n_f32 * 4);
+    PnCursor cur;
+    pn_cursor_load(S, 0, cur);
+    float* flat = a.flat ? sld(a.flat, v) : nullptr;
+    PnRegs<kIt> regs[kD];
+#pragma unroll
+    for (int j = 0; j < kD; ++j) pn_issue<kWp, kIt>(a, S, cur, rx, rb, uint32_t(j), w, lane, regs[j]);
+    for (uint32_t t = 0; t < nbar; t += kD) {
+#pragma unroll
+      for (int j = 0; j < kD; ++j) {
+        pn_write<kWp, kIt, kNT>(a, S, ring + ((t + j) & 1) * kSlot, flat, t + j, w, lane, v, regs[j]);
+        // past the last tile every load reads the arena's first elements: valid, never consumed
+        const uint32_t nxt = t + j + kD;
+        pn_issue<kWp, kIt>(a, S, cur, rx, rb, nxt < ntiles ? nxt : ntiles, w, lane, regs[j]);
+        __builtin_amdgcn_s_barrier();  // tile t + j published in slot (t + j) & 1
+      }
+    }
+    return;
+  }
+  // chain wave: lane & 7 walks chain j over row j (lanes 8..63 repeat rows 0..7)
+  __builtin_amdgcn_s_setprio(3);
+  const int j = lane & 7;
+  float acc = 0.f;
+  for (uint32_t t = 0; t < nbar; ++t) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    __builtin_amdgcn_s_barrier();
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (t >= ntiles) continue;
+    const f4* row = reinterpret_cast<const f4*>(ring + (t & 1) * kSlot + j * kR);
+    // 16 steps per block as 4 ds_read_b128, the next block's reads in flight (positions past m are +0:
+    // fma(0, 0, acc) leaves the non-negative sum unchanged)
+    f4 cur4[4], nxt4[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cur4[q] = row[q];
+#pragma unroll
+    for (int blk = 0; blk < kSteps / 16; ++blk) {
+      if (blk + 1 < kSteps / 16) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) nxt4[q] = row[4 * (blk + 1) + q];
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        acc = __builtin_fmaf(cur4[q].x, cur4[q].x, acc);
+        acc = __builtin_fmaf(cur4[q].y, cur4[q].y, acc);
+        acc = __builtin_fmaf(cur4[q].z, cur4[q].z, acc);
+        acc = __builtin_fmaf(cur4[q].w, cur4[q].w, acc);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cur4[q] = nxt4[q];
+    }
+  }
+  // the 8 lanes added in order (ATen's buffer[0] + buffer[1] + ...), then the scalar tail
+  float s = __shfl(acc, 0, 64);
+  for (int l = 1; l < kLanes; ++l) s = s + __shfl(acc, l, 64);
+  if (lane != 0) return;
+  int idx = 0;
+  float* flat = a.flat ? sld(a.flat, v) : nullptr;
+  for (uint32_t e = a.m; e < a.n; ++e) {
+    const float d = pn_value(a, S, idx, e, v);
+    if (flat) flat[e] = d;
+    s = pn_tail_step(s, d, e, a.m, a.n);
+  }
+  a.out[v] = sqrtf(s);
+}
+
+using PnFn = void (*)(const PnArgs&, hipStream_t, int);
+template <int kWp, int kD, bool kNT = false>
+void launch_pn(const PnArgs& a, hipStream_t st, int V) {
+  hipLaunchKernelGGL((port_norms_kernel<kWp, kD, kNT>), dim3(uint32_t(V)), dim3(64 * (1 + kWp)), 0, st, a);
+}
+// producer waves x tiles of loads in flight
+constexpr PnFn kPnDefault = &launch_pn<8, 3, true>;
+#ifdef PLATO_AGG_TUNE
+const PnFn kPnVariants[] = {
+    &launch_pn<4, 2>,  // 0: 4.33 ms on 129 ResNet-18 vectors, 5.12 storing the flat vectors (profiles/r03l_port.log)
+    &launch_pn<1, 2>,  // 1: 7.99 ms
+    &launch_pn<1, 4>,  // 2: 6.53 ms
+    &launch_pn<2, 2>,  // 3: 5.40 ms
+    &launch_pn<2, 3>,  // 4: 5.33 ms
+    &launch_pn<4, 3>,  // 5: 4.45 ms
+    &launch_pn<8, 2>,  // 6
+    &launch_pn<8, 3>,  // 7
+    &launch_pn<4, 4>,  // 8
+    &launch_pn<4, 2, true>,  // 9: non-temporal stores of the flattened vectors
+    &launch_pn<8, 2, true>,  // 10
+    &launch_pn<8, 3, true>,  // 11: the default, 4.81 ms storing the flat vectors
+};
+constexpr int kNumPnVariants = sizeof(kPnVariants) / sizeof(kPnVariants[0]);
+#endif
+
+int run_port_norms(PnFn fn, const void* const* d_x_f32, const void* const* d_x_i64, const void* const* d_b_f32,
+                   const void* const* d_b_i64, int n_vectors, const plato_agg_segment* d_segs, uint32_t n_segs,
+                   size_t n_flat, size_t n_f32, int flags, float* d_out, float* const* d_flat_out,
+                   hipStream_t stream) {
+  if (n_vectors <= 0) return set_error(PLATO_AGG_EINVAL, "n_vectors must be >= 1");
+  if (!d_x_f32 || !d_x_i64 || !d_b_f32 || !d_b_i64 || !d_segs || !d_out) return set_error(PLATO_AGG_EINVAL, "null pointer");
+  if (n_segs == 0 || n_segs > uint32_t(kMaxSegs)) return set_error(PLATO_AGG_EINVAL, "segment count must be in [1, 2048]");
+  if (n_flat == 0 || n_flat >= (size_t(1) << 31)) return set_error(PLATO_AGG_EINVAL, "flat length must be in [1, 2^31)");
+  if (n_f32 >= (size_t(1) << 30)) return set_error(PLATO_AGG_EINVAL, "fp32 arena must be < 2^30 elements");
+  if (flags & ~PLATO_AGG_PORT_CAST_FIRST) return set_error(PLATO_AGG_EINVAL, "unknown flags");
+  PnArgs a{};
+  a.xf = reinterpret_cast<const float* const*>(d_x_f32);
+  a.xi = reinterpret_cast<const int64_t* const*>(d_x_i64);
+  a.bf = reinterpret_cast<const float* const*>(d_b_f32);
+  a.bi = reinterpret_cast<const int64_t* const*>(d_b_i64);
+  a.segs = d_segs;
+  a.n_segs = n_segs;
+  a.n = uint32_t(n_flat);
+  a.m = uint32_t(n_flat - n_flat % kLanes);
+  a.n_f32 = n_f32;
+  a.cast_first = (flags & PLATO_AGG_PORT_CAST_FIRST) ? 1 : 0;
+  a.out = d_out;
+  a.flat = d_flat_out;
+  fn(a, stream, n_vectors);
+  hipError_t err = hipGetLastError();
+  if (err != hipSuccess) return set_error(PLATO_AGG_EHIP, std::string("port_norms launch: ") + hipGetErrorString(err));
+  return clear_error();
+}
+
+}  // namespace
+
+extern "C" {
+
+int plato_agg_port_norms(const void* const* d_x_f32, const void* const* d_x_i64, const void* const* d_b_f32,
+                         const void* const* d_b_i64, int n_vectors, const plato_agg_segment* d_segs, uint32_t n_segs,
+                         size_t n_flat, size_t n_f32, int flags, float* d_out, float* const* d_flat_out,
+                         hipStream_t stream) {
+  return run_port_norms(kPnDefault, d_x_f32, d_x_i64, d_b_f32, d_b_i64, n_vectors, d_segs, n_segs, n_flat, n_f32, flags,
+                        d_out, d_flat_out, stream);
+}
+
+#ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
+int plato_agg_tune_num_port_norms_variants(void) { return kNumPnVariants; }
+
+int plato_agg_tune_port_norms(int variant, const void* const* d_x_f32, const void* const* d_x_i64,
+                              const void* const* d_b_f32, const void* const* d_b_i64, int n_vectors,
+                              const plato_agg_segment* d_segs, uint32_t n_segs, size_t n_flat, size_t n_f32, int flags,
+                              float* d_out, float* const* d_flat_out, hipStream_t stream) {
+  if (variant < 0 || variant >= kNumPnVariants) return set_error(PLATO_AGG_EINVAL, "bad port_norms variant");
+  return run_port_norms(kPnVariants[variant], d_x_f32, d_x_i64, d_b_f32, d_b_i64, n_vectors, d_segs, n_segs, n_flat,
+                        n_f32, flags, d_out, d_flat_out, stream);
+}
+#endif  // PLATO_AGG_TUNE
+
+}  // extern "C"

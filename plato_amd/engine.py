@@ -719,6 +719,11 @@ class AggregationRound:
             raise ValueError("per-entry kernels take fp32 rows: run them on rnd.decoded() for coded payloads")
         return slots
 
+    def stage_reference(self, state_dict: Mapping[str, torch.Tensor]) -> DeviceArena:
+        """Port's stored global model as a device arena, staged ahead of :meth:`model_similarities`
+        (which otherwise stages it itself: a PCIe copy of the whole model on the similarity's path)."""
+        return self._stage_model(state_dict, "reference model", torch.cuda.current_stream(self.engine.device))
+
     def _stage_model(self, state_dict, what: str, stream) -> DeviceArena:
         """A native model (e.g. Port's stored global model) as a device arena of this round's layout."""
         self.layout.check_compatible(state_dict, what)
@@ -1070,7 +1075,7 @@ class AggregationRound:
         return out
 
     def model_similarities(self, reference: Mapping[str, torch.Tensor], slots: Sequence[int],
-                           eps: float = 1e-8, threads: int | None = None) -> list[np.float32]:
+                           eps: float = 1e-8, threads: int | None = None, flat_norms: bool = False) -> list[np.float32]:
         """Port's cosine similarity of each client delta with ``baseline - reference``, bit-exact.
 
         ``F.cosine_similarity(current - previous, delta, dim=0)`` over the
@@ -1078,9 +1083,14 @@ class AggregationRound:
         (examples/async/port/port_server.py:24-52), computed on the device in
         the order x86-64 PyTorch 2.10 uses on ``threads`` CPU threads (default
         ``torch.get_num_threads()``: what the reference's call would use in this
-        process): ``plato_agg_flatten`` -> ``plato_agg_entry_norms_f32`` (the
-        vector norms) -> ``plato_agg_torch_cosine_sum``.  Returned as fp32 like
-        the reference's 0-dim tensor.
+        process).  ``plato_agg_port_norms`` gathers ``current - previous`` and
+        every client delta straight from the staged arenas for the vector norms
+        (serial-chain bound) and stores the flattened vectors as it goes; the
+        cascade cosine sums (``plato_agg_torch_cosine_sum``) then read those.
+        ``flat_norms=True`` runs the round-2 path instead — ``plato_agg_flatten``,
+        then ``plato_agg_entry_norms_f32`` over the flat rows — kept as a device
+        cross-check.
+        Returned as fp32 like the reference's 0-dim tensor.
         """
         if not self.has_baseline:
             raise ValueError("baseline not staged")
@@ -1095,32 +1105,54 @@ class AggregationRound:
         eng = self.engine
         lay = self.layout
         stream = torch.cuda.current_stream(eng.device)
-        prev = self._stage_model(reference, "reference model", stream)
+        if isinstance(reference, DeviceArena):  # staged ahead by stage_reference
+            if reference.layout is not lay:
+                raise ValueError("reference arena was staged for another round / layout")
+            prev = reference
+        else:
+            prev = self._stage_model(reference, "reference model", stream)
         self.stager.fence(stream)
         segs, n_flat = self._flat_segments(list(range(len(lay.entries))), False)
         n_segs = len(lay.entries)
-        # current - previous, then each client's delta, as torch.cat lays them out
-        cur, stride = self._flatten(_lib.PLATO_AGG_FLAT_CAST_DIFF, segs, n_segs, n_flat, [_ptr(self._base.f32)],
-                                    [_ptr(self._base.i64)], (_ptr(prev.f32), _ptr(prev.i64)), 0.0, stream)
+        base = (_ptr(self._base.f32), _ptr(self._base.i64))
+        stride = max(64, -(-n_flat // 64) * 64)
         k = len(slots)
-        deltas, _ = self._flatten(_lib.PLATO_AGG_FLAT_DELTA, segs, n_segs, n_flat, [self._pf[i] for i in slots],
-                                  [self._pi[i] for i in slots], (_ptr(self._base.f32), _ptr(self._base.i64)), 0.0,
-                                  stream)
-        rows = [cur.data_ptr()] + [deltas.data_ptr() + r * stride * 4 for r in range(k)]
-        tab = torch.from_numpy(np.asarray(rows, dtype=np.int64)).to(eng.device)
-        chunk = torch.from_numpy(np.asarray([[0, 0, n_flat, 0]], dtype=np.uint32).view(np.int32)).to(eng.device)
-        norms = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         h = _stream_handle(stream)
-        # the rows are `stride` long (the padding past n_flat is read, never summed): declaring that length keeps the
-        # one n_flat-long piece off the kernel's partial-last-float4 fallback (a per-wave path ~1.5x slower)
-        _lib.call("plato_agg_entry_norms_f32", tab.data_ptr(), None, k + 1, None, None, chunk.data_ptr(), 1, None,
-                  0, 1, stride, 0, norms.data_ptr(), h)
+        norms = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         ws = torch.empty(max(1, eng.lib.plato_agg_torch_cosine_workspace(k, threads) // 4), dtype=torch.float32,
                          device=eng.device)
         out = torch.empty(k, dtype=torch.float32, device=eng.device)
-        _lib.call("plato_agg_torch_cosine_sum", cur.data_ptr(), tab.data_ptr() + 8, k, n_flat, norms.data_ptr(),
-                  norms.data_ptr() + 4, float(eps), threads, ws.data_ptr(), out.data_ptr(), h)
+        if flat_norms:  # the round-2 path: flattened vectors, norms and sums over them
+            cur, _ = self._flatten(_lib.PLATO_AGG_FLAT_CAST_DIFF, segs, n_segs, n_flat, [base[0]], [base[1]],
+                                   (_ptr(prev.f32), _ptr(prev.i64)), 0.0, stream)
+            deltas, _ = self._flatten(_lib.PLATO_AGG_FLAT_DELTA, segs, n_segs, n_flat, [self._pf[i] for i in slots],
+                                      [self._pi[i] for i in slots], base, 0.0, stream)
+            rows = [cur.data_ptr()] + [deltas.data_ptr() + r * stride * 4 for r in range(k)]
+            tab = torch.from_numpy(np.asarray(rows, dtype=np.int64)).to(eng.device)
+            chunk = torch.from_numpy(np.asarray([[0, 0, n_flat, 0]], dtype=np.uint32).view(np.int32)).to(eng.device)
+            # the rows are `stride` long (the padding past n_flat is read, never summed): declaring that length keeps
+            # the one n_flat-long piece off the kernel's partial-last-float4 fallback (a per-wave path ~1.5x slower)
+            _lib.call("plato_agg_entry_norms_f32", tab.data_ptr(), None, k + 1, None, None, chunk.data_ptr(), 1, None,
+                      0, 1, stride, 0, norms.data_ptr(), h)
+            _lib.call("plato_agg_torch_cosine_sum", cur.data_ptr(), tab.data_ptr() + 8, k, n_flat, norms.data_ptr(),
+                      norms.data_ptr() + 4, float(eps), threads, ws.data_ptr(), out.data_ptr(), h)
+            keep = (cur, deltas, tab, chunk)
+        else:  # norms straight from the arenas; the same kernel stores the flattened vectors for the sums
+            flat = torch.empty((k + 1, stride), dtype=torch.float32, device=eng.device)
+            vec = np.asarray([base[0]] + [self._pf[i] for i in slots]
+                             + [base[1] or 0] + [self._pi[i] or 0 for i in slots]
+                             + [_ptr(prev.f32)] + [base[0]] * k
+                             + [_ptr(prev.i64) or 0] + [base[1] or 0] * k
+                             + [flat.data_ptr() + r * stride * 4 for r in range(k + 1)], dtype=np.int64)
+            vt = torch.from_numpy(vec).to(eng.device)
+            v8, n1 = vt.data_ptr(), 8 * (k + 1)
+            _lib.call("plato_agg_port_norms", v8, v8 + n1, v8 + 2 * n1, v8 + 3 * n1, k + 1, segs.data_ptr(), n_segs,
+                      n_flat, lay.n_f32, _lib.PLATO_AGG_PORT_CAST_FIRST, norms.data_ptr(), v8 + 4 * n1, h)
+            _lib.call("plato_agg_torch_cosine_sum", flat.data_ptr(), v8 + 4 * n1 + 8, k, n_flat, norms.data_ptr(),
+                      norms.data_ptr() + 4, float(eps), threads, ws.data_ptr(), out.data_ptr(), h)
+            keep = (vt, flat)
         stream.synchronize()
+        del keep
         self.last_norms = norms.cpu().numpy()
         return [np.float32(v) for v in out.cpu().numpy()]
 

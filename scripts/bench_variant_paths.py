@@ -47,6 +47,9 @@ def main():
     ap.add_argument("--fedadp-only", action="store_true", help="only the fedadp kernel timing (for PMC passes)")
     ap.add_argument("--fedadp-cycles", type=int, default=None, metavar="VARIANT",
                     help="run a cycle-count probe variant of plato_agg_tune_fedadp_dots and summarise its workspace")
+    ap.add_argument("--port-only", action="store_true", help="only the port path (for kernel traces)")
+    ap.add_argument("--port-gathered", action="store_true",
+                    help="HIP-event time of every plato_agg_tune_port_norms variant on the arenas")
     ap.add_argument("--port-norms", action="store_true",
                     help="time the entry_norms variants on Port's K+1 flattened vectors (one entry each)")
     args = ap.parse_args()
@@ -93,10 +96,18 @@ def main():
         grads = rnd.launch_entrywise(w, add_base=False, device=True)
         rnd.fedadp_dots_flat(grads, slots, 0.01)
 
+    prev_arena = rnd.stage_reference(previous)
     paths = {
         "port": (lambda: rnd.model_similarities(previous, slots),
                  client_bytes + 3 * n_f * 4, (n_f + n_i) // 8,
-                 "flatten + vector_norm (8 fma chains over the flattened model) + cascade cosine sums"),
+                 "stage the reference model (H2D) + norms gathered from the arenas (8 fma chains over the flattened "
+                 "model; the kernel stores the flat vectors) + cascade cosine sums"),
+        "port_staged": (lambda: rnd.model_similarities(prev_arena, slots),
+                        client_bytes + 3 * n_f * 4, (n_f + n_i) // 8,
+                        "the same with the reference model staged ahead (AggregationRound.stage_reference)"),
+        "port_flat": (lambda: rnd.model_similarities(prev_arena, slots, flat_norms=True),
+                      client_bytes + 3 * n_f * 4, (n_f + n_i) // 8,
+                      "round 2: flatten + vector_norm over the flat rows + cascade cosine sums (reference staged)"),
         "fedadp": (fedadp, 2 * client_bytes, (n_f + n_i) // 64,
                    "global gradient + g flatten + fused gather/sdot (64 fma chains over the flattened model)"),
         "fedadp_flat": (fedadp_flat, 2 * client_bytes, (n_f + n_i) // 64,
@@ -107,8 +118,10 @@ def main():
                    "per-entry torch norms: 8 fma chains per (entry, client)"),
     }
     for name, (fn, nbytes, chain, what) in paths.items():
-        if args.sdot_only or args.fedadp_only or args.fedadp_cycles is not None:
+        if args.sdot_only or args.fedadp_only or args.fedadp_cycles is not None or args.port_gathered:
             break
+        if args.port_only and not name.startswith("port"):
+            continue
         fn()
         torch.cuda.synchronize(dev)
         ts = []
@@ -127,6 +140,8 @@ def main():
         sdot_kernels(dev, k, n_f + n_i, args.reps)
     if args.port_norms:
         port_norms(dev, k, n_f + n_i, args.reps)
+    if args.port_gathered:
+        port_gathered(dev, rnd, slots, layout, previous, args.reps)
 
 
 def fedadp_kernel(dev, rnd, slots, layout, reps, cycles_variant=None):
@@ -194,6 +209,49 @@ def fedadp_kernel(dev, rnd, slots, layout, reps, cycles_variant=None):
         print(json.dumps({"fedadp_dots": name, "pairs": k + 1, "n_flat": n_flat, "ms_median": round(med, 4),
                           "ms_min": round(min(ts), 4), "GBps_unique_bytes": round(uniq / (med * 1e-3) / 1e9, 1),
                           "unique_bytes": uniq, "bitwise_equal_to_flat_path": ok and same}), flush=True)
+
+
+def port_gathered(dev, rnd, slots, layout, previous, reps):
+    """plato_agg_port_norms (norms from the arenas) per tuning variant vs the flatten + entry_norms norms."""
+    from plato_amd import _lib
+    from plato_amd.engine import _ptr
+
+    k = len(slots)
+    rnd.model_similarities(previous, slots, flat_norms=True)
+    want = rnd.last_norms.copy()
+    prev = rnd._stage_model(previous, "reference model", torch.cuda.current_stream(dev))
+    segs, n_flat = rnd._flat_segments(list(range(len(layout.entries))), False)
+    bf, bi = _ptr(rnd._base.f32), _ptr(rnd._base.i64)
+    vec = np.asarray([bf] + [rnd._pf[i] for i in slots] + [bi] + [rnd._pi[i] for i in slots]
+                     + [_ptr(prev.f32)] + [bf] * k + [_ptr(prev.i64)] + [bi] * k, dtype=np.int64)
+    stride = max(64, -(-n_flat // 64) * 64)
+    flat = torch.empty((k + 1, stride), device=dev)
+    vec = np.concatenate([vec, np.asarray([flat.data_ptr() + r * stride * 4 for r in range(k + 1)], dtype=np.int64)])
+    vt = torch.from_numpy(vec).to(dev)
+    v8 = vt.data_ptr()
+    out = torch.empty(k + 1, device=dev)
+    h = torch.cuda.current_stream(dev).cuda_stream
+    for v, store in [(v, st) for v in range(_lib.tune().plato_agg_tune_num_port_norms_variants()) for st in (False, True)]:
+        def fn():
+            _lib.tune_call("plato_agg_tune_port_norms", v, v8, v8 + 8 * (k + 1), v8 + 16 * (k + 1), v8 + 24 * (k + 1),
+                           k + 1, segs.data_ptr(), len(layout.entries), n_flat, layout.n_f32,
+                           _lib.PLATO_AGG_PORT_CAST_FIRST, out.data_ptr(), v8 + 32 * (k + 1) if store else None, h)
+        fn()
+        torch.cuda.synchronize(dev)
+        ok = out.cpu().numpy().tobytes() == want.tobytes()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        med = statistics.median(ts)
+        print(json.dumps({"port_norms_gathered_variant": v, "stores_flat": store, "vectors": k + 1, "n": n_flat,
+                          "ms_median": round(med, 4),
+                          "cycles_per_step_at_2.4GHz": round(med * 1e-3 * 2.4e9 / (n_flat // 8), 2),
+                          "bitwise_equal_to_flat_path": ok}), flush=True)
 
 
 def port_norms(dev, k, n, reps):

@@ -530,3 +530,52 @@ def test_he_plaintext_half_matches_reference(engine, case):
     got = engine.weighted_sum(vecs, W.fedavg(recipe["num_samples"]))
     assert got.dtype == torch.float64 and got.numel() == exp["n_unencrypted"]
     assert G.sha(np.ascontiguousarray(got.numpy())) == exp["unencrypted_avg_sha256"]
+
+
+# ragged layouts for the gathered Port norms: int64 counters first, between and last; entries shorter than a
+# 256-position gather iteration, entries straddling 2,048-position tiles, n % 8 tails of 0-7
+PORT_SPECS = {
+    "i64_first_tail5": [("n0", (), "i64"), ("a", (3,), "f32"), ("b", (5000,), "f32"), ("n1", (2,), "i64"),
+                        ("c", (7, 9), "f32"), ("d", (4099,), "f32"), ("n2", (), "i64")],
+    "tail0_big": [("w", (3, 4097), "f32"), ("n0", (), "i64"), ("b", (255,), "f32"), ("c", (2, 2049), "f32"),
+                  ("n1", (), "i64"), ("e", (11,), "f32")],
+    "tiny": [("a", (5,), "f32")],
+    "i64_only_tail": [("a", (2048,), "f32"), ("n0", (3,), "i64")],
+}
+
+
+@pytest.mark.parametrize("spec", list(PORT_SPECS), ids=list(PORT_SPECS))
+def test_port_norms_gathered_match_oracle(engine, spec):
+    """plato_agg_port_norms (norms straight from the arenas) == the flatten + entry_norms path == the
+    oracle's torch-order norm of torch.cat(...), bit for bit, including int64 counters (cast-first for
+    current - previous, cast-once for the deltas) and every n % 8 tail."""
+    from oracle import reductions as R
+
+    layout = ArenaLayout.from_shapes(PORT_SPECS[spec])
+    rng = np.random.default_rng(len(spec))
+    k = 5
+    bf = rng.standard_normal(layout.n_f32).astype(np.float32)
+    bi = rng.integers(-2**40, 2**40, layout.n_i64)
+    pf = (bf + rng.standard_normal(layout.n_f32).astype(np.float32) * 0.1).astype(np.float32)
+    pi = bi + rng.integers(-2**35, 2**35, layout.n_i64)
+    baseline = layout.unpack(torch.from_numpy(bf), torch.from_numpy(bi))
+    previous = layout.unpack(torch.from_numpy(pf), torch.from_numpy(pi))
+    clients = []
+    for _ in range(k):
+        xf = (bf + rng.standard_normal(layout.n_f32).astype(np.float32) * 0.01).astype(np.float32)
+        xi = bi + rng.integers(-2**62, 2**62, layout.n_i64)  # wrapping int64 differences
+        clients.append((xf, xi))
+    rnd = engine.begin(baseline, k)
+    rnd.put_baseline(baseline)
+    for c, (xf, xi) in enumerate(clients):
+        rnd.put_client(c, layout.unpack(torch.from_numpy(xf), torch.from_numpy(xi)))
+    sims = rnd.model_similarities(previous, range(k), threads=4)
+    got = rnd.last_norms.copy()
+    sims_flat = rnd.model_similarities(previous, range(k), threads=4, flat_norms=True)
+    assert got.tobytes() == rnd.last_norms.tobytes()
+    sims_staged = rnd.model_similarities(rnd.stage_reference(previous), range(k), threads=4)
+    assert np.asarray(sims, np.float32).tobytes() == np.asarray(sims_staged, np.float32).tobytes()
+    assert np.asarray(sims, np.float32).tobytes() == np.asarray(sims_flat, np.float32).tobytes()
+    v = R.port_current_minus_previous(layout.entries, bf, bi, pf, pi)
+    want = [R.torch_norm(v)] + [R.torch_norm(R.port_delta(layout.entries, bf, bi, xf, xi)) for xf, xi in clients]
+    assert got.tobytes() == np.asarray(want, np.float32).tobytes()
