@@ -378,7 +378,8 @@ __device__ __forceinline__ void adp_write_v(const AdpArgs& a, const AdpSeg* S, i
   else adp_write<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, slot, pair0, w, lane, r);
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
+          int kCP = 1>
 __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kernel(AdpArgs a) {
   using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, kV>;
   static_assert(!kIso || kW <= 9, "kIso: at most 9 producer waves");
@@ -488,38 +489,37 @@ __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kern
     const uint64_t left = nsteps - t * kS;
     typedef float f4 __attribute__((ext_vector_type(4)));
     if (left >= uint64_t(kS)) {
-      // 16 steps per block of 4 ds_read_b128 pairs, the next block's reads in flight
-      f4 av[4], bv[4], an[4], bn[4];
+      // 16 steps per block of 4 ds_read_b128 pairs; the reads of the next kCP blocks in flight
+      constexpr int kNB = kS / 16, kRS = kCP + 1;
+      f4 av[kRS][4], bv[kRS][4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        av[q] = *reinterpret_cast<const f4*>(A + 4 * q);
-        bv[q] = *reinterpret_cast<const f4*>(B + 4 * q);
+      for (int d = 0; d < kCP; ++d) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          av[d][q] = *reinterpret_cast<const f4*>(A + 16 * d + 4 * q);
+          bv[d][q] = *reinterpret_cast<const f4*>(B + 16 * d + 4 * q);
+        }
       }
 #pragma unroll
-      for (int blk = 0; blk < kS / 16; ++blk) {
-        if (kProbe != 5 && blk + 1 < kS / 16) {  // probe 5: no LDS reads after the first block
+      for (int blk = 0; blk < kNB; ++blk) {
+        const int nb = blk + kCP;
+        if (kProbe != 5 && nb < kNB) {  // probe 5: no LDS reads after the first blocks
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            an[q] = *reinterpret_cast<const f4*>(A + 16 * (blk + 1) + 4 * q);
-            bn[q] = *reinterpret_cast<const f4*>(B + 16 * (blk + 1) + 4 * q);
+            av[nb % kRS][q] = *reinterpret_cast<const f4*>(A + 16 * nb + 4 * q);
+            bv[nb % kRS][q] = *reinterpret_cast<const f4*>(B + 16 * nb + 4 * q);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
+        const int cb = kProbe == 5 ? 0 : blk % kRS;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          acc = chain_fma(av[q].x, bv[q].x, acc);
-          acc = chain_fma(av[q].y, bv[q].y, acc);
-          acc = chain_fma(av[q].z, bv[q].z, acc);
-          acc = chain_fma(av[q].w, bv[q].w, acc);
+          acc = chain_fma(av[cb][q].x, bv[cb][q].x, acc);
+          acc = chain_fma(av[cb][q].y, bv[cb][q].y, acc);
+          acc = chain_fma(av[cb][q].z, bv[cb][q].z, acc);
+          acc = chain_fma(av[cb][q].w, bv[cb][q].w, acc);
         }
         __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          if (kProbe != 5) {
-            av[q] = an[q];
-            bv[q] = bn[q];
-          }
-        }
       }
     } else {
       for (int s = 0; s < int(left); ++s) acc = chain_fma(A[s], B[s], acc);
@@ -633,12 +633,13 @@ __global__ __launch_bounds__(64) void fedadp_finish_kernel(AdpArgs a, float* out
   out_yy[pair] = float(tyy + kyy);
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
+          int kCP = 1>
 void launch_adp(const AdpArgs& a, hipStream_t st) {
   constexpr int kGroups = 64 / kC;
   uint32_t pgs = uint32_t((a.n_pairs + kP - 1) / kP);
   pgs = (pgs + 7) / 8 * 8;  // whole XCD rounds (padding workgroups return at once)
-  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe, kIso, kV, kD>), dim3(pgs * kGroups),
+  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe, kIso, kV, kD, kCP>), dim3(pgs * kGroups),
                      dim3((64 * adp_waves<kW, kIso>())), 0, st, a);
 }
 using AdpFn = void (*)(const AdpArgs&, hipStream_t);
@@ -681,10 +682,17 @@ const AdpFn kAdpVariants[] = {
     &launch_adp<1, 32, 128, 8, 2, 0, 6, 0, 4, 3>,   // 29: probe of 26: cycle counts per wave into the workspace
     &launch_adp<1, 32, 128, 8, 2, 0, 0, 1, 4, 3>,   // 30: variant 26, chain waves on a SIMD of their own
     &launch_adp<1, 32, 128, 8, 8, 0, 0, 0, 1, 3>,   // 31: variant 3, 3 stages of loads in flight
+    &launch_adp<1, 32, 192, 8, 3, 0, 0, 0, 4>,      // 32: variant 23 with 192-step stages
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 2>,  // 33: variant 23, chain reads 2 blocks ahead
+    &launch_adp<1, 32, 192, 8, 3, 0, 0, 0, 4, 2, 2>,  // 34: variant 32, chain reads 2 blocks ahead
+    &launch_adp<1, 32, 128, 8, 2, 0, 4, 0, 4>,      // 35: probe of 23: the chains alone (wrong results)
+    &launch_adp<1, 32, 128, 8, 2, 0, 2, 0, 4>,      // 36: probe of 23: no chains (wrong results)
+    &launch_adp<1, 32, 128, 8, 2, 0, 6, 0, 4>,      // 37: probe of 23: cycle counts per wave
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 3>,  // 38: variant 23, chain reads 3 blocks ahead
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)
-constexpr int kAdpProbes[] = {6, 7, 8, 9, 10, 15, 16, 17, 18, 25, 29};
+constexpr int kAdpProbes[] = {6, 7, 8, 9, 10, 15, 16, 17, 18, 25, 29, 35, 36, 37};
 #endif
 
 int run_fedadp(AdpFn fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,

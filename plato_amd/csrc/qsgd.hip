@@ -244,7 +244,13 @@ __device__ __forceinline__ float apply_sign(uint32_t word, float mag) {
   return __uint_as_float((s & 0x80000000u) | __float_as_uint(mag));
 }
 
-template <int kBlock, int kU, bool kVerify = false>
+// Sign-rotated tables (kRot): the entry of code b sits at index b ^ ((b & 0x80) >> 2), so a code +z and
+// its negative 128 + z fall 32 banks apart instead of into the same bank (bank = index mod 64) — the
+// 2-way conflict that QSGD's sign-symmetric, small-magnitude codes produce in most 32-lane groups.
+__device__ __forceinline__ uint32_t rot_word(uint32_t w) { return w ^ ((w & 0x80808080u) >> 2); }
+__device__ __forceinline__ uint32_t rot_byte(uint32_t b) { return b ^ ((b & 0x80u) >> 2); }
+
+template <int kBlock, int kU, bool kVerify = false, bool kRot = false>
 __device__ __forceinline__ void build_tables(const QArgs& a, const float* mrow, int i0, int nu, float (*lut)[256],
                                              int* bad = nullptr, float rcp = 0.f) {
   for (int t = threadIdx.x; t < kU * 128; t += kBlock) {
@@ -256,7 +262,7 @@ __device__ __forceinline__ void build_tables(const QArgs& a, const float* mrow, 
       const float m = sld(mrow, i0 + u);
       const float v = decode(uint32_t(z), m, a.divisor);
       lut[u][z] = v;
-      lut[u][z + 128] = z ? -v : v;
+      lut[u][kRot ? rot_byte(uint32_t(z + 128)) : z + 128] = z ? -v : v;
       if (kVerify) {
         const float f = decode_fast(float(z), m, a.divisor, rcp);
         const uint32_t neg = __float_as_uint(f) | 0x80000000u;  // what apply_sign makes of code 128 + z
@@ -287,7 +293,7 @@ __device__ __forceinline__ void load_codes(const QArgs& a, int i0, int K, uint64
   }
 }
 
-template <int kU, int kG2, bool TWO, bool kNoLds = false>
+template <int kU, int kG2, bool TWO, bool kNoLds = false, bool kRot = false>
 __device__ __forceinline__ void sum_batch(int nu, const CodeOf<kG2> (&code)[kU], const float (&wu)[kU],
                                           const float (&su)[kU], const float (*lut)[256], const float (&b)[kG2],
                                           float (&acc)[kG2]) {
@@ -296,7 +302,7 @@ __device__ __forceinline__ void sum_batch(int nu, const CodeOf<kG2> (&code)[kU],
     for (int u = 0; u < kU; ++u) {
 #pragma unroll
       for (int q = 0; q < kG2; ++q) {
-        const uint32_t word = code[u][q >> 2];
+        const uint32_t word = kRot ? rot_word(code[u][q >> 2]) : code[u][q >> 2];
         const float x = kNoLds ? float((word >> (8 * (q & 3))) & 255u) : lut[u][(word >> (8 * (q & 3))) & 255u];
         acc[q] = acc[q] + term(x, b[q], wu[u], su[u], TWO);
       }
@@ -307,7 +313,7 @@ __device__ __forceinline__ void sum_batch(int nu, const CodeOf<kG2> (&code)[kU],
       if (u < nu) {
 #pragma unroll
         for (int q = 0; q < kG2; ++q) {
-          const uint32_t word = code[u][q >> 2];
+          const uint32_t word = kRot ? rot_word(code[u][q >> 2]) : code[u][q >> 2];
           const float x = lut[u][(word >> (8 * (q & 3))) & 255u];
           acc[q] = acc[q] + term(x, b[q], wu[u], su[u], TWO);
         }
@@ -378,8 +384,8 @@ __device__ __forceinline__ void pipe_step(const QArgs& a, const Chunk& ch, const
   load_weights<kU, TWO>(a, i0, wu, su);
   if (bi + 1 < nb) {
     const int i1 = i0 + kU;
-    build_tables<kBlock, kU, (kA > 0)>(a, mrow, i1, K - i1 < kU ? K - i1 : kU, lut[(bi + 1) & 1],
-                                       bad[(bi + 1) & 1], rcp);
+    build_tables<kBlock, kU, (kA > 0), (kA == -4)>(a, mrow, i1, K - i1 < kU ? K - i1 : kU, lut[(bi + 1) & 1],
+                                                   bad[(bi + 1) & 1], rcp);
     if (full) {
       if (kA == -1 || kA == -3) {  // timing probe: no code loads
 #pragma unroll
@@ -402,7 +408,7 @@ __device__ __forceinline__ void pipe_step(const QArgs& a, const Chunk& ch, const
     for (int u = 0; u < kU; ++u) mu[u] = sld(mrow, i0 + u);
     sum_batch_hybrid<kU, kG2, TWO, (kA > 0 ? kA : 1)>(cur, wu, su, mu, a.divisor, rcp, lut[bi & 1], b, acc);
   } else if (full) {
-    sum_batch<kU, kG2, TWO, (kA == -2 || kA == -3)>(nu, cur, wu, su, lut[bi & 1], b, acc);
+    sum_batch<kU, kG2, TWO, (kA == -2 || kA == -3), (kA == -4)>(nu, cur, wu, su, lut[bi & 1], b, acc);
   } else if (have) {
     for (int u = 0; u < nu; ++u) {
       const uint8_t* p = sld(a.cf, i0 + u);
@@ -411,7 +417,8 @@ __device__ __forceinline__ void pipe_step(const QArgs& a, const Chunk& ch, const
 #pragma unroll
       for (int q = 0; q < kG2; ++q) {
         const uint64_t e = e0 + q;
-        if (e >= ch.begin && e < ch.end) acc[q] = acc[q] + term(lut[bi & 1][u][p[e]], b[q], wu, su, TWO);
+        if (e >= ch.begin && e < ch.end)
+          acc[q] = acc[q] + term(lut[bi & 1][u][kA == -4 ? rot_byte(p[e]) : p[e]], b[q], wu, su, TWO);
       }
     }
   }
@@ -458,7 +465,7 @@ __device__ void qsgd_f32_chunk_pipe(const QArgs& a, uint32_t c, float (*lut)[kU]
     CodeOf<kG2> ca[kU], cb[kU];
     if (gp != g0) __syncthreads();  // the previous pass's last lookups are done (multi-pass chunks only)
     const float rcp = 1.0f / a.divisor;  // RN(1 / divisor): the IEEE division
-    build_tables<kBlock, kU, (kA > 0)>(a, mrow, 0, K < kU ? K : kU, lut[0], bad[0], rcp);
+    build_tables<kBlock, kU, (kA > 0), (kA == -4)>(a, mrow, 0, K < kU ? K : kU, lut[0], bad[0], rcp);
     if (full) load_codes<kU, kG2>(a, 0, K, e0, ca);
     __syncthreads();
     for (int bi = 0; bi < nb; bi += 2) {
@@ -816,6 +823,10 @@ const QVariant kQVariants[] = {
     {512, 32, 8, {&launch_qr<512, 8, false, 8, 32>, &launch_qr<512, 8, true, 8, 32>}},          // 58
     {512, 32, 4, {&launch_qr<512, 16, false, 4, 32>, &launch_qr<512, 16, true, 4, 32>}},        // 59
     {512, 32, 4, {&launch_qr<512, 8, false, 4, 32>, &launch_qr<512, 8, true, 4, 32>}},          // 60
+    // sign-rotated tables (+z and -z 32 banks apart) on the default's shape and two others
+    {512, 4, 8, {&launch_qp<512, 4, false, 8, 1, -4>, &launch_qp<512, 4, true, 8, 1, -4>}},     // 61
+    {1024, 8, 8, {&launch_qp<1024, 8, false, 8, 1, -4>, &launch_qp<1024, 8, true, 8, 1, -4>}},  // 62
+    {512, 4, 16, {&launch_qp<512, 4, false, 16, 1, -4>, &launch_qp<512, 4, true, 16, 1, -4>}},  // 63
 };
 #else  // libplato_agg.so: the default only
 const QVariant kQVariants[] = {
