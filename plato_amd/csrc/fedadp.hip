@@ -379,7 +379,7 @@ __device__ __forceinline__ void adp_write_v(const AdpArgs& a, const AdpSeg* S, i
 }
 
 template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
-          int kCP = 1>
+          int kCP = 1, int kPrio = 3>
 __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kernel(AdpArgs a) {
   using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, kV>;
   static_assert(!kIso || kW <= 9, "kIso: at most 9 producer waves");
@@ -467,7 +467,7 @@ __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kern
   }
   // chain waves: wave 0 the kP pairs' dots, wave 1 g . g (pair group 0 only; elsewhere it only
   // keeps the barrier count)
-  __builtin_amdgcn_s_setprio(3);
+  if (kPrio) __builtin_amdgcn_s_setprio(kPrio);  // the chain wave issues first
   const bool xx = chain_role == 1;
   const bool active = !xx || (pg == 0 && a.with_xx);
   const int kind = xx ? 0 : lane >> 5, c = xx ? lane % kC : (lane & 31) / kP, p = lane % kP;
@@ -634,12 +634,12 @@ __global__ __launch_bounds__(64) void fedadp_finish_kernel(AdpArgs a, float* out
 }
 
 template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
-          int kCP = 1>
+          int kCP = 1, int kPrio = 3>
 void launch_adp(const AdpArgs& a, hipStream_t st) {
   constexpr int kGroups = 64 / kC;
   uint32_t pgs = uint32_t((a.n_pairs + kP - 1) / kP);
   pgs = (pgs + 7) / 8 * 8;  // whole XCD rounds (padding workgroups return at once)
-  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe, kIso, kV, kD, kCP>), dim3(pgs * kGroups),
+  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe, kIso, kV, kD, kCP, kPrio>), dim3(pgs * kGroups),
                      dim3((64 * adp_waves<kW, kIso>())), 0, st, a);
 }
 using AdpFn = void (*)(const AdpArgs&, hipStream_t);
@@ -689,6 +689,11 @@ const AdpFn kAdpVariants[] = {
     &launch_adp<1, 32, 128, 8, 2, 0, 2, 0, 4>,      // 36: probe of 23: no chains (wrong results)
     &launch_adp<1, 32, 128, 8, 2, 0, 6, 0, 4>,      // 37: probe of 23: cycle counts per wave
     &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 3>,  // 38: variant 23, chain reads 3 blocks ahead
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 0>,  // 39: variant 23, chain wave at priority 0
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 1>,  // 40: variant 23, chain wave at priority 1
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 1, 4, 2, 1, 0>,  // 41: variant 30 (isolated chain SIMD), priority 0
+    &launch_adp<1, 32, 128, 4, 4, 0, 0, 0, 4, 2>,        // 42: variant 23 with 4 producer waves
+    &launch_adp<1, 32, 192, 12, 2, 0, 0, 0, 4, 2>,       // 43: variant 32 with 12 producer waves
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)
