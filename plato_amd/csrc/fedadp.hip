@@ -114,7 +114,7 @@ __device__ __forceinline__ int seg_walk(const AdpSeg* S, int n_segs, uint32_t p,
 // stage; kW producer waves, kIt gather iterations of 64 positions each per stage; kVRpad floats
 // between vectors (chosen with the row pitch kS + 4 so that the chain wave's ds_read_b128 pairs
 // are conflict-free for the lane map kind * 32 + chain * kP + pair: DESIGN.md §12)
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad = 0, int kV = 1>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad = 0, int kV = 1, int kSw = 0>
 struct AdpShape {
   static_assert(kP * kC == 32, "one chain wave: kind * 32 + chain * kP + pair");
   static_assert(kV == 1 || kV == 4, "one or four consecutive positions per lane and gather iteration");
@@ -122,7 +122,13 @@ struct AdpShape {
   static_assert(kS * kC == 64 * kV * kW * kIt, "a stage is kW x kIt gather iterations of 64 * kV positions");
   static_assert(kS % 16 == 0, "the chain wave reads 16 steps per block");
   static constexpr int kR = kS + 4;          // transposed row pitch (floats)
-  static constexpr int kVR = kC * kR + kVRpad;  // rows of one vector (x, loc_0 .. loc_{kP-1})
+  // kSw: the upper half of a vector's rows sits 32 floats further on, so that 4-position producer
+  // lanes (rows 4 (L mod kC/4) .. + 3) writing one column hit 64 different banks (a row pitch of
+  // 4 mod 64 alone puts rows r and r + 16 in one bank) while the chain's ds_read_b128 stay
+  // conflict-free
+  static constexpr int kGap = kSw ? 32 : 0;
+  static constexpr int kVR = kC * kR + kVRpad + kGap;  // rows of one vector (x, loc_0 .. loc_{kP-1})
+  __device__ static constexpr int row(int r) { return r * kR + (r >= kC / 2 ? kGap : 0); }
   static constexpr int kSlot = (1 + kP) * kVR;
   static constexpr int kBlkPerIt = 64 * kV / kC;  // 64-blocks per gather iteration
   static constexpr int kLpB = kC / kV;             // lanes per 64-block in a gather iteration
@@ -317,16 +323,16 @@ __device__ __forceinline__ float adp_value_at(const AdpArgs& a, const AdpSeg* S,
   return adp_f32(a.xf[pair][el], a.base_f[el], sg.info & kSegNeg, a.lr);
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kSw>
 __device__ __forceinline__ void adp_write4(const AdpArgs& a, const AdpSeg* S, int n_segs, float* slot, int pair0,
                                            int w, int lane, AdpRegs4<kP, kIt>& r) {
-  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, 4>;
+  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, 4, kSw>;
   const float lr = a.lr;
 #pragma unroll
   for (int i = 0; i < kIt; ++i) {
     const int g = i * kW + w;
     const int col = g * Sh::kBlkPerIt + lane / Sh::kLpB;  // step within the stage
-    float* dst = slot + (lane % Sh::kLpB) * 4 * Sh::kR + col;  // chain c0 = 4 * (lane % kLpB), rows c0 .. c0 + 3
+    float* dst = slot + Sh::row((lane % Sh::kLpB) * 4) + col;  // chain c0 = 4 * (lane % kLpB), rows c0 .. c0 + 3
 #pragma unroll
     for (int j = 0; j < 4; ++j) dst[j * Sh::kR] = r.x[i][j];
     if (r.fast & (1u << i)) {  // wave-uniform: one entry, one sign/divide mode
@@ -371,17 +377,18 @@ __device__ __forceinline__ void adp_issue_v(const AdpArgs& a, const AdpSeg* S, i
   else adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cur, src, t, cg, w, lane, r);
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe, int kV>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe, int kV, int kSw>
 __device__ __forceinline__ void adp_write_v(const AdpArgs& a, const AdpSeg* S, int n_segs, float* slot, int pair0,
                                             int w, int lane, AdpRegsV<kP, kIt, kV>& r) {
-  if constexpr (kV == 4) adp_write4<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, slot, pair0, w, lane, r);
+  static_assert(!kSw || kV == 4, "the row gap is laid out for 4-position producer lanes");
+  if constexpr (kV == 4) adp_write4<kP, kC, kS, kW, kIt, kVRpad, kSw>(a, S, n_segs, slot, pair0, w, lane, r);
   else adp_write<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, slot, pair0, w, lane, r);
 }
 
 template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
-          int kCP = 1, int kPrio = 3>
+          int kCP = 1, int kPrio = 3, int kSw = 0>
 __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kernel(AdpArgs a) {
-  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, kV>;
+  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, kV, kSw>;
   static_assert(!kIso || kW <= 9, "kIso: at most 9 producer waves");
   __shared__ __attribute__((aligned(16))) float ring[2 * Sh::kSlot];
   __shared__ AdpSeg S[kMaxSegs];
@@ -443,7 +450,7 @@ __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kern
 #pragma unroll
       for (int j = 0; j < kD; ++j) {
         if (kProbe == 6) c0 = __builtin_readcyclecounter();
-        adp_write_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV>(a, S, n_segs, ring + ((t + j) & 1) * Sh::kSlot, pair0, w,
+        adp_write_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV, kSw>(a, S, n_segs, ring + ((t + j) & 1) * Sh::kSlot, pair0, w,
                                                              lane, regs[j]);
         if (kProbe == 6) t_write += __builtin_readcyclecounter() - c0;
         // past the last stage (t = nst) every position clamps to the last block: valid addresses,
@@ -471,8 +478,8 @@ __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kern
   const bool xx = chain_role == 1;
   const bool active = !xx || (pg == 0 && a.with_xx);
   const int kind = xx ? 0 : lane >> 5, c = xx ? lane % kC : (lane & 31) / kP, p = lane % kP;
-  const int arow = (xx || kind == 0 ? 0 : (1 + p) * Sh::kVR) + c * Sh::kR;
-  const int brow = (xx ? 0 : (1 + p) * Sh::kVR) + c * Sh::kR;
+  const int arow = (xx || kind == 0 ? 0 : (1 + p) * Sh::kVR) + Sh::row(c);
+  const int brow = (xx ? 0 : (1 + p) * Sh::kVR) + Sh::row(c);
   float acc = 0.f;
   uint64_t t_start = 0, t_wait = 0, c0 = 0;  // probe 6: cycle counts
   if (kProbe == 6) t_start = __builtin_readcyclecounter();
@@ -634,12 +641,12 @@ __global__ __launch_bounds__(64) void fedadp_finish_kernel(AdpArgs a, float* out
 }
 
 template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
-          int kCP = 1, int kPrio = 3>
+          int kCP = 1, int kPrio = 3, int kSw = 0>
 void launch_adp(const AdpArgs& a, hipStream_t st) {
   constexpr int kGroups = 64 / kC;
   uint32_t pgs = uint32_t((a.n_pairs + kP - 1) / kP);
   pgs = (pgs + 7) / 8 * 8;  // whole XCD rounds (padding workgroups return at once)
-  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe, kIso, kV, kD, kCP, kPrio>), dim3(pgs * kGroups),
+  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe, kIso, kV, kD, kCP, kPrio, kSw>), dim3(pgs * kGroups),
                      dim3((64 * adp_waves<kW, kIso>())), 0, st, a);
 }
 using AdpFn = void (*)(const AdpArgs&, hipStream_t);
@@ -694,6 +701,10 @@ const AdpFn kAdpVariants[] = {
     &launch_adp<1, 32, 128, 8, 2, 0, 0, 1, 4, 2, 1, 0>,  // 41: variant 30 (isolated chain SIMD), priority 0
     &launch_adp<1, 32, 128, 4, 4, 0, 0, 0, 4, 2>,        // 42: variant 23 with 4 producer waves
     &launch_adp<1, 32, 192, 12, 2, 0, 0, 0, 4, 2>,       // 43: variant 32 with 12 producer waves
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 1>,  // 44: variant 23 with the row gap (conflict-free writes)
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 1, 4, 2, 1, 3, 1>,  // 45: variant 30 with the row gap
+    &launch_adp<1, 32, 192, 8, 3, 0, 0, 0, 4, 2, 1, 3, 1>,  // 46: variant 32 with the row gap
+    &launch_adp<2, 16, 128, 8, 1, 32, 0, 0, 4, 2, 1, 3, 1>, // 47: variant 20 with the row gap
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)

@@ -5,8 +5,8 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method threa
 rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/r03n_pytest.log
 [ $rc -ne 0 ] && exit $rc
 timeout -k 10 300 python -u scripts/bench_variant_paths.py --fedadp-only --reps 7 > gpurun_out/r03n_fedadp.log 2>&1
-rc=$?; echo "rc=$rc"; grep -v amdgpu.ids gpurun_out/r03n_fedadp.log | grep -E "\"(default|v23|v3[0-9]|v4[0-9])\"" | cut -c1-110
+rc=$?; echo "rc=$rc"; grep -v amdgpu.ids gpurun_out/r03n_fedadp.log | grep -E "\"(default|v23|v30|v4[4-9])\"" | cut -c1-110
 [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 python -u scripts/bench_variant_paths.py --fedadp-cycles 37 --reps 3 > gpurun_out/r03n_cycles.log 2>&1
+true
 rc=$?; echo "rc=$rc"; grep cycles gpurun_out/r03n_cycles.log | cut -c1-600
 exit $rc
