@@ -136,6 +136,13 @@ int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const*
                                size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
                                float* d_out_yy, hipStream_t stream);
 
+/* plato_agg_np_sumsq with an explicit kernel (0: one client per workgroup; 1/2/3: 4/8/16 clients per
+ * workgroup sharing the baseline; csrc/flat.hip). */
+int plato_agg_tune_num_np_sumsq_variants(void);
+int plato_agg_tune_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base,
+                            const plato_agg_chunk* d_pieces, const uint32_t* d_first_chunk, uint32_t n_pieces,
+                            uint32_t n_chunks, void* d_workspace, float* d_out, hipStream_t stream);
+
 /* plato_agg_port_norms with an explicit shape (see csrc/port.hip). */
 int plato_agg_tune_num_port_norms_variants(void);
 int plato_agg_tune_port_norms(int variant, const void* const* d_x_f32, const void* const* d_x_i64,

@@ -937,6 +937,71 @@ __global__ __launch_bounds__(256) void np_sumsq_chunks_lds_kernel(SumsqArgs a) {
   }
 }
 
+// G clients per workgroup: the chunk's baseline is read once into registers (32 values per lane)
+// and each client's x streams against it; squares are staged in two LDS buffers, and the leaves of
+// client g are summed by wave g mod 4 while every wave stages client g + 1 (its x loads issued
+// before the leaf work).  Same sums, same order as np_sumsq_chunks_lds_kernel.
+template <int G>
+__global__ __launch_bounds__(256) void np_sumsq_group_kernel(SumsqArgs a) {
+  __shared__ float sq[2][kNpBuf + kNpBuf / kPW];
+  constexpr int kQ = int(kNpBuf / 256);  // 32 elements per lane: element q * 256 + tid
+  const uint32_t c = blockIdx.x;
+  const int k0 = int(blockIdx.y) * G;
+  const int ng = a.K - k0 < G ? a.K - k0 : G;
+  uint32_t lo = 0, hi = a.n_pieces;  // the piece holding chunk c
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.first_chunk[mid] <= c) lo = mid; else hi = mid;
+  }
+  const plato_agg_chunk p = a.pieces[lo];
+  const uint64_t begin = uint64_t(p.begin) + uint64_t(c - a.first_chunk[lo]) * kNpBuf;
+  const uint64_t end = begin + kNpBuf < uint64_t(p.end) ? begin + kNpBuf : uint64_t(p.end);
+  const uint32_t n = uint32_t(end - begin);
+  const int tid = int(threadIdx.x), wave = tid >> 6;
+  const float* b = a.base + begin;
+  float bv[kQ], xv[kQ];
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    const uint32_t i = uint32_t(q * 256 + tid);
+    bv[q] = i < n ? b[i] : 0.f;
+  }
+  auto load_x = [&](int g) {
+    const float* x = sld(a.x, k0 + g) + begin;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const uint32_t i = uint32_t(q * 256 + tid);
+      xv[q] = i < n ? __builtin_nontemporal_load(x + i) : 0.f;
+    }
+  };
+  load_x(0);
+  for (int g = 0; g < ng; ++g) {
+    float* buf = sq[g & 1];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const uint32_t i = uint32_t(q * 256 + tid);
+      const float d = xv[q] - bv[q];
+      if (i < n) buf[np_pad(i)] = d * d;
+    }
+    __syncthreads();  // client g staged; the leaves of client g - 1 (other buffer) are done
+    if (g + 1 < ng) load_x(g + 1);  // in flight during the leaf work
+    if (wave == (g & 3)) {
+      const int lane = tid & 63;
+      const auto v = [&](uint64_t e) { return buf[np_pad(e)]; };
+      float* dst = a.chunk_sums + uint64_t(k0 + g) * a.n_chunks + c;
+      if (n == kNpBuf) {
+        float s = pw_leaf(v, uint64_t(lane) * kPW, kPW);
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) s = s + __shfl_xor(s, m);
+        if (lane == 0) *dst = s;
+      } else if (lane == 0) {
+        uint32_t so[16], sn[16], stage[16];
+        float sl[16];
+        *dst = pw_walk([&](uint32_t o, uint32_t m) { return pw_leaf(v, o, m); }, 0, n, PwStack{so, sn, sl, stage});
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   if (t >= uint64_t(a.n_pieces) * uint64_t(a.K)) return;
@@ -947,6 +1012,25 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   for (uint32_t c = c0; c < c1; ++c) out += a.chunk_sums[uint64_t(k) * a.n_chunks + c];
   a.out[uint64_t(k) * a.n_pieces + pc] = out;
 }
+
+// variant 0: one client per workgroup (np_sumsq_chunks_lds_kernel); 1..: G clients per workgroup
+void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
+  const uint32_t nc = a.n_chunks;
+  auto grid = [&](int g) { return dim3(nc, uint32_t((a.K + g - 1) / g)); };
+  switch (variant) {
+    case 1: hipLaunchKernelGGL(np_sumsq_group_kernel<4>, grid(4), dim3(256), 0, st, a); break;
+    case 2: hipLaunchKernelGGL(np_sumsq_group_kernel<8>, grid(8), dim3(256), 0, st, a); break;
+    case 3: hipLaunchKernelGGL(np_sumsq_group_kernel<16>, grid(16), dim3(256), 0, st, a); break;
+    default:
+      hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, dim3(uint32_t(uint64_t(nc) * uint64_t(a.K))), dim3(256), 0, st, a);
+  }
+}
+constexpr int kNumSumsqVariants = 4;
+constexpr int kSumsqDefault = 0;  // the grouped kernels measured 2.4-3.5x slower
+int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
+                 const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
+                 float* d_out, hipStream_t stream);
+
 
 }  // namespace
 
@@ -959,6 +1043,28 @@ size_t plato_agg_np_sumsq_workspace(int K, uint32_t n_chunks) {
 int plato_agg_np_sumsq(const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                        const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
                        float* d_out, hipStream_t stream) {
+  return run_np_sumsq(kSumsqDefault, d_x, K, d_base, d_pieces, d_first_chunk, n_pieces, n_chunks, d_workspace, d_out,
+                      stream);
+}
+
+#ifdef PLATO_AGG_TUNE
+int plato_agg_tune_num_np_sumsq_variants(void) { return kNumSumsqVariants; }
+
+int plato_agg_tune_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base,
+                            const plato_agg_chunk* d_pieces, const uint32_t* d_first_chunk, uint32_t n_pieces,
+                            uint32_t n_chunks, void* d_workspace, float* d_out, hipStream_t stream) {
+  if (variant < 0 || variant >= kNumSumsqVariants) return set_error(PLATO_AGG_EINVAL, "bad np_sumsq variant");
+  return run_np_sumsq(variant, d_x, K, d_base, d_pieces, d_first_chunk, n_pieces, n_chunks, d_workspace, d_out,
+                      stream);
+}
+#endif
+
+}  // extern "C"
+
+namespace {
+int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
+                 const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
+                 float* d_out, hipStream_t stream) {
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (!n_pieces) return clear_error();
   if (!d_x || !d_base || !d_pieces || !d_first_chunk || !d_workspace || !d_out)
@@ -976,12 +1082,15 @@ int plato_agg_np_sumsq(const float* const* d_x, int K, const float* d_base, cons
   const uint64_t t1 = uint64_t(n_chunks) * uint64_t(K), t2 = uint64_t(n_pieces) * uint64_t(K);
   if (t1) {
     if (t1 > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "too many chunks");
-    hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, dim3(uint32_t(t1)), dim3(256), 0, stream, a);
+    launch_sumsq(variant, a, stream);
     if (int rc = check_launch("np_sumsq chunks launch")) return rc;
   }
   hipLaunchKernelGGL(np_sumsq_pieces_kernel, dim3(uint32_t((t2 + 255) / 256)), dim3(256), 0, stream, a);
   return check_launch("np_sumsq pieces launch");
 }
+}  // namespace
+
+extern "C" {
 
 
 int plato_agg_flatten(int mode, const void* const* d_src_f32, const void* const* d_src_i64, int K,

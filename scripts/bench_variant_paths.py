@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--fedadp-cycles", type=int, default=None, metavar="VARIANT",
                     help="run a cycle-count probe variant of plato_agg_tune_fedadp_dots and summarise its workspace")
     ap.add_argument("--port-only", action="store_true", help="only the port path (for kernel traces)")
+    ap.add_argument("--polaris-variants", action="store_true",
+                    help="HIP-event time of every plato_agg_tune_np_sumsq variant (bitwise vs the default)")
     ap.add_argument("--port-gathered", action="store_true",
                     help="HIP-event time of every plato_agg_tune_port_norms variant on the arenas")
     ap.add_argument("--port-norms", action="store_true",
@@ -118,7 +120,8 @@ def main():
                    "per-entry torch norms: 8 fma chains per (entry, client)"),
     }
     for name, (fn, nbytes, chain, what) in paths.items():
-        if args.sdot_only or args.fedadp_only or args.fedadp_cycles is not None or args.port_gathered:
+        if (args.sdot_only or args.fedadp_only or args.fedadp_cycles is not None or args.port_gathered
+                or args.polaris_variants):
             break
         if args.port_only and not name.startswith("port"):
             continue
@@ -142,6 +145,8 @@ def main():
         port_norms(dev, k, n_f + n_i, args.reps)
     if args.port_gathered:
         port_gathered(dev, rnd, slots, layout, previous, args.reps)
+    if args.polaris_variants:
+        polaris_variants(dev, rnd, slots, layout, args.reps)
 
 
 def fedadp_kernel(dev, rnd, slots, layout, reps, cycles_variant=None):
@@ -209,6 +214,39 @@ def fedadp_kernel(dev, rnd, slots, layout, reps, cycles_variant=None):
         print(json.dumps({"fedadp_dots": name, "pairs": k + 1, "n_flat": n_flat, "ms_median": round(med, 4),
                           "ms_min": round(min(ts), 4), "GBps_unique_bytes": round(uniq / (med * 1e-3) / 1e9, 1),
                           "unique_bytes": uniq, "bitwise_equal_to_flat_path": ok and same}), flush=True)
+
+
+def polaris_variants(dev, rnd, slots, layout, reps):
+    """plato_agg_np_sumsq kernels: one client per workgroup vs G clients sharing the baseline."""
+    from plato_amd import _lib
+
+    k = len(slots)
+    want = rnd.np_sumsq(slots)
+    pieces, first, entry_of, n_chunks = rnd.layout._cache[("np_sumsq_pieces", str(dev))]
+    tf = torch.from_numpy(np.asarray([rnd._pf[i] for i in slots], dtype=np.int64)).to(dev)
+    ws = torch.empty(max(1, rnd.engine.lib.plato_agg_np_sumsq_workspace(k, n_chunks) // 4), device=dev)
+    out = torch.empty((k, int(entry_of.size)), device=dev)
+    h = torch.cuda.current_stream(dev).cuda_stream
+    uniq = k * layout.n_f32 * 4 + layout.n_f32 * 4
+    for v in range(_lib.tune().plato_agg_tune_num_np_sumsq_variants()):
+        def fn():
+            _lib.tune_call("plato_agg_tune_np_sumsq", v, tf.data_ptr(), k, rnd._base.f32.data_ptr(), pieces.data_ptr(),
+                           first.data_ptr(), int(entry_of.size), n_chunks, ws.data_ptr(), out.data_ptr(), h)
+        fn()
+        torch.cuda.synchronize(dev)
+        ok = out.cpu().numpy().tobytes() == want[:, entry_of].tobytes()
+        ts = []
+        for _ in range(reps):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn()
+            e1.record()
+            e1.synchronize()
+            ts.append(e0.elapsed_time(e1))
+        med = statistics.median(ts)
+        print(json.dumps({"np_sumsq_variant": v, "clients": k, "ms_median": round(med, 4), "ms_min": round(min(ts), 4),
+                          "GBps_unique_bytes": round(uniq / (med * 1e-3) / 1e9, 1),
+                          "bitwise_equal_to_default": ok}), flush=True)
 
 
 def port_gathered(dev, rnd, slots, layout, previous, reps):

@@ -122,6 +122,39 @@ def test_cosine_of_a_zero_vector_uses_eps():
     assert out.item() == float(R.torch_cosine(a, b, 8)) == 0.0
 
 
+@pytest.mark.parametrize("k", [3, 11])
+def test_np_sumsq_variants_agree_bitwise(k):
+    """Every np_sumsq kernel (one client per workgroup; 4 / 8 / 16 clients sharing the baseline, K not a
+    multiple of the group) equals the product default, which the test below pins to numpy."""
+    from plato_amd.arena import ArenaLayout
+    from plato_amd.engine import FedAvgEngine
+
+    spec = [("a", (7,), "f32"), ("b", (8192,), "f32"), ("n", (1,), "i64"), ("c", (8193,), "f32"),
+            ("d", (70001,), "f32"), ("e", (129,), "f32")]
+    layout = ArenaLayout.from_shapes(spec)
+    rng = np.random.default_rng(k)
+    bf = rng.standard_normal(layout.n_f32).astype(np.float32)
+    bi = rng.integers(0, 100, layout.n_i64)
+    eng = FedAvgEngine(DEV)
+    base = layout.unpack(torch.from_numpy(bf), torch.from_numpy(bi))
+    rnd = eng.begin(base, k)
+    rnd.put_baseline(base)
+    for c in range(k):
+        xf = (bf + rng.standard_normal(layout.n_f32).astype(np.float32) * 1e-2).astype(np.float32)
+        rnd.put_client(c, layout.unpack(torch.from_numpy(xf), torch.from_numpy(bi)))
+    want = rnd.np_sumsq(range(k))
+    pieces, first, entry_of, n_chunks = rnd.layout._cache[("np_sumsq_pieces", str(eng.device))]
+    tf = torch.from_numpy(np.asarray([rnd._pf[i] for i in range(k)], dtype=np.int64)).to(DEV)
+    ws = torch.empty(max(1, eng.lib.plato_agg_np_sumsq_workspace(k, n_chunks) // 4), dtype=torch.float32, device=DEV)
+    for v in range(_lib.tune().plato_agg_tune_num_np_sumsq_variants()):
+        out = torch.full((k, int(entry_of.size)), float("nan"), device=DEV)
+        _lib.tune_call("plato_agg_tune_np_sumsq", v, tf.data_ptr(), k, rnd._base.f32.data_ptr(), pieces.data_ptr(),
+                       first.data_ptr(), int(entry_of.size), n_chunks, ws.data_ptr(), out.data_ptr(),
+                       torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert out.cpu().numpy().tobytes() == want[:, entry_of].tobytes(), v
+
+
 def test_np_sumsq_equals_numpy_order():
     from oracle import fedavg_oracle as ref
     from plato_amd.arena import ArenaLayout
