@@ -444,6 +444,18 @@ int plato_agg_torch_cosine_sum(const float* d_a, const float* const* d_b, int K,
                                hipStream_t stream);
 
 /*
+ * plato_agg_torch_cosine_sum with a already divided by its clamped norm
+ * (F.cosine_similarity's x1 / x1_norm, the same fp32 quotients: one division
+ * per element and client instead of two).  plato_agg_scale_by_norm forms it:
+ * d_out[i] = d_a[i] / max(*d_norm, eps) (NaN norms stay NaN).
+ */
+int plato_agg_torch_cosine_sum_scaled(const float* d_a_scaled, const float* const* d_b, int K, size_t n,
+                                      const float* d_norm_b, float eps, int threads, void* d_workspace, float* d_out,
+                                      hipStream_t stream);
+int plato_agg_scale_by_norm(const float* d_a, size_t n, const float* d_norm, float eps, float* d_out,
+                            hipStream_t stream);
+
+/*
  * numpy's float32 np.sum(np.square(x_k - b)) of each fp32 piece (one per
  * entry, d_pieces rows (entry, begin, end)): the ufunc reduction's 8192-element
  * inner loops, out += pairwise_sum(chunk) from 0, pairwise_sum as numpy's

@@ -131,6 +131,10 @@ SIGNATURES = {
         [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, ctypes.c_uint32, _c_size_t, _c_size_t, _c_int,
          _c_void_p, _c_void_p, _c_void_p]),
     "plato_agg_torch_cosine_workspace": (_c_size_t, [_c_int, _c_int]),
+    "plato_agg_torch_cosine_sum_scaled": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p, _c_float, _c_int, _c_void_p, _c_void_p, _c_void_p]),
+    "plato_agg_scale_by_norm": (_c_int, [_c_void_p, _c_size_t, _c_void_p, _c_float, _c_void_p, _c_void_p]),
     "plato_agg_torch_cosine_sum": (
         _c_int,
         [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p, _c_void_p, _c_float, _c_int, _c_void_p, _c_void_p,

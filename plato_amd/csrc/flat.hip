@@ -618,17 +618,23 @@ __device__ __forceinline__ int ceil_log2_u64(uint64_t x) {
   return r;
 }
 
-struct QSrc {
+// q = (a / |a|) * (b / |b|); kScaled: a already divided by its (clamped) norm, once for all K clients
+// (plato_agg_scale_by_norm) — the same fp32 quotient, one division per element instead of two
+template <bool kScaled>
+struct QSrcT {
   const float* a;
   const float* b;
   float na, nb;
-  __device__ __forceinline__ float operator()(uint64_t p) const { return (a[p] / na) * (b[p] / nb); }
+  __device__ __forceinline__ float av(float x) const { return kScaled ? x : x / na; }
+  __device__ __forceinline__ float operator()(uint64_t p) const { return av(a[p]) * (b[p] / nb); }
 };
+using QSrc = QSrcT<false>;
 
 // One chunk [b0, b0+size0) -> final_acc of vectorized_inner_sum (size0 >= 8).
 // Level-0 groups (L rows of 32 values: 4 ILP rows x 8 lanes) are summed in
 // parallel by the workgroup, the higher levels in order by lanes 0..31 of wave 0.
-__device__ float chunk_cascade(const QSrc& q, uint64_t b0, uint64_t size0, float* lds_s0) {
+template <class Q>
+__device__ float chunk_cascade(const Q& q, uint64_t b0, uint64_t size0, float* lds_s0) {
   const uint64_t vec_size = size0 / 8;
   const uint64_t size_ilp = vec_size / 4;
   int lp = ceil_log2_u64(size_ilp) / 4;
@@ -647,8 +653,32 @@ __device__ float chunk_cascade(const QSrc& q, uint64_t b0, uint64_t size0, float
     return s;
   };
   for (uint64_t g1 = 0; g1 < G1; ++g1) {
-    for (uint64_t j = uint64_t(gslot); j < L; j += kSumThreads / 32)
-      lds_s0[j * 32 + uint64_t(acc_id)] = s0_of(g1 * L + j);
+    if (L == 16) {
+      // the common case (chunks of 2^14 .. 2^22 elements): both of this thread's level-0 groups with
+      // all 64 loads issued before the first add (the generic loop waits on each row's loads in turn)
+      constexpr int kL = 16, kJ = 16 / (kSumThreads / 32);
+      float av[kJ][kL], bv[kJ][kL];
+#pragma unroll
+      for (int jj = 0; jj < kJ; ++jj) {
+        const uint64_t row0 = (g1 * kL + uint64_t(gslot + jj * (kSumThreads / 32))) * kL;
+#pragma unroll
+        for (int i = 0; i < kL; ++i) {
+          const uint64_t p = b0 + (row0 + uint64_t(i)) * 32 + uint64_t(acc_id);
+          av[jj][i] = q.a[p];
+          bv[jj][i] = q.b[p];
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < kJ; ++jj) {
+        float s = 0.f;
+#pragma unroll
+        for (int i = 0; i < kL; ++i) s += q.av(av[jj][i]) * (bv[jj][i] / q.nb);
+        lds_s0[uint64_t(gslot + jj * (kSumThreads / 32)) * 32 + uint64_t(acc_id)] = s;
+      }
+    } else {
+      for (uint64_t j = uint64_t(gslot); j < L; j += kSumThreads / 32)
+        lds_s0[j * 32 + uint64_t(acc_id)] = s0_of(g1 * L + j);
+    }
     __syncthreads();
     if (tid < 32) {
       float s1 = 0.f;
@@ -747,16 +777,17 @@ __device__ float small_inner_sum(const float* in, int n) {
   return ps[0][0];
 }
 
+template <bool kScaled>
 __global__ __launch_bounds__(kSumThreads) void cosine_chunks_kernel(CosArgs a) {
   __shared__ float lds_s0[64 * 32];  // L <= 64 level-0 groups of 32 values
   const int k = blockIdx.y, t = blockIdx.x;
   const uint64_t b0 = uint64_t(t) * a.chunk;
   if (b0 >= a.n) return;
   const uint64_t e0 = b0 + a.chunk < a.n ? b0 + a.chunk : a.n;
-  QSrc q;
+  QSrcT<kScaled> q;
   q.a = a.av;
   q.b = sld(a.bv, k);
-  q.na = a.norm_a[0];
+  q.na = kScaled ? 1.f : a.norm_a[0];
   q.nb = a.norm_b[k];
   if (q.na < a.eps) q.na = a.eps;  // clamp_min_: NaN stays NaN
   if (q.nb < a.eps) q.nb = a.eps;
@@ -773,6 +804,14 @@ __global__ __launch_bounds__(kSumThreads) void cosine_chunks_kernel(CosArgs a) {
     }
   }
   if (threadIdx.x == 0) a.partial[uint64_t(k) * a.T + t] = 0.f + r;
+}
+
+// a / max(|a|, eps) (F.cosine_similarity's x1 / x1_norm after clamp_min_), once for the K sums
+__global__ __launch_bounds__(256) void scale_by_norm_kernel(const float* a, uint64_t n, const float* norm, float eps,
+                                                            float* out) {
+  float na = norm[0];
+  if (na < eps) na = eps;  // clamp_min_: NaN stays NaN
+  for (uint64_t i = uint64_t(blockIdx.x) * 256 + threadIdx.x; i < n; i += uint64_t(gridDim.x) * 256) out[i] = a[i] / na;
 }
 
 __global__ void cosine_combine_kernel(CosArgs a, int K) {
@@ -1090,6 +1129,53 @@ int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_bas
 }
 }  // namespace
 
+namespace {
+int run_cosine(bool scaled, const float* d_a, const float* const* d_b, int K, size_t n, const float* d_norm_a,
+               const float* d_norm_b, float eps, int threads, void* d_workspace, float* d_out, hipStream_t stream) {
+  if (K <= 0 || K > 65535) return set_error(PLATO_AGG_EINVAL, "K must be in [1, 65535]");
+  if (threads < 1 || threads > 1024) return set_error(PLATO_AGG_EINVAL, "threads must be in [1, 1024]");
+  if (!d_a || !d_b || (!scaled && !d_norm_a) || !d_norm_b || !d_workspace || !d_out)
+    return set_error(PLATO_AGG_EINVAL, "null pointer");
+  if (n == 0) return set_error(PLATO_AGG_EINVAL, "empty vectors");
+  CosArgs a{};
+  a.av = d_a;
+  a.bv = d_b;
+  a.norm_a = d_norm_a;
+  a.norm_b = d_norm_b;
+  a.eps = eps;
+  a.n = n;
+  a.T = threads;
+  a.partial = static_cast<float*>(d_workspace);
+  a.out = d_out;
+  // TensorIterator's parallel_reduce: one pass below the grain or on one
+  // thread, else two passes over min(T, ceil(n / 32768)) OpenMP chunks
+  const uint64_t grain = 32768;
+  a.single = (n < grain || threads == 1) ? 1 : 0;
+  if (a.single) {
+    a.nt = 1;
+    a.chunk = n;
+  } else {
+    uint64_t nt = uint64_t(threads);
+    const uint64_t by_grain = (n + grain - 1) / grain;
+    if (by_grain < nt) nt = by_grain;
+    a.chunk = (n + nt - 1) / nt;
+    a.nt = int((n + a.chunk - 1) / a.chunk);
+  }
+  // the level-0 sums of one level-1 group are staged in LDS: L = 2^lp <= 64 rows
+  {
+    const uint64_t size_ilp = (a.chunk / 8) / 4;
+    int r = 0;
+    while ((uint64_t(1) << r) < size_ilp) ++r;
+    if (r / 4 > 6) return set_error(PLATO_AGG_EINVAL, "thread chunk too long (> 2^33 elements)");
+  }
+  if (scaled) hipLaunchKernelGGL(cosine_chunks_kernel<true>, dim3(uint32_t(a.nt), uint32_t(K)), dim3(kSumThreads), 0, stream, a);
+  else hipLaunchKernelGGL(cosine_chunks_kernel<false>, dim3(uint32_t(a.nt), uint32_t(K)), dim3(kSumThreads), 0, stream, a);
+  if (int rc = check_launch("cosine chunks launch")) return rc;
+  hipLaunchKernelGGL(cosine_combine_kernel, dim3(uint32_t((K + 63) / 64)), dim3(64), 0, stream, a, K);
+  return check_launch("cosine combine launch");
+}
+}  // namespace
+
 extern "C" {
 
 
@@ -1158,46 +1244,23 @@ size_t plato_agg_torch_cosine_workspace(int K, int threads) {
 int plato_agg_torch_cosine_sum(const float* d_a, const float* const* d_b, int K, size_t n, const float* d_norm_a,
                                const float* d_norm_b, float eps, int threads, void* d_workspace, float* d_out,
                                hipStream_t stream) {
-  if (K <= 0 || K > 65535) return set_error(PLATO_AGG_EINVAL, "K must be in [1, 65535]");
-  if (threads < 1 || threads > 1024) return set_error(PLATO_AGG_EINVAL, "threads must be in [1, 1024]");
-  if (!d_a || !d_b || !d_norm_a || !d_norm_b || !d_workspace || !d_out)
-    return set_error(PLATO_AGG_EINVAL, "null pointer");
-  if (n == 0) return set_error(PLATO_AGG_EINVAL, "empty vectors");
-  CosArgs a{};
-  a.av = d_a;
-  a.bv = d_b;
-  a.norm_a = d_norm_a;
-  a.norm_b = d_norm_b;
-  a.eps = eps;
-  a.n = n;
-  a.T = threads;
-  a.partial = static_cast<float*>(d_workspace);
-  a.out = d_out;
-  // TensorIterator's parallel_reduce: one pass below the grain or on one
-  // thread, else two passes over min(T, ceil(n / 32768)) OpenMP chunks
-  const uint64_t grain = 32768;
-  a.single = (n < grain || threads == 1) ? 1 : 0;
-  if (a.single) {
-    a.nt = 1;
-    a.chunk = n;
-  } else {
-    uint64_t nt = uint64_t(threads);
-    const uint64_t by_grain = (n + grain - 1) / grain;
-    if (by_grain < nt) nt = by_grain;
-    a.chunk = (n + nt - 1) / nt;
-    a.nt = int((n + a.chunk - 1) / a.chunk);
-  }
-  // the level-0 sums of one level-1 group are staged in LDS: L = 2^lp <= 64 rows
-  {
-    const uint64_t size_ilp = (a.chunk / 8) / 4;
-    int r = 0;
-    while ((uint64_t(1) << r) < size_ilp) ++r;
-    if (r / 4 > 6) return set_error(PLATO_AGG_EINVAL, "thread chunk too long (> 2^33 elements)");
-  }
-  hipLaunchKernelGGL(cosine_chunks_kernel, dim3(uint32_t(a.nt), uint32_t(K)), dim3(kSumThreads), 0, stream, a);
-  if (int rc = check_launch("cosine chunks launch")) return rc;
-  hipLaunchKernelGGL(cosine_combine_kernel, dim3(uint32_t((K + 63) / 64)), dim3(64), 0, stream, a, K);
-  return check_launch("cosine combine launch");
+  return run_cosine(false, d_a, d_b, K, n, d_norm_a, d_norm_b, eps, threads, d_workspace, d_out, stream);
+}
+
+int plato_agg_torch_cosine_sum_scaled(const float* d_a_scaled, const float* const* d_b, int K, size_t n,
+                                      const float* d_norm_b, float eps, int threads, void* d_workspace, float* d_out,
+                                      hipStream_t stream) {
+  return run_cosine(true, d_a_scaled, d_b, K, n, nullptr, d_norm_b, eps, threads, d_workspace, d_out, stream);
+}
+
+int plato_agg_scale_by_norm(const float* d_a, size_t n, const float* d_norm, float eps, float* d_out,
+                            hipStream_t stream) {
+  if (!d_a || !d_norm || !d_out) return set_error(PLATO_AGG_EINVAL, "null pointer");
+  if (n == 0) return clear_error();
+  const uint64_t blocks = (uint64_t(n) + 255) / 256;
+  hipLaunchKernelGGL(scale_by_norm_kernel, dim3(uint32_t(blocks < 8192 ? blocks : 8192)), dim3(256), 0, stream, d_a,
+                     uint64_t(n), d_norm, eps, d_out);
+  return check_launch("scale_by_norm launch");
 }
 
 }  // extern "C"

@@ -1148,9 +1148,13 @@ class AggregationRound:
             v8, n1 = vt.data_ptr(), 8 * (k + 1)
             _lib.call("plato_agg_port_norms", v8, v8 + n1, v8 + 2 * n1, v8 + 3 * n1, k + 1, segs.data_ptr(), n_segs,
                       n_flat, lay.n_f32, _lib.PLATO_AGG_PORT_CAST_FIRST, norms.data_ptr(), v8 + 4 * n1, h)
-            _lib.call("plato_agg_torch_cosine_sum", flat.data_ptr(), v8 + 4 * n1 + 8, k, n_flat, norms.data_ptr(),
+            # current - previous over its norm once (not once per client), then the K cascade sums
+            scaled = torch.empty(stride, dtype=torch.float32, device=eng.device)
+            _lib.call("plato_agg_scale_by_norm", flat.data_ptr(), n_flat, norms.data_ptr(), float(eps), scaled.data_ptr(),
+                      h)
+            _lib.call("plato_agg_torch_cosine_sum_scaled", scaled.data_ptr(), v8 + 4 * n1 + 8, k, n_flat,
                       norms.data_ptr() + 4, float(eps), threads, ws.data_ptr(), out.data_ptr(), h)
-            keep = (vt, flat)
+            keep = (vt, flat, scaled)
         stream.synchronize()
         del keep
         self.last_norms = norms.cpu().numpy()
