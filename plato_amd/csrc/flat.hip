@@ -976,6 +976,95 @@ __global__ __launch_bounds__(256) void np_sumsq_chunks_lds_kernel(SumsqArgs a) {
   }
 }
 
+// One client per workgroup, latency-shaped: a full chunk's 64 loads per lane (32 of x, 32 of b) go
+// out before the first square is staged (one memory round trip per workgroup instead of four), and
+// the leaves are summed by 8 lanes each — lane (leaf, j) runs numpy's accumulator r[j] over its 16
+// steps, the 8 partials of a leaf combine by xor 1, 2, 4 shuffles (((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)),
+// a + b == b + a), then the 64 leaves by the same butterfly as before; a leaf pitch of 136 floats
+// keeps the 64 lanes' reads in 64 banks.  Partial chunks walk as before.
+constexpr int kLeafPitch = kPW + 8;
+__device__ __forceinline__ uint32_t np_pad8(uint64_t e) { return uint32_t(e + (e / kPW) * 8); }
+
+template <int kMap>
+__global__ __launch_bounds__(256) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
+  __shared__ float sq[kNpBuf / kPW * kLeafPitch];
+  __shared__ float leaf_sum[kNpBuf / kPW];
+  constexpr int kQ = int(kNpBuf / 256);
+  // kMap 0: client-major (the K passes over the baseline are a whole model apart: L2 misses);
+  // 1: chunk-major, the K clients of a chunk are consecutive workgroups (dealt over the 8 XCDs
+  // together: each XCD's L2 serves the chunk's baseline to its share of them); 2: the K clients of
+  // chunk c all on XCD c mod 8 (workgroups are dealt to the XCDs round-robin), one baseline fetch
+  uint32_t k, c;
+  if (kMap == 0) {
+    k = blockIdx.x / a.n_chunks;
+    c = blockIdx.x % a.n_chunks;
+  } else if (kMap == 1) {
+    k = blockIdx.x % uint32_t(a.K);
+    c = blockIdx.x / uint32_t(a.K);
+  } else {
+    const uint32_t idx = blockIdx.x >> 3;
+    k = idx % uint32_t(a.K);
+    c = (idx / uint32_t(a.K)) * 8 + (blockIdx.x & 7);
+    if (c >= a.n_chunks) return;  // padding (whole workgroup, before any barrier)
+  }
+  uint32_t lo = 0, hi = a.n_pieces;  // the piece holding chunk c
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a.first_chunk[mid] <= c) lo = mid; else hi = mid;
+  }
+  const plato_agg_chunk p = a.pieces[lo];
+  const uint64_t begin = uint64_t(p.begin) + uint64_t(c - a.first_chunk[lo]) * kNpBuf;
+  const uint64_t end = begin + kNpBuf < uint64_t(p.end) ? begin + kNpBuf : uint64_t(p.end);
+  const uint32_t n = uint32_t(end - begin);
+  const float* x = a.x[k] + begin;
+  const float* b = a.base + begin;
+  const int tid = int(threadIdx.x);
+  {
+    float xv[kQ], bv[kQ];
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const uint32_t i = uint32_t(q * 256 + tid);
+      xv[q] = i < n ? __builtin_nontemporal_load(x + i) : 0.f;
+      bv[q] = i < n ? b[i] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const uint32_t i = uint32_t(q * 256 + tid);
+      const float d = xv[q] - bv[q];
+      if (i < n) sq[np_pad8(i)] = d * d;
+    }
+  }
+  __syncthreads();
+  float* dst = a.chunk_sums + uint64_t(k) * a.n_chunks + c;
+  if (n == kNpBuf) {
+    // 64 leaves x 8 accumulators = 512 lanes: two passes of the 256 threads
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      const int slot = pass * 256 + tid, leaf = slot >> 3, j = slot & 7;
+      const float* l = sq + leaf * kLeafPitch + j;
+      float r = l[0];
+#pragma unroll
+      for (int i = 8; i < kPW; i += 8) r += l[i];
+      r = r + __shfl_xor(r, 1);
+      r = r + __shfl_xor(r, 2);
+      r = r + __shfl_xor(r, 4);
+      if (j == 0) leaf_sum[leaf] = r;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      float s = leaf_sum[tid];
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) s = s + __shfl_xor(s, m);
+      if (tid == 0) *dst = s;
+    }
+  } else if (tid == 0) {
+    const auto v = [&](uint64_t e) { return sq[np_pad8(e)]; };
+    uint32_t so[16], sn[16], stage[16];
+    float sl[16];
+    *dst = pw_walk([&](uint32_t o, uint32_t m) { return pw_leaf(v, o, m); }, 0, n, PwStack{so, sn, sl, stage});
+  }
+}
+
 // G clients per workgroup: the chunk's baseline is read once into registers (32 values per lane)
 // and each client's x streams against it; squares are staged in two LDS buffers, and the leaves of
 // client g are summed by wave g mod 4 while every wave stages client g + 1 (its x loads issued
@@ -1060,12 +1149,24 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
     case 1: hipLaunchKernelGGL(np_sumsq_group_kernel<4>, grid(4), dim3(256), 0, st, a); break;
     case 2: hipLaunchKernelGGL(np_sumsq_group_kernel<8>, grid(8), dim3(256), 0, st, a); break;
     case 3: hipLaunchKernelGGL(np_sumsq_group_kernel<16>, grid(16), dim3(256), 0, st, a); break;
+    case 4:
+      hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel<0>, dim3(uint32_t(uint64_t(nc) * uint64_t(a.K))), dim3(256), 0, st,
+                         a);
+      break;
+    case 5:
+      hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel<1>, dim3(uint32_t(uint64_t(nc) * uint64_t(a.K))), dim3(256), 0, st,
+                         a);
+      break;
+    case 6:
+      hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel<2>, dim3(uint32_t(uint64_t((nc + 7) / 8 * 8) * uint64_t(a.K))),
+                         dim3(256), 0, st, a);
+      break;
     default:
       hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, dim3(uint32_t(uint64_t(nc) * uint64_t(a.K))), dim3(256), 0, st, a);
   }
 }
-constexpr int kNumSumsqVariants = 4;
-constexpr int kSumsqDefault = 0;  // the grouped kernels measured 2.4-3.5x slower
+constexpr int kNumSumsqVariants = 7;
+constexpr int kSumsqDefault = 5;  // chunk-major v2: 1.24-1.27 ms vs 1.65 (variant 0) on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
                  float* d_out, hipStream_t stream);
