@@ -780,7 +780,9 @@ __device__ float small_inner_sum(const float* in, int n) {
 template <bool kScaled>
 __global__ __launch_bounds__(kSumThreads) void cosine_chunks_kernel(CosArgs a) {
   __shared__ float lds_s0[64 * 32];  // L <= 64 level-0 groups of 32 values
-  const int k = blockIdx.y, t = blockIdx.x;
+  // the K clients of a chunk are consecutive workgroups (dealt over the 8 XCDs together): the XCD L2s
+  // serve the chunk of a to them (chunk-major numbering; DESIGN.md §12, np_sumsq)
+  const int k = blockIdx.x, t = blockIdx.y;
   const uint64_t b0 = uint64_t(t) * a.chunk;
   if (b0 >= a.n) return;
   const uint64_t e0 = b0 + a.chunk < a.n ? b0 + a.chunk : a.n;
@@ -1269,8 +1271,8 @@ int run_cosine(bool scaled, const float* d_a, const float* const* d_b, int K, si
     while ((uint64_t(1) << r) < size_ilp) ++r;
     if (r / 4 > 6) return set_error(PLATO_AGG_EINVAL, "thread chunk too long (> 2^33 elements)");
   }
-  if (scaled) hipLaunchKernelGGL(cosine_chunks_kernel<true>, dim3(uint32_t(a.nt), uint32_t(K)), dim3(kSumThreads), 0, stream, a);
-  else hipLaunchKernelGGL(cosine_chunks_kernel<false>, dim3(uint32_t(a.nt), uint32_t(K)), dim3(kSumThreads), 0, stream, a);
+  if (scaled) hipLaunchKernelGGL(cosine_chunks_kernel<true>, dim3(uint32_t(K), uint32_t(a.nt)), dim3(kSumThreads), 0, stream, a);
+  else hipLaunchKernelGGL(cosine_chunks_kernel<false>, dim3(uint32_t(K), uint32_t(a.nt)), dim3(kSumThreads), 0, stream, a);
   if (int rc = check_launch("cosine chunks launch")) return rc;
   hipLaunchKernelGGL(cosine_combine_kernel, dim3(uint32_t((K + 63) / 64)), dim3(64), 0, stream, a, K);
   return check_launch("cosine combine launch");
