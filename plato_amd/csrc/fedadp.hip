@@ -640,6 +640,153 @@ __global__ __launch_bounds__(64) void fedadp_finish_kernel(AdpArgs a, float* out
   out_yy[pair] = float(tyy + kyy);
 }
 
+// Flag-synchronised form (tuning; one pair per workgroup, 4-position lanes): no s_barrier between
+// producers and chains.  Each producer wave adds 1 to full[slot] (an LDS counter) after writing its
+// part of a stage, the chain waves wait for kW arrivals, run the stage and add 1 to `done`; a
+// producer waits for the chains to have finished stage t - kRing before overwriting its slot.  So a
+// slow stage on one side no longer stalls the other at every tile (the barrier form pays the max of
+// both per tile).  Every wait is bounded: a wave that spins past kSpinMax raises `abort` in LDS and
+// every wait then returns at once, so the grid always drains (results of such a launch are garbage
+// and flagged in ws[0] as NaN by the finish kernel's inputs).
+constexpr uint32_t kSpinMax = 1u << 20;
+
+__device__ __forceinline__ bool adp_wait_geq(const uint32_t* ctr, uint32_t target, uint32_t* abort_flag) {
+  for (uint32_t spin = 0;; ++spin) {
+    if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
+    if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+    if (spin > kSpinMax) {
+      __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+template <int kC, int kS, int kW, int kIt, int kD, int kRing>
+__global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_flag_kernel(AdpArgs a) {
+  using Sh = AdpShape<1, kC, kS, kW, kIt, 0, 4>;
+  static_assert(kRing >= 2 && kRing <= 3, "2-3 tile slots");
+  __shared__ __attribute__((aligned(16))) float ring[kRing * Sh::kSlot];
+  __shared__ AdpSeg S[kMaxSegs];
+  __shared__ uint32_t full[kRing], done, abort_flag;
+  constexpr int kGroups = 64 / kC;
+  const int b = int(blockIdx.x), lo = b & 7;
+  const int cg = (b / 8) % kGroups;
+  const int pg = (b / (8 * kGroups)) * 8 + lo;
+  if (pg >= a.n_pairs) return;  // padding workgroup (before the barrier)
+  const int n_segs = int(a.n_segs);
+  for (int j = int(threadIdx.x); j < n_segs; j += int(blockDim.x)) {
+    const plato_agg_segment sg = a.segs[j];
+    S[j] = AdpSeg{uint32_t(sg.flat_offset), uint32_t(sg.flat_offset + sg.numel), uint32_t(sg.src_offset),
+                  (sg.region ? kSegI64 : 0u) | ((sg.flags & PLATO_AGG_SEG_NEG_DIV) ? kSegNeg : 0u)};
+  }
+  if (threadIdx.x < kRing) full[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    done = 0;
+    abort_flag = 0;
+  }
+  __syncthreads();  // the only workgroup barrier
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = int(threadIdx.x & 63);
+  const uint32_t nst = uint32_t((a.nsteps + kS - 1) / kS);
+  const bool xx_active = pg == 0 && a.with_xx;
+  const uint32_t nchain = xx_active ? 2u : 1u;
+  if (wave >= 2) {  // producer
+    const int w = wave - 2;
+    AdpSrc<1> src;
+    src.x = adp_rsrc(a.x, a.nsteps * 256);
+    src.b = adp_rsrc(a.base_f, a.n_f32 * 4);
+    src.y[0] = adp_rsrc(sld(a.xf, pg), a.n_f32 * 4);
+    AdpCursor cursor;
+    adp_cursor_load(S, 0, cursor);
+    AdpRegs4<1, kIt> regs[kD];
+#pragma unroll
+    for (int j = 0; j < kD; ++j)
+      adp_issue4<1, kC, kS, kW, kIt, 0>(a, S, n_segs, cursor, src, uint32_t(j) < nst ? uint32_t(j) : nst, cg, w, lane,
+                                        regs[j]);
+    for (uint32_t t0 = 0; t0 < nst; t0 += kD) {
+#pragma unroll
+      for (int j = 0; j < kD; ++j) {
+        const uint32_t t = t0 + j;
+        if (t < nst) {  // wave-uniform
+          if (t >= uint32_t(kRing)) adp_wait_geq(&done, nchain * (t + 1 - kRing), &abort_flag);
+          adp_write4<1, kC, kS, kW, kIt, 0, 0>(a, S, n_segs, ring + (t % kRing) * Sh::kSlot, pg, w, lane, regs[j]);
+          const uint32_t nxt = t + kD;
+          adp_issue4<1, kC, kS, kW, kIt, 0>(a, S, n_segs, cursor, src, nxt < nst ? nxt : nst, cg, w, lane, regs[j]);
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this wave's part of stage t is in LDS
+          if (lane == 0) atomicAdd(&full[t % kRing], 1u);
+        }
+      }
+    }
+    return;
+  }
+  const bool xx = wave == 1;
+  if (xx && !xx_active) return;
+  __builtin_amdgcn_s_setprio(3);
+  const int kind = xx ? 0 : lane >> 5, c = xx ? lane % kC : (lane & 31);
+  const int arow = (xx || kind == 0 ? 0 : Sh::kVR) + Sh::row(c);
+  const int brow = (xx ? 0 : Sh::kVR) + Sh::row(c);
+  float acc = 0.f;
+  for (uint32_t t = 0; t < nst; ++t) {
+    adp_wait_geq(&full[t % kRing], uint32_t(kW) * (t / kRing + 1), &abort_flag);
+    const float* slot = ring + (t % kRing) * Sh::kSlot;
+    const float* A = slot + arow;
+    const float* B = slot + brow;
+    const uint64_t left = a.nsteps - uint64_t(t) * kS;
+    if (left >= uint64_t(kS)) {
+      f4v av[4], bv[4], an[4], bn[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        av[q] = *reinterpret_cast<const f4v*>(A + 4 * q);
+        bv[q] = *reinterpret_cast<const f4v*>(B + 4 * q);
+      }
+#pragma unroll
+      for (int blk = 0; blk < kS / 16; ++blk) {
+        if (blk + 1 < kS / 16) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            an[q] = *reinterpret_cast<const f4v*>(A + 16 * (blk + 1) + 4 * q);
+            bn[q] = *reinterpret_cast<const f4v*>(B + 16 * (blk + 1) + 4 * q);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          acc = chain_fma(av[q].x, bv[q].x, acc);
+          acc = chain_fma(av[q].y, bv[q].y, acc);
+          acc = chain_fma(av[q].z, bv[q].z, acc);
+          acc = chain_fma(av[q].w, bv[q].w, acc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          av[q] = an[q];
+          bv[q] = bn[q];
+        }
+      }
+    } else {
+      for (int s = 0; s < int(left); ++s) acc = chain_fma(A[s], B[s], acc);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this stage's reads are consumed
+    if (lane == 0) atomicAdd(&done, 1u);
+  }
+  if (__hip_atomic_load(&abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) acc = __builtin_nanf("");
+  const int chain = cg * kC + c;
+  if (!xx) {
+    a.ws[uint64_t(pg) * 128 + uint64_t(kind) * 64 + chain] = acc;
+  } else if (lane < kC) {  // the virtual pair (g, g)
+    a.ws[uint64_t(a.n_pairs) * 128 + chain] = acc;
+    a.ws[uint64_t(a.n_pairs) * 128 + 64 + chain] = acc;
+  }
+}
+
+template <int kC, int kS, int kW, int kIt, int kD, int kRing>
+void launch_adp_flag(const AdpArgs& a, hipStream_t st) {
+  constexpr int kGroups = 64 / kC;
+  const uint32_t pgs = uint32_t((a.n_pairs + 7) / 8 * 8);
+  hipLaunchKernelGGL((fedadp_dots_flag_kernel<kC, kS, kW, kIt, kD, kRing>), dim3(pgs * kGroups), dim3(64 * (kW + 2)), 0,
+                     st, a);
+}
+
 template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
           int kCP = 1, int kPrio = 3, int kSw = 0>
 void launch_adp(const AdpArgs& a, hipStream_t st) {
@@ -705,6 +852,9 @@ const AdpFn kAdpVariants[] = {
     &launch_adp<1, 32, 128, 8, 2, 0, 0, 1, 4, 2, 1, 3, 1>,  // 45: variant 30 with the row gap
     &launch_adp<1, 32, 192, 8, 3, 0, 0, 0, 4, 2, 1, 3, 1>,  // 46: variant 32 with the row gap
     &launch_adp<2, 16, 128, 8, 1, 32, 0, 0, 4, 2, 1, 3, 1>, // 47: variant 20 with the row gap
+    &launch_adp_flag<32, 128, 8, 2, 2, 2>,  // 48: variant 23 synchronised by LDS counters, 2 tile slots
+    &launch_adp_flag<32, 128, 8, 2, 2, 3>,  // 49: the same, 3 tile slots
+    &launch_adp_flag<32, 128, 8, 2, 3, 3>,  // 50: 3 tile slots, 3 stages of loads in flight
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)
