@@ -159,16 +159,21 @@ def _buffer(data):
     return arr.ctypes.data, arr.size, arr
 
 
+_parse_cap = 256  # output capacity of the last parse that fitted (payloads of one server repeat their size)
+
+
 def parse(data) -> tuple[list[TensorInfo], list[str], object]:
     """Parse pickled payload bytes; returns (tensor infos, keys, keepalive)."""
+    global _parse_cap
     addr, n, keep = _buffer(data)
     h = lib()
-    cap = 64
+    cap = _parse_cap
     while True:
         out = (TensorInfo * cap)()
         rc = h.plato_ingest_parse(addr, n, out, cap)
-        if rc == -5:  # capacity
-            cap *= 8
+        if rc == -5:  # capacity: the parser's failure path is slow (~20 ms on a ResNet-18 payload), so the
+            cap *= 8  # capacity that fitted is remembered for the next payload
+            _parse_cap = cap
             continue
         if rc < 0:
             raise IngestError(f"payload rejected ({rc}): {h.plato_ingest_last_error().decode()}")
