@@ -891,7 +891,10 @@ int plato_ingest_parse(const uint8_t* buf, size_t len, plato_ingest_tensor* out,
     Reader r{c, 0, len};
     P top = run(c, r, nullptr);
     if (top->k != K::Dict) fail(PLATO_INGEST_EUNSUPPORTED, "payload is not a dict of tensors");
-    if (int64_t(top->dict.size()) > max_tensors) fail(PLATO_INGEST_ECAPACITY, "more tensors than the output array");
+    if (int64_t(top->dict.size()) > max_tensors) {  // not an exception: a C++ throw from a library loaded
+      g_err = "more tensors than the output array";  // beside torch's costs ~20 ms of FDE lookups
+      return PLATO_INGEST_ECAPACITY;
+    }
     int n = 0;
     for (auto& kv : top->dict) {
       if (kv.first->k != K::Str) fail(PLATO_INGEST_EUNSUPPORTED, "non-string key");
