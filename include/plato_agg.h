@@ -421,12 +421,16 @@ int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const 
  * device pointers each (arenas of n_f32 fp32 elements / the int64 counters).
  * d_flat_out: null, or n_vectors 16-byte aligned rows of >= n_flat floats that
  * receive the flattened vectors (what plato_agg_torch_cosine_sum then reads).
+ * d_lengths: null, or n_vectors lengths <= n_flat, vector v taking only its
+ * first d_lengths[v] positions (FedAtt's per-(entry, client) norms,
+ * fedatt_algorithm.py:34-39: one fp32 entry of one client per vector, the
+ * pointers offset to the entry and one segment covering it).
  */
 #define PLATO_AGG_PORT_CAST_FIRST 1
 int plato_agg_port_norms(const void* const* d_x_f32, const void* const* d_x_i64, const void* const* d_b_f32,
-                         const void* const* d_b_i64, int n_vectors, const plato_agg_segment* d_segs, uint32_t n_segs,
-                         size_t n_flat, size_t n_f32, int flags, float* d_out, float* const* d_flat_out,
-                         hipStream_t stream);
+                         const void* const* d_b_i64, int n_vectors, const uint32_t* d_lengths,
+                         const plato_agg_segment* d_segs, uint32_t n_segs, size_t n_flat, size_t n_f32, int flags,
+                         float* d_out, float* const* d_flat_out, hipStream_t stream);
 
 /*
  * The sum in Port's F.cosine_similarity(a, b_k, dim=0) (port_server.py:50),

@@ -147,8 +147,8 @@ int plato_agg_tune_np_sumsq(int variant, const float* const* d_x, int K, const f
 int plato_agg_tune_num_port_norms_variants(void);
 int plato_agg_tune_port_norms(int variant, const void* const* d_x_f32, const void* const* d_x_i64,
                               const void* const* d_b_f32, const void* const* d_b_i64, int n_vectors,
-                              const plato_agg_segment* d_segs, uint32_t n_segs, size_t n_flat, size_t n_f32, int flags,
-                              float* d_out, float* const* d_flat_out, hipStream_t stream);
+                              const uint32_t* d_lengths, const plato_agg_segment* d_segs, uint32_t n_segs, size_t n_flat,
+                              size_t n_f32, int flags, float* d_out, float* const* d_flat_out, hipStream_t stream);
 
 #ifdef __cplusplus
 }

@@ -128,8 +128,8 @@ SIGNATURES = {
          _c_size_t, _c_size_t, _c_float, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
     "plato_agg_port_norms": (
         _c_int,
-        [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, ctypes.c_uint32, _c_size_t, _c_size_t, _c_int,
-         _c_void_p, _c_void_p, _c_void_p]),
+        [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,
+         _c_size_t, _c_int, _c_void_p, _c_void_p, _c_void_p]),
     "plato_agg_torch_cosine_workspace": (_c_size_t, [_c_int, _c_int]),
     "plato_agg_torch_cosine_sum_scaled": (
         _c_int,
@@ -196,8 +196,8 @@ TUNE_SIGNATURES = {
          _c_void_p, _c_void_p]),
     "plato_agg_tune_port_norms": (
         _c_int,
-        [_c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, ctypes.c_uint32, _c_size_t, _c_size_t,
-         _c_int, _c_void_p, _c_void_p, _c_void_p]),
+        [_c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,
+         _c_size_t, _c_int, _c_void_p, _c_void_p, _c_void_p]),
     "plato_agg_tune_fedadp_dots": (
         _c_int,
         [_c_int, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,

@@ -67,6 +67,7 @@ struct PnArgs {
   int cast_first;            // vector 0 subtracts its int64 entries as torch.cat(...) - torch.cat(...)
   float* out;                // [V]
   float* const* flat;        // [V] rows for the flattened vectors (16-byte aligned), or null
+  const uint32_t* lengths;   // [V] per-vector lengths (<= n), or null: every vector n long
 };
 
 // ATen's scalar tail of the last-dim 2-norm as x86-64 PyTorch 2.10 compiled it (entrywise.hip,
@@ -170,8 +171,13 @@ __device__ __forceinline__ void pn_write(const PnArgs& a, const PnSeg* S, float*
 }
 
 template <int kWp, int kD, bool kNT = false>
-__global__ __launch_bounds__(64 * (1 + kWp)) void port_norms_kernel(PnArgs a) {
+__global__ __launch_bounds__(64 * (1 + kWp)) void port_norms_kernel(PnArgs a_in) {
   constexpr int kIt = kIts / kWp;
+  PnArgs a = a_in;
+  if (a.lengths) {  // this vector's own length (FedAtt: one entry of one client)
+    a.n = a.lengths[blockIdx.x];
+    a.m = a.n - a.n % kLanes;
+  }
   static_assert(kIts % kWp == 0, "whole gather iterations per producer");
   __shared__ __attribute__((aligned(16))) float ring[2 * kSlot];
   __shared__ PnSeg S[kMaxSegs];
@@ -280,8 +286,8 @@ constexpr int kNumPnVariants = sizeof(kPnVariants) / sizeof(kPnVariants[0]);
 #endif
 
 int run_port_norms(PnFn fn, const void* const* d_x_f32, const void* const* d_x_i64, const void* const* d_b_f32,
-                   const void* const* d_b_i64, int n_vectors, const plato_agg_segment* d_segs, uint32_t n_segs,
-                   size_t n_flat, size_t n_f32, int flags, float* d_out, float* const* d_flat_out,
+                   const void* const* d_b_i64, int n_vectors, const uint32_t* d_lengths, const plato_agg_segment* d_segs,
+                   uint32_t n_segs, size_t n_flat, size_t n_f32, int flags, float* d_out, float* const* d_flat_out,
                    hipStream_t stream) {
   if (n_vectors <= 0) return set_error(PLATO_AGG_EINVAL, "n_vectors must be >= 1");
   if (!d_x_f32 || !d_x_i64 || !d_b_f32 || !d_b_i64 || !d_segs || !d_out) return set_error(PLATO_AGG_EINVAL, "null pointer");
@@ -302,6 +308,7 @@ int run_port_norms(PnFn fn, const void* const* d_x_f32, const void* const* d_x_i
   a.cast_first = (flags & PLATO_AGG_PORT_CAST_FIRST) ? 1 : 0;
   a.out = d_out;
   a.flat = d_flat_out;
+  a.lengths = d_lengths;
   fn(a, stream, n_vectors);
   hipError_t err = hipGetLastError();
   if (err != hipSuccess) return set_error(PLATO_AGG_EHIP, std::string("port_norms launch: ") + hipGetErrorString(err));
@@ -313,11 +320,11 @@ int run_port_norms(PnFn fn, const void* const* d_x_f32, const void* const* d_x_i
 extern "C" {
 
 int plato_agg_port_norms(const void* const* d_x_f32, const void* const* d_x_i64, const void* const* d_b_f32,
-                         const void* const* d_b_i64, int n_vectors, const plato_agg_segment* d_segs, uint32_t n_segs,
-                         size_t n_flat, size_t n_f32, int flags, float* d_out, float* const* d_flat_out,
-                         hipStream_t stream) {
-  return run_port_norms(kPnDefault, d_x_f32, d_x_i64, d_b_f32, d_b_i64, n_vectors, d_segs, n_segs, n_flat, n_f32, flags,
-                        d_out, d_flat_out, stream);
+                         const void* const* d_b_i64, int n_vectors, const uint32_t* d_lengths,
+                         const plato_agg_segment* d_segs, uint32_t n_segs, size_t n_flat, size_t n_f32, int flags,
+                         float* d_out, float* const* d_flat_out, hipStream_t stream) {
+  return run_port_norms(kPnDefault, d_x_f32, d_x_i64, d_b_f32, d_b_i64, n_vectors, d_lengths, d_segs, n_segs, n_flat,
+                        n_f32, flags, d_out, d_flat_out, stream);
 }
 
 #ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
@@ -325,11 +332,11 @@ int plato_agg_tune_num_port_norms_variants(void) { return kNumPnVariants; }
 
 int plato_agg_tune_port_norms(int variant, const void* const* d_x_f32, const void* const* d_x_i64,
                               const void* const* d_b_f32, const void* const* d_b_i64, int n_vectors,
-                              const plato_agg_segment* d_segs, uint32_t n_segs, size_t n_flat, size_t n_f32, int flags,
-                              float* d_out, float* const* d_flat_out, hipStream_t stream) {
+                              const uint32_t* d_lengths, const plato_agg_segment* d_segs, uint32_t n_segs, size_t n_flat,
+                              size_t n_f32, int flags, float* d_out, float* const* d_flat_out, hipStream_t stream) {
   if (variant < 0 || variant >= kNumPnVariants) return set_error(PLATO_AGG_EINVAL, "bad port_norms variant");
-  return run_port_norms(kPnVariants[variant], d_x_f32, d_x_i64, d_b_f32, d_b_i64, n_vectors, d_segs, n_segs, n_flat,
-                        n_f32, flags, d_out, d_flat_out, stream);
+  return run_port_norms(kPnVariants[variant], d_x_f32, d_x_i64, d_b_f32, d_b_i64, n_vectors, d_lengths, d_segs, n_segs,
+                        n_flat, n_f32, flags, d_out, d_flat_out, stream);
 }
 #endif  // PLATO_AGG_TUNE
 

@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--fedadp-cycles", type=int, default=None, metavar="VARIANT",
                     help="run a cycle-count probe variant of plato_agg_tune_fedadp_dots and summarise its workspace")
     ap.add_argument("--port-only", action="store_true", help="only the port path (for kernel traces)")
+    ap.add_argument("--only", default=None, help="comma-separated paths to time")
+    ap.add_argument("--norms-threshold", type=int, default=-1,
+                    help="FedAvgEngine.norms_long_threshold for the fedatt path (0 = None; -1 = the default)")
     ap.add_argument("--polaris-variants", action="store_true",
                     help="HIP-event time of every plato_agg_tune_np_sumsq variant (bitwise vs the default)")
     ap.add_argument("--port-gathered", action="store_true",
@@ -67,6 +70,8 @@ def main():
     k = args.clients
     layout = ArenaLayout.from_shapes(workloads.resnet(18, 10))
     engine = FedAvgEngine(dev)
+    if args.norms_threshold >= 0:
+        engine.norms_long_threshold = args.norms_threshold or None
     base = DeviceArena(layout, dev)
     fill_baseline(base, 0)
     n_f, n_i = layout.n_f32, layout.n_i64
@@ -125,6 +130,8 @@ def main():
             break
         if args.port_only and not name.startswith("port"):
             continue
+        if args.only and name not in args.only.split(","):
+            continue
         fn()
         torch.cuda.synchronize(dev)
         ts = []
@@ -134,7 +141,8 @@ def main():
             torch.cuda.synchronize(dev)
             ts.append(time.perf_counter() - t0)
         med = statistics.median(ts) * 1e3
-        print(json.dumps({"path": name, "clients": k, "ms_median": round(med, 3), "ms_min": round(min(ts) * 1e3, 3),
+        print(json.dumps({"path": name, "clients": k, "norms_long_threshold": engine.norms_long_threshold,
+                          "ms_median": round(med, 3), "ms_min": round(min(ts) * 1e3, 3),
                           "min_bytes": int(nbytes), "GBps_of_min_bytes": round(nbytes / (med * 1e-3) / 1e9, 1),
                           "serial_chain_steps": int(chain), "what": what}), flush=True)
     if args.fedadp_kernel:
@@ -272,7 +280,7 @@ def port_gathered(dev, rnd, slots, layout, previous, reps):
     for v, store in [(v, st) for v in range(_lib.tune().plato_agg_tune_num_port_norms_variants()) for st in (False, True)]:
         def fn():
             _lib.tune_call("plato_agg_tune_port_norms", v, v8, v8 + 8 * (k + 1), v8 + 16 * (k + 1), v8 + 24 * (k + 1),
-                           k + 1, segs.data_ptr(), len(layout.entries), n_flat, layout.n_f32,
+                           k + 1, None, segs.data_ptr(), len(layout.entries), n_flat, layout.n_f32,
                            _lib.PLATO_AGG_PORT_CAST_FIRST, out.data_ptr(), v8 + 32 * (k + 1) if store else None, h)
         fn()
         torch.cuda.synchronize(dev)

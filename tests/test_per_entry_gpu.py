@@ -96,7 +96,12 @@ def test_entry_stats_match_oracle(engine, monkeypatch, cap):
     assert none_dv is None and none_vv is None and dd2.tobytes() == dd.tobytes()
 
 
-def test_entry_norms_follow_torch_cpu_order(engine):
+@pytest.mark.parametrize("long_threshold", [None, 1 << 17, 8, 1])
+def test_entry_norms_follow_torch_cpu_order(engine, monkeypatch, long_threshold):
+    """Every entry's norm in torch's CPU order, whichever kernel takes it: the long entries through
+    plato_agg_port_norms on the side stream (threshold 8 / 1: nearly every fp32 entry, ragged lengths,
+    n % 8 tails, unaligned arena offsets), the rest through plato_agg_entry_norms_f32."""
+    monkeypatch.setattr(engine, "norms_long_threshold", long_threshold)
     k = 7
     layout, rnd, bf, bi, xs_f, xs_i, _ = _random_round(engine, k, 5)
     got = rnd.entry_norms(range(k))
