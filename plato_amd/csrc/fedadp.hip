@@ -20,7 +20,8 @@
 //     the two chain groups of a pair run on one XCD, so x and b are served from its L2.
 //   * chain wave: lane = kind * 32 + chain, kind 0 = g . loc, kind 1 = loc . loc: ONE dependent
 //     fma per step per lane (the dots are split over lanes, not interleaved), 4 steps per
-//     ds_read_b128 of a transposed row (row pitch kS + 4 floats: conflict-free reads and writes).
+//     ds_read_b128 of a transposed row (row pitch kS + 16 floats, rows 4m .. 4m + 3 shifted by
+//     4m floats: conflict-free ds_read_b128 and ds_write_b32).
 //   * 8 producer waves, 2 gather iterations each per 128-block stage; their global loads run
 //     kD = 2 stages ahead of the tile being written (kD register sets), the tile ring has two
 //     slots, one s_barrier per stage.  A wave's current entry is cached in SGPRs: the segment
@@ -121,14 +122,19 @@ struct AdpShape {
   static_assert(kC % kV == 0, "a lane's positions lie in one 64-block");
   static_assert(kS * kC == 64 * kV * kW * kIt, "a stage is kW x kIt gather iterations of 64 * kV positions");
   static_assert(kS % 16 == 0, "the chain wave reads 16 steps per block");
-  static constexpr int kR = kS + 4;          // transposed row pitch (floats)
-  // kSw: the upper half of a vector's rows sits 32 floats further on, so that 4-position producer
-  // lanes (rows 4 (L mod kC/4) .. + 3) writing one column hit 64 different banks (a row pitch of
-  // 4 mod 64 alone puts rows r and r + 16 in one bank) while the chain's ds_read_b128 stay
-  // conflict-free
-  static constexpr int kGap = kSw ? 32 : 0;
+  // transposed row pitch (floats).  kSw = 2 (kC = 32, 4-position producer lanes): pitch kS + 16
+  // and rows 4m .. 4m + 3 shifted by 4m floats.  A ds_write_b32 half-wave (banks (a/4) mod 32) of
+  // the producers then writes rows 4m + j, m = 0..7, on 8 different 4-bank slots (4-way conflicted
+  // with pitch kS + 4: 268 M extra LDS cycles per launch, all of them these writes), and every
+  // 16-lane group of the chain's ds_read_b128 (banks mod 64) still covers 16 different slots.
+  static constexpr int kR = kSw == 2 ? kS + 16 : kS + 4;
+  static_assert(kSw != 2 || (kC == 32 && kS % 64 == 0), "swizzled rows: one chain wave of 32 chains");
+  // kSw = 1 (measured no better): the upper half of a vector's rows sits 32 floats further on
+  static constexpr int kGap = kSw == 1 ? 32 : kSw == 2 ? 4 * (kC / 4) : 0;
   static constexpr int kVR = kC * kR + kVRpad + kGap;  // rows of one vector (x, loc_0 .. loc_{kP-1})
-  __device__ static constexpr int row(int r) { return r * kR + (r >= kC / 2 ? kGap : 0); }
+  __device__ static constexpr int row(int r) {
+    return r * kR + (kSw == 2 ? 4 * (r >> 2) : (r >= kC / 2 ? kGap : 0));
+  }
   static constexpr int kSlot = (1 + kP) * kVR;
   static constexpr int kBlkPerIt = 64 * kV / kC;  // 64-blocks per gather iteration
   static constexpr int kLpB = kC / kV;             // lanes per 64-block in a gather iteration
@@ -800,8 +806,10 @@ using AdpFn = void (*)(const AdpArgs&, hipStream_t);
 // pairs x chains per workgroup, steps per stage, producer waves, iterations, vector pad
 // The product's shape (tuning variant 23): one pair and 32 of its 64 chains per workgroup, so a
 // gather reads whole 128-byte lines, 16 bytes per lane (x and b come once per pair, from L2);
-// 1.94 ms for 128 ResNet-18 clients against 5.4 ms for variant 0 (profiles/r03i_fedadp.log)
-constexpr AdpFn kAdpDefault = &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4>;
+// 1.94 ms for 128 ResNet-18 clients against 5.4 ms for variant 0 (profiles/r03i_fedadp.log); with
+// the swizzled rows (variant 51: no LDS bank conflicts, LDS-array cycles 450 M -> 181 M) 1.90 ms
+// (profiles/r03w_fedadp.log)
+constexpr AdpFn kAdpDefault = &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2>;
 #ifdef PLATO_AGG_TUNE
 const AdpFn kAdpVariants[] = {
     &launch_adp<8, 4, 256, 8, 2, 0>,     // 0: 16 B per block per vector, x and b shared by 8 pairs
@@ -855,10 +863,14 @@ const AdpFn kAdpVariants[] = {
     &launch_adp_flag<32, 128, 8, 2, 2, 2>,  // 48: variant 23 synchronised by LDS counters, 2 tile slots
     &launch_adp_flag<32, 128, 8, 2, 2, 3>,  // 49: the same, 3 tile slots
     &launch_adp_flag<32, 128, 8, 2, 3, 3>,  // 50: 3 tile slots, 3 stages of loads in flight
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2>,  // 51: variant 23 with swizzled rows (conflict-free writes)
+    &launch_adp<1, 32, 128, 8, 2, 0, 4, 0, 4, 2, 1, 3, 2>,  // 52: probe of 51: the chains alone (wrong results)
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 3, 1, 3, 2>,  // 53: variant 51, 3 stages of loads in flight
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 2, 3, 2>,  // 54: variant 51, chain reads 2 blocks ahead
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)
-constexpr int kAdpProbes[] = {6, 7, 8, 9, 10, 15, 16, 17, 18, 25, 29, 35, 36, 37};
+constexpr int kAdpProbes[] = {6, 7, 8, 9, 10, 15, 16, 17, 18, 25, 29, 35, 36, 37, 52};
 #endif
 
 int run_fedadp(AdpFn fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
