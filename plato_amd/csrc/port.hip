@@ -44,7 +44,7 @@ __device__ __forceinline__ T sld(const T* p, int i) {
 constexpr int kLanes = 8;                 // torch's 8-lane vectorised accumulation
 constexpr int kT = 2048;                  // positions per tile
 constexpr int kSteps = kT / kLanes;       // 256 steps per chain and tile
-constexpr int kR = kSteps + 8;            // row pitch: conflict-free writes (see pn_write) and reads
+constexpr int kR = kSteps + 4;            // row pitch: conflict-free writes (see pn_write) and reads
 constexpr int kSlot = kLanes * kR;        // one tile
 constexpr int kIts = kT / 256;            // gather iterations of 256 positions (4 per lane) per tile
 constexpr int kMaxSegs = 2048;
@@ -142,7 +142,10 @@ __device__ __forceinline__ void pn_issue(const PnArgs& a, const PnSeg* S, PnCurs
 }
 
 // Lane L holds positions p .. p + 3 (p = pf + 4L): chains 4 (L & 1) .. + 3, step (p - tile) / 8.
-// Row pitch kR = 264 (= 8 mod 64 banks): for each of the four writes the 64 lanes hit 64 banks.
+// Row pitch kR = 260: ds_write_b32 banks (a/4) mod 32 per 32-lane half, and rows 0 and 4 are
+// 4 kR = 16 mod 32 apart, so each write's half-wave covers 32 banks (pitch 264 put lanes L and L ^ 1
+// on one bank: 45 M extra LDS cycles per 129-vector launch, profiles/r03x_pmc_paths.txt); the chain
+// wave's ds_read_b128 of rows 0..7 (banks mod 64) sit on 8 different 16-byte slots.
 template <int kWp, int kIt, bool kNT>
 __device__ __forceinline__ void pn_write(const PnArgs& a, const PnSeg* S, float* slot, float* flat, uint32_t t, int w,
                                          int lane, int v, const PnRegs<kIt>& r) {
