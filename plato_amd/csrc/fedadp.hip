@@ -279,11 +279,13 @@ struct AdpRegs4 {
   uint32_t fast;       // bit i: iteration i lies in one fp32 entry (wave-uniform)
 };
 
+// kAux: the load's cache policy (2 = nt: a streaming read, kept out of the way of the re-read x and b)
+template <int kAux = 0>
 __device__ __forceinline__ f4v bload4(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
-  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, 0));
+  return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kAux));
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kNt = 0>
 __device__ __forceinline__ void adp_issue4(const AdpArgs& a, const AdpSeg* S, int n_segs, AdpCursor& cur,
                                            const AdpSrc<kP>& src, uint32_t t, int cg, int w, int lane,
                                            AdpRegs4<kP, kIt>& r) {
@@ -311,10 +313,11 @@ __device__ __forceinline__ void adp_issue4(const AdpArgs& a, const AdpSeg* S, in
     }
     r.code[i] = code;
     r.pos[i] = p;
-    r.x[i] = bload4(src.x, p * 4u);
-    r.b[i] = bload4(src.b, e * 4u);
+    // kNt: 1 = the client arenas (read once) as nt loads, 2 = every load nt
+    r.x[i] = bload4<kNt == 2 ? 2 : 0>(src.x, p * 4u);
+    r.b[i] = bload4<kNt == 2 ? 2 : 0>(src.b, e * 4u);
 #pragma unroll
-    for (int k = 0; k < kP; ++k) r.y[i][k] = bload4(src.y[k], e * 4u);
+    for (int k = 0; k < kP; ++k) r.y[i][k] = bload4<kNt ? 2 : 0>(src.y[k], e * 4u);
   }
 }
 
@@ -375,11 +378,11 @@ constexpr int adp_waves() { return kIso ? 12 : kW + 2; }
 template <int kP, int kIt, int kV>
 using AdpRegsV = std::conditional_t<kV == 4, AdpRegs4<kP, kIt>, AdpRegs<kP, kIt>>;
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe, int kV>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe, int kV, int kNt = 0>
 __device__ __forceinline__ void adp_issue_v(const AdpArgs& a, const AdpSeg* S, int n_segs, AdpCursor& cur,
                                             const AdpSrc<kP>& src, uint32_t t, int cg, int w, int lane,
                                             AdpRegsV<kP, kIt, kV>& r) {
-  if constexpr (kV == 4) adp_issue4<kP, kC, kS, kW, kIt, kVRpad>(a, S, n_segs, cur, src, t, cg, w, lane, r);
+  if constexpr (kV == 4) adp_issue4<kP, kC, kS, kW, kIt, kVRpad, kNt>(a, S, n_segs, cur, src, t, cg, w, lane, r);
   else adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cur, src, t, cg, w, lane, r);
 }
 
@@ -392,7 +395,7 @@ __device__ __forceinline__ void adp_write_v(const AdpArgs& a, const AdpSeg* S, i
 }
 
 template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
-          int kCP = 1, int kPrio = 3, int kSw = 0>
+          int kCP = 1, int kPrio = 3, int kSw = 0, int kNt = 0>
 __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kernel(AdpArgs a) {
   using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, kV, kSw>;
   static_assert(!kIso || kW <= 9, "kIso: at most 9 producer waves");
@@ -447,7 +450,7 @@ __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kern
     AdpRegsV<kP, kIt, kV> regs[kD];
 #pragma unroll
     for (int j = 0; j < kD; ++j)
-      adp_issue_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV>(a, S, n_segs, cursor, src, uint32_t(j), cg, w, lane, regs[j]);
+      adp_issue_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV, kNt>(a, S, n_segs, cursor, src, uint32_t(j), cg, w, lane, regs[j]);
     uint64_t t_start = 0, t_wait = 0, t_write = 0, c0 = 0;  // probe 6: cycle counts
     if (kProbe == 6) t_start = __builtin_readcyclecounter();
     // whole trips of kD stages (the last trip may run idle stages): no branch inside the loop, so the
@@ -462,7 +465,7 @@ __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kern
         // past the last stage (t = nst) every position clamps to the last block: valid addresses,
         // never consumed, and every trip issues the same loads
         const uint32_t nxt = t + j + kD;
-        adp_issue_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV>(a, S, n_segs, cursor, src, nxt < nst ? nxt : uint32_t(nst),
+        adp_issue_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV, kNt>(a, S, n_segs, cursor, src, nxt < nst ? nxt : uint32_t(nst),
                                                              cg, w, lane, regs[j]);
         if (kProbe == 6) c0 = __builtin_readcyclecounter();
         __builtin_amdgcn_s_barrier();  // stage t + j published in slot (t + j) & 1
@@ -499,6 +502,10 @@ __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kern
     const float* slot = ring + (t & 1) * Sh::kSlot;
     const float* A = slot + arow;
     const float* B = slot + brow;
+    if (kProbe == 7) {  // probe 7: the producers alone — one LDS read per stage keeps their stores live
+      acc += A[t & 15] * B[t & 15];
+      continue;
+    }
     const uint64_t left = nsteps - t * kS;
     typedef float f4 __attribute__((ext_vector_type(4)));
     if (left >= uint64_t(kS)) {
@@ -794,12 +801,12 @@ void launch_adp_flag(const AdpArgs& a, hipStream_t st) {
 }
 
 template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
-          int kCP = 1, int kPrio = 3, int kSw = 0>
+          int kCP = 1, int kPrio = 3, int kSw = 0, int kNt = 0>
 void launch_adp(const AdpArgs& a, hipStream_t st) {
   constexpr int kGroups = 64 / kC;
   uint32_t pgs = uint32_t((a.n_pairs + kP - 1) / kP);
   pgs = (pgs + 7) / 8 * 8;  // whole XCD rounds (padding workgroups return at once)
-  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe, kIso, kV, kD, kCP, kPrio, kSw>), dim3(pgs * kGroups),
+  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe, kIso, kV, kD, kCP, kPrio, kSw, kNt>), dim3(pgs * kGroups),
                      dim3((64 * adp_waves<kW, kIso>())), 0, st, a);
 }
 using AdpFn = void (*)(const AdpArgs&, hipStream_t);
@@ -867,10 +874,15 @@ const AdpFn kAdpVariants[] = {
     &launch_adp<1, 32, 128, 8, 2, 0, 4, 0, 4, 2, 1, 3, 2>,  // 52: probe of 51: the chains alone (wrong results)
     &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 3, 1, 3, 2>,  // 53: variant 51, 3 stages of loads in flight
     &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 2, 3, 2>,  // 54: variant 51, chain reads 2 blocks ahead
+    &launch_adp<1, 32, 128, 8, 2, 0, 7, 0, 4, 2, 1, 3, 2>,  // 55: probe of 51: the producers alone (wrong results)
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2, 1>,  // 56: variant 51, client arenas read nt
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2, 2>,  // 57: variant 51, every load nt
+    &launch_adp<1, 32, 128, 8, 2, 0, 7, 0, 4, 2, 1, 3, 2, 1>,  // 58: probe of 56: the producers alone (wrong results)
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 3, 1, 3, 2, 1>,  // 59: variant 56, 3 stages of loads in flight
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)
-constexpr int kAdpProbes[] = {6, 7, 8, 9, 10, 15, 16, 17, 18, 25, 29, 35, 36, 37, 52};
+constexpr int kAdpProbes[] = {6, 7, 8, 9, 10, 15, 16, 17, 18, 25, 29, 35, 36, 37, 52, 55, 58};
 #endif
 
 int run_fedadp(AdpFn fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
