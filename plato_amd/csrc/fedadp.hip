@@ -313,11 +313,11 @@ __device__ __forceinline__ void adp_issue4(const AdpArgs& a, const AdpSeg* S, in
     }
     r.code[i] = code;
     r.pos[i] = p;
-    // kNt: 1 = the client arenas (read once) as nt loads, 2 = every load nt
-    r.x[i] = bload4<kNt == 2 ? 2 : 0>(src.x, p * 4u);
-    r.b[i] = bload4<kNt == 2 ? 2 : 0>(src.b, e * 4u);
+    // kNt & 3: 1 = the client arenas (read once) as nt loads, 2 = every load nt
+    r.x[i] = bload4<(kNt & 3) == 2 ? 2 : 0>(src.x, p * 4u);
+    r.b[i] = bload4<(kNt & 3) == 2 ? 2 : 0>(src.b, e * 4u);
 #pragma unroll
-    for (int k = 0; k < kP; ++k) r.y[i][k] = bload4<kNt ? 2 : 0>(src.y[k], e * 4u);
+    for (int k = 0; k < kP; ++k) r.y[i][k] = bload4<(kNt & 3) ? 2 : 0>(src.y[k], e * 4u);
   }
 }
 
@@ -332,11 +332,18 @@ __device__ __forceinline__ float adp_value_at(const AdpArgs& a, const AdpSeg* S,
   return adp_f32(a.xf[pair][el], a.base_f[el], sg.info & kSegNeg, a.lr);
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kSw>
+// (-d) / lr, correctly rounded, as RN32(RN64(-d * RN64(1 / lr))) (kNt & 4): the float64 product is
+// within 2^-52 (relative) of the quotient, while a quotient of two floats that is not a float lies
+// at least 2^-49 (relative) from every midpoint of the float grid (and is never on one), so the one
+// rounding to float gives the float32 division's bits — 3 instructions instead of the division's ~10
+__device__ __forceinline__ float adp_div_lr_f64(float v, double inv_lr) { return float(double(v) * inv_lr); }
+
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kSw, int kNt = 0>
 __device__ __forceinline__ void adp_write4(const AdpArgs& a, const AdpSeg* S, int n_segs, float* slot, int pair0,
                                            int w, int lane, AdpRegs4<kP, kIt>& r) {
   using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, 4, kSw>;
   const float lr = a.lr;
+  const double inv_lr = (kNt & 4) ? 1.0 / double(lr) : 0.0;
 #pragma unroll
   for (int i = 0; i < kIt; ++i) {
     const int g = i * kW + w;
@@ -349,7 +356,10 @@ __device__ __forceinline__ void adp_write4(const AdpArgs& a, const AdpSeg* S, in
 #pragma unroll
         for (int k = 0; k < kP; ++k)
 #pragma unroll
-          for (int j = 0; j < 4; ++j) dst[(1 + k) * Sh::kVR + j * Sh::kR] = (-(r.y[i][k][j] - r.b[i][j])) / lr;
+          for (int j = 0; j < 4; ++j) {
+            const float nv = -(r.y[i][k][j] - r.b[i][j]);
+            dst[(1 + k) * Sh::kVR + j * Sh::kR] = (kNt & 4) ? adp_div_lr_f64(nv, inv_lr) : nv / lr;
+          }
       } else {
 #pragma unroll
         for (int k = 0; k < kP; ++k)
@@ -386,11 +396,11 @@ __device__ __forceinline__ void adp_issue_v(const AdpArgs& a, const AdpSeg* S, i
   else adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cur, src, t, cg, w, lane, r);
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe, int kV, int kSw>
+template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe, int kV, int kSw, int kNt = 0>
 __device__ __forceinline__ void adp_write_v(const AdpArgs& a, const AdpSeg* S, int n_segs, float* slot, int pair0,
                                             int w, int lane, AdpRegsV<kP, kIt, kV>& r) {
   static_assert(!kSw || kV == 4, "the row gap is laid out for 4-position producer lanes");
-  if constexpr (kV == 4) adp_write4<kP, kC, kS, kW, kIt, kVRpad, kSw>(a, S, n_segs, slot, pair0, w, lane, r);
+  if constexpr (kV == 4) adp_write4<kP, kC, kS, kW, kIt, kVRpad, kSw, kNt>(a, S, n_segs, slot, pair0, w, lane, r);
   else adp_write<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, slot, pair0, w, lane, r);
 }
 
@@ -459,7 +469,7 @@ __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kern
 #pragma unroll
       for (int j = 0; j < kD; ++j) {
         if (kProbe == 6) c0 = __builtin_readcyclecounter();
-        adp_write_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV, kSw>(a, S, n_segs, ring + ((t + j) & 1) * Sh::kSlot, pair0, w,
+        adp_write_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV, kSw, kNt>(a, S, n_segs, ring + ((t + j) & 1) * Sh::kSlot, pair0, w,
                                                              lane, regs[j]);
         if (kProbe == 6) t_write += __builtin_readcyclecounter() - c0;
         // past the last stage (t = nst) every position clamps to the last block: valid addresses,
@@ -879,10 +889,13 @@ const AdpFn kAdpVariants[] = {
     &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2, 2>,  // 57: variant 51, every load nt
     &launch_adp<1, 32, 128, 8, 2, 0, 7, 0, 4, 2, 1, 3, 2, 1>,  // 58: probe of 56: the producers alone (wrong results)
     &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 3, 1, 3, 2, 1>,  // 59: variant 56, 3 stages of loads in flight
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2, 4>,  // 60: variant 51, division as a float64 product
+    &launch_adp<1, 32, 128, 8, 2, 0, 7, 0, 4, 2, 1, 3, 2, 4>,  // 61: probe of 60: the producers alone (wrong results)
+    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2, 5>,  // 62: variant 60, client arenas read nt
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)
-constexpr int kAdpProbes[] = {6, 7, 8, 9, 10, 15, 16, 17, 18, 25, 29, 35, 36, 37, 52, 55, 58};
+constexpr int kAdpProbes[] = {6, 7, 8, 9, 10, 15, 16, 17, 18, 25, 29, 35, 36, 37, 52, 55, 58, 61};
 #endif
 
 int run_fedadp(AdpFn fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
