@@ -60,6 +60,9 @@ def parse():
     p.add_argument("--pieces", type=int, default=4,
                    help="strong scaling, N>1: each rank's bucket in this many pieces, the all-gather of "
                         "piece p running on RCCL's stream while the kernels of the later pieces run")
+    p.add_argument("--no-variants", action="store_true",
+                   help="skip the variant servers' reductions leg (SURVEY.md §8(f), N=1 only)")
+    p.add_argument("--variant-reps", type=int, default=5)
     p.add_argument("--engine-devices", type=int, default=0,
                    help="single-process multi-GPU engine (plato_amd.multi) over this many devices: host-inclusive "
                         "and device-resident timings of the server's own path (repeats cuda:0 on a 1-GPU box)")
@@ -552,6 +555,10 @@ def main():
     if rank == 0 and world == 1 and args.streaming:
         result["streaming"] = streaming(engine, layout, base, slab, k, weights, dev)
 
+    if rank == 0 and world == 1 and not args.no_variants and args.config == "C2" and args.codec == "native":
+        progress("variant reductions leg")
+        result["variants"] = variant_legs(dev, k, args.variant_reps)
+
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         progress("cpu baseline leg")
         result["cpu_baseline"] = cpu_baseline(layout, base, slab, k, weights, out_f, out_i, args.cpu_reps,
@@ -564,6 +571,156 @@ def main():
         import torch.distributed as dist
 
         dist.destroy_process_group()
+
+
+CHAIN_CYCLES = 6.0   # one dependent v_fma_f32 step on MI355X (scripts/micro/fma_chain.hip)
+CLOCK_HZ = 2.4e9
+
+
+def variant_legs(dev, k: int, reps: int) -> dict:
+    """The variant servers' whole-model reductions on the headline's inputs.
+
+    K synthetic ResNet-18 clients in HBM, after the headline's timed region.  Per path: the
+    HIP-event time of its kernels as the engine launches them (``AggregationRound.timings``), the
+    wall time of the engine call (host sync and small D2H included), the kernels' algorithmic bytes
+    and floor — the larger of those bytes at the HBM peak and, where the reference's float32 order
+    is one serial fma chain per vector, that chain at CHAIN_CYCLES per step — and floor / kernel.
+    FedAdp runs on arenas aligned to its flattened positions, as FedAdpServerMixin's rounds do.
+    """
+    from plato_amd import _lib
+    from plato_amd.arena import F32, ArenaLayout
+    from plato_amd.engine import ClientSlab, DeviceArena, FedAvgEngine, _ptr
+    from plato_amd.synthetic import fill_baseline, fill_clients
+
+    spec = model_spec("resnet18")
+    slots = list(range(k))
+
+    def make_round(align):
+        lay = ArenaLayout.from_shapes(spec, align=align)
+        base = DeviceArena(lay, dev)
+        fill_baseline(base, 0)
+        baseline = lay.unpack(base.f32.cpu(), base.i64.cpu())
+        eng = FedAvgEngine(dev)
+        eng.layout_align = align
+        rnd = eng.begin(baseline, k)
+        rnd.put_baseline(baseline)
+        torch.cuda.synchronize(dev)
+        fill_clients(rnd.slab, eng._base, 0, k)
+        for s in range(k):
+            pf, pi = rnd.slab.row_pointers([s])
+            rnd._pf[s], rnd._pi[s] = int(pf[0]), int(pi[0])
+            rnd.staged[s] = True
+        torch.cuda.synchronize(dev)
+        return lay, base, rnd
+
+    def measure(fn, rnd, keys):
+        fn()
+        torch.cuda.synchronize(dev)
+        walls, kernel = [], {key: [] for key in keys}
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize(dev)
+            walls.append((time.perf_counter() - t0) * 1e3)
+            for key in keys:
+                kernel[key].append(rnd.timings[key + "_ms"])
+        return statistics.median(walls), {key: statistics.median(v) for key, v in kernel.items()}
+
+    def entry(kernel_ms, nbytes, chain_steps=0):
+        floor = max(nbytes / (HBM_PEAK_GBS * 1e9) * 1e3, chain_steps * CHAIN_CYCLES / CLOCK_HZ * 1e3)
+        return {"kernel_ms": round(kernel_ms, 4), "algorithmic_bytes": int(nbytes),
+                "GBps": round(nbytes / (kernel_ms * 1e-3) / 1e9, 1), "serial_chain_steps": int(chain_steps),
+                "floor_ms": round(floor, 4), "frac_of_floor": round(floor / kernel_ms, 4)}
+
+    out = {"clients": k, "model": "resnet18", "reps": reps,
+           "note": "HIP events around each engine launch (AggregationRound.timings); outside the headline's timed "
+                   "region; floor = max(algorithmic bytes at 8 TB/s, serial fma chain at 6 cycles/step, 2.4 GHz)"}
+    lay, base, rnd = make_round(None)
+    n_f, n_i = lay.n_f32_data, lay.n_i64
+    model_bytes = n_f * 4 + n_i * 8
+    n_flat = n_f + n_i
+    longest = max(e.numel for e in lay.entries if e.region == F32)
+
+    # FedAdp: global gradient (entrywise pass) + the fused gather/sdot kernel, aligned arenas
+    lay_a, _, rnd_a = make_round("fedadp")
+    w1 = np.full((len(lay_a.entries), k), 1.0 / k)
+
+    def fedadp():
+        grads = rnd_a.launch_entrywise(w1, add_base=False, device=True)
+        rnd_a.fedadp_dots(grads, slots, 0.01)
+
+    wall, km = measure(fedadp, rnd_a, ["fedadp_dots"])
+    out["fedadp"] = dict(entry(km["fedadp_dots"], k * model_bytes + 3 * n_flat * 4, n_flat // 64),
+                         path_ms=round(wall, 3), kernel="plato_agg_fedadp_dots (prep + dots + finish)",
+                         reference="examples/server_aggregation/fedadp/fedadp_server.py:91-99")
+    del rnd_a
+    torch.cuda.empty_cache()
+
+    # Port: norms gathered from the arenas (8 torch-order chains per vector) + cosine sums
+    prev = DeviceArena(lay, dev)
+    fill_baseline(prev, 1)
+    previous = lay.unpack(prev.f32.cpu(), prev.i64.cpu())
+    del prev
+    prev_arena = rnd.stage_reference(previous)
+    wall, km = measure(lambda: rnd.model_similarities(prev_arena, slots), rnd, ["port_norms", "port_cosine"])
+    out["port_norms"] = dict(entry(km["port_norms"], (k + 2) * model_bytes + (k + 1) * n_flat * 4, n_flat // 8),
+                             path_ms=round(wall, 3), kernel="plato_agg_port_norms",
+                             reference="examples/async/port/port_server.py:38-50")
+    out["port_cosine"] = dict(entry(km["port_cosine"], (k + 1) * n_flat * 4), kernel="plato_agg_scale_by_norm + "
+                              "plato_agg_torch_cosine_sum_scaled", reference="examples/async/port/port_server.py:50")
+    torch.cuda.empty_cache()
+
+    # FedAtt: per-(entry, client) torch norms; Polaris: numpy pairwise squared sums per entry
+    wall, km = measure(lambda: rnd.entry_norms(slots), rnd, ["entry_norms"])
+    out["fedatt_norms"] = dict(entry(km["entry_norms"], (k + 1) * n_f * 4, longest // 8), path_ms=round(wall, 3),
+                               kernel="plato_agg_entry_norms_f32",
+                               reference="examples/server_aggregation/fedatt/fedatt_algorithm.py:34-39")
+    wall, km = measure(lambda: rnd.np_sumsq(slots), rnd, ["np_sumsq"])
+    out["polaris_sumsq"] = dict(entry(km["np_sumsq"], (k + 1) * n_f * 4), path_ms=round(wall, 3),
+                                kernel="plato_agg_np_sumsq",
+                                reference="examples/client_selection/polaris/polaris_server.py:78-81")
+
+    # QSGD-coded FedAvg: one code byte per element through HBM, decoded in the kernel
+    qslab = ClientSlab(lay, k, dev, codec="qsgd")
+    g = torch.Generator(device=dev).manual_seed(1)
+    for r in range(k):  # what the client quantizer makes of normal deltas at level 64
+        shape = qslab.f32[r].shape
+        mag = torch.floor(torch.randn(shape, device=dev, generator=g).abs() * (63 / 5)
+                          + torch.rand(shape, device=dev, generator=g)).clamp_(0, 127)
+        sign = (torch.rand(shape, device=dev, generator=g) < 0.5).to(torch.float32) * 128
+        qslab.f32[r].copy_((mag + sign).to(torch.uint8))
+    qslab.i64.fill_(3)
+    qpf, qpi = qslab.row_pointers(range(k))
+    qtf, qti = torch.from_numpy(qpf).to(dev), torch.from_numpy(qpi).to(dev)
+    n_e = len(lay.entries)
+    max_v = torch.rand((n_e, k), device=dev, generator=g) * 0.1 + 0.01
+    w = torch.full((k,), 1.0 / k, device=dev)
+    cf, ci = rnd.engine._chunks(lay, rnd.engine.QSGD_CHUNK)
+    out_f = torch.empty(lay.row_f32, device=dev)
+    out_i = torch.empty(lay.row_i64, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def qsgd():
+        _lib.call("plato_agg_fedavg_qsgd", _ptr(qtf), _ptr(qti), k, _ptr(max_v), n_e, 63.0, _ptr(w), None,
+                  _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(out_f),
+                  _ptr(out_i), lay.n_f32, n_i, stream.cuda_stream)
+
+    qsgd()
+    torch.cuda.synchronize(dev)
+    ts = []
+    for _ in range(max(reps, 10)):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        qsgd()
+        e1.record(stream)
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1))
+    out["qsgd_fedavg"] = dict(entry(statistics.median(ts), k * n_flat + 2 * model_bytes),
+                              kernel="plato_agg_fedavg_qsgd",
+                              reference="plato/processors/model_dequantize_qsgd.py:34-60 + servers/fedavg.py:137-159")
+    del qslab, rnd
+    torch.cuda.empty_cache()
+    return out
 
 
 def engine_devices_bench(args):

@@ -76,7 +76,7 @@
 extern "C" {
 #endif
 
-#define PLATO_AGG_ABI_VERSION 2
+#define PLATO_AGG_ABI_VERSION 3
 
 #define PLATO_AGG_OK 0
 #define PLATO_AGG_EINVAL (-1)   /* bad argument (null, misaligned, K <= 0) */
@@ -398,11 +398,15 @@ int plato_agg_sdot_shared(const float* d_x, const float* const* d_y, int n_pairs
  * (examples/server_aggregation/fedadp/fedadp_server.py:91-99, 122-133).  d_x is
  * the flattened global gradient (plato_agg_flatten RAW, 16-byte aligned, at
  * least n_flat rounded up to 64 floats); with_xx = 1 also writes x . x to
- * d_out_xy[n_pairs] and d_out_yy[n_pairs].  Segments: 1..2048, n_flat < 2^32;
- * n_f32 / n_i64 = lengths of the arenas' fp32 (< 2^30) and int64 regions.
- * d_workspace: plato_agg_fedadp_dots_workspace(n_pairs, with_xx, n_i64) bytes.
+ * d_out_xy[n_pairs] and d_out_yy[n_pairs].  Segments: 1 .. 2^22 - 1 (ABI 3: no
+ * longer capped at 2048 entries), n_flat < 2^30, n_pairs <= 65535; n_f32 / n_i64 =
+ * lengths of the arenas' fp32 (< 2^30) and int64 regions.  d_workspace (256-byte
+ * aligned): plato_agg_fedadp_dots_workspace(n_pairs, with_xx, n_i64, n_flat,
+ * n_segs) bytes — chain sums, per-group descriptors, the finished values of
+ * the groups that cross an entry boundary and the chain-group-major copy of x
+ * and the flattened baseline the kernel streams.
  */
-size_t plato_agg_fedadp_dots_workspace(int n_pairs, int with_xx, size_t n_i64);
+size_t plato_agg_fedadp_dots_workspace(int n_pairs, int with_xx, size_t n_i64, size_t n_flat, uint32_t n_segs);
 int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
                           const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
                           uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,

@@ -14,7 +14,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libplato_agg.so")
 TUNE_LIB_PATH = os.path.join(_HERE, "libplato_agg_tune.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 PLATO_AGG_OK = 0
 PLATO_AGG_EINVAL = -1
@@ -121,7 +121,7 @@ SIGNATURES = {
     "plato_agg_sdot_shared_workspace": (_c_size_t, [_c_int, _c_int]),
     "plato_agg_sdot_shared": (
         _c_int, [_c_void_p, _c_void_p, _c_int, _c_size_t, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
-    "plato_agg_fedadp_dots_workspace": (_c_size_t, [_c_int, _c_int, _c_size_t]),
+    "plato_agg_fedadp_dots_workspace": (_c_size_t, [_c_int, _c_int, _c_size_t, _c_size_t, ctypes.c_uint32]),
     "plato_agg_fedadp_dots": (
         _c_int,
         [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,

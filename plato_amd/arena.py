@@ -62,55 +62,106 @@ class Entry:
     shape: tuple
 
 
+# Arena alignments (``ArenaLayout.align``).  None: fp32 entries back to back.  "fedadp": every fp32
+# entry starts at an arena offset congruent, mod FEDADP_ALIGN elements, to its position in FedAdp's
+# flattened vector (process_grad: entries sorted by name.lower(), int64 counters one position per
+# element; examples/server_aggregation/fedadp/fedadp_server.py:122-133), so the dot kernel's
+# 16-byte gathers of a client arena start on whole 128-byte lines (csrc/fedadp.hip; an entry whose
+# arena offset and flat position differ mod 4 costs ~15 % of the kernel's time).
+# The padding (< FEDADP_ALIGN floats per entry) is never read as model data.
+ALIGNMENTS = (None, "fedadp")
+FEDADP_ALIGN = 32
+
+
+def fedadp_order(names) -> list[int]:
+    """Entry indices in FedAdp's flattening order (sorted by ``name.lower()``, stable)."""
+    return sorted(range(len(names)), key=lambda i: names[i].lower())
+
+
 class ArenaLayout:
     """Key -> region offsets for one model's ``state_dict``."""
 
-    def __init__(self, entries: list[Entry], n_f32: int, n_i64: int):
+    def __init__(self, entries: list[Entry], n_f32: int, n_i64: int, align: str | None = None):
+        if align not in ALIGNMENTS:
+            raise ValueError(f"unknown arena alignment {align!r}")
         self.entries = entries
-        self.n_f32 = n_f32
+        self.n_f32 = n_f32  # fp32 region length, padding included
         self.n_i64 = n_i64
+        self.align = align
+        # model elements of the fp32 region (algorithmic bytes count these, not the padding)
+        self.n_f32_data = sum(e.numel for e in entries if e.region == F32)
         self.row_f32 = _round_up(max(n_f32, 1), ROW_ALIGN)
         self.row_i64 = max(n_i64, 1)
         self._by_name = {e.name: e for e in entries}
-        self.signature = tuple((e.name, e.region, e.shape) for e in entries)
+        self.signature = tuple((e.name, e.region, e.shape) for e in entries) + ((("align", align),) if align else ())
         self._cache: dict = {}
+
+    @property
+    def packed(self) -> bool:
+        """fp32 entries back to back (no alignment padding)."""
+        return self.n_f32 == self.n_f32_data
 
     # ------------------------------------------------------------------ build
     @classmethod
-    def from_state_dict(cls, state_dict: Mapping[str, torch.Tensor]) -> "ArenaLayout":
+    def _build(cls, items, align: str | None) -> "ArenaLayout":
+        """``items``: [(name, region, numel, shape)] in state_dict order."""
+        if align not in ALIGNMENTS:
+            raise ValueError(f"unknown arena alignment {align!r}")
+        flat_at = None
+        if align == "fedadp":
+            flat_at, flat = {}, 0
+            for i in fedadp_order([it[0] for it in items]):
+                flat_at[i] = flat
+                flat += items[i][2]
         entries = []
-        n_f32 = 0
-        n_i64 = 0
+        n = {F32: 0, I64: 0}
+        for i, (name, region, numel, shape) in enumerate(items):
+            off = n[region]
+            if region == F32 and flat_at is not None:
+                off += (flat_at[i] - off) % FEDADP_ALIGN
+            entries.append(Entry(name, region, off, numel, shape))
+            n[region] = off + numel
+        return cls(entries, n[F32], n[I64], align)
+
+    @classmethod
+    def from_state_dict(cls, state_dict: Mapping[str, torch.Tensor], align: str | None = None) -> "ArenaLayout":
+        items = []
         for name, tensor in state_dict.items():
             if not isinstance(tensor, torch.Tensor):
                 raise TypeError(f"state_dict entry {name!r} is not a tensor")
-            numel = tensor.numel()
-            shape = tuple(tensor.shape)
             if tensor.dtype == torch.float32:
-                entries.append(Entry(name, F32, n_f32, numel, shape))
-                n_f32 += numel
+                region = F32
             elif tensor.dtype == torch.int64:
-                entries.append(Entry(name, I64, n_i64, numel, shape))
-                n_i64 += numel
+                region = I64
             else:
                 raise TypeError(
                     f"state_dict entry {name!r} has dtype {tensor.dtype}; the aggregation "
                     "engine handles torch.float32 and torch.int64 entries"
                 )
-        return cls(entries, n_f32, n_i64)
+            items.append((name, region, tensor.numel(), tuple(tensor.shape)))
+        return cls._build(items, align)
 
     @classmethod
-    def from_shapes(cls, spec) -> "ArenaLayout":
+    def from_shapes(cls, spec, align: str | None = None) -> "ArenaLayout":
         """Build from ``[(name, shape, 'f32'|'i64'), ...]`` (synthetic workloads)."""
-        entries = []
-        n = {F32: 0, I64: 0}
+        items = []
         for name, shape, region in spec:
             numel = 1
             for dim in shape:
                 numel *= int(dim)
-            entries.append(Entry(name, region, n[region], numel, tuple(shape)))
-            n[region] += numel
-        return cls(entries, n[F32], n[I64])
+            items.append((name, region, numel, tuple(shape)))
+        return cls._build(items, align)
+
+    def aligned(self, align: str | None) -> "ArenaLayout":
+        """The same entries under another alignment (self if it already has it)."""
+        if align == self.align:
+            return self
+        key = ("aligned", align)
+        hit = self._cache.get(key)
+        if hit is None:
+            hit = self._cache[key] = ArenaLayout._build([(e.name, e.region, e.numel, e.shape) for e in self.entries],
+                                                        align)
+        return hit
 
     # ---------------------------------------------------------------- queries
     def __len__(self) -> int:
@@ -125,9 +176,10 @@ class ArenaLayout:
     def algorithmic_bytes(self, k: int) -> int:
         """HBM bytes of one fused FedAvg launch: read K clients + baseline, write result.
 
-        SURVEY.md §8(d): (K+2)·P_f32·4 + (K+2)·P_i64·8.
+        SURVEY.md §8(d): (K+2)·P_f32·4 + (K+2)·P_i64·8 over the model's elements (alignment
+        padding, which the kernels also stream, is not counted).
         """
-        return (k + 2) * (self.n_f32 * 4 + self.n_i64 * 8)
+        return (k + 2) * (self.n_f32_data * 4 + self.n_i64 * 8)
 
     def check_compatible(self, state_dict: Mapping[str, torch.Tensor], what: str,
                          codec: str = "native") -> None:
@@ -192,7 +244,7 @@ class ArenaLayout:
         if hit is None:
             entries = [e if e.region == F32 else Entry(e.name, F32, self.row_f32 + e.offset, e.numel, e.shape)
                        for e in self.entries]
-            hit = ArenaLayout(entries, self.row_f32 + self.n_i64 if self.n_i64 else self.n_f32, 0)
+            hit = ArenaLayout(entries, self.row_f32 + self.n_i64 if self.n_i64 else self.n_f32, 0, self.align)
             self._cache["promoted"] = hit
         return hit
 
@@ -202,8 +254,12 @@ class ArenaLayout:
         """Copy ``state_dict`` into flat (host or device) buffers ``out_f32``/``out_i64``."""
         f32 = [state_dict[e.name].reshape(-1) for e in self.entries if e.region == F32]
         i64 = [state_dict[e.name].reshape(-1) for e in self.entries if e.region == I64]
-        if f32:
+        if f32 and self.packed:
             torch.cat(f32, out=out_f32[: self.n_f32])
+        elif f32:
+            for e in self.entries:
+                if e.region == F32:
+                    out_f32[e.offset:e.offset + e.numel].copy_(state_dict[e.name].reshape(-1))
         if i64:
             torch.cat(i64, out=out_i64[: self.n_i64])
 

@@ -8,33 +8,40 @@
 // sdot_k_SKYLAKEX, 64 fma chains (chain j sums positions = j mod 64, serially over the
 // 64-element blocks), a fold, one 32-element block, a fixed horizontal sum and a float64 tail.
 //
-// plato_agg_flatten + plato_agg_sdot_shared (flat.hip) materialise the K flattened deltas
-// (5.7 GB for 128 ResNet-18 clients written and read again).  Here the flattening is folded
-// into the dot kernel: producer waves gather positions from the staged arenas through the
-// segment map, form loc = (x - b) or -(x - b) / lr in registers and write them transposed
-// into an LDS tile; chain waves only run the fma chains out of LDS.
+// The flattening is folded into the dot kernel: producer waves gather positions from the staged
+// client arenas, form loc = (y - b) or -(y - b) / lr in registers and write them transposed into
+// an LDS tile; a chain wave only runs the fma chains out of LDS.
 //
-// Shape (the product default, kAdpDefault; one workgroup per CU for 128 clients):
-//   * 1 pair (client) x 32 of the 64 chains per workgroup: a gather iteration reads whole
-//     128-byte lines (16 bytes per lane, buffer_load_dwordx4) of the client arena, of b and of g;
-//     the two chain groups of a pair run on one XCD, so x and b are served from its L2.
+// Shape (one workgroup per CU for 128 clients):
+//   * 1 pair (client) x 32 of the 64 chains per workgroup (chain group cg = half of every
+//     64-block); a gather iteration of a producer wave covers the cg halves of 8 consecutive
+//     blocks (a "group", 256 positions): 16 bytes per lane, whole 128-byte lines of the client
+//     arena; the two chain groups of a pair run on one XCD.
+//   * per (cg, group) one 8-byte descriptor (fedadp_desc_kernel, read by a scalar load): a group
+//     inside one fp32 entry ("fast") reads the client arena at position + (arena offset - flat
+//     offset) and divides by -lr or not; a group that crosses an entry boundary or holds int64
+//     positions ("boundary", at most two per entry) reads its 256 finished values from a table
+//     fedadp_boundary_kernel fills per pair before the launch — the same one 16-byte load per
+//     lane, so the stream never waits on a per-position lookup.
+//   * x (the flattened global gradient) and b (the baseline, flattened once per round by
+//     fedadp_prep_kernel) come from one chain-group-major buffer: per (cg, group) the 256 x values
+//     then the 256 b values — every x or b load of a wave is 1 KiB contiguous and 16-byte aligned.
+//     (Gathered from the arena, b's 16-byte loads start 4-12 bytes off a 16-byte boundary wherever
+//     an entry's arena offset and flat position differ mod 4, half of ResNet-18's elements;
+//     scripts/micro/adp_stream.hip, profiles/r04*_adp_stream.log.)
 //   * chain wave: lane = kind * 32 + chain, kind 0 = g . loc, kind 1 = loc . loc: ONE dependent
-//     fma per step per lane (the dots are split over lanes, not interleaved), 4 steps per
-//     ds_read_b128 of a transposed row (row pitch kS + 16 floats, rows 4m .. 4m + 3 shifted by
-//     4m floats: conflict-free ds_read_b128 and ds_write_b32).
-//   * 8 producer waves, 2 gather iterations each per 128-block stage; their global loads run
-//     kD = 2 stages ahead of the tile being written (kD register sets), the tile ring has two
-//     slots, one s_barrier per stage.  A wave's current entry is cached in SGPRs: the segment
-//     map in LDS is read only at entry boundaries.
+//     fma per step per lane, 4 steps per ds_read_b128 of a transposed row (row pitch kS + 16
+//     floats, rows 4m .. 4m + 3 shifted by 4m floats: conflict-free ds_read_b128 and
+//     ds_write_b32).
+//   * kW producer waves, kIt gather iterations each per stage; their global loads run kD stages
+//     ahead of the tile being written, the tile ring has two slots, one s_barrier per stage.
 //   * g . g: an extra chain wave in the workgroups of pair 0 (x . x over the same tile).
-// The other shapes (8 / 4 / 2 pairs per workgroup, 4-byte gathers, deeper pipelines, chain waves
-// isolated on a SIMD) and the timing probes are tuning variants (PLATO_AGG_TUNE); DESIGN.md §13.
-// Compiled with -ffp-contract=off; the chain fma is an explicit v_fma_f32.
+// No segment map in the stream: any entry count.  Compiled with -ffp-contract=off; the chain fma
+// is an explicit v_fma_f32.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 #include <string>
-#include <type_traits>
 
 #include "common.h"
 #include "plato_agg.h"
@@ -51,7 +58,7 @@ int check_launch(const char* what) {
 }
 
 template <class T>
-__device__ __forceinline__ T sld(const T* p, int i) {
+__device__ __forceinline__ T sld(const T* p, uint64_t i) {
   return ((__attribute__((address_space(4))) const T*)p)[i];
 }
 
@@ -60,32 +67,38 @@ __device__ __forceinline__ float chain_fma(float a, float b, float c) {
   return c;
 }
 
-typedef __attribute__((address_space(1))) const float gfloat;
 typedef float f4v __attribute__((ext_vector_type(4)));
 
-// Segment map entry in LDS: positions [flat, end) read element src + (p - flat) of the region.
-struct AdpSeg {
-  uint32_t flat;
-  uint32_t end;
-  uint32_t src;
-  uint32_t info;  // bit 0: int64 region, bit 1: NEG_DIV
+constexpr uint32_t kDescBoundary = 1u, kDescNeg = 2u;
+
+// Per (chain group, 8-block group): fast groups: `off` = arena offset - flat offset (mod 2^32) of
+// the one fp32 entry the group lies in, flags kDescNeg if it is divided by -lr; boundary groups:
+// flags kDescBoundary, `off` = the group's row of the boundary table
+struct AdpDesc {
+  uint32_t off;
+  uint32_t flags;
 };
-constexpr uint32_t kSegI64 = 1u, kSegNeg = 2u;
-constexpr int kMaxSegs = 2048;
 
 struct AdpArgs {
   const float* x;                // flattened global gradient (process_grad(g)), >= nsteps * 64 floats
+  const float* xb;               // [2][ngroups][512]: chain-group-major x and b (fedadp_prep_kernel)
   const float* const* xf;        // client fp32 arenas
   const int64_t* const* xi;      // client int64 arenas
   const float* base_f;
   const int64_t* base_i;
   const plato_agg_segment* segs;
+  AdpDesc* desc;                 // [2][ngroups]
+  uint32_t* bnd_at;              // [max_bnd]: (cg, group) of each boundary row
+  uint32_t* n_bnd;               // number of boundary rows
+  float* bnd;                    // [n_pairs][max_bnd][256]: process_grad's values of the boundary groups
   uint32_t n_segs;
+  uint32_t ngroups;              // 8-block groups: ceil(nsteps / 8)
+  uint32_t max_bnd;              // >= boundary groups (adp_max_bnd)
   uint64_t n;                    // flat length
   uint64_t nsteps;               // whole 64-element blocks before sdot's 32-block and tail
   float lr;
+  double inv_lr;                 // 1 / double(lr)
   float* ws;                     // [n_pairs + with_xx][128]: chain sums of x.y, then of y.y
-  float* y64;                    // [n_pairs][n_i64]: process_grad's value of every int64 element
   uint64_t n_i64;
   uint64_t n_f32;                // fp32 arena length (buffer bounds)
   int n_pairs;
@@ -104,180 +117,74 @@ __device__ __forceinline__ float adp_i64(int64_t x, int64_t b, bool neg, float l
   return neg ? float(int64_t(uint64_t(0) - d)) / lr : float(int64_t(d));
 }
 
-// The last segment with flat <= p, walking forward from `from` (segments are in flat order).
-__device__ __forceinline__ int seg_walk(const AdpSeg* S, int n_segs, uint32_t p, int from) {
-  int s = from;
-  while (s + 1 < n_segs && S[s + 1].flat <= p) ++s;
-  return s;
+// (-d) / lr, correctly rounded, as RN32(RN64(-d * RN64(1 / lr))): the float64 product is within
+// 2^-52 (relative) of the quotient, while a quotient of two floats that is not a float lies at
+// least 2^-49 (relative) from every midpoint of the float grid (and is never on one), so the one
+// rounding to float gives the float32 division's bits (tests/test_division.py) — 3 instructions
+// instead of the division's ~10
+__device__ __forceinline__ float adp_div_lr_f64(float v, double inv_lr) { return float(double(v) * inv_lr); }
+
+// The last segment with flat_offset <= p (segments are in flat order).
+__device__ __forceinline__ uint32_t adp_find(const plato_agg_segment* segs, uint32_t n, uint64_t p) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (segs[mid].flat_offset <= p) lo = mid; else hi = mid;
+  }
+  return lo;
 }
 
-// kP pairs x kC chains per workgroup (kP * kC = 32: one chain wave of 2 kinds); kS steps per
-// stage; kW producer waves, kIt gather iterations of 64 positions each per stage; kVRpad floats
-// between vectors (chosen with the row pitch kS + 4 so that the chain wave's ds_read_b128 pairs
-// are conflict-free for the lane map kind * 32 + chain * kP + pair: DESIGN.md §12)
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad = 0, int kV = 1, int kSw = 0>
+// process_grad's value at any position of pair `pair` (the boundary groups and the epilogue)
+__device__ float adp_y_at(const AdpArgs& a, int pair, uint64_t p) {
+  const plato_agg_segment sg = a.segs[adp_find(a.segs, a.n_segs, p)];
+  const uint64_t e = sg.src_offset + (p - sg.flat_offset);
+  const bool neg = sg.flags & PLATO_AGG_SEG_NEG_DIV;
+  if (sg.region) return adp_i64(a.xi[pair][e], a.base_i[e], neg, a.lr);
+  return adp_f32(a.xf[pair][e], a.base_f[e], neg, a.lr);
+}
+
+// Tuning flags (kF): client arenas read non-temporally, the division as a float64 product, x and
+// b from the chain-group-major buffer (else x from the flat vector and b from the baseline arena)
+constexpr int kFYnt = 1, kFDiv64 = 4, kFXB = 8;
+
+// 32 of the 64 chains per workgroup; kS steps per stage; kW producer waves, kIt gather iterations
+// of one group (8 half-blocks x 32 positions) each per stage
+template <int kS, int kW, int kIt>
 struct AdpShape {
-  static_assert(kP * kC == 32, "one chain wave: kind * 32 + chain * kP + pair");
-  static_assert(kV == 1 || kV == 4, "one or four consecutive positions per lane and gather iteration");
-  static_assert(kC % kV == 0, "a lane's positions lie in one 64-block");
-  static_assert(kS * kC == 64 * kV * kW * kIt, "a stage is kW x kIt gather iterations of 64 * kV positions");
-  static_assert(kS % 16 == 0, "the chain wave reads 16 steps per block");
-  // transposed row pitch (floats).  kSw = 2 (kC = 32, 4-position producer lanes): pitch kS + 16
-  // and rows 4m .. 4m + 3 shifted by 4m floats.  A ds_write_b32 half-wave (banks (a/4) mod 32) of
-  // the producers then writes rows 4m + j, m = 0..7, on 8 different 4-bank slots (4-way conflicted
-  // with pitch kS + 4: 268 M extra LDS cycles per launch, all of them these writes), and every
-  // 16-lane group of the chain's ds_read_b128 (banks mod 64) still covers 16 different slots.
-  static constexpr int kR = kSw == 2 ? kS + 16 : kS + 4;
-  static_assert(kSw != 2 || (kC == 32 && kS % 64 == 0), "swizzled rows: one chain wave of 32 chains");
-  // kSw = 1 (measured no better): the upper half of a vector's rows sits 32 floats further on
-  static constexpr int kGap = kSw == 1 ? 32 : kSw == 2 ? 4 * (kC / 4) : 0;
-  static constexpr int kVR = kC * kR + kVRpad + kGap;  // rows of one vector (x, loc_0 .. loc_{kP-1})
-  __device__ static constexpr int row(int r) {
-    return r * kR + (kSw == 2 ? 4 * (r >> 2) : (r >= kC / 2 ? kGap : 0));
-  }
-  static constexpr int kSlot = (1 + kP) * kVR;
-  static constexpr int kBlkPerIt = 64 * kV / kC;  // 64-blocks per gather iteration
-  static constexpr int kLpB = kC / kV;             // lanes per 64-block in a gather iteration
+  static constexpr int kC = 32;
+  static_assert(kS * kC == 256 * kW * kIt, "a stage is kW x kIt gather iterations of 256 positions");
+  static_assert(kS % 64 == 0, "swizzled rows: whole 64-step row groups");
+  // transposed row pitch (floats) kS + 16 and rows 4m .. 4m + 3 shifted by 4m floats: a
+  // ds_write_b32 half-wave (banks (a/4) mod 32) of the producers writes rows 4m + j, m = 0..7, on
+  // 8 different 4-bank slots, and every 16-lane group of the chain's ds_read_b128 (banks mod 64)
+  // covers 16 different slots (pitch = 16 mod 64)
+  static constexpr int kR = kS + 16;
+  static constexpr int kVR = kC * kR + 4 * (kC / 4);  // rows of one vector (x or loc)
+  __device__ static constexpr int row(int r) { return r * kR + 4 * (r >> 2); }
+  static constexpr int kSlot = 2 * kVR;
+  static constexpr int kBlkPerIt = 8;  // 64-blocks per gather iteration (one group)
+  static constexpr int kLpB = 8;       // lanes per half-block
 };
 
-// One producer wave's loads for one stage: x, b and the kP arenas at kIt positions per lane.
-template <int kP, int kIt>
+// One producer wave's loads for kIt iterations: 4 consecutive positions per lane, 16-byte loads
+template <int kIt>
 struct AdpRegs {
-  float x[kIt];
-  float b[kIt];
-  float y[kIt][kP];
-  uint32_t code[kIt];  // per lane: kSegNeg; kSegI64 (+ element << 8): an int64 position, fetched at write time
-  uint32_t fast;       // bit i: iteration i lies in one fp32 entry (wave-uniform)
+  f4v x[kIt];
+  f4v b[kIt];
+  f4v y[kIt];
+  uint32_t flags[kIt];  // the group's descriptor flags (wave-uniform)
 };
 
-// Buffer resources of a producer wave: raw buffer loads take a 32-bit byte offset per lane against
-// a descriptor in SGPRs, so a gathered load costs no 64-bit address arithmetic (and an offset past
-// num_records reads 0 instead of faulting).
-template <int kP>
 struct AdpSrc {
-  __amdgpu_buffer_rsrc_t x, b, y[kP];
+  __amdgpu_buffer_rsrc_t x, b, y, bnd;
 };
 
+// Buffer resources: raw buffer loads take a 32-bit byte offset per lane against a descriptor in
+// SGPRs, so a gathered load costs no 64-bit address arithmetic (an offset past num_records reads 0)
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t adp_rsrc(const void* base, uint64_t bytes) {
   const uint64_t n = bytes < 0xffffffffull ? bytes : 0xffffffffull;
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)uint32_t(n), 0x00020000);
 }
-
-__device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, uint32_t byte_off) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, byte_off, 0, 0));
-}
-
-// A producer wave's current segment, wave-uniform (SGPRs): the positions a wave gathers only move
-// forward, so the segment map in LDS is read only when an iteration crosses into the next entry
-struct AdpCursor {
-  int idx;
-  uint32_t flat, end, src, info;
-};
-
-__device__ __forceinline__ void adp_cursor_load(const AdpSeg* S, int idx, AdpCursor& c) {
-  c.idx = idx;
-  c.flat = __builtin_amdgcn_readfirstlane(S[idx].flat);
-  c.end = __builtin_amdgcn_readfirstlane(S[idx].end);
-  c.src = __builtin_amdgcn_readfirstlane(S[idx].src);
-  c.info = __builtin_amdgcn_readfirstlane(S[idx].info);
-}
-
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe>
-__device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpSeg* S, int n_segs, AdpCursor& cur,
-                                          const AdpSrc<kP>& src, uint32_t t, int cg, int w, int lane,
-                                          AdpRegs<kP, kIt>& r) {
-  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad>;
-  const uint32_t last = uint32_t(a.nsteps - 1);
-  r.fast = 0;
-#pragma unroll
-  for (int i = 0; i < kIt; ++i) {
-    const int g = i * kW + w;
-    const uint32_t s0 = t * kS + uint32_t(g * Sh::kBlkPerIt);  // nsteps < 2^26: 32-bit block indices
-    const uint32_t s = min(s0 + uint32_t(lane / kC), last);     // a ragged last stage re-reads a valid block
-    const uint32_t p = s * 64 + uint32_t(cg * kC + lane % kC);
-    const uint32_t pf = min(s0, last) * 64 + uint32_t(cg * kC);
-    const uint32_t pl = min(s0 + uint32_t(Sh::kBlkPerIt - 1), last) * 64 + uint32_t(cg * kC + kC - 1);
-    while (pf >= cur.end && cur.idx + 1 < n_segs) adp_cursor_load(S, cur.idx + 1, cur);  // rare: next entry
-    uint32_t e, code;
-    // the loads below are the same on both paths (no branch around them): every trip issues
-    // kIt * (kP + 2) loads and the compiler's vmcnt bookkeeping covers exactly one stage
-    if (!(cur.info & kSegI64) && pl < cur.end) {
-      r.fast |= 1u << i;  // the whole iteration inside one fp32 entry: one shift for every lane
-      e = p - cur.flat + cur.src;
-      code = cur.info;
-    } else {  // an entry boundary inside the iteration: per-lane entries
-      const AdpSeg ls = S[seg_walk(S, n_segs, p, cur.idx)];
-      const uint32_t el = p - ls.flat + ls.src;
-      const bool i64 = ls.info & kSegI64;
-      e = i64 ? 0u : el;
-      code = i64 ? (ls.info | (el << 8)) : ls.info;
-    }
-    r.code[i] = code;
-    if (kProbe == 3) {  // timing probe: no loads (wrong results)
-      r.x[i] = float(p);
-      r.b[i] = float(e);
-#pragma unroll
-      for (int k = 0; k < kP; ++k) r.y[i][k] = float(e + k);
-      continue;
-    }
-    r.x[i] = bload(src.x, p * 4u);
-    r.b[i] = bload(src.b, e * 4u);
-#pragma unroll
-    for (int k = 0; k < kP; ++k) r.y[i][k] = bload(src.y[k], e * 4u);
-  }
-}
-
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe>
-__device__ __forceinline__ void adp_write(const AdpArgs& a, float* slot, int pair0, int w, int lane,
-                                          AdpRegs<kP, kIt>& r) {
-  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad>;
-  const float lr = a.lr;
-#pragma unroll
-  for (int i = 0; i < kIt; ++i) {
-    const int g = i * kW + w;
-    const int col = g * Sh::kBlkPerIt + lane / kC;  // step within the stage
-    float* dst = slot + (lane % kC) * Sh::kR + col;
-    dst[0] = r.x[i];
-    const uint32_t code = r.code[i];
-    if (r.fast & (1u << i)) {  // wave-uniform: one entry, one sign/divide mode
-      if (kProbe != 1 && (__builtin_amdgcn_readfirstlane(int(code)) & kSegNeg)) {  // probe 1: no division
-#pragma unroll
-        for (int k = 0; k < kP; ++k) dst[(1 + k) * Sh::kVR] = (-(r.y[i][k] - r.b[i])) / lr;
-      } else {
-#pragma unroll
-        for (int k = 0; k < kP; ++k) dst[(1 + k) * Sh::kVR] = r.y[i][k] - r.b[i];
-      }
-    } else {
-      const bool neg = code & kSegNeg;
-      if (code & kSegI64) {
-        // rare (one per int64 entry and chain group): the finished value from fedadp_i64_kernel's table
-#pragma unroll
-        for (int k = 0; k < kP; ++k) {
-          const int pair = pair0 + k < a.n_pairs ? pair0 + k : a.n_pairs - 1;
-          r.y[i][k] = a.y64[uint64_t(pair) * a.n_i64 + (code >> 8)];
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < kP; ++k)
-        dst[(1 + k) * Sh::kVR] = (code & kSegI64) ? r.y[i][k] : adp_f32(r.y[i][k], r.b[i], neg, lr);
-    }
-  }
-}
-
-// Four consecutive positions per lane (kV = 4): a lane's x, b and loc_k come from one 16-byte
-// buffer load each (an arena position is 4-byte aligned only: dword-aligned dwordx4 loads are
-// legal, MI355X_MICROARCH.md), so a gather iteration of 256 positions costs kP + 2 load
-// instructions instead of 4 x (kP + 2).  An iteration that crosses an entry keeps the loads
-// (their values are unused) and its lanes fetch their four positions one by one at write time.
-template <int kP, int kIt>
-struct AdpRegs4 {
-  f4v x[kIt];
-  f4v b[kIt];
-  f4v y[kIt][kP];
-  uint32_t code[kIt];  // fast iterations: the entry's info; otherwise the segment index of pos[i]
-  uint32_t pos[kIt];   // first position of the lane
-  uint32_t fast;       // bit i: iteration i lies in one fp32 entry (wave-uniform)
-};
 
 // kAux: the load's cache policy (2 = nt: a streaming read, kept out of the way of the re-read x and b)
 template <int kAux = 0>
@@ -285,65 +192,42 @@ __device__ __forceinline__ f4v bload4(__amdgpu_buffer_rsrc_t r, uint32_t byte_of
   return __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(r, byte_off, 0, kAux));
 }
 
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kNt = 0>
-__device__ __forceinline__ void adp_issue4(const AdpArgs& a, const AdpSeg* S, int n_segs, AdpCursor& cur,
-                                           const AdpSrc<kP>& src, uint32_t t, int cg, int w, int lane,
-                                           AdpRegs4<kP, kIt>& r) {
-  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, 4>;
+template <int kS, int kW, int kIt, int kF>
+__device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpDesc* desc, const AdpSrc& src, uint32_t t, int cg,
+                                          int w, int lane, AdpRegs<kIt>& r) {
+  using Sh = AdpShape<kS, kW, kIt>;
   const uint32_t last = uint32_t(a.nsteps - 1);
-  r.fast = 0;
+  const uint32_t glast = a.ngroups - 1;
 #pragma unroll
   for (int i = 0; i < kIt; ++i) {
-    const int g = i * kW + w;
-    const uint32_t s0 = t * kS + uint32_t(g * Sh::kBlkPerIt);
-    const uint32_t s = min(s0 + uint32_t(lane / Sh::kLpB), last);
-    const uint32_t p = s * 64 + uint32_t(cg * kC + (lane % Sh::kLpB) * 4);
-    const uint32_t pf = min(s0, last) * 64 + uint32_t(cg * kC);
-    const uint32_t pl = min(s0 + uint32_t(Sh::kBlkPerIt - 1), last) * 64 + uint32_t(cg * kC + kC - 1);
-    while (pf >= cur.end && cur.idx + 1 < n_segs) adp_cursor_load(S, cur.idx + 1, cur);  // rare: next entry
-    uint32_t e, code;
-    if (!(cur.info & kSegI64) && pl < cur.end) {
-      r.fast |= 1u << i;
-      e = p - cur.flat + cur.src;
-      code = cur.info;
+    const uint32_t grp = min(t * uint32_t(kS / 8) + uint32_t(i * kW + w), glast);  // past the end: re-read a valid group
+    const uint32_t s = min(grp * 8u + uint32_t(lane / Sh::kLpB), last);  // a ragged last group re-reads a valid block
+    const uint32_t p = s * 64 + uint32_t(cg * Sh::kC + (lane % Sh::kLpB) * 4);
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(desc);  // wave-uniform: one scalar load
+    const AdpDesc d{sld(dw, 2 * uint64_t(grp)), sld(dw, 2 * uint64_t(grp) + 1)};
+    r.flags[i] = d.flags;
+    // one load of the client's values per lane on both paths (the compiler's vmcnt bookkeeping
+    // covers exactly one stage): the arena for a fast group, the boundary table otherwise
+    const bool bnd = d.flags & kDescBoundary;
+    const __amdgpu_buffer_rsrc_t ry = bnd ? src.bnd : src.y;
+    const uint32_t yo = bnd ? (d.off * 256u + uint32_t(lane) * 4u) * 4u : (p + d.off) * 4u;
+    r.y[i] = bload4<(kF & kFYnt) ? 2 : 0>(ry, yo);
+    if constexpr ((kF & kFXB) != 0) {  // [cg][group][x: 256 | b: 256], lane l at 4 l
+      const uint32_t q = (grp * 512u + uint32_t(lane) * 4u) * 4u;
+      r.x[i] = bload4<0>(src.x, q);
+      r.b[i] = bload4<0>(src.x, q + 1024u);
     } else {
-      const int idx = seg_walk(S, n_segs, p, cur.idx);
-      e = 0u;  // the loads still go out (same count on every path); the write fetches the values
-      code = uint32_t(idx);
+      r.x[i] = bload4<0>(src.x, p * 4u);
+      r.b[i] = bload4<0>(src.b, bnd ? 0u : (p + d.off) * 4u);
     }
-    r.code[i] = code;
-    r.pos[i] = p;
-    // kNt & 3: 1 = the client arenas (read once) as nt loads, 2 = every load nt
-    r.x[i] = bload4<(kNt & 3) == 2 ? 2 : 0>(src.x, p * 4u);
-    r.b[i] = bload4<(kNt & 3) == 2 ? 2 : 0>(src.b, e * 4u);
-#pragma unroll
-    for (int k = 0; k < kP; ++k) r.y[i][k] = bload4<(kNt & 3) ? 2 : 0>(src.y[k], e * 4u);
   }
 }
 
-// process_grad's value at flat position p of pair `pair`, walking the segment map from `idx`
-// (the slow path of an iteration that crosses an entry)
-__device__ __forceinline__ float adp_value_at(const AdpArgs& a, const AdpSeg* S, int n_segs, int& idx, uint32_t p,
-                                              int pair) {
-  idx = seg_walk(S, n_segs, p, idx);
-  const AdpSeg sg = S[idx];
-  const uint32_t el = p - sg.flat + sg.src;
-  if (sg.info & kSegI64) return a.y64[uint64_t(pair) * a.n_i64 + el];
-  return adp_f32(a.xf[pair][el], a.base_f[el], sg.info & kSegNeg, a.lr);
-}
-
-// (-d) / lr, correctly rounded, as RN32(RN64(-d * RN64(1 / lr))) (kNt & 4): the float64 product is
-// within 2^-52 (relative) of the quotient, while a quotient of two floats that is not a float lies
-// at least 2^-49 (relative) from every midpoint of the float grid (and is never on one), so the one
-// rounding to float gives the float32 division's bits — 3 instructions instead of the division's ~10
-__device__ __forceinline__ float adp_div_lr_f64(float v, double inv_lr) { return float(double(v) * inv_lr); }
-
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kSw, int kNt = 0>
-__device__ __forceinline__ void adp_write4(const AdpArgs& a, const AdpSeg* S, int n_segs, float* slot, int pair0,
-                                           int w, int lane, AdpRegs4<kP, kIt>& r) {
-  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, 4, kSw>;
+template <int kS, int kW, int kIt, int kF>
+__device__ __forceinline__ void adp_write(const AdpArgs& a, float* slot, int w, int lane, AdpRegs<kIt>& r) {
+  using Sh = AdpShape<kS, kW, kIt>;
   const float lr = a.lr;
-  const double inv_lr = (kNt & 4) ? 1.0 / double(lr) : 0.0;
+  const double inv_lr = a.inv_lr;
 #pragma unroll
   for (int i = 0; i < kIt; ++i) {
     const int g = i * kW + w;
@@ -351,197 +235,120 @@ __device__ __forceinline__ void adp_write4(const AdpArgs& a, const AdpSeg* S, in
     float* dst = slot + Sh::row((lane % Sh::kLpB) * 4) + col;  // chain c0 = 4 * (lane % kLpB), rows c0 .. c0 + 3
 #pragma unroll
     for (int j = 0; j < 4; ++j) dst[j * Sh::kR] = r.x[i][j];
-    if (r.fast & (1u << i)) {  // wave-uniform: one entry, one sign/divide mode
-      if (__builtin_amdgcn_readfirstlane(int(r.code[i])) & kSegNeg) {
+    const uint32_t flags = __builtin_amdgcn_readfirstlane(r.flags[i]);
+    if (flags & kDescBoundary) {  // the finished values
 #pragma unroll
-        for (int k = 0; k < kP; ++k)
+      for (int j = 0; j < 4; ++j) dst[Sh::kVR + j * Sh::kR] = r.y[i][j];
+    } else if (flags & kDescNeg) {
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float nv = -(r.y[i][k][j] - r.b[i][j]);
-            dst[(1 + k) * Sh::kVR + j * Sh::kR] = (kNt & 4) ? adp_div_lr_f64(nv, inv_lr) : nv / lr;
-          }
-      } else {
-#pragma unroll
-        for (int k = 0; k < kP; ++k)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) dst[(1 + k) * Sh::kVR + j * Sh::kR] = r.y[i][k][j] - r.b[i][j];
+      for (int j = 0; j < 4; ++j) {
+        const float nv = -(r.y[i][j] - r.b[i][j]);
+        dst[Sh::kVR + j * Sh::kR] = (kF & kFDiv64) ? adp_div_lr_f64(nv, inv_lr) : nv / lr;
       }
-    } else {  // rare: an entry boundary (or an int64 entry) inside the iteration
-      for (int k = 0; k < kP; ++k) {
-        const int pair = pair0 + k < a.n_pairs ? pair0 + k : a.n_pairs - 1;
-        int idx = int(r.code[i]);
-        for (int j = 0; j < 4; ++j) dst[(1 + k) * Sh::kVR + j * Sh::kR] = adp_value_at(a, S, n_segs, idx, r.pos[i] + j, pair);
-      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dst[Sh::kVR + j * Sh::kR] = r.y[i][j] - r.b[i][j];
     }
   }
 }
 
-// Waves per workgroup: kW producers + 2 chain waves, or with kIso 12 waves placed so that the chain
-// waves share a SIMD with no producer (waves are dealt to the CU's 4 SIMDs round-robin, so waves 0, 4
-// and 8 share one: wave 0 runs the pairs' chains, wave 4 g . g, wave 8 idles; producers are the other 9
-// waves, the last of them idle when kW = 8).  A producer's VALU instruction (the division sequence, the
-// 64-bit address arithmetic) holds its SIMD for several cycles, and on a shared SIMD the serial fma
-// chain waits for it at every step (timing probes).
-template <int kW, int kIso>
-constexpr int adp_waves() { return kIso ? 12 : kW + 2; }
-
-template <int kP, int kIt, int kV>
-using AdpRegsV = std::conditional_t<kV == 4, AdpRegs4<kP, kIt>, AdpRegs<kP, kIt>>;
-
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe, int kV, int kNt = 0>
-__device__ __forceinline__ void adp_issue_v(const AdpArgs& a, const AdpSeg* S, int n_segs, AdpCursor& cur,
-                                            const AdpSrc<kP>& src, uint32_t t, int cg, int w, int lane,
-                                            AdpRegsV<kP, kIt, kV>& r) {
-  if constexpr (kV == 4) adp_issue4<kP, kC, kS, kW, kIt, kVRpad, kNt>(a, S, n_segs, cur, src, t, cg, w, lane, r);
-  else adp_issue<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, S, n_segs, cur, src, t, cg, w, lane, r);
-}
-
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe, int kV, int kSw, int kNt = 0>
-__device__ __forceinline__ void adp_write_v(const AdpArgs& a, const AdpSeg* S, int n_segs, float* slot, int pair0,
-                                            int w, int lane, AdpRegsV<kP, kIt, kV>& r) {
-  static_assert(!kSw || kV == 4, "the row gap is laid out for 4-position producer lanes");
-  if constexpr (kV == 4) adp_write4<kP, kC, kS, kW, kIt, kVRpad, kSw, kNt>(a, S, n_segs, slot, pair0, w, lane, r);
-  else adp_write<kP, kC, kS, kW, kIt, kVRpad, kProbe>(a, slot, pair0, w, lane, r);
-}
-
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
-          int kCP = 1, int kPrio = 3, int kSw = 0, int kNt = 0>
-__global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kernel(AdpArgs a) {
-  using Sh = AdpShape<kP, kC, kS, kW, kIt, kVRpad, kV, kSw>;
-  static_assert(!kIso || kW <= 9, "kIso: at most 9 producer waves");
+// kProbe (tuning only, wrong results by design): 1 = the chains alone (producers keep only the
+// barrier count), 2 = the producers alone (the chain wave reads one value per stage, which keeps
+// the producers' stores and loads live)
+template <int kS, int kW, int kIt, int kD, int kF, int kProbe = 0>
+__global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
+  using Sh = AdpShape<kS, kW, kIt>;
+  static_assert(kD >= 2 && kD <= 4, "2-4 stages of loads in flight per producer wave");
   __shared__ __attribute__((aligned(16))) float ring[2 * Sh::kSlot];
-  __shared__ AdpSeg S[kMaxSegs];
-  constexpr int kGroups = 64 / kC;
-  // workgroups are dealt to the 8 XCDs round-robin: the kGroups chain groups of a pair group
-  // get ids that agree mod 8, so they share one XCD and its L2
+  // workgroups are dealt to the 8 XCDs round-robin: the 2 chain groups of a pair get ids that
+  // agree mod 8, so they share one XCD and its L2
   const int b = int(blockIdx.x), lo = b & 7;
-  const int cg = (b / 8) % kGroups;
-  const int pg = (b / (8 * kGroups)) * 8 + lo;
-  if (pg * kP >= a.n_pairs) return;  // padding workgroup (before any barrier)
-  const int n_segs = int(a.n_segs);
-  for (int j = int(threadIdx.x); j < n_segs; j += int(blockDim.x)) {
-    const plato_agg_segment sg = a.segs[j];
-    S[j] = AdpSeg{uint32_t(sg.flat_offset), uint32_t(sg.flat_offset + sg.numel), uint32_t(sg.src_offset),
-                  (sg.region ? kSegI64 : 0u) | ((sg.flags & PLATO_AGG_SEG_NEG_DIV) ? kSegNeg : 0u)};
-  }
-  __syncthreads();
+  const int cg = (b / 8) % 2;
+  const int pg = (b / 16) * 8 + lo;
+  if (pg >= a.n_pairs) return;  // padding workgroup (before any barrier)
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = int(threadIdx.x & 63);
   const uint64_t nsteps = a.nsteps;
   const uint64_t nst = (nsteps + kS - 1) / kS;
-  static_assert(kD >= 2 && kD <= 4, "2-4 stages of loads in flight per producer wave");
   const uint64_t nst2 = (nst + kD - 1) / kD * kD;  // barriers: one per stage, in whole trips of kD stages
-  // role: chain wave 0 (pairs) / 1 (g . g), or producer w; idle waves end here (a wave that has ended
-  // is no longer counted by s_barrier)
-  int chain_role = -1, w = -1;
-  if (kIso) {
-    if ((wave & 3) == 0) chain_role = wave >> 2;
-    else w = (wave >> 2) * 3 + (wave & 3) - 1;
-    if (chain_role > 1 || w >= kW) return;
-  } else {
-    if (wave >= 2) w = wave - 2;
-    else chain_role = wave;
-  }
-  if (w >= 0) {  // producer
-    if (kProbe == 4) {  // timing probe: the chains alone (producers only keep the barrier count)
+  if (wave >= 2) {  // producer w
+    const int w = wave - 2;
+    if (kProbe == 1) {
       for (uint64_t t = 0; t < nst2; ++t) __builtin_amdgcn_s_barrier();
       return;
     }
-    const int pair0 = pg * kP;
-    AdpSrc<kP> src;
-    src.x = adp_rsrc(a.x, a.nsteps * 256);
-    src.b = adp_rsrc(a.base_f, a.n_f32 * 4);
-#pragma unroll
-    for (int k = 0; k < kP; ++k)
-      src.y[k] = adp_rsrc(sld(a.xf, pair0 + k < a.n_pairs ? pair0 + k : a.n_pairs - 1), a.n_f32 * 4);
-    AdpCursor cursor;
-    adp_cursor_load(S, 0, cursor);
+    AdpSrc src;
+    if (kF & kFXB) {
+      src.x = adp_rsrc(a.xb + uint64_t(cg) * a.ngroups * 512, uint64_t(a.ngroups) * 512 * 4);
+      src.b = src.x;
+    } else {
+      src.x = adp_rsrc(a.x, a.nsteps * 256);
+      src.b = adp_rsrc(a.base_f, a.n_f32 * 4);
+    }
+    src.y = adp_rsrc(sld(a.xf, uint64_t(pg)), a.n_f32 * 4);
+    src.bnd = adp_rsrc(a.bnd + uint64_t(pg) * a.max_bnd * 256, uint64_t(a.max_bnd) * 256 * 4);
+    const AdpDesc* desc = a.desc + uint64_t(cg) * a.ngroups;
     // kD register sets: the loads of stage t + kD go out right after stage t is written, so every
     // producer wave keeps kD stages of loads in flight; the tile ring in LDS has two slots
-    AdpRegsV<kP, kIt, kV> regs[kD];
+    AdpRegs<kIt> regs[kD];
 #pragma unroll
-    for (int j = 0; j < kD; ++j)
-      adp_issue_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV, kNt>(a, S, n_segs, cursor, src, uint32_t(j), cg, w, lane, regs[j]);
-    uint64_t t_start = 0, t_wait = 0, t_write = 0, c0 = 0;  // probe 6: cycle counts
-    if (kProbe == 6) t_start = __builtin_readcyclecounter();
+    for (int j = 0; j < kD; ++j) adp_issue<kS, kW, kIt, kF>(a, desc, src, uint32_t(j), cg, w, lane, regs[j]);
     // whole trips of kD stages (the last trip may run idle stages): no branch inside the loop, so the
     // compiler's vmcnt bookkeeping sees the same kD stages in flight on every trip
     for (uint32_t t = 0; t < uint32_t(nst2); t += kD) {
 #pragma unroll
       for (int j = 0; j < kD; ++j) {
-        if (kProbe == 6) c0 = __builtin_readcyclecounter();
-        adp_write_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV, kSw, kNt>(a, S, n_segs, ring + ((t + j) & 1) * Sh::kSlot, pair0, w,
-                                                             lane, regs[j]);
-        if (kProbe == 6) t_write += __builtin_readcyclecounter() - c0;
-        // past the last stage (t = nst) every position clamps to the last block: valid addresses,
-        // never consumed, and every trip issues the same loads
+        adp_write<kS, kW, kIt, kF>(a, ring + ((t + j) & 1) * Sh::kSlot, w, lane, regs[j]);
+        // past the last stage every group clamps to the last one: valid addresses, never consumed
         const uint32_t nxt = t + j + kD;
-        adp_issue_v<kP, kC, kS, kW, kIt, kVRpad, kProbe, kV, kNt>(a, S, n_segs, cursor, src, nxt < nst ? nxt : uint32_t(nst),
-                                                             cg, w, lane, regs[j]);
-        if (kProbe == 6) c0 = __builtin_readcyclecounter();
+        adp_issue<kS, kW, kIt, kF>(a, desc, src, nxt < nst ? nxt : uint32_t(nst), cg, w, lane, regs[j]);
         __builtin_amdgcn_s_barrier();  // stage t + j published in slot (t + j) & 1
-        if (kProbe == 6) t_wait += __builtin_readcyclecounter() - c0;
       }
-    }
-    if (kProbe == 6 && lane == 0) {  // probe 6: [total, barrier wait, write, HW_ID] of every producer
-      uint32_t* o = reinterpret_cast<uint32_t*>(a.ws) + blockIdx.x * 48 + 8 + 4 * w;
-      o[0] = uint32_t(__builtin_readcyclecounter() - t_start);
-      o[1] = uint32_t(t_wait);
-      o[2] = uint32_t(t_write);
-      o[3] = uint32_t(__builtin_amdgcn_s_getreg((31 << 11) | 4));  // hwreg(HW_REG_HW_ID): wave, SIMD, CU ...
     }
     return;
   }
-  // chain waves: wave 0 the kP pairs' dots, wave 1 g . g (pair group 0 only; elsewhere it only
-  // keeps the barrier count)
-  if (kPrio) __builtin_amdgcn_s_setprio(kPrio);  // the chain wave issues first
-  const bool xx = chain_role == 1;
+  // chain waves: wave 0 the pair's dots, wave 1 g . g (pair group 0 only; elsewhere it only keeps
+  // the barrier count)
+  __builtin_amdgcn_s_setprio(3);  // the chain wave issues first
+  const bool xx = wave == 1;
   const bool active = !xx || (pg == 0 && a.with_xx);
-  const int kind = xx ? 0 : lane >> 5, c = xx ? lane % kC : (lane & 31) / kP, p = lane % kP;
-  const int arow = (xx || kind == 0 ? 0 : (1 + p) * Sh::kVR) + Sh::row(c);
-  const int brow = (xx ? 0 : (1 + p) * Sh::kVR) + Sh::row(c);
+  const int kind = xx ? 0 : lane >> 5, c = lane & 31;
+  const int arow = (xx || kind == 0 ? 0 : Sh::kVR) + Sh::row(c);
+  const int brow = (xx ? 0 : Sh::kVR) + Sh::row(c);
   float acc = 0.f;
-  uint64_t t_start = 0, t_wait = 0, c0 = 0;  // probe 6: cycle counts
-  if (kProbe == 6) t_start = __builtin_readcyclecounter();
   for (uint64_t t = 0; t < nst2; ++t) {
-    if (kProbe == 6) c0 = __builtin_readcyclecounter();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_s_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (kProbe == 6) t_wait += __builtin_readcyclecounter() - c0;
-    if (!active || t >= nst || kProbe == 2) continue;  // probe 2: no chains
+    if (!active || t >= nst) continue;
     const float* slot = ring + (t & 1) * Sh::kSlot;
     const float* A = slot + arow;
     const float* B = slot + brow;
-    if (kProbe == 7) {  // probe 7: the producers alone — one LDS read per stage keeps their stores live
+    if (kProbe == 2) {
       acc += A[t & 15] * B[t & 15];
       continue;
     }
     const uint64_t left = nsteps - t * kS;
-    typedef float f4 __attribute__((ext_vector_type(4)));
     if (left >= uint64_t(kS)) {
-      // 16 steps per block of 4 ds_read_b128 pairs; the reads of the next kCP blocks in flight
-      constexpr int kNB = kS / 16, kRS = kCP + 1;
-      f4 av[kRS][4], bv[kRS][4];
+      // 16 steps per block of 4 ds_read_b128 pairs; the next block's reads in flight
+      constexpr int kNB = kS / 16;
+      f4v av[2][4], bv[2][4];
 #pragma unroll
-      for (int d = 0; d < kCP; ++d) {
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          av[d][q] = *reinterpret_cast<const f4*>(A + 16 * d + 4 * q);
-          bv[d][q] = *reinterpret_cast<const f4*>(B + 16 * d + 4 * q);
-        }
+      for (int q = 0; q < 4; ++q) {
+        av[0][q] = *reinterpret_cast<const f4v*>(A + 4 * q);
+        bv[0][q] = *reinterpret_cast<const f4v*>(B + 4 * q);
       }
 #pragma unroll
       for (int blk = 0; blk < kNB; ++blk) {
-        const int nb = blk + kCP;
-        if (kProbe != 5 && nb < kNB) {  // probe 5: no LDS reads after the first blocks
+        const int nb = blk + 1;
+        if (nb < kNB) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) {
-            av[nb % kRS][q] = *reinterpret_cast<const f4*>(A + 16 * nb + 4 * q);
-            bv[nb % kRS][q] = *reinterpret_cast<const f4*>(B + 16 * nb + 4 * q);
+            av[nb % 2][q] = *reinterpret_cast<const f4v*>(A + 16 * nb + 4 * q);
+            bv[nb % 2][q] = *reinterpret_cast<const f4v*>(B + 16 * nb + 4 * q);
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-        const int cb = kProbe == 5 ? 0 : blk % kRS;
+        const int cb = blk % 2;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           acc = chain_fma(av[cb][q].x, bv[cb][q].x, acc);
@@ -555,55 +362,103 @@ __global__ __launch_bounds__((64 * adp_waves<kW, kIso>())) void fedadp_dots_kern
       for (int s = 0; s < int(left); ++s) acc = chain_fma(A[s], B[s], acc);
     }
   }
-  const int chain = cg * kC + c;
-  if (kProbe == 6) {  // probe 6: [total, barrier wait, HW_ID] of the pairs' chain wave, HW_ID of g . g (no results)
-    uint32_t* o = reinterpret_cast<uint32_t*>(a.ws) + blockIdx.x * 48;
-    if (!xx && lane == 0) {
-      o[0] = uint32_t(__builtin_readcyclecounter() - t_start);
-      o[1] = uint32_t(t_wait);
-      o[2] = uint32_t(__builtin_amdgcn_s_getreg((31 << 11) | 4));
-    }
-    if (xx && lane == 0) o[3] = uint32_t(__builtin_amdgcn_s_getreg((31 << 11) | 4));
-    if (acc == 12345.f) a.ws[blockIdx.x] = acc;  // keep the chains
-    return;
-  }
+  const int chain = cg * Sh::kC + c;
   if (!xx) {
-    const int pair = pg * kP + p;
-    if (pair < a.n_pairs) a.ws[uint64_t(pair) * 128 + uint64_t(kind) * 64 + chain] = acc;
-  } else if (active && lane < kC) {  // the virtual pair (g, g): its x.y and y.y chains are both g.g
+    a.ws[uint64_t(pg) * 128 + uint64_t(kind) * 64 + chain] = acc;
+  } else if (active && lane < Sh::kC) {  // the virtual pair (g, g): its x.y and y.y chains are both g.g
     a.ws[uint64_t(a.n_pairs) * 128 + chain] = acc;
     a.ws[uint64_t(a.n_pairs) * 128 + 64 + chain] = acc;
   }
 }
 
-// process_grad's value of every int64 element (num_batches_tracked deltas), per pair: the gather
-// reads these finished values instead of doing int64 arithmetic in the stream
-__global__ __launch_bounds__(64) void fedadp_i64_kernel(AdpArgs a) {
-  const int pair = blockIdx.x;
-  const int64_t* xi = a.xi[pair];
-  for (uint32_t j = 0; j < a.n_segs; ++j) {
-    const plato_agg_segment sg = a.segs[j];
-    if (!sg.region) continue;
-    const bool neg = sg.flags & PLATO_AGG_SEG_NEG_DIV;
-    for (uint64_t q = threadIdx.x; q < sg.numel; q += 64) {
-      const uint64_t e = sg.src_offset + q;
-      a.y64[uint64_t(pair) * a.n_i64 + e] = adp_i64(xi[e], a.base_i[e], neg, a.lr);
-    }
+// The descriptor of every (cg, group): fast if all its positions (whole blocks only) lie in one
+// fp32 entry, else a boundary group (its row in the table comes from fedadp_rows_kernel)
+__global__ __launch_bounds__(256) void fedadp_desc_kernel(AdpArgs a) {
+  const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+  if (j >= 2 * a.ngroups) return;
+  const uint32_t cg = j / a.ngroups, grp = j % a.ngroups;
+  const uint64_t s_last = min(uint64_t(grp) * 8 + 7, a.nsteps - 1);
+  const uint64_t pf = uint64_t(grp) * 8 * 64 + cg * 32, pl = s_last * 64 + cg * 32 + 31;
+  const plato_agg_segment sg = a.segs[adp_find(a.segs, a.n_segs, pf)];
+  AdpDesc d;
+  if (!sg.region && pl < sg.flat_offset + sg.numel) {
+    d.off = uint32_t(sg.src_offset - sg.flat_offset);  // mod 2^32: position + off = arena element
+    d.flags = (sg.flags & PLATO_AGG_SEG_NEG_DIV) ? kDescNeg : 0u;
+  } else {
+    d.off = 0;
+    d.flags = kDescBoundary;
   }
+  a.desc[j] = d;
 }
 
-// process_grad's value at any position (binary search of the segment map; the epilogue's few positions)
-__device__ float adp_y_at(const AdpArgs& a, int pair, uint64_t p) {
-  uint32_t lo = 0, hi = a.n_segs;
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (a.segs[mid].flat_offset <= p) lo = mid; else hi = mid;
+// Rows of the boundary table, in (cg, group) order: one workgroup; thread t counts the boundary
+// groups of its contiguous run of descriptors, an exclusive scan of the 1,024 counts (wave
+// shuffles, then the 16 wave totals) gives each run its first row, and the run is numbered in order
+__global__ __launch_bounds__(1024) void fedadp_rows_kernel(AdpArgs a) {
+  __shared__ uint32_t wave_tot[16];
+  const uint32_t n = 2 * a.ngroups;
+  const uint32_t run = (n + 1023) / 1024;
+  const uint32_t j0 = min(threadIdx.x * run, n), j1 = min(j0 + run, n);
+  uint32_t cnt = 0;
+  for (uint32_t j = j0; j < j1; ++j) cnt += (a.desc[j].flags & kDescBoundary) ? 1u : 0u;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t incl = cnt;  // inclusive scan within the wave
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += v;
   }
-  const plato_agg_segment sg = a.segs[lo];
-  const uint64_t e = sg.src_offset + (p - sg.flat_offset);
-  const bool neg = sg.flags & PLATO_AGG_SEG_NEG_DIV;
-  if (sg.region) return adp_i64(a.xi[pair][e], a.base_i[e], neg, a.lr);
-  return adp_f32(a.xf[pair][e], a.base_f[e], neg, a.lr);
+  if (lane == 63) wave_tot[wave] = incl;
+  __syncthreads();
+  uint32_t row = incl - cnt;
+  for (int v = 0; v < wave; ++v) row += wave_tot[v];
+  for (uint32_t j = j0; j < j1; ++j) {
+    if (a.desc[j].flags & kDescBoundary) {
+      a.desc[j].off = row;
+      if (row < a.max_bnd) a.bnd_at[row] = j;
+      ++row;
+    }
+  }
+  if (threadIdx.x == 1023) *a.n_bnd = row;  // the last run ends at the total
+}
+
+// The boundary table: process_grad's values of every boundary group of every pair, in the lane
+// order of the stream (index u * 32 + v: block 8 group + u, position cg * 32 + v); 0 past the
+// last whole block
+__global__ __launch_bounds__(256) void fedadp_boundary_kernel(AdpArgs a) {
+  const uint32_t row = blockIdx.x;
+  const int pair = int(blockIdx.y);
+  if (row >= min(*a.n_bnd, a.max_bnd)) return;
+  const uint32_t j = a.bnd_at[row];
+  const uint32_t cg = j / a.ngroups, grp = j % a.ngroups;
+  const uint32_t u = threadIdx.x / 32, v = threadIdx.x % 32;
+  const uint64_t s = uint64_t(grp) * 8 + u;
+  const float val = s < a.nsteps ? adp_y_at(a, pair, s * 64 + cg * 32 + v) : 0.f;
+  a.bnd[(uint64_t(pair) * a.max_bnd + row) * 256 + threadIdx.x] = val;
+}
+
+// The chain-group-major x / b buffer: xb[cg][grp][0..255] = x at the group's half-block positions
+// (block 8 grp + u, position cg * 32 + v at index u * 32 + v), xb[cg][grp][256..511] = b at the
+// same positions (the baseline through the segment map; 0 at int64 positions, whose values come
+// from the boundary table).  A workgroup takes 2,048 consecutive flat positions and walks the
+// segments overlapping them (workgroup-uniform), consecutive positions on consecutive lanes:
+// coalesced reads of x and of each entry's baseline run, 128-byte runs of writes.
+constexpr int kPrepSpan = 2048;
+__global__ __launch_bounds__(256) void fedadp_prep_kernel(AdpArgs a, float* xb) {
+  const uint64_t np = a.nsteps * 64;  // whole blocks only
+  const uint64_t b0 = uint64_t(blockIdx.x) * kPrepSpan;
+  const uint64_t b1 = min(b0 + kPrepSpan, np);
+  for (uint32_t sidx = adp_find(a.segs, a.n_segs, b0); sidx < a.n_segs; ++sidx) {
+    const plato_agg_segment sg = a.segs[sidx];
+    if (sg.flat_offset >= b1) break;
+    const uint64_t lo = max(uint64_t(sg.flat_offset), b0), hi = min(uint64_t(sg.flat_offset + sg.numel), b1);
+    const bool i64 = sg.region;
+    for (uint64_t p = lo + threadIdx.x; p < hi; p += 256) {
+      const uint64_t s = p / 64, c = p % 64;
+      float* o = xb + ((c / 32) * a.ngroups + s / 8) * 512 + (s % 8) * 32 + (c % 32);
+      o[0] = a.x[p];
+      o[256] = i64 ? 0.f : a.base_f[p - sg.flat_offset + sg.src_offset];
+    }
+  }
 }
 
 // The rest of sdot_k_SKYLAKEX per pair from the 64 chain sums (flat.hip sdot_finish_kernel), with
@@ -663,253 +518,77 @@ __global__ __launch_bounds__(64) void fedadp_finish_kernel(AdpArgs a, float* out
   out_yy[pair] = float(tyy + kyy);
 }
 
-// Flag-synchronised form (tuning; one pair per workgroup, 4-position lanes): no s_barrier between
-// producers and chains.  Each producer wave adds 1 to full[slot] (an LDS counter) after writing its
-// part of a stage, the chain waves wait for kW arrivals, run the stage and add 1 to `done`; a
-// producer waits for the chains to have finished stage t - kRing before overwriting its slot.  So a
-// slow stage on one side no longer stalls the other at every tile (the barrier form pays the max of
-// both per tile).  Every wait is bounded: a wave that spins past kSpinMax raises `abort` in LDS and
-// every wait then returns at once, so the grid always drains (results of such a launch are garbage
-// and flagged in ws[0] as NaN by the finish kernel's inputs).
-constexpr uint32_t kSpinMax = 1u << 20;
+struct AdpLaunch {
+  void (*fn)(const AdpArgs&, hipStream_t);
+  bool uses_xb;
+};
 
-__device__ __forceinline__ bool adp_wait_geq(const uint32_t* ctr, uint32_t target, uint32_t* abort_flag) {
-  for (uint32_t spin = 0;; ++spin) {
-    if (__hip_atomic_load(ctr, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) return true;
-    if (__hip_atomic_load(abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
-    if (spin > kSpinMax) {
-      __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      return false;
-    }
-    __builtin_amdgcn_s_sleep(1);
-  }
+template <int kS, int kW, int kIt, int kD, int kF, int kProbe>
+void launch_adp_impl(const AdpArgs& a, hipStream_t st) {
+  const uint32_t pgs = uint32_t((a.n_pairs + 7) / 8 * 8);  // whole XCD rounds (padding workgroups return at once)
+  hipLaunchKernelGGL((fedadp_dots_kernel<kS, kW, kIt, kD, kF, kProbe>), dim3(pgs * 2), dim3(64 * (kW + 2)), 0, st, a);
 }
 
-template <int kC, int kS, int kW, int kIt, int kD, int kRing>
-__global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_flag_kernel(AdpArgs a) {
-  using Sh = AdpShape<1, kC, kS, kW, kIt, 0, 4>;
-  static_assert(kRing >= 2 && kRing <= 3, "2-3 tile slots");
-  __shared__ __attribute__((aligned(16))) float ring[kRing * Sh::kSlot];
-  __shared__ AdpSeg S[kMaxSegs];
-  __shared__ uint32_t full[kRing], done, abort_flag;
-  constexpr int kGroups = 64 / kC;
-  const int b = int(blockIdx.x), lo = b & 7;
-  const int cg = (b / 8) % kGroups;
-  const int pg = (b / (8 * kGroups)) * 8 + lo;
-  if (pg >= a.n_pairs) return;  // padding workgroup (before the barrier)
-  const int n_segs = int(a.n_segs);
-  for (int j = int(threadIdx.x); j < n_segs; j += int(blockDim.x)) {
-    const plato_agg_segment sg = a.segs[j];
-    S[j] = AdpSeg{uint32_t(sg.flat_offset), uint32_t(sg.flat_offset + sg.numel), uint32_t(sg.src_offset),
-                  (sg.region ? kSegI64 : 0u) | ((sg.flags & PLATO_AGG_SEG_NEG_DIV) ? kSegNeg : 0u)};
-  }
-  if (threadIdx.x < kRing) full[threadIdx.x] = 0;
-  if (threadIdx.x == 0) {
-    done = 0;
-    abort_flag = 0;
-  }
-  __syncthreads();  // the only workgroup barrier
-  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = int(threadIdx.x & 63);
-  const uint32_t nst = uint32_t((a.nsteps + kS - 1) / kS);
-  const bool xx_active = pg == 0 && a.with_xx;
-  const uint32_t nchain = xx_active ? 2u : 1u;
-  if (wave >= 2) {  // producer
-    const int w = wave - 2;
-    AdpSrc<1> src;
-    src.x = adp_rsrc(a.x, a.nsteps * 256);
-    src.b = adp_rsrc(a.base_f, a.n_f32 * 4);
-    src.y[0] = adp_rsrc(sld(a.xf, pg), a.n_f32 * 4);
-    AdpCursor cursor;
-    adp_cursor_load(S, 0, cursor);
-    AdpRegs4<1, kIt> regs[kD];
-#pragma unroll
-    for (int j = 0; j < kD; ++j)
-      adp_issue4<1, kC, kS, kW, kIt, 0>(a, S, n_segs, cursor, src, uint32_t(j) < nst ? uint32_t(j) : nst, cg, w, lane,
-                                        regs[j]);
-    for (uint32_t t0 = 0; t0 < nst; t0 += kD) {
-#pragma unroll
-      for (int j = 0; j < kD; ++j) {
-        const uint32_t t = t0 + j;
-        if (t < nst) {  // wave-uniform
-          if (t >= uint32_t(kRing)) adp_wait_geq(&done, nchain * (t + 1 - kRing), &abort_flag);
-          adp_write4<1, kC, kS, kW, kIt, 0, 0>(a, S, n_segs, ring + (t % kRing) * Sh::kSlot, pg, w, lane, regs[j]);
-          const uint32_t nxt = t + kD;
-          adp_issue4<1, kC, kS, kW, kIt, 0>(a, S, n_segs, cursor, src, nxt < nst ? nxt : nst, cg, w, lane, regs[j]);
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this wave's part of stage t is in LDS
-          if (lane == 0) atomicAdd(&full[t % kRing], 1u);
-        }
-      }
-    }
-    return;
-  }
-  const bool xx = wave == 1;
-  if (xx && !xx_active) return;
-  __builtin_amdgcn_s_setprio(3);
-  const int kind = xx ? 0 : lane >> 5, c = xx ? lane % kC : (lane & 31);
-  const int arow = (xx || kind == 0 ? 0 : Sh::kVR) + Sh::row(c);
-  const int brow = (xx ? 0 : Sh::kVR) + Sh::row(c);
-  float acc = 0.f;
-  for (uint32_t t = 0; t < nst; ++t) {
-    adp_wait_geq(&full[t % kRing], uint32_t(kW) * (t / kRing + 1), &abort_flag);
-    const float* slot = ring + (t % kRing) * Sh::kSlot;
-    const float* A = slot + arow;
-    const float* B = slot + brow;
-    const uint64_t left = a.nsteps - uint64_t(t) * kS;
-    if (left >= uint64_t(kS)) {
-      f4v av[4], bv[4], an[4], bn[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        av[q] = *reinterpret_cast<const f4v*>(A + 4 * q);
-        bv[q] = *reinterpret_cast<const f4v*>(B + 4 * q);
-      }
-#pragma unroll
-      for (int blk = 0; blk < kS / 16; ++blk) {
-        if (blk + 1 < kS / 16) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            an[q] = *reinterpret_cast<const f4v*>(A + 16 * (blk + 1) + 4 * q);
-            bn[q] = *reinterpret_cast<const f4v*>(B + 16 * (blk + 1) + 4 * q);
-          }
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          acc = chain_fma(av[q].x, bv[q].x, acc);
-          acc = chain_fma(av[q].y, bv[q].y, acc);
-          acc = chain_fma(av[q].z, bv[q].z, acc);
-          acc = chain_fma(av[q].w, bv[q].w, acc);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          av[q] = an[q];
-          bv[q] = bn[q];
-        }
-      }
-    } else {
-      for (int s = 0; s < int(left); ++s) acc = chain_fma(A[s], B[s], acc);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");  // this stage's reads are consumed
-    if (lane == 0) atomicAdd(&done, 1u);
-  }
-  if (__hip_atomic_load(&abort_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) acc = __builtin_nanf("");
-  const int chain = cg * kC + c;
-  if (!xx) {
-    a.ws[uint64_t(pg) * 128 + uint64_t(kind) * 64 + chain] = acc;
-  } else if (lane < kC) {  // the virtual pair (g, g)
-    a.ws[uint64_t(a.n_pairs) * 128 + chain] = acc;
-    a.ws[uint64_t(a.n_pairs) * 128 + 64 + chain] = acc;
-  }
+template <int kS, int kW, int kIt, int kD, int kF, int kProbe = 0>
+constexpr AdpLaunch adp_launch() {
+  return AdpLaunch{&launch_adp_impl<kS, kW, kIt, kD, kF, kProbe>, (kF & kFXB) != 0};
 }
 
-template <int kC, int kS, int kW, int kIt, int kD, int kRing>
-void launch_adp_flag(const AdpArgs& a, hipStream_t st) {
-  constexpr int kGroups = 64 / kC;
-  const uint32_t pgs = uint32_t((a.n_pairs + 7) / 8 * 8);
-  hipLaunchKernelGGL((fedadp_dots_flag_kernel<kC, kS, kW, kIt, kD, kRing>), dim3(pgs * kGroups), dim3(64 * (kW + 2)), 0,
-                     st, a);
-}
-
-template <int kP, int kC, int kS, int kW, int kIt, int kVRpad, int kProbe = 0, int kIso = 0, int kV = 1, int kD = 2,
-          int kCP = 1, int kPrio = 3, int kSw = 0, int kNt = 0>
-void launch_adp(const AdpArgs& a, hipStream_t st) {
-  constexpr int kGroups = 64 / kC;
-  uint32_t pgs = uint32_t((a.n_pairs + kP - 1) / kP);
-  pgs = (pgs + 7) / 8 * 8;  // whole XCD rounds (padding workgroups return at once)
-  hipLaunchKernelGGL((fedadp_dots_kernel<kP, kC, kS, kW, kIt, kVRpad, kProbe, kIso, kV, kD, kCP, kPrio, kSw, kNt>), dim3(pgs * kGroups),
-                     dim3((64 * adp_waves<kW, kIso>())), 0, st, a);
-}
-using AdpFn = void (*)(const AdpArgs&, hipStream_t);
-// pairs x chains per workgroup, steps per stage, producer waves, iterations, vector pad
-// The product's shape (tuning variant 23): one pair and 32 of its 64 chains per workgroup, so a
-// gather reads whole 128-byte lines, 16 bytes per lane (x and b come once per pair, from L2);
-// 1.94 ms for 128 ResNet-18 clients against 5.4 ms for variant 0 (profiles/r03i_fedadp.log); with
-// the swizzled rows (variant 51: no LDS bank conflicts, LDS-array cycles 450 M -> 181 M) 1.90 ms
-// (profiles/r03w_fedadp.log)
-constexpr AdpFn kAdpDefault = &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2>;
+// The product's shape: 192-step stages of 12 producer waves x 2 iterations, x and b from the
+// chain-group-major buffer, the client arenas read non-temporally (once-read, kept out of the L2
+// the re-read x and b live in), the division as a float64 product
+constexpr AdpLaunch kAdpDefault = adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB>();
 #ifdef PLATO_AGG_TUNE
-const AdpFn kAdpVariants[] = {
-    &launch_adp<8, 4, 256, 8, 2, 0>,     // 0: 16 B per block per vector, x and b shared by 8 pairs
-    &launch_adp<4, 8, 256, 8, 4, 16>,    // 1: 32 B
-    &launch_adp<2, 16, 256, 8, 8, 32>,   // 2: 64 B
-    &launch_adp<1, 32, 128, 8, 8, 0>,    // 3: whole 128-byte lines, x and b per pair (from L2)
-    &launch_adp<2, 16, 192, 12, 4, 32>,  // 4: variant 2 with 12 producer waves
-    &launch_adp<2, 16, 128, 8, 4, 32>,   // 5: variant 2, half stages
-    &launch_adp<2, 16, 256, 8, 8, 32, 1>,  // 6: probe of 2 without the division (wrong results)
-    &launch_adp<2, 16, 256, 8, 8, 32, 2>,  // 7: probe of 2 without the chains (wrong results)
-    &launch_adp<2, 16, 256, 8, 8, 32, 3>,  // 8: probe of 2 without the loads (wrong results)
-    &launch_adp<2, 16, 256, 8, 8, 32, 4>,  // 9: probe of 2: the chains alone (wrong results)
-    &launch_adp<2, 16, 256, 8, 8, 32, 5>,  // 10: probe of 2: chains without LDS reads (wrong results)
-    &launch_adp<2, 16, 256, 8, 8, 32, 0, 1>,  // 11: variant 2, chain waves on a SIMD of their own
-    &launch_adp<2, 16, 128, 8, 4, 32, 0, 1>,  // 12: variant 5, chain waves on a SIMD of their own
-    &launch_adp<4, 8, 256, 8, 4, 16, 0, 1>,   // 13: variant 1, chain waves on a SIMD of their own
-    &launch_adp<1, 32, 128, 8, 8, 0, 0, 1>,   // 14: variant 3, chain waves on a SIMD of their own
-    &launch_adp<2, 16, 256, 8, 8, 32, 4, 1>,  // 15: probe of 11: the chains alone (wrong results)
-    &launch_adp<2, 16, 256, 8, 8, 32, 2, 1>,  // 16: probe of 11: no chains (wrong results)
-    &launch_adp<2, 16, 256, 8, 8, 32, 6>,     // 17: probe of 2: cycle counts per wave into the workspace
-    &launch_adp<2, 16, 128, 8, 4, 32, 6, 1>,  // 18: probe of 12: cycle counts per wave into the workspace
-    &launch_adp<2, 16, 256, 8, 2, 32, 0, 0, 4>,  // 19: variant 2, 16-byte gathers
-    &launch_adp<2, 16, 128, 8, 1, 32, 0, 0, 4>,  // 20: variant 5, 16-byte gathers
-    &launch_adp<2, 16, 256, 8, 2, 32, 0, 1, 4>,  // 21: variant 19, chain waves on a SIMD of their own
-    &launch_adp<4, 8, 256, 8, 1, 16, 0, 0, 4>,   // 22: variant 1, 16-byte gathers
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4>,   // 23: variant 3, 16-byte gathers
-    &launch_adp<8, 4, 256, 4, 1, 0, 0, 0, 4>,    // 24: variant 0, 16-byte gathers (4 producer waves)
-    &launch_adp<2, 16, 256, 8, 2, 32, 6, 0, 4>,  // 25: probe of 19: cycle counts per wave into the workspace
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 3>,   // 26: variant 23, 3 stages of loads in flight
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 4>,   // 27: variant 23, 4 stages of loads in flight
-    &launch_adp<2, 16, 128, 8, 1, 32, 0, 0, 4, 4>,  // 28: variant 20, 4 stages of loads in flight
-    &launch_adp<1, 32, 128, 8, 2, 0, 6, 0, 4, 3>,   // 29: probe of 26: cycle counts per wave into the workspace
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 1, 4, 3>,   // 30: variant 26, chain waves on a SIMD of their own
-    &launch_adp<1, 32, 128, 8, 8, 0, 0, 0, 1, 3>,   // 31: variant 3, 3 stages of loads in flight
-    &launch_adp<1, 32, 192, 8, 3, 0, 0, 0, 4>,      // 32: variant 23 with 192-step stages
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 2>,  // 33: variant 23, chain reads 2 blocks ahead
-    &launch_adp<1, 32, 192, 8, 3, 0, 0, 0, 4, 2, 2>,  // 34: variant 32, chain reads 2 blocks ahead
-    &launch_adp<1, 32, 128, 8, 2, 0, 4, 0, 4>,      // 35: probe of 23: the chains alone (wrong results)
-    &launch_adp<1, 32, 128, 8, 2, 0, 2, 0, 4>,      // 36: probe of 23: no chains (wrong results)
-    &launch_adp<1, 32, 128, 8, 2, 0, 6, 0, 4>,      // 37: probe of 23: cycle counts per wave
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 3>,  // 38: variant 23, chain reads 3 blocks ahead
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 0>,  // 39: variant 23, chain wave at priority 0
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 1>,  // 40: variant 23, chain wave at priority 1
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 1, 4, 2, 1, 0>,  // 41: variant 30 (isolated chain SIMD), priority 0
-    &launch_adp<1, 32, 128, 4, 4, 0, 0, 0, 4, 2>,        // 42: variant 23 with 4 producer waves
-    &launch_adp<1, 32, 192, 12, 2, 0, 0, 0, 4, 2>,       // 43: variant 32 with 12 producer waves
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 1>,  // 44: variant 23 with the row gap (conflict-free writes)
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 1, 4, 2, 1, 3, 1>,  // 45: variant 30 with the row gap
-    &launch_adp<1, 32, 192, 8, 3, 0, 0, 0, 4, 2, 1, 3, 1>,  // 46: variant 32 with the row gap
-    &launch_adp<2, 16, 128, 8, 1, 32, 0, 0, 4, 2, 1, 3, 1>, // 47: variant 20 with the row gap
-    &launch_adp_flag<32, 128, 8, 2, 2, 2>,  // 48: variant 23 synchronised by LDS counters, 2 tile slots
-    &launch_adp_flag<32, 128, 8, 2, 2, 3>,  // 49: the same, 3 tile slots
-    &launch_adp_flag<32, 128, 8, 2, 3, 3>,  // 50: 3 tile slots, 3 stages of loads in flight
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2>,  // 51: variant 23 with swizzled rows (conflict-free writes)
-    &launch_adp<1, 32, 128, 8, 2, 0, 4, 0, 4, 2, 1, 3, 2>,  // 52: probe of 51: the chains alone (wrong results)
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 3, 1, 3, 2>,  // 53: variant 51, 3 stages of loads in flight
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 2, 3, 2>,  // 54: variant 51, chain reads 2 blocks ahead
-    &launch_adp<1, 32, 128, 8, 2, 0, 7, 0, 4, 2, 1, 3, 2>,  // 55: probe of 51: the producers alone (wrong results)
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2, 1>,  // 56: variant 51, client arenas read nt
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2, 2>,  // 57: variant 51, every load nt
-    &launch_adp<1, 32, 128, 8, 2, 0, 7, 0, 4, 2, 1, 3, 2, 1>,  // 58: probe of 56: the producers alone (wrong results)
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 3, 1, 3, 2, 1>,  // 59: variant 56, 3 stages of loads in flight
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2, 4>,  // 60: variant 51, division as a float64 product
-    &launch_adp<1, 32, 128, 8, 2, 0, 7, 0, 4, 2, 1, 3, 2, 4>,  // 61: probe of 60: the producers alone (wrong results)
-    &launch_adp<1, 32, 128, 8, 2, 0, 0, 0, 4, 2, 1, 3, 2, 5>,  // 62: variant 60, client arenas read nt
+const AdpLaunch kAdpVariants[] = {
+    kAdpDefault,                                            // 0: the default
+    adp_launch<128, 8, 2, 2, kFDiv64>(),                    // 1: round 3's stream (x flat, b from the arena), 128-step stages
+    adp_launch<128, 8, 2, 2, kFDiv64 | kFXB>(),             // 2: x and b chain-group-major, 128-step stages
+    adp_launch<192, 12, 2, 2, kFDiv64 | kFXB>(),            // 3: the default with plain (not nt) client loads
+    adp_launch<256, 8, 4, 2, kFYnt | kFDiv64 | kFXB>(),     // 4: 256-step stages of 8 waves x 4 iterations
+    adp_launch<128, 8, 2, 3, kFYnt | kFDiv64 | kFXB>(),     // 5: 128-step stages, 3 stages of loads in flight
+    adp_launch<192, 12, 2, 2, kFYnt | kFXB>(),              // 6: the default with the IEEE division
+    adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB, 1>(), // 7: probe: the default's chains alone
+    adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB, 2>(), // 8: probe: the default's producers alone
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)
-constexpr int kAdpProbes[] = {6, 7, 8, 9, 10, 15, 16, 17, 18, 25, 29, 35, 36, 37, 52, 55, 58, 61};
+constexpr int kAdpProbes[] = {7, 8};
 #endif
 
-int run_fedadp(AdpFn fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
-               const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs, uint32_t n_segs,
-               size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
-               float* d_out_yy, hipStream_t stream);
+int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64,
+               int n_pairs, const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
+               uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
+               float* d_out_xy, float* d_out_yy, hipStream_t stream);
+
+// workspace: [chain sums][descriptors][boundary rows + count][boundary table][xb], 256-byte aligned parts
+size_t align256(size_t v) { return (v + 255) / 256 * 256; }
+// Boundary groups per chain group: one ends at (and so holds) each segment start — at most n_segs
+// — plus the groups that lie wholly inside int64 entries, each holding 256 of the chain group's
+// int64 positions: at most n_i64 / 256
+size_t adp_max_bnd(uint32_t n_segs, size_t n_i64) { return 2 * (size_t(n_segs) + n_i64 / 256 + 1); }
+struct AdpWs {
+  size_t chains, desc, bnd_at, bnd, xb, total;
+};
+AdpWs adp_ws(int n_pairs, int with_xx, size_t n_i64, size_t n_flat, uint32_t n_segs) {
+  const size_t k = size_t(n_pairs > 0 ? n_pairs : 0);
+  const size_t nsteps = (n_flat & ~size_t(31)) / 64, ngroups = (nsteps + 7) / 8;
+  const size_t max_bnd = adp_max_bnd(n_segs, n_i64);
+  AdpWs w{};
+  w.chains = 0;
+  w.desc = align256((k + (with_xx ? 1 : 0)) * 128 * sizeof(float));
+  w.bnd_at = align256(w.desc + 2 * ngroups * sizeof(AdpDesc));
+  w.bnd = align256(w.bnd_at + (max_bnd + 1) * sizeof(uint32_t));
+  w.xb = align256(w.bnd + k * max_bnd * 256 * sizeof(float));
+  w.total = w.xb + 2 * ngroups * 512 * sizeof(float);
+  return w;
+}
 
 }  // namespace
 
 extern "C" {
 
-size_t plato_agg_fedadp_dots_workspace(int n_pairs, int with_xx, size_t n_i64) {
-  const size_t k = size_t(n_pairs > 0 ? n_pairs : 0);
-  return ((k + (with_xx ? 1 : 0)) * 128 + k * n_i64) * sizeof(float);
+size_t plato_agg_fedadp_dots_workspace(int n_pairs, int with_xx, size_t n_i64, size_t n_flat, uint32_t n_segs) {
+  return adp_ws(n_pairs, with_xx, n_i64, n_flat, n_segs).total;
 }
 
 int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
@@ -943,20 +622,23 @@ int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const*
 }  // extern "C"
 
 namespace {
-int run_fedadp(AdpFn fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,
-               const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs, uint32_t n_segs,
-               size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
-               float* d_out_yy, hipStream_t stream) {
-  if (n_pairs <= 0 || n_pairs > (1 << 20)) return set_error(PLATO_AGG_EINVAL, "n_pairs must be in [1, 2^20]");
+int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64,
+               int n_pairs, const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
+               uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
+               float* d_out_xy, float* d_out_yy, hipStream_t stream) {
+  if (n_pairs <= 0 || n_pairs > 65535) return set_error(PLATO_AGG_EINVAL, "n_pairs must be in [1, 65535]");
   if (with_xx != 0 && with_xx != 1) return set_error(PLATO_AGG_EINVAL, "with_xx must be 0 or 1");
   if (!d_x || !d_src_f32 || !d_src_i64 || !d_base_f32 || !d_segs || !d_workspace || !d_out_xy || !d_out_yy ||
       (n_i64 && !d_base_i64))
     return set_error(PLATO_AGG_EINVAL, "null pointer");
-  if (reinterpret_cast<uintptr_t>(d_x) & 15u) return set_error(PLATO_AGG_EINVAL, "x must be 16-byte aligned");
-  if (n_segs == 0 || n_segs > uint32_t(kMaxSegs))
-    return set_error(PLATO_AGG_EINVAL, "segment count must be in [1, 2048]");
-  if (n_flat == 0 || n_flat >= (size_t(1) << 32)) return set_error(PLATO_AGG_EINVAL, "flat length must be in [1, 2^32)");
+  if ((reinterpret_cast<uintptr_t>(d_x) & 15u) || (reinterpret_cast<uintptr_t>(d_workspace) & 255u))
+    return set_error(PLATO_AGG_EINVAL, "x must be 16-byte and the workspace 256-byte aligned");
+  if (n_segs == 0 || n_segs >= (1u << 22)) return set_error(PLATO_AGG_EINVAL, "segment count must be in [1, 2^22)");
+  if (n_flat == 0 || n_flat >= (size_t(1) << 30)) return set_error(PLATO_AGG_EINVAL, "flat length must be in [1, 2^30)");
   if (n_f32 >= (size_t(1) << 30)) return set_error(PLATO_AGG_EINVAL, "fp32 arena must be < 2^30 elements");
+  if (n_i64 >= (size_t(1) << 30)) return set_error(PLATO_AGG_EINVAL, "int64 region must be < 2^30 elements");
+  const AdpWs w = adp_ws(n_pairs, with_xx, n_i64, n_flat, n_segs);
+  char* ws = static_cast<char*>(d_workspace);
   AdpArgs a{};
   a.x = d_x;
   a.xf = reinterpret_cast<const float* const*>(d_src_f32);
@@ -967,22 +649,36 @@ int run_fedadp(AdpFn fn, const float* d_x, const void* const* d_src_f32, const v
   a.n_segs = n_segs;
   a.n = n_flat;
   a.nsteps = (uint64_t(n_flat) & ~uint64_t(31)) / 64;
+  a.ngroups = uint32_t((a.nsteps + 7) / 8);
+  a.max_bnd = uint32_t(adp_max_bnd(n_segs, n_i64));
   a.lr = lr;
-  a.ws = static_cast<float*>(d_workspace);
-  a.y64 = a.ws + (uint64_t(n_pairs) + (with_xx ? 1 : 0)) * 128;
+  a.inv_lr = 1.0 / double(lr);
+  a.ws = reinterpret_cast<float*>(ws + w.chains);
+  a.desc = reinterpret_cast<AdpDesc*>(ws + w.desc);
+  a.bnd_at = reinterpret_cast<uint32_t*>(ws + w.bnd_at);
+  a.n_bnd = a.bnd_at + a.max_bnd;
+  a.bnd = reinterpret_cast<float*>(ws + w.bnd);
+  a.xb = reinterpret_cast<const float*>(ws + w.xb);
   a.n_i64 = n_i64;
   a.n_f32 = n_f32;
   a.n_pairs = n_pairs;
   a.with_xx = with_xx;
-  if (n_i64) {
-    hipLaunchKernelGGL(fedadp_i64_kernel, dim3(uint32_t(n_pairs)), dim3(64), 0, stream, a);
-    if (int rc = check_launch("fedadp_i64 launch")) return rc;
-  }
   if (a.nsteps) {
-    fn(a, stream);
+    hipLaunchKernelGGL(fedadp_desc_kernel, dim3((2 * a.ngroups + 255) / 256), dim3(256), 0, stream, a);
+    if (int rc = check_launch("fedadp_desc launch")) return rc;
+    hipLaunchKernelGGL(fedadp_rows_kernel, dim3(1), dim3(1024), 0, stream, a);
+    if (int rc = check_launch("fedadp_rows launch")) return rc;
+    hipLaunchKernelGGL(fedadp_boundary_kernel, dim3(a.max_bnd, uint32_t(n_pairs)), dim3(256), 0, stream, a);
+    if (int rc = check_launch("fedadp_boundary launch")) return rc;
+    if (fn.uses_xb) {
+      hipLaunchKernelGGL(fedadp_prep_kernel, dim3(uint32_t((a.nsteps * 64 + kPrepSpan - 1) / kPrepSpan)), dim3(256), 0,
+                         stream, a, reinterpret_cast<float*>(ws + w.xb));
+      if (int rc = check_launch("fedadp_prep launch")) return rc;
+    }
+    fn.fn(a, stream);
     if (int rc = check_launch("fedadp_dots launch")) return rc;
   } else {
-    (void)hipMemsetAsync(d_workspace, 0, (size_t(n_pairs) + (with_xx ? 1 : 0)) * 128 * sizeof(float), stream);
+    (void)hipMemsetAsync(a.ws, 0, (size_t(n_pairs) + (with_xx ? 1 : 0)) * 128 * sizeof(float), stream);
   }
   hipLaunchKernelGGL(fedadp_finish_kernel, dim3(uint32_t(n_pairs + with_xx)), dim3(64), 0, stream, a, d_out_xy,
                      d_out_yy);

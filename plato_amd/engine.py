@@ -29,7 +29,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .arena import CODECS, F32, I64, ArenaLayout, payload_codec
+from .arena import CODECS, F32, I64, ArenaLayout, fedadp_order, payload_codec
 from .staging import HostPacker, PinnedRing, ResultPool, arena_source, payload_fingerprint
 
 
@@ -159,6 +159,8 @@ class FedAvgEngine:
 
     #: QSGD kernel variant (tuning / tests; None = the library default)
     qsgd_variant: int | None = None
+    #: arena alignment of the layouts this engine builds (arena.ALIGNMENTS; FedAdp servers: "fedadp")
+    layout_align: str | None = None
 
     def __init__(self, device=None, variant: int | None = None):
         self.device = require_device(device)
@@ -179,7 +181,7 @@ class FedAvgEngine:
     def _prepare(self, template: Mapping[str, torch.Tensor], k: int, codec: str = "native") -> ArenaLayout:
         if codec not in CODECS:
             raise ValueError(f"unknown payload codec {codec!r}")
-        layout = ArenaLayout.from_state_dict(template)
+        layout = ArenaLayout.from_state_dict(template, align=self.layout_align)
         if self._layout is None or self._layout.signature != layout.signature:
             self._layout = layout
             self._slabs = {}
@@ -549,6 +551,25 @@ class FedAvgEngine:
         return layout.unpack(out_f[: layout.n_f32].to("cpu"), out_i[: layout.n_i64].to("cpu"))
 
 
+class _KernelTimer:
+    """HIP events on ``stream`` around the launches of a ``with`` block; the round's ``timings[name + "_ms"]``
+    is filled once the stream has passed them (``AggregationRound._resolve_timers``, after the method's sync)."""
+
+    def __init__(self, rnd: "AggregationRound", name: str, stream):
+        self.rnd, self.name, self.stream = rnd, name, stream
+
+    def __enter__(self):
+        self.e0 = torch.cuda.Event(enable_timing=True)
+        self.e0.record(self.stream)
+        return self
+
+    def __exit__(self, *exc):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(self.stream)
+        self.rnd._timers.append((self.name, self.e0, e1))
+        return False
+
+
 class AggregationRound:
     """One aggregation: client rows staged H2D (in any order), then one launch.
 
@@ -579,6 +600,16 @@ class AggregationRound:
         self.timings: dict = {}
         self._k = 0
         self._decoded = None
+        self._timers: list = []
+
+    def _timed(self, name: str, stream) -> _KernelTimer:
+        return _KernelTimer(self, name, stream)
+
+    def _resolve_timers(self) -> None:
+        """Device times of the timed launches (call after the stream has been synchronised)."""
+        for name, e0, e1 in self._timers:
+            self.timings[name + "_ms"] = e0.elapsed_time(e1)
+        self._timers = []
 
     @property
     def _base(self) -> DeviceArena:
@@ -602,6 +633,7 @@ class AggregationRound:
         pf, pi = self.slab.row_pointers([slot])
         self._pf[slot], self._pi[slot] = int(pf[0]), int(pi[0])
         self.staged[slot] = True
+        self._decoded = None  # decoded rows are per staged set
 
     def _coded_scales(self, slot: int, payload) -> None:
         if self.codec != "qsgd":
@@ -626,6 +658,7 @@ class AggregationRound:
         self._coded_scales(slot, payload)
         self._pf[slot], self._pi[slot] = hit
         self.staged[slot] = True
+        self._decoded = None  # decoded rows are per staged set
         return True
 
     def launch(self, weights: Sequence[float], scales: Sequence[float] | None = None,
@@ -903,12 +936,14 @@ class AggregationRound:
             keep = (dt, dl, ds, dn, idx)
         nef, nei = int(ef.shape[0]), int(ei.shape[0])
         if nef or nei:
-            _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti) if n_i else None, k, _ptr(self._base.f32),
-                      _ptr(self._base.i64) if n_i else None, _ptr(ef) if nef else None, nef, _ptr(ei) if nei else None,
-                      nei, n_e, lay.n_f32, n_i, _ptr(out), _stream_handle(stream))
+            with self._timed("entry_norms", stream):
+                _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti) if n_i else None, k, _ptr(self._base.f32),
+                          _ptr(self._base.i64) if n_i else None, _ptr(ef) if nef else None, nef,
+                          _ptr(ei) if nei else None, nei, n_e, lay.n_f32, n_i, _ptr(out), _stream_handle(stream))
         if long_ids:
             stream.wait_stream(eng.side_stream())
         res = np.ascontiguousarray(out.cpu().numpy().reshape(k, n_e).T)
+        self._resolve_timers()
         del keep
         return res
 
@@ -1005,8 +1040,7 @@ class AggregationRound:
 
     def _fedadp_order(self):
         lay = self.layout
-        names = lay.keys()
-        order = sorted(range(len(names)), key=lambda i: names[i].lower())
+        order = fedadp_order(lay.keys())
         if order and lay.entries[order[0]].region != F32:
             raise ValueError("FedAdp: the first entry in name order is int64, so the reference flattens to "
                              "float64 (np.append) and takes float64 dots; the device path reproduces the "
@@ -1041,13 +1075,15 @@ class AggregationRound:
                                            dtype=np.int64)).to(eng.device)
         xy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         yy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
-        ws = torch.empty(-(-_lib.lib().plato_agg_fedadp_dots_workspace(k, 1, lay.n_i64) // 4), dtype=torch.float32,
-                         device=eng.device)
+        ws = torch.empty(-(-_lib.lib().plato_agg_fedadp_dots_workspace(k, 1, lay.n_i64, n_flat, len(order)) // 4),
+                         dtype=torch.float32, device=eng.device)
         n_i = lay.n_i64
-        _lib.call("plato_agg_fedadp_dots", g_flat.data_ptr(), ptrs.data_ptr(), ptrs.data_ptr() + 8 * k, k,
-                  _ptr(self._base.f32), _ptr(self._base.i64) if n_i else None, segs.data_ptr(), len(order), n_flat,
-                  lay.n_f32, n_i, float(lr), 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(), _stream_handle(stream))
+        with self._timed("fedadp_dots", stream):
+            _lib.call("plato_agg_fedadp_dots", g_flat.data_ptr(), ptrs.data_ptr(), ptrs.data_ptr() + 8 * k, k,
+                      _ptr(self._base.f32), _ptr(self._base.i64) if n_i else None, segs.data_ptr(), len(order), n_flat,
+                      lay.n_f32, n_i, float(lr), 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(), _stream_handle(stream))
         xy_h, yy_h = xy.cpu().numpy(), yy.cpu().numpy()  # stream-ordered D2H (syncs this stream)
+        self._resolve_timers()
         self._keep_flat = (g_flat, ptrs, ws)
         return xy_h[:k], xy_h[k], yy_h[:k]
 
@@ -1133,10 +1169,14 @@ class AggregationRound:
         ws = torch.empty(max(1, eng.lib.plato_agg_np_sumsq_workspace(k, n_chunks) // 4), dtype=torch.float32,
                          device=eng.device)
         dev_out = torch.empty((k, n_p), dtype=torch.float32, device=eng.device)
-        _lib.call("plato_agg_np_sumsq", tf.data_ptr(), k, _ptr(self._base.f32), pieces.data_ptr(), first.data_ptr(),
-                  n_p, n_chunks, ws.data_ptr(), dev_out.data_ptr(), _stream_handle(stream))
+        with self._timed("np_sumsq", stream):
+            _lib.call("plato_agg_np_sumsq", tf.data_ptr(), k, _ptr(self._base.f32), pieces.data_ptr(),
+                      first.data_ptr(), n_p, n_chunks, ws.data_ptr(), dev_out.data_ptr(), _stream_handle(stream))
         out[:, entry_of] = dev_out.cpu().numpy()
+        self._resolve_timers()
         return out
+
+    PORT_NORMS_MAX_SEGS = 2048  # csrc/port.hip kMaxSegs
 
     def model_similarities(self, reference: Mapping[str, torch.Tensor], slots: Sequence[int],
                            eps: float = 1e-8, threads: int | None = None, flat_norms: bool = False) -> list[np.float32]:
@@ -1182,6 +1222,10 @@ class AggregationRound:
         stride = max(64, -(-n_flat // 64) * 64)
         k = len(slots)
         h = _stream_handle(stream)
+        # plato_agg_port_norms keeps the segment map in LDS (<= PORT_NORMS_MAX_SEGS entries) and takes
+        # n_flat < 2^31, n_f32 < 2^30: larger models take the flatten + entry_norms path (same bits)
+        if n_segs > self.PORT_NORMS_MAX_SEGS or n_flat >= 1 << 31 or lay.n_f32 >= 1 << 30:
+            flat_norms = True
         norms = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         ws = torch.empty(max(1, eng.lib.plato_agg_torch_cosine_workspace(k, threads) // 4), dtype=torch.float32,
                          device=eng.device)
@@ -1210,16 +1254,19 @@ class AggregationRound:
                              + [flat.data_ptr() + r * stride * 4 for r in range(k + 1)], dtype=np.int64)
             vt = torch.from_numpy(vec).to(eng.device)
             v8, n1 = vt.data_ptr(), 8 * (k + 1)
-            _lib.call("plato_agg_port_norms", v8, v8 + n1, v8 + 2 * n1, v8 + 3 * n1, k + 1, None, segs.data_ptr(),
-                      n_segs, n_flat, lay.n_f32, _lib.PLATO_AGG_PORT_CAST_FIRST, norms.data_ptr(), v8 + 4 * n1, h)
-            # current - previous over its norm once (not once per client), then the K cascade sums
             scaled = torch.empty(stride, dtype=torch.float32, device=eng.device)
-            _lib.call("plato_agg_scale_by_norm", flat.data_ptr(), n_flat, norms.data_ptr(), float(eps), scaled.data_ptr(),
-                      h)
-            _lib.call("plato_agg_torch_cosine_sum_scaled", scaled.data_ptr(), v8 + 4 * n1 + 8, k, n_flat,
-                      norms.data_ptr() + 4, float(eps), threads, ws.data_ptr(), out.data_ptr(), h)
+            with self._timed("port_norms", stream):
+                _lib.call("plato_agg_port_norms", v8, v8 + n1, v8 + 2 * n1, v8 + 3 * n1, k + 1, None, segs.data_ptr(),
+                          n_segs, n_flat, lay.n_f32, _lib.PLATO_AGG_PORT_CAST_FIRST, norms.data_ptr(), v8 + 4 * n1, h)
+            # current - previous over its norm once (not once per client), then the K cascade sums
+            with self._timed("port_cosine", stream):
+                _lib.call("plato_agg_scale_by_norm", flat.data_ptr(), n_flat, norms.data_ptr(), float(eps),
+                          scaled.data_ptr(), h)
+                _lib.call("plato_agg_torch_cosine_sum_scaled", scaled.data_ptr(), v8 + 4 * n1 + 8, k, n_flat,
+                          norms.data_ptr() + 4, float(eps), threads, ws.data_ptr(), out.data_ptr(), h)
             keep = (vt, flat, scaled)
         stream.synchronize()
+        self._resolve_timers()
         del keep
         self.last_norms = norms.cpu().numpy()
         return [np.float32(v) for v in out.cpu().numpy()]
@@ -1278,6 +1325,7 @@ class _DecodedRound(AggregationRound):
         self._t0 = parent._t0
         self._kernel_events = None
         self.timings = {}
+        self._timers = []
         self._k = 0
         self._decoded = None
         self._own_base = DeviceArena(layout, eng.device)

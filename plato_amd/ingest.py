@@ -159,24 +159,34 @@ def _buffer(data):
     return arr.ctypes.data, arr.size, arr
 
 
-_parse_cap = 256  # output capacity of the last parse that fitted (payloads of one server repeat their size)
+# output capacity per payload length: the parser's capacity-exceeded exit is slow (~20 ms on a ResNet-18
+# payload), and the payloads of one server repeat their length, so the tensor count a length parsed to is
+# remembered (a bounded table: one large payload no longer makes every later parse allocate for it)
+_PARSE_CAP_DEFAULT = 256
+_parse_caps: "OrderedDict[int, int]" = OrderedDict()
+_PARSE_CAPS_KEPT = 64
+_parse_caps_lock = threading.Lock()
 
 
 def parse(data) -> tuple[list[TensorInfo], list[str], object]:
     """Parse pickled payload bytes; returns (tensor infos, keys, keepalive)."""
-    global _parse_cap
     addr, n, keep = _buffer(data)
     h = lib()
-    cap = _parse_cap
+    with _parse_caps_lock:
+        cap = _parse_caps.get(n, _PARSE_CAP_DEFAULT)
     while True:
         out = (TensorInfo * cap)()
         rc = h.plato_ingest_parse(addr, n, out, cap)
-        if rc == -5:  # capacity: the parser's failure path is slow (~20 ms on a ResNet-18 payload), so the
-            cap *= 8  # capacity that fitted is remembered for the next payload
-            _parse_cap = cap
+        if rc == -5:  # capacity
+            cap *= 8
             continue
         if rc < 0:
             raise IngestError(f"payload rejected ({rc}): {h.plato_ingest_last_error().decode()}")
+        with _parse_caps_lock:
+            _parse_caps[n] = max(rc, 1)
+            _parse_caps.move_to_end(n)
+            while len(_parse_caps) > _PARSE_CAPS_KEPT:
+                _parse_caps.popitem(last=False)
         infos = list(out[:rc])
         keys = [bytes(keep[t.name_offset : t.name_offset + t.name_len]).decode("utf-8") for t in infos]
         return infos, keys, keep

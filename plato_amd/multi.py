@@ -140,8 +140,21 @@ class MultiDeviceEngine:
         return self._entries
 
     # ------------------------------------------------------------ layout
+    @property
+    def layout_align(self) -> str | None:
+        """Arena alignment of the layouts this engine builds (passed on to every per-device engine)."""
+        return self.primary.layout_align
+
+    @layout_align.setter
+    def layout_align(self, align: str | None) -> None:
+        self.primary.layout_align = align
+        if self._entries is not None:
+            for eng in self._entries._engines:
+                eng.layout_align = align
+
     def _prepare(self, template: Mapping[str, torch.Tensor] | ArenaLayout) -> ArenaLayout:
-        layout = template if isinstance(template, ArenaLayout) else ArenaLayout.from_state_dict(template)
+        layout = (template if isinstance(template, ArenaLayout)
+                  else ArenaLayout.from_state_dict(template, align=self.layout_align))
         if self._layout is None or self._layout.signature != layout.signature:
             self._layout = layout
             self._plan = BucketPlan.for_layout(layout, self.world)

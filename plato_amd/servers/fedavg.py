@@ -48,8 +48,12 @@ class _EngineHolder:
     #: the round is sharded by whole entries over ``aggregation_devices``
     entry_local_weights = False
     #: FedAdp / Port: before the first round, check that this host's numpy / torch
-    #: reduction order is the one the device reproduces (plato_amd.hostorder)
-    host_order_check = True
+    #: reduction order is the one the device reproduces (plato_amd.hostorder):
+    #: "warn" logs a mismatch once and goes on, "strict" (or True) raises, False skips
+    host_order_check = "warn"
+    #: arena alignment of the round layouts (plato_amd.arena.ALIGNMENTS): FedAdp's servers align
+    #: every fp32 entry to its flattened position so the dot kernel reads whole lines
+    arena_alignment = None
 
     def aggregation_engine(self):
         eng = getattr(self, "_plato_amd_engine", None)
@@ -64,6 +68,7 @@ class _EngineHolder:
                 device = devices[0] if devices else self.aggregation_device
                 device = f"cuda:{device}" if isinstance(device, int) else device
                 eng = FedAvgEngine(device, variant=self.aggregation_variant)
+            eng.layout_align = self.arena_alignment
             self._plato_amd_engine = eng
         return eng
 

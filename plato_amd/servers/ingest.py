@@ -39,7 +39,7 @@ class WireIngestMixin:
     def _ingest_layout(self):
         try:
             baseline = self.algorithm.extract_weights()
-            layout = ArenaLayout.from_state_dict(baseline)
+            layout = ArenaLayout.from_state_dict(baseline, align=getattr(self, "arena_alignment", None))
         except (AttributeError, TypeError):
             return None
         cached = getattr(self, "_plato_amd_ingest_layout", None)

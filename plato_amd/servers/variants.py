@@ -72,8 +72,9 @@ class PortWeights(_EngineHolder):
 
         previous = torch.load(path, map_location="cpu", weights_only=True)
         threads = torch.get_num_threads() if self.port_threads is None else int(self.port_threads)
-        if self.host_order_check:
-            hostorder.check_port(rnd.engine.device, threads)  # this host's F.cosine_similarity order
+        check = hostorder.mode(self.host_order_check)
+        if check:  # this host's F.cosine_similarity order (a mismatch warns; "strict" refuses)
+            hostorder.check_port(rnd.engine.device, threads, strict=check == "strict")
         # coded payloads: the per-entry reductions run on the dequantized rows (model_dequantize semantics)
         sims = rnd.decoded().model_similarities(previous, need, threads=threads)
         out = [1.0] * len(updates)
@@ -221,6 +222,9 @@ class FedAdpWeights(_EngineHolder):
     """
 
     needs_staged_round = True
+    #: every fp32 entry at an arena offset congruent to its flattened position (arena.FEDADP_ALIGN):
+    #: the dot kernel's gathers then read whole 128-byte lines
+    arena_alignment = "fedadp"
 
     #: FedAdp's alpha; None = Config().algorithm.alpha, else 5 (fedadp_server.py:112-114)
     fedadp_alpha = None
@@ -246,8 +250,9 @@ class FedAdpWeights(_EngineHolder):
             if lr is None:
                 raise ValueError("FedAdp needs parameters.optimizer.lr (or set fedadp_lr)")
         alpha = self.fedadp_alpha if self.fedadp_alpha is not None else _config_attr("algorithm", "alpha", 5)
-        if self.host_order_check:
-            hostorder.check_fedadp(rnd.engine.device)  # this host's numpy sdot order
+        check = hostorder.mode(self.host_order_check)
+        if check:  # this host's numpy sdot order (a mismatch warns; "strict" refuses)
+            hostorder.check_fedadp(rnd.engine.device, lr, strict=check == "strict")
         inner, g_sq, l_sq = rnd.fedadp_dots(grads, range(k), lr)
         angles = W.fedadp_angles_from_dots(inner, g_sq, l_sq)
         contribs = W.fedadp_contributions(angles, self.selected_clients, self.local_angles,

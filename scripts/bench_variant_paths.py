@@ -45,9 +45,8 @@ def main():
     ap.add_argument("--fedadp-kernel", action="store_true",
                     help="HIP-event time of plato_agg_fedadp_dots alone (+ bitwise check against the flat path)")
     ap.add_argument("--fedadp-only", action="store_true", help="only the fedadp kernel timing (for PMC passes)")
-    ap.add_argument("--fedadp-cycles", type=int, default=None, metavar="VARIANT",
-                    help="run a cycle-count probe variant of plato_agg_tune_fedadp_dots and summarise its workspace")
     ap.add_argument("--port-only", action="store_true", help="only the port path (for kernel traces)")
+    ap.add_argument("--fedadp-align", default="fedadp", help="arena alignment of the FedAdp rounds ('' = packed)")
     ap.add_argument("--only", default=None, help="comma-separated paths to time")
     ap.add_argument("--norms-threshold", type=int, default=-1,
                     help="FedAvgEngine.norms_long_threshold for the fedatt path (0 = None; -1 = the default)")
@@ -59,7 +58,7 @@ def main():
                     help="time the entry_norms variants on Port's K+1 flattened vectors (one entry each)")
     args = ap.parse_args()
     args.sdot = args.sdot or args.sdot_only
-    args.fedadp_kernel = args.fedadp_kernel or args.fedadp_only or args.fedadp_cycles is not None
+    args.fedadp_kernel = args.fedadp_kernel or args.fedadp_only
 
     from plato_amd import workloads
     from plato_amd.arena import ArenaLayout
@@ -80,14 +79,23 @@ def main():
     fill_baseline(prev, 1)
     previous = layout.unpack(prev.f32[:n_f].cpu(), prev.i64[:n_i].cpu())
     del prev
-    rnd = engine.begin(baseline, k)
-    rnd.put_baseline(baseline)
-    fill_clients(rnd.slab, base, 0, k)  # the round's own slab, filled on the device
-    for s in range(k):
-        pf, pi = rnd.slab.row_pointers([s])
-        rnd._pf[s], rnd._pi[s] = int(pf[0]), int(pi[0])
-        rnd.staged[s] = True
-    torch.cuda.synchronize(dev)
+    def make_round(eng):
+        r = eng.begin(baseline, k)
+        r.put_baseline(baseline)
+        torch.cuda.synchronize(dev)  # the baseline's H2D (copy stream) before the fill reads it
+        fill_clients(r.slab, r.engine._base, 0, k)  # the round's own slab, filled on the device
+        for s in range(k):
+            pf, pi = r.slab.row_pointers([s])
+            r._pf[s], r._pi[s] = int(pf[0]), int(pi[0])
+            r.staged[s] = True
+        torch.cuda.synchronize(dev)
+        return r
+
+    rnd = make_round(engine)
+    # FedAdp's rounds run on arenas aligned to the flattened positions (FedAdpServerMixin.arena_alignment)
+    adp_engine = FedAvgEngine(dev)
+    adp_engine.layout_align = args.fedadp_align or None
+    rnd_adp = make_round(adp_engine) if (args.fedadp_kernel or not args.only or "fedadp" in args.only) else rnd
     slots = list(range(k))
     n_e = len(layout.entries)
     longest = max(e.numel for e in layout.entries)
@@ -95,13 +103,13 @@ def main():
 
     def fedadp():
         w = np.full((n_e, k), 1.0 / k)
-        grads = rnd.launch_entrywise(w, add_base=False, device=True)
-        rnd.fedadp_dots(grads, slots, 0.01)
+        grads = rnd_adp.launch_entrywise(w, add_base=False, device=True)
+        rnd_adp.fedadp_dots(grads, slots, 0.01)
 
     def fedadp_flat():
         w = np.full((n_e, k), 1.0 / k)
-        grads = rnd.launch_entrywise(w, add_base=False, device=True)
-        rnd.fedadp_dots_flat(grads, slots, 0.01)
+        grads = rnd_adp.launch_entrywise(w, add_base=False, device=True)
+        rnd_adp.fedadp_dots_flat(grads, slots, 0.01)
 
     prev_arena = rnd.stage_reference(previous)
     paths = {
@@ -125,7 +133,7 @@ def main():
                    "per-entry torch norms: 8 fma chains per (entry, client)"),
     }
     for name, (fn, nbytes, chain, what) in paths.items():
-        if (args.sdot_only or args.fedadp_only or args.fedadp_cycles is not None or args.port_gathered
+        if (args.sdot_only or args.fedadp_only or args.port_gathered
                 or args.polaris_variants):
             break
         if args.port_only and not name.startswith("port"):
@@ -146,7 +154,7 @@ def main():
                           "min_bytes": int(nbytes), "GBps_of_min_bytes": round(nbytes / (med * 1e-3) / 1e9, 1),
                           "serial_chain_steps": int(chain), "what": what}), flush=True)
     if args.fedadp_kernel:
-        fedadp_kernel(dev, rnd, slots, layout, args.reps, args.fedadp_cycles)
+        fedadp_kernel(dev, rnd_adp, slots, rnd_adp.layout, args.reps)
     if args.sdot:
         sdot_kernels(dev, k, n_f + n_i, args.reps)
     if args.port_norms:
@@ -157,7 +165,7 @@ def main():
         polaris_variants(dev, rnd, slots, layout, args.reps)
 
 
-def fedadp_kernel(dev, rnd, slots, layout, reps, cycles_variant=None):
+def fedadp_kernel(dev, rnd, slots, layout, reps):
     """plato_agg_fedadp_dots alone (HIP events on the launch stream), against the flatten + sdot_shared path."""
     from plato_amd import _lib
 
@@ -184,24 +192,6 @@ def fedadp_kernel(dev, rnd, slots, layout, reps, cycles_variant=None):
                                                     eng._base.i64.data_ptr(), segs.data_ptr(), len(order), n_flat,
                                                     layout.n_f32, layout.n_i64, 0.01, 1, ws.data_ptr(), xy.data_ptr(),
                                                     yy.data_ptr(), h))
-    if cycles_variant is not None:
-        ws.zero_()
-        runs[f"v{cycles_variant}"]()
-        torch.cuda.synchronize(dev)
-        c = ws[:256 * 48].view(torch.int32).cpu().numpy().astype(np.int64).reshape(256, 48)
-        simd = lambda hw: (hw >> 4) & 3  # HW_REG_HW_ID bits 5:4
-        out = {"fedadp_cycles_variant": cycles_variant, "chain_total": int(np.median(c[:, 0])),
-               "chain_barrier_wait": int(np.median(c[:, 1])), "chain_simd_of_wg0": int(simd(c[0, 2])),
-               "gg_simd_of_wg0": int(simd(c[0, 3]))}
-        for w in range(9):
-            blk = c[:, 8 + 4 * w: 12 + 4 * w]
-            if not blk[:, 0].any():
-                continue
-            out[f"p{w}"] = {"total": int(np.median(blk[:, 0])), "wait": int(np.median(blk[:, 1])),
-                            "write": int(np.median(blk[:, 2])), "simd_wg0": int(simd(blk[0, 3])),
-                            "same_simd_as_chain": float(np.mean(simd(blk[:, 3]) == simd(c[:, 2])))}
-        print(json.dumps(out), flush=True)
-        return
     # unique bytes: each client's fp32 arena + int64 counters once, the baseline and g_flat once
     uniq = k * (layout.n_f32 * 4 + layout.n_i64 * 8) + 2 * layout.n_f32 * 4 + n_flat * 4
     for name, fn in runs.items():

@@ -541,6 +541,8 @@ PORT_SPECS = {
                   ("n1", (), "i64"), ("e", (11,), "f32")],
     "tiny": [("a", (5,), "f32")],
     "i64_only_tail": [("a", (2048,), "f32"), ("n0", (3,), "i64")],
+    # more entries than plato_agg_port_norms' 2,048-entry segment map: the engine takes the flatten path
+    "many_entries": [(f"e{i}", (1 + i % 37,), "f32") if i % 11 else (f"n{i}", (), "i64") for i in range(2600)],
 }
 
 

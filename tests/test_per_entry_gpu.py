@@ -212,8 +212,11 @@ def test_fedatt_algorithm_is_bit_exact(engine, name):
     assert G.sha(ref.trunc_to_int64(_flat(layout, updated, "i64"))) == exp["loaded_i64_sha256"]
 
 
+@pytest.mark.parametrize("align", [None, "fedadp"])
 @pytest.mark.parametrize("name", ["fedadp_lenet5_k6", "fedadp_resnet18_k8"])
-def test_fedadp_server_matches_reference(engine, name):
+def test_fedadp_server_matches_reference(name, align):
+    """The product path (FedAdpServerMixin: arenas aligned to the flattened positions) and the packed
+    layout give the reference's weights, angles and model bit for bit."""
     from plato_amd.servers.variants import FedAdpServerMixin
 
     recipe, exp = CASES[name]["recipe"], CASES[name]["expected"]
@@ -222,9 +225,11 @@ def test_fedadp_server_matches_reference(engine, name):
     class Server(FedAdpServerMixin):
         aggregation_device = DEV
         fedadp_lr = 0.01
+        arena_alignment = align
 
     server = Server()
-    server._plato_amd_engine = engine
+    engine = server.aggregation_engine()
+    assert engine.layout_align == align
     server.current_round = recipe["current_round"]
     server.selected_clients = [c + 1 for c in G.order_of(recipe)]
     server.local_angles = {int(c): np.float32(float.fromhex(a)) for c, a in recipe.get("local_angles", {}).items()}
@@ -240,14 +245,16 @@ def test_fedadp_server_matches_reference(engine, name):
 
     # global gradient (deltas pass, no baseline) bit-exact; model bit-exact given the reference's weights
     rnd = engine.begin(base, recipe["k"])
+    assert rnd.layout.align == align
     rnd.put_baseline(base)
     for i, p in enumerate(pays):
         rnd.put_client(i, p)
     w1 = np.tile(np.asarray([u.report.num_samples for u in updates], dtype=np.float64)
                  / sum(u.report.num_samples for u in updates), (len(layout.entries), 1))
     g_f, g_i = rnd.launch_entrywise(w1, add_base=False, device=True)
-    assert G.sha(G.canon(g_f[: layout.n_f32].cpu().numpy())) == exp["global_grads_f32_sha256"]
-    assert G.sha(G.canon(g_i[: layout.n_i64].cpu().numpy())) == exp["global_grads_i64f_sha256"]
+    g_model = rnd.layout.unpack(g_f.cpu(), g_i.cpu())  # (the aligned arena has padding between entries)
+    assert G.sha(G.canon(_flat(layout, g_model, "f32"))) == exp["global_grads_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, g_model, "i64"))) == exp["global_grads_i64f_sha256"]
     # the fused gather kernel against the materialised-flatten path, whole and in batches of 1 and 3
     # clients (g.g rides with the last batch), and on client subsets and orders
     whole = rnd.fedadp_dots((g_f, g_i), range(recipe["k"]), 0.01)
@@ -293,15 +300,20 @@ def test_polaris_server_matches_reference(engine):
     assert sorted(set(range(1024)) - set(server.unexplored_clients)) == sorted(c for c in G.order_of(recipe))
 
 
+@pytest.mark.parametrize("align", [None, "fedadp"])
 @pytest.mark.parametrize("name", ["fedadp_lenet5_k6", "fedadp_resnet18_k8"])
-def test_fedadp_dots_tile_shapes_agree_bitwise(engine, name):
-    """Every tile shape of the fused gather + sdot kernel (tuning library) equals the flatten + sdot path."""
+def test_fedadp_dots_tile_shapes_agree_bitwise(name, align):
+    """Every tile shape of the fused gather + sdot kernel (tuning library) equals the flatten + sdot path,
+    on packed and on FedAdp-aligned arenas."""
     from plato_amd import _lib
 
     recipe = CASES[name]["recipe"]
     layout, base, pays, _, updates = _host(recipe)
     k = recipe["k"]
+    engine = FedAvgEngine(DEV)
+    engine.layout_align = align
     rnd = engine.begin(base, k)
+    layout = rnd.layout
     rnd.put_baseline(base)
     for i, p in enumerate(pays):
         rnd.put_client(i, p)
@@ -453,3 +465,60 @@ def test_port_coded_payloads_with_stale_model_match_reference(tmp_path):
     updated = asyncio.run(Server().aggregate_weights(updates, base, pays))
     assert G.sha(G.canon(_flat(layout, updated, "f32"))) == case["expected"]["updated_f32_sha256"]
     assert G.sha(G.canon(_flat(layout, updated, "i64"))) == case["expected"]["updated_i64f_sha256"]
+
+
+def _many_entries(n_entries, seed):
+    """A model of n_entries small entries (1-300 elements, every 13th an int64 counter), names in
+    scrambled order so that FedAdp's name order reorders the arena."""
+    rng = np.random.default_rng(seed)
+    perm = rng.permutation(n_entries)
+    spec = []
+    for i in range(n_entries):
+        name = f"m{perm[i]:05d}"
+        if i % 13 == 5:
+            spec.append((name + ".num_batches_tracked", (), "i64"))
+        else:
+            spec.append((name + ".weight", (int(rng.integers(1, 300)),), "f32"))
+    # name order must start with an fp32 entry (the float32 case the device reproduces)
+    first = min(range(n_entries), key=lambda i: spec[i][0].lower())
+    spec[first] = (spec[first][0].replace(".num_batches_tracked", ".weight"), (7,), "f32")
+    return ArenaLayout.from_shapes(spec)
+
+
+@pytest.mark.parametrize("n_entries", [300, 2600])
+def test_fedadp_dots_many_entries_match_oracle(engine, n_entries):
+    """More entries than the round-3 kernel's 2,048-entry segment map: every boundary group goes through
+    the boundary table; the dots equal numpy's sdot order (oracle) and the flatten + sdot path bit for bit."""
+    from oracle import fedavg_oracle as FO
+    from oracle import reductions as R
+
+    layout = _many_entries(n_entries, n_entries)
+    rng = np.random.default_rng(7)
+    k, lr = 3, 0.03
+    bf = rng.standard_normal(layout.n_f32).astype(np.float32)
+    bi = rng.integers(-2**40, 2**40, layout.n_i64)
+    xs = [((bf + 0.01 * rng.standard_normal(layout.n_f32)).astype(np.float32), bi + rng.integers(-50, 50, layout.n_i64))
+          for _ in range(k)]
+    base = layout.unpack(torch.from_numpy(bf), torch.from_numpy(bi))
+    rnd = engine.begin(base, k)
+    rnd.put_baseline(base)
+    for i, (xf, xi) in enumerate(xs):
+        rnd.put_client(i, layout.unpack(torch.from_numpy(xf), torch.from_numpy(xi)))
+    w1 = np.tile(np.full(k, 1.0 / k), (len(layout.entries), 1))
+    g_f, g_i = rnd.launch_entrywise(w1, add_base=False, device=True)
+    inner, g_sq, l_sq = rnd.fedadp_dots((g_f, g_i), range(k), lr)
+    flat = rnd.fedadp_dots_flat((g_f, g_i), range(k), lr)
+    assert np.asarray(inner).tobytes() == np.asarray(flat[0]).tobytes()
+    assert np.float32(g_sq).tobytes() == np.float32(flat[1]).tobytes()
+    assert np.asarray(l_sq).tobytes() == np.asarray(flat[2]).tobytes()
+    # the oracle: process_grad in numpy / torch semantics, then sdot_k_SKYLAKEX's order
+    gh = layout.unpack(g_f[: layout.row_f32].cpu(), g_i[: max(1, layout.n_i64)].cpu())
+    g = FO.fedadp_flatten(gh, lr)
+    assert R.sdot(g, g).tobytes() == np.float32(g_sq).tobytes()
+    for i, (xf, xi) in enumerate(xs):
+        delta = {e.name: (layout.unpack(torch.from_numpy(xf), torch.from_numpy(xi))[e.name] - base[e.name])
+                 for e in layout.entries}
+        loc = FO.fedadp_flatten(delta, lr)
+        assert loc.dtype == np.float32 and loc.size == layout.n_f32 + layout.n_i64
+        assert R.sdot(g, loc).tobytes() == np.float32(inner[i]).tobytes(), i
+        assert R.sdot(loc, loc).tobytes() == np.float32(l_sq[i]).tobytes(), i
