@@ -27,8 +27,14 @@ sharded by whole entries instead (:attr:`MultiDeviceEngine.entries`,
 on its contiguous group of entries, every value stays on one GPU and the
 per-entry results are concatenated in layout order.  Rounds whose weights need
 serial reductions over the whole flattened model (Port's cosine similarity,
-FedAdp's dots: one fma chain per vector in the reference's order) run on the
-first device's engine (:attr:`MultiDeviceEngine.primary`).
+FedAdp's dots: one fma chain per vector in the reference's order) cannot cut the
+model, but each client's chain is independent of the others': they are staged and
+finished bucket-sharded like a plain round, and the reductions are split by
+client (:attr:`MultiDeviceEngine.clients`, :class:`ClientRound`) — client j's
+whole arena is assembled on GPU j mod N from the buckets, FedAdp's global
+gradient is formed bucket-sharded and all-gathered, and every GPU runs the
+single-GPU kernels on its own clients, so every value is still computed by one
+chain on one GPU, bit-identical to the one-GPU result.
 """
 
 from __future__ import annotations
@@ -127,10 +133,43 @@ class MultiDeviceEngine:
         self._arrival_free: dict = {}
         self._comm = None
         self._entries: "EntryShardedEngine | None" = None
+        self._clients: "ClientShardedEngine | None" = None
+        self._client_engines: list[FedAvgEngine] = [self.primary]
+        self._pool = None
 
     @property
     def world(self) -> int:
         return len(self.devices)
+
+    @property
+    def device(self) -> torch.device:
+        return self.devices[0]
+
+    @property
+    def clients(self) -> "ClientShardedEngine":
+        """The same devices for FedAdp / Port rounds: bucket-sharded staging, reductions split by client."""
+        if self._clients is None:
+            self._clients = ClientShardedEngine(self)
+        return self._clients
+
+    def client_engine(self, g: int) -> FedAvgEngine:
+        """The single-GPU engine on device g that holds the whole arenas of the clients ClientRound gives it."""
+        while len(self._client_engines) <= g:
+            eng = FedAvgEngine(self.devices[len(self._client_engines)], variant=self.variant)
+            eng.layout_align = self.layout_align
+            self._client_engines.append(eng)
+        return self._client_engines[g]
+
+    def each(self, fn, items):
+        """``[fn(item) ...]`` with one worker thread per device (torch / HIP calls release the GIL)."""
+        items = list(items)
+        if len(items) <= 1:
+            return [fn(x) for x in items]
+        if self._pool is None:
+            import concurrent.futures
+
+            self._pool = concurrent.futures.ThreadPoolExecutor(self.world, thread_name_prefix="plato-amd-device")
+        return list(self._pool.map(fn, items))
 
     @property
     def entries(self) -> "EntryShardedEngine":
@@ -148,6 +187,8 @@ class MultiDeviceEngine:
     @layout_align.setter
     def layout_align(self, align: str | None) -> None:
         self.primary.layout_align = align
+        for eng in self._client_engines:
+            eng.layout_align = align
         if self._entries is not None:
             for eng in self._entries._engines:
                 eng.layout_align = align
@@ -191,17 +232,20 @@ class MultiDeviceEngine:
             ring.fence(j, events)
 
     # ------------------------------------------------------------ rounds
-    def begin(self, template, capacity: int, codec: str = "native") -> "MultiRound":
+    def begin(self, template, capacity: int, codec: str = "native", client_split: bool = False) -> "MultiRound":
+        """A bucket-sharded round (``client_split``: a :class:`ClientRound`, native payloads)."""
         if capacity <= 0:
             raise ValueError("no client payloads to aggregate")
         if codec not in MULTI_CODECS:
             raise ValueError(f"codec {codec!r} is aggregated on one device (use .primary)")
+        if client_split and codec != "native":
+            raise ValueError("client-split rounds take native payloads (coded ones run on .primary)")
         layout = self._prepare(template)
         for shard in self._shards:
             shard.slab(codec, capacity)
             # the previous round's kernel may still read this round's rows
             shard.copy_stream.wait_stream(shard.stream)
-        return MultiRound(self, layout, capacity, codec)
+        return (ClientRound if client_split else MultiRound)(self, layout, capacity, codec)
 
     def prestage(self, payload: Mapping[str, torch.Tensor], baseline_layout: ArenaLayout) -> bool:
         """Copy an arriving payload's buckets to their GPUs now (adopted by the next round)."""
@@ -230,7 +274,7 @@ class MultiDeviceEngine:
             return None
         if hit[6] != payload_fingerprint(payload):
             return None  # edited after arrival: the round stages its current tensors
-        return hit[3]
+        return hit[3], [(f[hit[5]], i[hit[5]]) for f, i in hit[4]]
 
     def release_arrivals(self) -> None:
         for _, codec, _, _, slabs, row, _ in self._arrivals.values():
@@ -305,6 +349,7 @@ class MultiRound:
         self.codec = codec
         self.staged = [False] * capacity
         self._ptrs: list = [None] * capacity  # per slot: per shard (fp32 row ptr, int64 row ptr)
+        self._rows: list = [None] * capacity  # per slot: per shard (fp32 row, int64 row) tensors
         self.has_baseline = False
         self.events: list = []
         self._out = None
@@ -333,6 +378,7 @@ class MultiRound:
             ptrs.append((_row_ptr(f, slot), _row_ptr(i, slot)))
         eng._stage(payload, self.codec, rows)
         self._ptrs[slot] = ptrs
+        self._rows[slot] = rows
         self.staged[slot] = True
 
     def adopt(self, slot: int, payload) -> bool:
@@ -341,7 +387,7 @@ class MultiRound:
         hit = self.engine._arrival_rows(payload, self.layout, self.codec)
         if hit is None:
             return False
-        self._ptrs[slot] = hit
+        self._ptrs[slot], self._rows[slot] = hit
         self.staged[slot] = True
         return True
 
@@ -475,6 +521,263 @@ class MultiRound:
         self._out = None
         self._keep = None
         return self.layout.unpack(host_f, host_i)
+
+
+# --------------------------------------------------------------- client-split reductions
+class ClientShardedEngine:
+    """The devices of a :class:`MultiDeviceEngine` for rounds whose weights reduce the whole model per client.
+
+    FedAdp's dots (fedadp_server.py:91-99) and Port's similarity (port_server.py:36-52) are one serial
+    fma chain per (client, chain) over the flattened model: a bucket cut would reorder the chain, a
+    client cut does not.  Same surface as an engine (``begin`` / ``prestage`` / ``release_arrivals``);
+    the rounds are :class:`ClientRound`.
+    """
+
+    def __init__(self, multi: MultiDeviceEngine):
+        self.multi = multi
+
+    @property
+    def world(self) -> int:
+        return self.multi.world
+
+    @property
+    def devices(self):
+        return self.multi.devices
+
+    @property
+    def device(self) -> torch.device:
+        return self.multi.device
+
+    def begin(self, template, capacity: int, codec: str = "native") -> "ClientRound":
+        return self.multi.begin(template, capacity, codec, client_split=True)
+
+    def prestage(self, payload, baseline_layout: ArenaLayout) -> bool:
+        return self.multi.prestage(payload, baseline_layout)
+
+    def release_arrivals(self) -> None:
+        self.multi.release_arrivals()
+
+
+class ClientRound(MultiRound):
+    """A bucket-sharded round whose whole-model reductions are split by client over the devices.
+
+    Staging (N PCIe links, each carrying 1/N of every payload) and the final FedAvg launch are the
+    :class:`MultiRound`'s.  For the reductions, client slot j's whole arena is assembled on device
+    j mod N from the bucket shards (device-to-device copies over xGMI) into a single-GPU
+    :class:`~plato_amd.engine.AggregationRound` per device, with the baseline; FedAdp's global
+    gradient is formed bucket-sharded (``plato_agg_fedavg_entrywise`` per bucket, the same
+    per-element arithmetic as one GPU) and all-gathered to every device; then each device runs the
+    single-GPU kernels (``plato_agg_fedadp_dots``, ``plato_agg_port_norms`` + cosine sums) on its
+    own clients.  Every value is computed by one chain on one GPU: bit-identical to one GPU.
+    """
+
+    def __init__(self, engine: MultiDeviceEngine, layout: ArenaLayout, capacity: int, codec: str):
+        super().__init__(engine, layout, capacity, codec)
+        self._baseline_sd = None
+        self._split = None  # [(AggregationRound on device g, {slot: local slot})]
+        self.last_norms = None
+
+    def put_baseline(self, baseline) -> None:
+        super().put_baseline(baseline)
+        self._baseline_sd = baseline
+        self._split = None
+
+    def put_client(self, slot: int, payload, what: str = "weights_received") -> None:
+        super().put_client(slot, payload, what)
+        self._split = None
+
+    def adopt(self, slot: int, payload) -> bool:
+        ok = super().adopt(slot, payload)
+        if ok:
+            self._split = None
+        return ok
+
+    def decoded(self) -> "ClientRound":
+        return self  # native payloads only (coded rounds run on the primary device)
+
+    # ------------------------------------------------------------ client split
+    def _client_rounds(self):
+        """Per device g: a single-GPU round holding the whole arenas of the staged slots j = g mod N."""
+        if self._split is not None:
+            return self._split
+        if self._baseline_sd is None:
+            raise ValueError("baseline not staged")
+        eng = self.engine
+        world = eng.world
+        staged = [j for j in range(self.capacity) if self.staged[j]]
+        for d in dict.fromkeys(eng.devices):  # the buckets' H2D copies (copy streams) are done
+            torch.cuda.synchronize(d)
+
+        def build(g):
+            mine = [j for j in staged if j % world == g]
+            dev = eng.devices[g]
+            e = eng.client_engine(g)
+            with torch.cuda.device(dev):
+                r = e.begin(self._baseline_sd, max(1, len(mine)), "native")
+                if r.layout.signature != self.layout.signature:
+                    raise RuntimeError("client engine built another arena layout")
+                for sh in eng._shards:  # the baseline, bucket by bucket
+                    if sh.n:
+                        e._base.f32[sh.lo:sh.hi].copy_(sh.base_f[: sh.n])
+                    if sh.ni:
+                        e._base.i64[sh.ilo:sh.ihi].copy_(sh.base_i[: sh.ni])
+                r.has_baseline = True
+                for local, j in enumerate(mine):
+                    dst_f, dst_i = r.slab.f32[local], r.slab.i64[local]
+                    for sh, (src_f, src_i) in zip(eng._shards, self._rows[j]):
+                        if sh.n:
+                            dst_f[sh.lo:sh.hi].copy_(src_f[: sh.n])
+                        if sh.ni:
+                            dst_i[sh.ilo:sh.ihi].copy_(src_i[: sh.ni])
+                    pf, pi = r.slab.row_pointers([local])
+                    r._pf[local], r._pi[local] = int(pf[0]), int(pi[0])
+                    r.staged[local] = True
+                torch.cuda.synchronize(dev)
+            return r, {j: local for local, j in enumerate(mine)}
+
+        self._split = eng.each(build, range(world))
+        return self._split
+
+    def _by_device(self, slots):
+        """[(device g, [local slots], [positions in ``slots``])] for the devices holding some of ``slots``."""
+        split = self._client_rounds()
+        groups = []
+        for g, (_, where) in enumerate(split):
+            pos = [i for i, j in enumerate(slots) if j in where]
+            if pos:
+                groups.append((g, [where[slots[i]] for i in pos], pos))
+        missing = [j for j in slots if not any(j in where for _, where in split)]
+        if missing:
+            raise ValueError(f"client slots {missing} were not staged")
+        return groups
+
+    def launch_entrywise(self, weights: np.ndarray, order: Sequence[int] | None = None, scale: float = 1.0,
+                         noise=None, noise_scale: float = 0.0, add_base: bool = True, deltas: bool = False,
+                         device: bool = False):
+        """``plato_agg_fedavg_entrywise`` per bucket, all-gathered: [(fp32 arena, int64 values)] per device.
+
+        The device-resident form FedAdp's global gradient takes (``device=True``; no noise, not in deltas mode).
+        """
+        if not device or noise is not None or deltas:
+            raise ValueError("client-split rounds offer the device-resident entrywise sum only (FedAdp)")
+        if not self.has_baseline:
+            raise ValueError("baseline not staged")
+        eng, lay = self.engine, self.layout
+        n_e = len(lay.entries)
+        order = list(range(np.asarray(weights).shape[1])) if order is None else list(order)
+        for j in order:
+            if not (0 <= j < self.capacity and self.staged[j]):
+                raise ValueError(f"client slot {j} was not staged")
+        k = len(order)
+        w = np.ascontiguousarray(np.asarray(weights, dtype=np.float64).astype(np.float32))
+        if w.shape != (n_e, k):
+            raise ValueError(f"weights must be [entries={n_e}, clients={k}], got {w.shape}")
+        tables = self._bucket_chunks()
+        outs, keep = [], []
+        for s, (cf, ci) in zip(eng._shards, tables):
+            with torch.cuda.device(s.device), torch.cuda.stream(s.stream):
+                s.stream.wait_stream(s.copy_stream)
+                tf = torch.from_numpy(np.asarray([self._ptrs[j][s.index][0] for j in order], dtype=np.int64)).to(s.device)
+                ti = torch.from_numpy(np.asarray([self._ptrs[j][s.index][1] for j in order], dtype=np.int64)).to(s.device)
+                dw = torch.from_numpy(w).to(s.device)
+                dcf = torch.from_numpy(cf.view(np.int32)).to(s.device)
+                dci = torch.from_numpy(ci.view(np.int32)).to(s.device)
+                out_f = torch.empty(s.per, dtype=torch.float32, device=s.device)
+                out_i = torch.empty(max(s.ni, 1), dtype=torch.float32, device=s.device)
+                ncf, nci = int(cf.shape[0]), int(ci.shape[0])
+                if ncf or nci:
+                    _lib.call("plato_agg_fedavg_entrywise", _ptr(tf), _ptr(ti) if s.ni else None, k, _ptr(dw), n_e,
+                              _ptr(dcf) if ncf else None, ncf, _ptr(dci) if nci else None, nci,
+                              _ptr(s.base_f), _ptr(s.base_i) if s.ni else None, None, None, float(scale),
+                              float(noise_scale), _lib.PLATO_AGG_ADD_BASE if add_base else 0, _ptr(out_f),
+                              _ptr(out_i) if s.ni else None, s.n, s.ni, s.stream.cuda_stream)
+                outs.append((out_f, out_i))
+                keep.append((tf, ti, dw, dcf, dci))
+        fulls = self._gather(outs)
+        for d in dict.fromkeys(eng.devices):
+            torch.cuda.synchronize(d)
+        del keep
+        return fulls
+
+    def _bucket_chunks(self):
+        """Per bucket: (fp32, int64) ``plato_agg_chunk`` tables of the layout's entries cut to the bucket."""
+        eng, lay = self.engine, self.layout
+        key = ("bucket_chunks", eng.world, FedAvgEngine.ENTRYWISE_CHUNK)
+        hit = lay._cache.get(key)
+        if hit is None:
+            cap = FedAvgEngine.ENTRYWISE_CHUNK
+            hit = []
+            for s in eng._shards:
+                f32, i64 = [], []
+                for idx, e in enumerate(lay.entries):
+                    if e.numel == 0:
+                        continue
+                    if e.region != "f32":
+                        if s.ni:
+                            i64.append((idx, e.offset, e.offset + e.numel, 0))
+                        continue
+                    lo, end = max(e.offset, s.lo), min(e.offset + e.numel, s.hi)
+                    while lo < end:  # cuts at multiples of cap of the arena (s.lo is a multiple of 64)
+                        hi = min(end, (lo // cap + 1) * cap)
+                        f32.append((idx, lo - s.lo, hi - s.lo, 0))
+                        lo = hi
+                hit.append((np.asarray(f32, dtype=np.uint32).reshape(-1, 4),
+                            np.asarray(i64, dtype=np.uint32).reshape(-1, 4)))
+            lay._cache[key] = hit
+        return hit
+
+    def fedadp_dots(self, grads, slots: Sequence[int], lr: float):
+        """``AggregationRound.fedadp_dots`` on every device for its clients (``grads``: launch_entrywise's)."""
+        slots = list(slots)
+        groups = self._by_device(slots)
+        split = self._split
+
+        def run(item):
+            g, local, _ = item
+            with torch.cuda.device(self.engine.devices[g]):
+                return split[g][0].fedadp_dots(grads[g], local, lr)
+
+        parts = self.engine.each(run, groups)
+        inner = np.zeros(len(slots), dtype=np.float32)
+        l_sq = np.zeros(len(slots), dtype=np.float32)
+        for (g, _, pos), (xy, gg, yy) in zip(groups, parts):
+            inner[pos] = xy
+            l_sq[pos] = yy
+        g_sq = parts[0][1]  # the same g . g on every device (one chain, the same g)
+        self.timings["fedadp_dots_ms"] = max(split[g][0].timings.get("fedadp_dots_ms", 0.0) for g, _, _ in groups)
+        return inner, g_sq, l_sq
+
+    def model_similarities(self, reference, slots: Sequence[int], eps: float = 1e-8, threads: int | None = None,
+                           flat_norms: bool = False) -> list:
+        """``AggregationRound.model_similarities`` on every device for its clients (Port)."""
+        slots = list(slots)
+        if not slots:
+            return []
+        threads = torch.get_num_threads() if threads is None else int(threads)
+        groups = self._by_device(slots)
+        split = self._split
+
+        def run(item):
+            g, local, _ = item
+            with torch.cuda.device(self.engine.devices[g]):
+                rnd = split[g][0]
+                sims = rnd.model_similarities(reference, local, eps, threads, flat_norms)
+                return sims, rnd.last_norms
+
+        parts = self.engine.each(run, groups)
+        sims = [None] * len(slots)
+        norms = np.zeros(len(slots) + 1, dtype=np.float32)
+        for (g, _, pos), (vals, dev_norms) in zip(groups, parts):
+            for i, v in zip(pos, vals):
+                sims[i] = v
+            norms[0] = dev_norms[0]  # current - previous: the same on every device
+            norms[[1 + i for i in pos]] = dev_norms[1:]
+        self.last_norms = norms
+        for key in ("port_norms_ms", "port_cosine_ms"):
+            vals = [split[g][0].timings[key] for g, _, _ in groups if key in split[g][0].timings]
+            if vals:
+                self.timings[key] = max(vals)
+        return sims
 
 
 # --------------------------------------------------------------- entry-aligned shards

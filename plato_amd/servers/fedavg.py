@@ -78,15 +78,17 @@ class _EngineHolder:
         One GPU: its engine.  Several: parameter buckets for plain rounds of
         native / bf16 payloads; whole-entry shards (``MultiDeviceEngine.entries``)
         for QSGD payloads (per-entry scales) and entry-local staged weights
-        (Polaris); the first GPU for weights that reduce the whole flattened
-        model serially (Port's similarity, FedAdp's dots).
+        (Polaris); for weights that reduce the whole flattened model serially
+        per client (Port's similarity, FedAdp's dots) bucket-sharded staging with
+        the reductions split by client (``MultiDeviceEngine.clients``), or the
+        first GPU for coded payloads.
         """
         eng = self.aggregation_engine()
         primary = getattr(eng, "primary", None)
         if primary is None:
             return eng
         if self.needs_staged_round and not self.entry_local_weights:
-            return primary
+            return eng.clients if codec == "native" else primary
         if self.needs_staged_round or codec not in ("native", "bf16"):
             return eng.entries
         return eng

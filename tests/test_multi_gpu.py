@@ -94,8 +94,8 @@ def test_multi_device_deltas_and_variants(n):
         assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"], name
 
 
-def test_multi_device_routes_staged_round_variants_to_one_gpu():
-    """Port needs the whole staged model: it runs on the first device's engine, same digest."""
+def test_multi_device_routes_staged_round_variants():
+    """Port / FedAdp rounds of native payloads split their reductions by client; coded ones stay on GPU 0."""
     from plato_amd.servers import variants as V
 
     case = _case("port_resnet18_k16")
@@ -112,8 +112,111 @@ def test_multi_device_routes_staged_round_variants_to_one_gpu():
 
     server = Server()
     updated = asyncio.run(server.aggregate_weights(updates, baseline, [u.payload for u in updates]))
-    assert server.round_engine("native") is server.aggregation_engine().primary
+    eng = server.aggregation_engine()
+    assert server.round_engine("native") is eng.clients and server.round_engine("qsgd") is eng.primary
     assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    assert server.get_logged_items()["aggregation_gpus"] == 4
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("name", ["fedadp_lenet5_k6", "fedadp_resnet18_k8"])
+def test_client_split_fedadp_matches_reference(name, n):
+    """FedAdp over aggregation_devices: bucket-sharded staging and global gradient, dots split by client
+    (client j's whole arena on device j mod n), final FedAvg bucket-sharded: the reference's weights,
+    smoothed angles and model bit for bit, and every device used."""
+    from plato_amd.servers.variants import FedAdpServerMixin
+    from tests.test_per_entry_gpu import CASES as PE_CASES
+    from tests.test_per_entry_gpu import _host
+
+    recipe, exp = PE_CASES[name]["recipe"], PE_CASES[name]["expected"]
+    layout, base, pays, _, updates = _host(recipe)
+
+    class Server(FedAdpServerMixin):
+        aggregation_devices = _devices(n)
+        fedadp_lr = 0.01
+
+    server = Server()
+    server.current_round = recipe["current_round"]
+    server.selected_clients = [c + 1 for c in G.order_of(recipe)]
+    server.local_angles = {int(c): np.float32(float.fromhex(a)) for c, a in recipe.get("local_angles", {}).items()}
+    updated = asyncio.run(server.aggregate_weights(updates, base, pays))
+    assert server.round_engine("native") is server.aggregation_engine().clients
+    assert [float(x).hex() for x in server.adaptive_weighting] == exp["adaptive_weighting"]
+    assert {str(c): "%08x" % np.float32(a).view(np.uint32) for c, a in server.local_angles.items()} == \
+        exp["local_angles"]
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
+    items = server.get_logged_items()
+    assert items["aggregation_gpus"] == n
+    # one single-GPU engine per device holds its clients' arenas
+    assert len(server.aggregation_engine()._client_engines) == n
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("name", ["port_similarity_lenet5_k8", "port_similarity_resnet18_k4"])
+def test_client_split_port_matches_reference(tmp_path, name, n):
+    """Port over aggregation_devices: similarities split by client, the reference's model bit for bit."""
+    from plato_amd.servers.variants import PortServerMixin
+    from tests.test_golden_gpu import FIXTURE_TORCH_THREADS, _previous
+
+    case = _case(name)
+    recipe = case["recipe"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    path = tmp_path / f"model_{recipe['current_round'] - 2}.pth"
+    torch.save(_previous(recipe, layout), path)
+
+    class Server(PortServerMixin):
+        aggregation_devices = _devices(n)
+        staleness_weight = 3
+        current_round = recipe["current_round"]
+        port_threads = FIXTURE_TORCH_THREADS
+
+        def port_previous_model_path(self):
+            return str(path)
+
+    server = Server()
+    updated = asyncio.run(server.aggregate_weights(_updates(recipe, payloads), baseline, payloads))
+    assert server.round_engine("native") is server.aggregation_engine().clients
+    assert G.sha(G.canon(_flat(layout, updated, "f32"))) == case["expected"]["updated_f32_sha256"]
+    assert G.sha(G.canon(_flat(layout, updated, "i64"))) == case["expected"]["updated_i64f_sha256"]
+    assert server.get_logged_items()["aggregation_gpus"] == n
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_client_split_round_dots_equal_one_gpu(n):
+    """The client-split round's FedAdp dots and Port similarities equal the one-GPU round's, bit for bit,
+    on any client subset and order (ClientRound against AggregationRound on the same payloads)."""
+    from plato_amd.engine import FedAvgEngine
+    from plato_amd.multi import MultiDeviceEngine
+    from tests.test_golden_gpu import _previous
+
+    case = _case("port_similarity_resnet18_k4")
+    recipe = case["recipe"]
+    layout, baseline, payloads = _host_payloads(recipe)
+    previous = _previous(recipe, layout)
+    k = recipe["k"]
+    one = FedAvgEngine("cuda:0").begin(baseline, k)
+    one.put_baseline(baseline)
+    multi = MultiDeviceEngine(_devices(n)).clients.begin(baseline, k)
+    multi.put_baseline(baseline)
+    for c in range(k):
+        one.put_client(c, payloads[c])
+        multi.put_client(c, payloads[c])
+    w1 = np.tile(np.full(k, 1.0 / k), (len(layout.entries), 1))
+    g1 = one.launch_entrywise(w1, add_base=False, device=True)
+    gm = multi.launch_entrywise(w1, add_base=False, device=True)
+    for gf, gi in gm:
+        assert torch.equal(gf[: layout.n_f32].cpu(), g1[0][: layout.n_f32].cpu())
+        assert torch.equal(gi[: layout.n_i64].cpu(), g1[1][: layout.n_i64].cpu())
+    for slots in (list(range(k)), [k - 1, 0], [2]):
+        a = one.fedadp_dots(g1, slots, 0.05)
+        b = multi.fedadp_dots(gm, slots, 0.05)
+        assert np.asarray(a[0]).tobytes() == np.asarray(b[0]).tobytes()
+        assert np.float32(a[1]).tobytes() == np.float32(b[1]).tobytes()
+        assert np.asarray(a[2]).tobytes() == np.asarray(b[2]).tobytes()
+        sa = one.model_similarities(previous, slots, threads=4)
+        sb = multi.model_similarities(previous, slots, threads=4)
+        assert np.asarray(sa, np.float32).tobytes() == np.asarray(sb, np.float32).tobytes()
+        assert one.last_norms.tobytes() == multi.last_norms.tobytes()
 
 
 @pytest.mark.parametrize("name", ["bf16_codec_resnet18_k16", "bf16_codec_lenet5_k9"])
