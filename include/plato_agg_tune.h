@@ -65,58 +65,37 @@ int plato_agg_tune_fedavg_bf16(int variant, const uint16_t* const* d_x_bf16,
 int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n,
                           int blocks, hipStream_t stream);
 
-/* plato_agg_entry_norms_f32 kernel variants (bitwise identical results):
- *   0 = producer / consumer: per (entry, client) one wave streams
- *       x and b into an 8-stage LDS ring (LDS-DMA) and forms the deltas of
- *       512-element tiles, the other wave only walks the chains
- *   1 = one wavefront per (entry, client), one-tile register prefetch (first version)
- *   2, 3, 8 = LDS-DMA ring, one workgroup per (entry, 4 / 1 / 2 clients), each wave
- *       forming its own deltas and walking its chains
- *   4, 5 = variant 8 without the fma chains / without the loads: timing probes
- *          only, their outputs are meaningless
- *   6, 7 = producer / consumer with 1024- / 256-element tiles (6 / 12 stages)
- *   9, 10 = producer / consumer writing the delta tiles transposed (each chain's
- *       steps contiguous), the chain wave reading 4 steps per ds_read_b128;
- *       512- / 1024-element tiles
- *   11 = variant 9 with the chain wave at s_setprio 3
- *   12 = variant 9 with the chain waves of the entries at least half as long as
- *        the table's first at s_setprio 3, the others at 1 (the engine passes the
- *        table longest first; the default until round 2)
- *   13 = variant 12 with those long entries' producer waves at s_setprio 2
- *   14, 15 = variant 12 with 1,024-element tiles, 4 / 5 stages (15 is the default for
- *        grids of more than 6,144 (entry, client) pairs)
- *   16 = variant 12 with 2,048-element tiles, 3 stages (the default for grids of at most
- *        6,144 pairs, e.g. Port's flattened vectors, FedAtt on ResNet-18 up to K = 64) */
+/* plato_agg_entry_norms_f32 kernel variants (bitwise identical results; csrc/entrywise.hip):
+ *   0, 1 = producer / consumer, one workgroup per (entry, client): a producer wave streams x and
+ *       b into an LDS-DMA ring (1,024-element tiles x 5 stages / 2,048 x 3) and writes the delta
+ *       tiles transposed, the chain wave walks the 8 chains (the long entries' chains at
+ *       s_setprio 3); the round-3 defaults for grids of more / at most 6,144 pairs
+ *   2 = one wavefront per (entry, client), one-tile register prefetch (the first version)
+ *   3.. = register-staged producer / consumer (P producer waves hold D tiles of x and b in
+ *       VGPRs; only the transposed delta ring is in LDS); shapes listed in entrywise.hip */
+int plato_agg_tune_num_entry_norms_variants(void);
 int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
                                const float* d_base_f32, const int64_t* d_base_i64,
                                const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
                                const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
                                size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream);
 
-/* plato_agg_sdot_shared kernel variants (pairs per workgroup x chains per
- * workgroup x 64-element blocks per stage x ring stages x producer waves):
- * 0 = 4x16x64x6x4, 1 = 2x32x32x8x3, 2 = 8x8x128x4x4,
- * 3 = 4x16x32x8x5, 4 = 4x16x64x4x2; 5-7 = variants 0-2 with the chain groups of a
- * pair group on one XCD (one L2); 8-11 = 2x16x64x6x4, 1x32x32x8x2, 2x16x64x4x3,
- * 1x16x64x4x2 on one XCD per pair group (32 / 16 chain lanes per workgroup: more
- * workgroups).  plato_agg_sdot_shared runs 8 (with_xx, <= 128 pairs), 11 (with_xx,
- * <= 64 pairs) or 5.  Bitwise identical results. */
+/* plato_agg_sdot_shared kernel variants (pairs per workgroup x chains per workgroup x 64-element
+ * blocks per stage x ring stages x producer waves): 0 = 4x16x64x6x4, 1 = 2x16x64x6x4,
+ * 2 = 1x16x64x4x2, each with a pair group's chain groups on one XCD (one L2); 3 = variant 0
+ * without the XCD grouping.  plato_agg_sdot_shared runs 1 (with_xx, <= 128 pairs), 2 (with_xx,
+ * <= 64 pairs) or 0.  Bitwise identical results. */
 int plato_agg_tune_num_sdot_shared_variants(void);
 int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const* d_y, int n_pairs, size_t n,
                                int with_xx, float* d_workspace, float* d_out_xy, float* d_out_yy,
                                hipStream_t stream);
 
-/* plato_agg_fedavg_qsgd kernel variants, workgroup size x clients per decode-table
- * batch x elements per lane: 0 = 512x4x8 pipelined (plato_agg_fedavg_qsgd), 1 = 256x8x16,
- * 2 = 512x16x16, 3 = 256x4x16, 4 = 1024x8x16, 5 = 256x8x8, 6 = 512x8x8,
- * 7 = 128x8x16, 8 = 512x16x8, 9 = 512x8x4, 10 = 512x8x16 (the first default),
- * 11 = 256x16x8, 12 = 1024x16x8, 13 = 1024x4x8; 14-26 the pipelined form
- * (double-buffered tables, next batch's codes loaded before the current batch is
- * summed, one barrier per batch), 27 = 1024x8x8 (the round-1 default), 28-35 hybrid
- * arithmetic/table decode, 36-40 more pipelined shapes, 41-43 timing probes (NOT the
- * FedAvg: no code loads / no table lookups / neither), 44-50 two-level batching, 51-57
- * resident tables; shapes listed in qsgd.hip.  plato_agg_tune_qsgd_chunk gives
- * the chunk capacity (elements per workgroup pass) the variant is built for. */
+/* plato_agg_fedavg_qsgd kernel variants, workgroup size x clients per decode-table batch x
+ * elements per lane: 0 = 512x4x8 pipelined (double-buffered tables, the next batch's codes loaded
+ * before the current batch is summed, one barrier per batch; plato_agg_fedavg_qsgd), 1 = 1024x8x8
+ * not pipelined (the round-1 default), 2-4 = timing probes of variant 0 (NOT the FedAvg: no code
+ * loads / no table lookups / neither).  plato_agg_tune_qsgd_chunk gives the chunk capacity
+ * (elements per workgroup pass) the variant is built for. */
 int plato_agg_tune_num_qsgd_variants(void);
 int plato_agg_tune_qsgd_chunk(int variant);
 int plato_agg_tune_fedavg_qsgd(int variant, const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64,
@@ -136,8 +115,8 @@ int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const*
                                size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy,
                                float* d_out_yy, hipStream_t stream);
 
-/* plato_agg_np_sumsq with an explicit kernel (0: one client per workgroup; 1/2/3: 4/8/16 clients per
- * workgroup sharing the baseline; csrc/flat.hip). */
+/* plato_agg_np_sumsq with an explicit kernel (0: chunk-major, latency-shaped, the default; 1: the
+ * round-2 client-major kernel; csrc/flat.hip). */
 int plato_agg_tune_num_np_sumsq_variants(void);
 int plato_agg_tune_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base,
                             const plato_agg_chunk* d_pieces, const uint32_t* d_first_chunk, uint32_t n_pieces,

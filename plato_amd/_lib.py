@@ -190,6 +190,7 @@ TUNE_SIGNATURES = {
     "plato_agg_tune_fedadp_is_probe": (_c_int, [_c_int]),
     "plato_agg_tune_num_port_norms_variants": (_c_int, []),
     "plato_agg_tune_num_np_sumsq_variants": (_c_int, []),
+    "plato_agg_tune_num_entry_norms_variants": (_c_int, []),
     "plato_agg_tune_np_sumsq": (
         _c_int,
         [_c_int, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, ctypes.c_uint32, _c_void_p,

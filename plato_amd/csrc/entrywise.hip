@@ -459,8 +459,6 @@ struct NormArgs {
   float* out;                 // [K][n_entries]
   uint64_t n_f32, n_i64;
   uint32_t nef, nei, n_entries;
-  uint32_t ngroups;           // ring kernel: ceil(K / G) client groups per entry
-  uint32_t probe;             // tuning only: bit 0 skips the chains, bit 1 skips the loads
   int K;
 };
 
@@ -561,34 +559,6 @@ __global__ __launch_bounds__(kBlock) void entry_norms_kernel(NormArgs a) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// entry_norms, ring version (the default): the same chains, fed through an
-// LDS ring by LDS-DMA.
-//
-// The per-wave version above keeps one 8 KiB tile in flight per chain, so the
-// largest ResNet entries (2.36 M elements per client) stream at ~4 GB/s per
-// (entry, client).  Here a workgroup of G waves owns one entry and G clients:
-// every stage holds a tile of the baseline and of the G client arenas (kRT
-// elements each, loaded with global_load_lds_dwordx4: no VGPRs, 1 KiB per
-// wave-instruction, spread over the G waves), kRS stages deep, so kRS - 1
-// stages stay in flight while one is consumed.  Per stage each wave forms
-// d = x - b for its client with all 64 lanes (in place, dwordx4 LDS traffic),
-// then walks its 8 chains over the tile (chain j reads positions j', j'+8, ...:
-// 8 consecutive dwords per step, no bank conflicts; whole tiles run on the
-// full wave, lanes 8..63 duplicating 0..7, because exec-masked fma chains ran
-// up to 2x slower, scripts/micro/fma_chain.hip).  The arithmetic and order
-// are exactly the per-wave version's (same chains, same lane sum, same tail),
-// so results are bitwise identical.  Tiles start on the arena's float4 grid;
-// `delta` = begin mod 4 shifts the chain positions.
-//
-// Measured: the launch is bound by the serial chain of the
-// largest entry (~15 cycles per step with the LDS traffic of the tile), not
-// by HBM; G = 2 is the fastest split of this design (variant 8); the
-// producer / consumer kernel below is faster and is the default.
-// ---------------------------------------------------------------------------
-constexpr int kRT = 1024;             // elements per operand per stage
-constexpr int kRS = 6;                // ring stages
-
 typedef __attribute__((address_space(1))) void gvoid;
 typedef __attribute__((address_space(3))) void lvoid;
 
@@ -598,177 +568,6 @@ template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
   __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
-
-// G = clients per workgroup (one wave each); stage = baseline tile + G client tiles
-template <int G, bool HAS_BASE>
-struct RingShape {
-  static constexpr int kRG = G;
-  static constexpr int kROps = 1 + G;                    // slots per stage (baseline first)
-  static constexpr int kOps = HAS_BASE ? kROps : kRG;  // operands loaded per stage
-  static constexpr int kChunks = kRT / 256;             // 1 KiB glds per operand
-  static constexpr int kPerWave = kOps * kChunks / G;   // glds per wave per stage
-  static_assert((kOps * kChunks) % G == 0, "stage must split evenly over the waves");
-};
-
-// This wave's glds sources: chunk r of every stage comes from operand
-// (wave + S::kRG * r) / kChunks, a fixed arena per wave (wave-uniform -> SGPRs).
-template <int G, bool HAS_BASE>
-__device__ __forceinline__ void ring_sources(const NormArgs& a, int grp, int wave,
-                                             const float* (&src)[RingShape<G, HAS_BASE>::kPerWave]) {
-  using S = RingShape<G, HAS_BASE>;
-#pragma unroll
-  for (int r = 0; r < S::kPerWave; ++r) {
-    const int o = (wave + S::kRG * r) / S::kChunks;
-    if (HAS_BASE && o == 0) {
-      src[r] = a.base_f;
-    } else {
-      const int i = grp * S::kRG + (HAS_BASE ? o - 1 : o);
-      src[r] = sld(a.xf, i < a.K ? i : a.K - 1);  // dead client slots load a live arena (never read)
-    }
-  }
-}
-
-// Issue this wave's share of one stage (tile starting at float4 group g0) into ring slot `slot`.
-template <int G, bool HAS_BASE>
-__device__ __forceinline__ void ring_issue(const float* const (&src)[RingShape<G, HAS_BASE>::kPerWave], float* ring,
-                                           uint32_t slot, uint64_t g0, uint64_t gmax, int wave, int lane) {
-  using S = RingShape<G, HAS_BASE>;
-#pragma unroll
-  for (int r = 0; r < S::kPerWave; ++r) {
-    const int q = wave + S::kRG * r;
-    const int o = q / S::kChunks, c = q % S::kChunks;
-    uint64_t g = g0 + uint64_t(c) * 64 + lane;
-    g = g < gmax ? g : gmax;
-    float* dst = ring + (slot * S::kROps + o) * kRT + c * 256;
-    __builtin_amdgcn_global_load_lds((gvoid*)(src[r] + 4 * g), (lvoid*)dst, 16, 0, 0);
-  }
-}
-
-template <int G, bool HAS_BASE>
-__device__ void norm_ring(const NormArgs& a, const Chunk ch, int grp, float* ring) {
-  using S = RingShape<G, HAS_BASE>;
-  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-  const int i = grp * S::kRG + wave;
-  const bool live = i < a.K;
-  const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
-  const uint32_t delta = ch.begin & 3u;
-  const uint64_t g_first = ch.begin >> 2;                      // float4 group of the first element
-  const uint64_t ntiles = (delta + m + kRT - 1) / kRT;
-  const uint64_t gmax = (a.n_f32 >> 2) - 1;                    // last whole float4 group
-  const int op = HAS_BASE ? 1 + wave : wave;                   // this wave's client operand
-  const int pj = int((uint32_t(lane) + delta) & 7u);           // chain lane's position in each 8-block
-  const int64_t s_shift = (uint32_t(lane) + delta) >= 8u ? -1 : 0;
-  const int64_t s_end = int64_t(m / kNormLanes);
-  float acc = 0.f;
-  const float* src[S::kPerWave];
-  ring_sources<G, HAS_BASE>(a, grp, wave, src);
-
-#pragma unroll
-  for (int p = 0; p < kRS - 1; ++p)
-    if (uint64_t(p) < ntiles && !(a.probe & 2)) ring_issue<G, HAS_BASE>(src, ring, p, g_first + uint64_t(p) * (kRT / 4), gmax, wave, lane);
-
-  for (uint64_t tt = 0; tt < ntiles; ++tt) {
-    // stage tt complete for this wave, then for every wave
-    if (tt + kRS - 2 < ntiles) {
-      wait_vmcnt<(kRS - 2) * S::kPerWave>();
-    } else {
-      wait_vmcnt<0>();
-    }
-    __builtin_amdgcn_s_barrier();
-    // slot (tt - 1) % kRS was consumed by every wave before the barrier
-    if (tt + kRS - 1 < ntiles && !(a.probe & 2))
-      ring_issue<G, HAS_BASE>(src, ring, uint32_t((tt + kRS - 1) % kRS), g_first + (tt + kRS - 1) * (kRT / 4), gmax,
-                           wave, lane);
-    float* col = ring + ((tt % kRS) * S::kROps + op) * kRT;
-    if (HAS_BASE) {
-      // d = x - b over the tile, in place (fp32, as compute_weight_deltas)
-      const float* bcol = ring + ((tt % kRS) * S::kROps) * kRT;
-#pragma unroll
-      for (int r = 0; r < kRT / 256; ++r) {
-        f4* px = reinterpret_cast<f4*>(col) + r * 64 + lane;
-        const f4 x = *px;
-        const f4 b = *(reinterpret_cast<const f4*>(bcol) + r * 64 + lane);
-        *px = x - b;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
-    if (a.probe & 1) continue;
-    const int64_t s0 = int64_t(tt) * (kRT / kNormLanes) + s_shift;
-    const float* p = col + pj;
-    if (tt >= 1 && int64_t(tt + 1) * (kRT / kNormLanes) <= s_end) {
-      // Whole tile for every chain (wave-uniform test).  All 64 lanes run the
-      // chain code, lanes 8..63 on copies of lanes 0..7's positions (LDS
-      // broadcast): an exec-masked fma chain ran up to 2x slower on MI355X
-      // than the same chain with the full wave active (scripts/micro/fma_chain.hip).
-      // Blocks of kCB steps, the next block's LDS reads in flight during this block's fmas.
-      constexpr int kCB = 16, kNB = kRT / kNormLanes / kCB;
-      float cur[kCB], nxt[kCB];
-#pragma unroll
-      for (int q = 0; q < kCB; ++q) cur[q] = p[8 * q];
-#pragma unroll
-      for (int blk = 0; blk < kNB; ++blk) {
-        if (blk + 1 < kNB) {
-#pragma unroll
-          for (int q = 0; q < kCB; ++q) nxt[q] = p[8 * (kCB * (blk + 1) + q)];
-        }
-        // keep the reads issued ahead of this block's chain (the scheduler would sink them)
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < kCB; ++q) acc = __builtin_fmaf(cur[q], cur[q], acc);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < kCB; ++q) cur[q] = nxt[q];
-      }
-    } else if (live && lane < kNormLanes) {
-      for (int u = 0; u < kRT / kNormLanes; ++u) {
-        const int64_t st = s0 + u;
-        if (st >= 0 && st < s_end) {
-          const float v = p[8 * u];
-          acc = __builtin_fmaf(v, v, acc);
-        }
-      }
-    }
-  }
-  if (!live) return;
-  // lanes added in order (ATen's buffer[0] + buffer[1] + ...), then the tail on top
-  float s = __shfl(acc, 0, 64);
-  for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, l, 64);
-  if (lane != 0) return;
-  const float* x = sld(a.xf, i);
-  for (uint64_t e = m; e < n; ++e) {
-    const uint64_t idx = ch.begin + e;
-    const float v = HAS_BASE ? x[idx] - a.base_f[idx] : x[idx];
-    s = torch_norm_tail_step(s, v, e, m, n);
-  }
-  if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
-}
-
-template <int G, bool HAS_BASE>
-__global__ __launch_bounds__(64 * G) void entry_norms_ring_kernel(NormArgs a) {
-  using S = RingShape<G, HAS_BASE>;
-  __shared__ __attribute__((aligned(16))) float ring[kRS * S::kROps * kRT];
-  const uint32_t ng = a.ngroups;
-  const uint64_t blk = blockIdx.x;
-  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-  float(*rows)[kNRow] = reinterpret_cast<float(*)[kNRow]>(ring + wave * kNormLanes * kNRow);
-  if (blk < uint64_t(a.nef) * ng) {
-    const Chunk ch = load_chunk(a.ef, uint32_t(blk / ng), a.n_f32);
-    const int grp = int(blk % ng);
-    if (uint64_t(ch.end) > (a.n_f32 & ~3ull)) {
-      // reaches the arena's partial last float4 group: the per-wave path (scalar loads)
-      const int i = grp * S::kRG + wave;
-      if (i < a.K) norm_pair<HAS_BASE, false>(a, ch, i, lane, rows);
-      return;
-    }
-    norm_ring<G, HAS_BASE>(a, ch, grp, ring);
-  } else {
-    const uint64_t j = blk - uint64_t(a.nef) * ng;  // int64 entries: tiny, per-wave path
-    const int i = int(j % ng) * G + wave;
-    if (i < a.K) norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, uint32_t(j / ng), a.n_i64), i, lane, rows);
-  }
 }
 
 // ---------------------------------------------------------------------------
@@ -868,21 +667,32 @@ __device__ void pc_produce(const NormArgs& a, const Chunk ch, const float* x, in
 // (lanes 8..63 duplicating lanes 0..7) over tile tt at dtile + (tt & 1) *
 // dstride, one s_barrier per tile.  Returns this lane's chain sum (torch's
 // accumulator lane & 7).
+// Tiles of an entry's vectorised part (tiles start on the arena's float4 grid, so the first one
+// also covers the delta = begin mod 4 positions before the entry).
+template <int T>
+__device__ __forceinline__ uint64_t pc_ntiles(const Chunk ch) {
+  const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+  return ((ch.begin & 3u) + m + T - 1) / T;
+}
+
+// nbar >= the tile count: barriers past the last tile (a producer that runs whole trips of D
+// tiles, entry_norms_rs_kernel) are met without reading a tile.
 template <int T, bool TR>
-__device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstride) {
+__device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstride, uint64_t nbar) {
   constexpr int kRT = T, kTS = DTile<T, TR>::kTS;
   const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
   const uint32_t delta = ch.begin & 3u;
-  const uint64_t ntiles = (delta + m + kRT - 1) / kRT;
+  const uint64_t ntiles = pc_ntiles<T>(ch);
   const int c = lane & 7;
   const int pj = int((uint32_t(c) + delta) & 7u);
   const int64_t s_shift = (uint32_t(c) + delta) >= 8u ? -1 : 0;
   const int64_t s_end = int64_t(m / kNormLanes);
   float acc = 0.f;
-  for (uint64_t tt = 0; tt < ntiles; ++tt) {
+  for (uint64_t tt = 0; tt < nbar; ++tt) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     __builtin_amdgcn_s_barrier();
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    if (tt >= ntiles) continue;
     const float* tile = dtile + (tt & 1) * dstride;
     const float* p = TR ? tile + pj * kTS : tile + pj;
     constexpr int kStep = TR ? 1 : 8;  // floats between a chain's consecutive steps
@@ -943,29 +753,12 @@ __device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstr
   return acc;
 }
 
-template <int T, int PS, bool HAS_BASE, bool TR = false, int PRIO = 0>
-__device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int lane, float (*raw)[2][T],
-                        float (*dbuf)[DTile<T, TR>::kSize]) {
+// The chain wave's epilogue: the 8 lanes added in order (ATen's buffer[0] + buffer[1] + ...),
+// then the scalar tail over positions m .. n - 1, then the square root.
+template <bool HAS_BASE>
+__device__ __forceinline__ void pc_finish(const NormArgs& a, const Chunk ch, int i, const float* x, int lane,
+                                          float acc) {
   const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
-  const float* x = sld(a.xf, i);
-  if (wave == 1) {  // producer
-    if constexpr (PRIO == -2) {  // the long entries' producers above every chain but their own
-      const Chunk c0 = load_chunk(a.ef, 0, a.n_f32);
-      if (2 * n >= uint64_t(c0.end - c0.begin)) __builtin_amdgcn_s_setprio(2);
-    }
-    pc_produce<T, PS, HAS_BASE, TR>(a, ch, x, lane, raw, dbuf[0], DTile<T, TR>::kSize);
-    return;
-  }
-  if constexpr (PRIO > 0) {
-    __builtin_amdgcn_s_setprio(PRIO);  // the chain wave issues first
-  } else if constexpr (PRIO < 0) {  // -1, -2
-    // the longest chains (the launch's critical path) first: entries at least half as long
-    // as the table's first (longest-first order) at priority 3, the rest at 1
-    const Chunk c0 = load_chunk(a.ef, 0, a.n_f32);
-    if (2 * n >= uint64_t(c0.end - c0.begin)) __builtin_amdgcn_s_setprio(3);
-    else __builtin_amdgcn_s_setprio(1);
-  }
-  const float acc = pc_chain<T, TR>(ch, lane, dbuf[0], DTile<T, TR>::kSize);
   float s = __shfl(acc, 0, 64);
   for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, l, 64);
   if (lane != 0) return;
@@ -975,6 +768,37 @@ __device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int 
     s = torch_norm_tail_step(s, v, e, m, n);
   }
   if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
+}
+
+// Long entries (at least half as long as the table's first: the engine passes the table longest
+// first) are the launch's critical path.
+__device__ __forceinline__ bool pc_long(const NormArgs& a, const Chunk ch) {
+  const Chunk c0 = load_chunk(a.ef, 0, a.n_f32);
+  return 2 * uint64_t(ch.end - ch.begin) >= uint64_t(c0.end - c0.begin);
+}
+
+// Chain-wave priority (PRIO): > 0 a flat s_setprio; -1 the long entries' chains at 3, the others at 1
+// (the longest chains, the launch's critical path, first).  The producers stay at 0.
+template <int PRIO>
+__device__ __forceinline__ void pc_chain_prio(const NormArgs& a, const Chunk ch) {
+  if constexpr (PRIO > 0) {
+    __builtin_amdgcn_s_setprio(PRIO);
+  } else if constexpr (PRIO < 0) {
+    if (pc_long(a, ch)) __builtin_amdgcn_s_setprio(3);
+    else __builtin_amdgcn_s_setprio(1);
+  }
+}
+
+template <int T, int PS, bool HAS_BASE, bool TR = false, int PRIO = 0>
+__device__ void norm_pc(const NormArgs& a, const Chunk ch, int i, int wave, int lane, float (*raw)[2][T],
+                        float (*dbuf)[DTile<T, TR>::kSize]) {
+  const float* x = sld(a.xf, i);
+  if (wave == 1) {  // producer
+    pc_produce<T, PS, HAS_BASE, TR>(a, ch, x, lane, raw, dbuf[0], DTile<T, TR>::kSize);
+    return;
+  }
+  pc_chain_prio<PRIO>(a, ch);
+  pc_finish<HAS_BASE>(a, ch, i, x, lane, pc_chain<T, TR>(ch, lane, dbuf[0], DTile<T, TR>::kSize, pc_ntiles<T>(ch)));
 }
 
 template <int T, int PS, bool HAS_BASE, bool TR = false, int PRIO = 0>
@@ -993,6 +817,102 @@ __global__ __launch_bounds__(128) void entry_norms_pc_kernel(NormArgs a) {
       return;
     }
     norm_pc<T, PS, HAS_BASE, TR, PRIO>(a, ch, i, wave, lane, raw, dbuf);
+  } else if (ent < a.nef + a.nei) {
+    if (wave == 0) norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// entry_norms, register-staged producer / consumer (round 4).  The kernel above
+// stages x and b through a kPS-deep LDS ring by LDS-DMA, so the bytes a pair
+// keeps in flight cost LDS (49-66 KB per workgroup, 2-3 workgroups per CU) and
+// every element crosses the LDS three times (DMA in, d pass out, transposed d).
+// Here P producer waves hold D tiles of x and b in VGPRs (the register file is
+// 4x the LDS and otherwise idle in this kernel), form d = x - b in registers and
+// write it transposed straight into the two-slot d tile ring the chain wave
+// reads: LDS per workgroup is the d ring alone (8.4 / 16.6 KB at T = 1,024 /
+// 2,048), a pair keeps D x T x 8 bytes in flight, and the chain wave (pc_chain,
+// same tiles, same order) meets the producers at one s_barrier per tile.
+// Producers run whole trips of D tiles (register slots are static); tiles past
+// the last reload the last tile (valid addresses, never read) and the chain wave
+// meets their barriers without reading.
+// ---------------------------------------------------------------------------
+template <int T, int P, int D, bool HAS_BASE>
+__device__ void rs_produce(const NormArgs& a, const Chunk ch, const float* x, int w, int lane, float* dtile,
+                           int dstride, uint64_t ntiles, uint64_t nbar) {
+  constexpr int kTS = DTile<T, true>::kTS;
+  constexpr int kIt = T / 256 / P;  // 256-element iterations (4 per lane) per producer and tile
+  static_assert(kIt >= 1 && kIt * P * 256 == T, "whole iterations per producer");
+  constexpr int kOps = HAS_BASE ? 2 : 1;
+  static_assert((D - 1) * kIt * kOps < 64, "vmcnt range");
+  const uint64_t g_first = ch.begin >> 2;
+  const uint64_t gmax = (a.n_f32 >> 2) - 1;
+  const gf4* xs = (const gf4*)(x);
+  const gf4* bs = (const gf4*)(a.base_f);
+  f4 xr[D][kIt], br[D][kIt];
+  auto issue = [&](f4(&xv)[kIt], f4(&bv)[kIt], uint64_t t) {
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      uint64_t g = g_first + t * (T / 4) + uint64_t(it * P + w) * 64 + lane;
+      g = g < gmax ? g : gmax;
+      xv[it] = __builtin_nontemporal_load(xs + g);
+      if (HAS_BASE) bv[it] = bs[g];
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < D; ++j) issue(xr[j], br[j], uint64_t(j) < ntiles ? uint64_t(j) : ntiles - 1);
+  for (uint64_t t0 = 0; t0 < nbar; t0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const uint64_t tt = t0 + j;
+      wait_vmcnt<(D - 1) * kIt * kOps>();  // tile tt's loads (the oldest D - 1 trips stay in flight)
+      float* dt = dtile + (tt & 1) * dstride;
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        f4 dv = xr[j][it];
+        if (HAS_BASE) dv = dv - br[j][it];  // fp32, as compute_weight_deltas
+        // tile elements 256 r + 4 lane + c: chain 4 (lane & 1) + c, step 32 r + lane / 2
+        float* col = dt + 32 * (it * P + w) + (lane >> 1) + 4 * (lane & 1) * kTS;
+        col[0] = dv.x;
+        col[kTS] = dv.y;
+        col[2 * kTS] = dv.z;
+        col[3 * kTS] = dv.w;
+      }
+      const uint64_t nt = tt + D;
+      issue(xr[j], br[j], nt < ntiles ? nt : ntiles - 1);
+      wait_lgkm0();  // d tile written (the loads stay in flight)
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __builtin_amdgcn_s_barrier();  // tile tt ready; the chain wave is done with tile tt - 1
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+  }
+  wait_vmcnt<0>();
+}
+
+template <int T, int P, int D, bool HAS_BASE, int PRIO>
+__global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rs_kernel(NormArgs a) {
+  constexpr int kSize = DTile<T, true>::kSize;
+  static_assert(2 * kSize >= kNormLanes * kNRow, "norm_pair's rows fit the d ring");
+  __shared__ __attribute__((aligned(16))) float dbuf[2 * kSize];
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  const uint64_t pair = blockIdx.x;  // entry-major over the (longest-first) tables
+  const uint32_t ent = uint32_t(pair / uint64_t(a.K));
+  const int i = int(pair % uint64_t(a.K));
+  float(*rows)[kNRow] = reinterpret_cast<float(*)[kNRow]>(dbuf);
+  if (ent < a.nef) {
+    const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
+    if (uint64_t(ch.end) > (a.n_f32 & ~3ull)) {  // the arena's partial last float4 group: per-wave path
+      if (wave == 0) norm_pair<HAS_BASE, false>(a, ch, i, lane, rows);
+      return;
+    }
+    const uint64_t ntiles = pc_ntiles<T>(ch), nbar = (ntiles + D - 1) / D * D;
+    const float* x = sld(a.xf, i);
+    if (wave > 0) {
+      if (ntiles) rs_produce<T, P, D, HAS_BASE>(a, ch, x, wave - 1, lane, dbuf, kSize, ntiles, nbar);
+      return;
+    }
+    pc_chain_prio<PRIO>(a, ch);
+    pc_finish<HAS_BASE>(a, ch, i, x, lane, pc_chain<T, true>(ch, lane, dbuf, kSize, nbar));
   } else if (ent < a.nef + a.nei) {
     if (wave == 0) norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows);
   }
@@ -1119,15 +1039,53 @@ int plato_agg_fedavg_entrywise(const float* const* d_x_f32, const int64_t* const
 }  // extern "C"
 
 namespace {
-int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
+using NormFn = void (*)(const NormArgs&, bool, dim3, hipStream_t);
+template <int T, int PS>
+void launch_pc(const NormArgs& a, bool hb, dim3 grid, hipStream_t st) {
+  if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<T, PS, true, true, -1>), grid, dim3(128), 0, st, a);
+  else hipLaunchKernelGGL((entry_norms_pc_kernel<T, PS, false, true, -1>), grid, dim3(128), 0, st, a);
+}
+template <int T, int P, int D, int PRIO = -1>
+void launch_rs(const NormArgs& a, bool hb, dim3 grid, hipStream_t st) {
+  if (hb) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, true, PRIO>), grid, dim3(64 * (1 + P)), 0, st, a);
+  else hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, false, PRIO>), grid, dim3(64 * (1 + P)), 0, st, a);
+}
+#ifdef PLATO_AGG_TUNE
+void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
+  const uint64_t threads = (uint64_t(a.nef) + a.nei) * uint64_t(a.K) * 64;  // a wave per pair
+  const dim3 grid{uint32_t((threads + kBlock - 1) / kBlock)};
+  if (hb) hipLaunchKernelGGL(entry_norms_kernel<true>, grid, dim3(kBlock), 0, st, a);
+  else hipLaunchKernelGGL(entry_norms_kernel<false>, grid, dim3(kBlock), 0, st, a);
+}
+#endif
+// Variants (include/plato_agg_tune.h; every one bitwise identical).  The rounds-1-3 sweep (natural
+// tiles, LDS-DMA ring kernels with 1-4 clients per workgroup, flat priorities, 256-1,024-element
+// tiles; DESIGN.md §11, profiles/r0*_norms*) is trimmed to the two round-3 defaults and the
+// per-wave first version; 3.. are the register-staged kernel's shapes (tile, producers, tiles in
+// flight).
+constexpr NormFn kNormDefaultLarge = &launch_pc<1024, 5>;
+constexpr NormFn kNormDefaultSmall = &launch_pc<2048, 3>;
+#ifdef PLATO_AGG_TUNE
+const NormFn kNormVariants[] = {
+    &launch_pc<1024, 5>,      // 0: LDS-DMA producer / consumer, 1,024-element tiles, 5 stages
+    &launch_pc<2048, 3>,      // 1: the same, 2,048-element tiles, 3 stages
+    &launch_per_wave,         // 2: one wavefront per (entry, client) (the first version)
+    &launch_rs<2048, 4, 3>,   // 3: register-staged
+    &launch_rs<2048, 4, 2>,   // 4
+    &launch_rs<2048, 4, 4>,   // 5
+    &launch_rs<2048, 8, 3>,   // 6
+    &launch_rs<1024, 2, 4>,   // 7
+    &launch_rs<1024, 4, 4>,   // 8
+    &launch_rs<2048, 2, 3>,   // 9
+    &launch_rs<2048, 4, 3, 3>,  // 10: variant 3, every chain wave at priority 3
+};
+constexpr int kNumNormVariants = sizeof(kNormVariants) / sizeof(kNormVariants[0]);
+#endif
+
+int run_norms(NormFn fn, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
               const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_chunk* d_entries_f32,
               uint32_t n_entries_f32, const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  if (variant < 0 || variant > 16) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
-#ifndef PLATO_AGG_TUNE
-  // libplato_agg.so carries the two defaults of plato_agg_entry_norms_f32 only
-  if (variant != 15 && variant != 16) return set_error(PLATO_AGG_EINVAL, "entry_norms variant not in this build");
-#endif
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (n_entries <= 0 || !d_out) return set_error(PLATO_AGG_EINVAL, "null output / no entries");
   if (n_entries_f32 && (!d_x_f32 || !d_entries_f32)) return set_error(PLATO_AGG_EINVAL, "null fp32 pointer");
@@ -1135,9 +1093,9 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
     return set_error(PLATO_AGG_EINVAL, "null int64 pointer");
   if (n_f32 > 0xffffffffull || n_i64 > 0xffffffffull)
     return set_error(PLATO_AGG_EINVAL, "arena too large for 32-bit chunk offsets");
-  const uint64_t threads = (uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K) * 64;  // a wave per pair
-  if (threads == 0) return clear_error();
-  if (threads / kBlock + 1 > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "too many (client, entry) pairs");
+  const uint64_t pairs = (uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K);
+  if (pairs == 0) return clear_error();
+  if (pairs > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "too many (client, entry) pairs");
   NormArgs a{};
   a.xf = d_x_f32;
   a.xi = d_x_i64;
@@ -1152,99 +1110,8 @@ int run_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_
   a.nei = n_entries_i64;
   a.n_entries = uint32_t(n_entries);
   a.K = K;
-  // Variants (include/plato_agg_tune.h): 15 / 16 (the defaults, by grid size) are
-  // variant 12 with 1,024- / 2,048-element tiles; 12 producer/consumer with
-  // transposed 512-element tiles and the long chains' waves at raised priority
-  // (the round-1 default); 9, 11 the same without / with a flat
-  // raised priority; 0 natural tiles; 1 per-wave; 2, 3, 8 LDS-DMA
-  // ring with 4 / 1 / 2 clients per workgroup; 4 / 5 variant 8 without the
-  // chains / without the loads (timing probes, wrong results); 6, 7
-  // producer/consumer with 1024- / 256-element tiles; 9, 10 producer/consumer
-  // with transposed d tiles (512 / 1,024 elements).
-#ifdef PLATO_AGG_TUNE
-  static const int kGroup[] = {0, 0, 4, 1, 2, 2, 0, 0, 2, 0, 0, 0, 0, 0, 0, 0, 0};
-  const int G = kGroup[variant];
-#endif
-  a.probe = variant == 4 ? 1u : variant == 5 ? 2u : 0u;
-  if (variant == 0 || variant == 6 || variant == 7 || variant >= 9) {
-    // producer / consumer, one workgroup per (entry, client)
-    const dim3 grid{uint32_t((uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K))};
-    const bool hb = d_base_f32 != nullptr;
-#ifndef PLATO_AGG_TUNE
-    if (variant == 15) {
-      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 5, true, true, -1>), grid, dim3(128), 0, stream, a);
-      else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 5, false, true, -1>), grid, dim3(128), 0, stream, a);
-    } else {
-      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<2048, 3, true, true, -1>), grid, dim3(128), 0, stream, a);
-      else hipLaunchKernelGGL((entry_norms_pc_kernel<2048, 3, false, true, -1>), grid, dim3(128), 0, stream, a);
-    }
-#else
-    if (variant == 0) {
-      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true>), grid, dim3(128), 0, stream, a);
-      else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false>), grid, dim3(128), 0, stream, a);
-    } else if (variant == 9) {
-      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true>), grid, dim3(128), 0, stream, a);
-      else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true>), grid, dim3(128), 0, stream, a);
-    } else if (variant == 11) {
-      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true, 3>), grid, dim3(128), 0, stream, a);
-      else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true, 3>), grid, dim3(128), 0, stream, a);
-    } else if (variant == 12) {
-      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true, -1>), grid, dim3(128), 0, stream, a);
-      else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true, -1>), grid, dim3(128), 0, stream, a);
-    } else if (variant == 13) {
-      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, true, true, -2>), grid, dim3(128), 0, stream, a);
-      else hipLaunchKernelGGL((entry_norms_pc_kernel<512, 8, false, true, -2>), grid, dim3(128), 0, stream, a);
-    } else if (variant >= 14) {  // 1,024 / 2,048-element transposed tiles at variant 12's priorities
-      if (variant == 14) {
-        if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 4, true, true, -1>), grid, dim3(128), 0, stream, a);
-        else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 4, false, true, -1>), grid, dim3(128), 0, stream, a);
-      } else if (variant == 15) {
-        if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 5, true, true, -1>), grid, dim3(128), 0, stream, a);
-        else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 5, false, true, -1>), grid, dim3(128), 0, stream, a);
-      } else {
-        if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<2048, 3, true, true, -1>), grid, dim3(128), 0, stream, a);
-        else hipLaunchKernelGGL((entry_norms_pc_kernel<2048, 3, false, true, -1>), grid, dim3(128), 0, stream, a);
-      }
-    } else if (variant == 10) {
-      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, true, true>), grid, dim3(128), 0, stream, a);
-      else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, false, true>), grid, dim3(128), 0, stream, a);
-    } else if (variant == 6) {
-      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, true>), grid, dim3(128), 0, stream, a);
-      else hipLaunchKernelGGL((entry_norms_pc_kernel<1024, 6, false>), grid, dim3(128), 0, stream, a);
-    } else {
-      if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<256, 12, true>), grid, dim3(128), 0, stream, a);
-      else hipLaunchKernelGGL((entry_norms_pc_kernel<256, 12, false>), grid, dim3(128), 0, stream, a);
-    }
-#endif
-    return launch_error("entry_norms launch");
-  }
-#ifdef PLATO_AGG_TUNE
-  a.ngroups = uint32_t((K + (G ? G : 1) - 1) / (G ? G : 1));
-  if (variant == 1) {  // per-wave chains (the first version)
-    const dim3 grid{uint32_t((threads + kBlock - 1) / kBlock)};
-    if (d_base_f32) {
-      hipLaunchKernelGGL(entry_norms_kernel<true>, grid, dim3(kBlock), 0, stream, a);
-    } else {
-      hipLaunchKernelGGL(entry_norms_kernel<false>, grid, dim3(kBlock), 0, stream, a);
-    }
-    return launch_error("entry_norms launch");
-  }
-  const dim3 grid{uint32_t((uint64_t(n_entries_f32) + n_entries_i64) * a.ngroups)};
-  const dim3 block{uint32_t(64 * G)};
-  if (G == 1) {
-    if (d_base_f32) hipLaunchKernelGGL((entry_norms_ring_kernel<1, true>), grid, block, 0, stream, a);
-    else hipLaunchKernelGGL((entry_norms_ring_kernel<1, false>), grid, block, 0, stream, a);
-  } else if (G == 2) {
-    if (d_base_f32) hipLaunchKernelGGL((entry_norms_ring_kernel<2, true>), grid, block, 0, stream, a);
-    else hipLaunchKernelGGL((entry_norms_ring_kernel<2, false>), grid, block, 0, stream, a);
-  } else {
-    if (d_base_f32) hipLaunchKernelGGL((entry_norms_ring_kernel<4, true>), grid, block, 0, stream, a);
-    else hipLaunchKernelGGL((entry_norms_ring_kernel<4, false>), grid, block, 0, stream, a);
-  }
+  fn(a, d_base_f32 != nullptr, dim3(uint32_t(pairs)), stream);  // one workgroup per (entry, client)
   return launch_error("entry_norms launch");
-#else
-  return launch_error("entry_norms launch");
-#endif
 }
 }  // namespace
 
@@ -1261,17 +1128,20 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
   // 4-6 % ahead of 1,024-element tiles), 1,024-element tiles (5 stages, 3 per CU) on large ones
   // (FedAtt at K = 128, 10,496 pairs: 1.22 vs 1.48 ms).  DESIGN.md §11.
   const uint64_t pairs = (uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K > 0 ? K : 0);
-  return run_norms(pairs <= 6144 ? 16 : 15, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32,
-                   n_entries_f32, d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
+  return run_norms(pairs <= 6144 ? kNormDefaultSmall : kNormDefaultLarge, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64,
+                   d_entries_f32, n_entries_f32, d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
 }
 
 #ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
+int plato_agg_tune_num_entry_norms_variants(void) { return kNumNormVariants; }
+
 int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
                                const float* d_base_f32, const int64_t* d_base_i64,
                                const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
                                const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
                                size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  return run_norms(variant, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32,
+  if (variant < 0 || variant >= kNumNormVariants) return set_error(PLATO_AGG_EINVAL, "bad entry_norms variant");
+  return run_norms(kNormVariants[variant], d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32,
                    d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
 }
 #endif  // PLATO_AGG_TUNE

@@ -380,25 +380,16 @@ constexpr Variant make_variant() {
 // Variant 0 is the default of the public entry points (fastest in the
 // interleaved sweep on MI355X).
 #ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so: every variant (bench.py --sweep, scripts/)
+// The round-1 sweep of 18 shapes (profiles/r01_sweep.log) is trimmed to one of each
+// kind; bench.py --sweep interleaves these.
 const Variant kVariants[] = {
-    make_variant<Cfg<256, 1, 8, true, true, false>>(),              // 0 (default): NT loads + NT stores
-    make_variant<Cfg<256, 2, 8, false, false, false>>(),            // 1 first version
-    make_variant<Cfg<256, 1, 8, false, false, false>>(),            // 2 plain loads
-    make_variant<Cfg<256, 1, 8, true, false, false>>(),             // 3 NT loads only
-    make_variant<Cfg<256, 1, 4, true, true, false>>(),              // 4
-    make_variant<Cfg<256, 1, 16, true, true, false>>(),             // 5
-    make_variant<Cfg<256, 1, 8, true, true, true>>(),               // 6 pipelined
-    make_variant<Cfg<64, 1, 8, true, true, false>>(),               // 7
-    make_variant<Cfg<256, 1, 8, true, true, false, true>>(),        // 8 buffer loads (nt)
-    make_variant<Cfg<256, 1, 4, true, true, false, true>>(),        // 9 buffer loads (nt)
-    make_variant<Cfg<256, 1, 8, true, true, false, false, 8>>(),    // 10 persistent 8/CU
-    make_variant<Cfg<256, 1, 8, true, true, false, false, 4>>(),    // 11 persistent 4/CU
-    make_variant<Cfg<256, 1, 8, true, true, false, true, 8>>(),     // 12 buffer + persistent 8/CU
-    make_variant<Cfg<256, 1, 8, false, true, false, true>>(),       // 13 buffer, plain loads
-    make_variant<Cfg<256, 1, 8, true, true, false, false, 0, true>>(),   // 14 XCD-contiguous chunks
-    make_variant<Cfg<512, 1, 8, true, true, false, false, 0, true>>(),   // 15 XCD, 512 threads
-    make_variant<Cfg<1024, 1, 8, true, true, false, false, 0, true>>(),  // 16 XCD, 1024 threads
-    make_variant<Cfg<256, 1, 16, true, true, false, false, 0, true>>(),  // 17 XCD, U=16
+    make_variant<Cfg<256, 1, 8, true, true, false>>(),                   // 0 (default): NT loads + NT stores
+    make_variant<Cfg<256, 2, 8, false, false, false>>(),                 // 1 first version
+    make_variant<Cfg<256, 1, 8, false, false, false>>(),                 // 2 plain loads
+    make_variant<Cfg<256, 1, 8, true, true, true>>(),                    // 3 pipelined
+    make_variant<Cfg<256, 1, 8, true, true, false, true>>(),             // 4 buffer loads (nt)
+    make_variant<Cfg<256, 1, 8, true, true, false, false, 8>>(),         // 5 persistent 8/CU
+    make_variant<Cfg<256, 1, 8, true, true, false, false, 0, true>>(),   // 6 XCD-contiguous chunks
 };
 #else  // libplato_agg.so: the default only
 const Variant kVariants[] = {

@@ -536,38 +536,29 @@ void launch_sdot_shared(const SdotSArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((sdot_shared_kernel<kP, kC, kS, kPS, kW, kXcd, false>), dim3(groups), dim3(64 * (1 + kW)), 0,
                        st, a);
 }
-// pairs per workgroup x chains per workgroup x blocks per stage x stages x producer waves
-#ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so: every shape
+// pairs per workgroup x chains per workgroup x blocks per stage x stages x producer waves.  The
+// round-2 sweep (12 shapes, profiles/r02*_sdot*) is in DESIGN.md §12; the tuning library keeps the
+// three size-picked defaults and variant 0's shape without the XCD grouping.
+#ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so
 const SdotSFn kSdotSVariants[] = {
-    &launch_sdot_shared<4, 16, 64, 6, 4>,   // 0: 64 B of each block per vector
-    &launch_sdot_shared<2, 32, 32, 8, 3>,   // 1: 128 B per block, x shared by 2 pairs
-    &launch_sdot_shared<8, 8, 128, 4, 4>,   // 2: 32 B per block, x shared by 8 pairs
-    &launch_sdot_shared<4, 16, 32, 8, 5>,   // 3: shorter stages, deeper ring
-    &launch_sdot_shared<4, 16, 64, 4, 2>,   // 4: shallower ring, 2 producers (2 workgroups / CU)
-    &launch_sdot_shared<4, 16, 64, 6, 4, true>,   // 5: variant 0, a pair group's chain groups on one XCD
-    &launch_sdot_shared<2, 32, 32, 8, 3, true>,   // 6: variant 1, likewise
-    &launch_sdot_shared<8, 8, 128, 4, 4, true>,   // 7: variant 2, likewise
-    // half / quarter chain waves: twice / four times the workgroups, all 256 CUs streaming
-    // (default_sdot_variant picks 8 / 11 when x.x rides along and the workgroups fit the CUs)
-    &launch_sdot_shared<2, 16, 64, 6, 4, true>,   // 8
-    &launch_sdot_shared<1, 32, 32, 8, 2, true>,   // 9
-    &launch_sdot_shared<2, 16, 64, 4, 3, true>,   // 10
-    &launch_sdot_shared<1, 16, 64, 4, 2, true>,   // 11
+    &launch_sdot_shared<4, 16, 64, 6, 4, true>,  // 0: 64 B of each block per vector, a pair group on one XCD
+    &launch_sdot_shared<2, 16, 64, 6, 4, true>,  // 1: half chain waves (twice the workgroups)
+    &launch_sdot_shared<1, 16, 64, 4, 2, true>,  // 2: quarter chain waves, 2 producers
+    &launch_sdot_shared<4, 16, 64, 6, 4>,        // 3: variant 0 without the XCD grouping
 };
-constexpr int kSdotV5 = 5, kSdotV8 = 8, kSdotV11 = 11;
 #else  // libplato_agg.so: the three defaults of default_sdot_variant
 const SdotSFn kSdotSVariants[] = {
-    &launch_sdot_shared<4, 16, 64, 6, 4, true>,  // tune variant 5
-    &launch_sdot_shared<2, 16, 64, 6, 4, true>,  // tune variant 8
-    &launch_sdot_shared<1, 16, 64, 4, 2, true>,  // tune variant 11
+    &launch_sdot_shared<4, 16, 64, 6, 4, true>,
+    &launch_sdot_shared<2, 16, 64, 6, 4, true>,
+    &launch_sdot_shared<1, 16, 64, 4, 2, true>,
 };
-constexpr int kSdotV5 = 0, kSdotV8 = 1, kSdotV11 = 2;
 #endif
+constexpr int kSdotV5 = 0, kSdotV8 = 1, kSdotV11 = 2;
 constexpr int kNumSdotSVariants = sizeof(kSdotSVariants) / sizeof(kSdotSVariants[0]);
 
 // The default by size: with x.x folded in, as many workgroups as CUs when the pairs allow it (a CU's
 // stream, ~24 GB/s, is what bounds a workgroup): 128 pairs -> 2 pairs x 16 chains per workgroup,
-// 64 x 4 = 256 workgroups; otherwise variant 5.
+// 64 x 4 = 256 workgroups; otherwise 4 pairs per workgroup.
 int default_sdot_variant(int n_pairs, int with_xx) {
   if (with_xx && n_pairs <= 64) return kSdotV11;
   if (with_xx && n_pairs <= 128) return kSdotV8;
@@ -987,28 +978,15 @@ __global__ __launch_bounds__(256) void np_sumsq_chunks_lds_kernel(SumsqArgs a) {
 constexpr int kLeafPitch = kPW + 8;
 __device__ __forceinline__ uint32_t np_pad8(uint64_t e) { return uint32_t(e + (e / kPW) * 8); }
 
-template <int kMap>
 __global__ __launch_bounds__(256) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
   __shared__ float sq[kNpBuf / kPW * kLeafPitch];
   __shared__ float leaf_sum[kNpBuf / kPW];
   constexpr int kQ = int(kNpBuf / 256);
-  // kMap 0: client-major (the K passes over the baseline are a whole model apart: L2 misses);
-  // 1: chunk-major, the K clients of a chunk are consecutive workgroups (dealt over the 8 XCDs
-  // together: each XCD's L2 serves the chunk's baseline to its share of them); 2: the K clients of
-  // chunk c all on XCD c mod 8 (workgroups are dealt to the XCDs round-robin), one baseline fetch
-  uint32_t k, c;
-  if (kMap == 0) {
-    k = blockIdx.x / a.n_chunks;
-    c = blockIdx.x % a.n_chunks;
-  } else if (kMap == 1) {
-    k = blockIdx.x % uint32_t(a.K);
-    c = blockIdx.x / uint32_t(a.K);
-  } else {
-    const uint32_t idx = blockIdx.x >> 3;
-    k = idx % uint32_t(a.K);
-    c = (idx / uint32_t(a.K)) * 8 + (blockIdx.x & 7);
-    if (c >= a.n_chunks) return;  // padding (whole workgroup, before any barrier)
-  }
+  // chunk-major: the K clients of a chunk are consecutive workgroups (dealt over the 8 XCDs
+  // together: each XCD's L2 serves the chunk's baseline to its share of them).  Client-major order
+  // (the K passes over the baseline a whole model apart) measured 1.61 ms against 1.26, all K
+  // clients of a chunk on one XCD 1.24.
+  const uint32_t k = blockIdx.x % uint32_t(a.K), c = blockIdx.x / uint32_t(a.K);
   uint32_t lo = 0, hi = a.n_pieces;  // the piece holding chunk c
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
@@ -1067,71 +1045,6 @@ __global__ __launch_bounds__(256) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
   }
 }
 
-// G clients per workgroup: the chunk's baseline is read once into registers (32 values per lane)
-// and each client's x streams against it; squares are staged in two LDS buffers, and the leaves of
-// client g are summed by wave g mod 4 while every wave stages client g + 1 (its x loads issued
-// before the leaf work).  Same sums, same order as np_sumsq_chunks_lds_kernel.
-template <int G>
-__global__ __launch_bounds__(256) void np_sumsq_group_kernel(SumsqArgs a) {
-  __shared__ float sq[2][kNpBuf + kNpBuf / kPW];
-  constexpr int kQ = int(kNpBuf / 256);  // 32 elements per lane: element q * 256 + tid
-  const uint32_t c = blockIdx.x;
-  const int k0 = int(blockIdx.y) * G;
-  const int ng = a.K - k0 < G ? a.K - k0 : G;
-  uint32_t lo = 0, hi = a.n_pieces;  // the piece holding chunk c
-  while (hi - lo > 1) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (a.first_chunk[mid] <= c) lo = mid; else hi = mid;
-  }
-  const plato_agg_chunk p = a.pieces[lo];
-  const uint64_t begin = uint64_t(p.begin) + uint64_t(c - a.first_chunk[lo]) * kNpBuf;
-  const uint64_t end = begin + kNpBuf < uint64_t(p.end) ? begin + kNpBuf : uint64_t(p.end);
-  const uint32_t n = uint32_t(end - begin);
-  const int tid = int(threadIdx.x), wave = tid >> 6;
-  const float* b = a.base + begin;
-  float bv[kQ], xv[kQ];
-#pragma unroll
-  for (int q = 0; q < kQ; ++q) {
-    const uint32_t i = uint32_t(q * 256 + tid);
-    bv[q] = i < n ? b[i] : 0.f;
-  }
-  auto load_x = [&](int g) {
-    const float* x = sld(a.x, k0 + g) + begin;
-#pragma unroll
-    for (int q = 0; q < kQ; ++q) {
-      const uint32_t i = uint32_t(q * 256 + tid);
-      xv[q] = i < n ? __builtin_nontemporal_load(x + i) : 0.f;
-    }
-  };
-  load_x(0);
-  for (int g = 0; g < ng; ++g) {
-    float* buf = sq[g & 1];
-#pragma unroll
-    for (int q = 0; q < kQ; ++q) {
-      const uint32_t i = uint32_t(q * 256 + tid);
-      const float d = xv[q] - bv[q];
-      if (i < n) buf[np_pad(i)] = d * d;
-    }
-    __syncthreads();  // client g staged; the leaves of client g - 1 (other buffer) are done
-    if (g + 1 < ng) load_x(g + 1);  // in flight during the leaf work
-    if (wave == (g & 3)) {
-      const int lane = tid & 63;
-      const auto v = [&](uint64_t e) { return buf[np_pad(e)]; };
-      float* dst = a.chunk_sums + uint64_t(k0 + g) * a.n_chunks + c;
-      if (n == kNpBuf) {
-        float s = pw_leaf(v, uint64_t(lane) * kPW, kPW);
-#pragma unroll
-        for (int m = 1; m < 64; m <<= 1) s = s + __shfl_xor(s, m);
-        if (lane == 0) *dst = s;
-      } else if (lane == 0) {
-        uint32_t so[16], sn[16], stage[16];
-        float sl[16];
-        *dst = pw_walk([&](uint32_t o, uint32_t m) { return pw_leaf(v, o, m); }, 0, n, PwStack{so, sn, sl, stage});
-      }
-    }
-  }
-}
-
 __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   if (t >= uint64_t(a.n_pieces) * uint64_t(a.K)) return;
@@ -1143,32 +1056,16 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   a.out[uint64_t(k) * a.n_pieces + pc] = out;
 }
 
-// variant 0: one client per workgroup (np_sumsq_chunks_lds_kernel); 1..: G clients per workgroup
+// variant 0: chunk-major, latency-shaped (np_sumsq_chunks_v2_kernel, the default); 1: the round-2
+// form (np_sumsq_chunks_lds_kernel, client-major, four memory round trips per workgroup).  G clients per
+// workgroup sharing the baseline (4.1-5.9 ms) were dropped after round 3.
 void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
-  const uint32_t nc = a.n_chunks;
-  auto grid = [&](int g) { return dim3(nc, uint32_t((a.K + g - 1) / g)); };
-  switch (variant) {
-    case 1: hipLaunchKernelGGL(np_sumsq_group_kernel<4>, grid(4), dim3(256), 0, st, a); break;
-    case 2: hipLaunchKernelGGL(np_sumsq_group_kernel<8>, grid(8), dim3(256), 0, st, a); break;
-    case 3: hipLaunchKernelGGL(np_sumsq_group_kernel<16>, grid(16), dim3(256), 0, st, a); break;
-    case 4:
-      hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel<0>, dim3(uint32_t(uint64_t(nc) * uint64_t(a.K))), dim3(256), 0, st,
-                         a);
-      break;
-    case 5:
-      hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel<1>, dim3(uint32_t(uint64_t(nc) * uint64_t(a.K))), dim3(256), 0, st,
-                         a);
-      break;
-    case 6:
-      hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel<2>, dim3(uint32_t(uint64_t((nc + 7) / 8 * 8) * uint64_t(a.K))),
-                         dim3(256), 0, st, a);
-      break;
-    default:
-      hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, dim3(uint32_t(uint64_t(nc) * uint64_t(a.K))), dim3(256), 0, st, a);
-  }
+  const dim3 grid(uint32_t(uint64_t(a.n_chunks) * uint64_t(a.K)));
+  if (variant == 1) hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, grid, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel, grid, dim3(256), 0, st, a);
 }
-constexpr int kNumSumsqVariants = 7;
-constexpr int kSumsqDefault = 5;  // chunk-major v2: 1.24-1.27 ms vs 1.65 (variant 0) on 128 ResNet-18 clients
+[[maybe_unused]] constexpr int kNumSumsqVariants = 2;
+constexpr int kSumsqDefault = 0;  // chunk-major v2: 1.24-1.27 ms vs 1.65 (variant 1) on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
                  float* d_out, hipStream_t stream);

@@ -271,19 +271,13 @@ void launch_pn(const PnArgs& a, hipStream_t st, int V) {
 // producer waves x tiles of loads in flight
 constexpr PnFn kPnDefault = &launch_pn<8, 3, true>;
 #ifdef PLATO_AGG_TUNE
+// The round-3 sweep (1-8 producer waves x 2-4 tiles in flight, plain or non-temporal flat stores;
+// profiles/r03l_port.log) is in DESIGN.md §13; kept: the default and the runners-up.
 const PnFn kPnVariants[] = {
-    &launch_pn<4, 2>,  // 0: 4.33 ms on 129 ResNet-18 vectors, 5.12 storing the flat vectors (profiles/r03l_port.log)
-    &launch_pn<1, 2>,  // 1: 7.99 ms
-    &launch_pn<1, 4>,  // 2: 6.53 ms
-    &launch_pn<2, 2>,  // 3: 5.40 ms
-    &launch_pn<2, 3>,  // 4: 5.33 ms
-    &launch_pn<4, 3>,  // 5: 4.45 ms
-    &launch_pn<8, 2>,  // 6
-    &launch_pn<8, 3>,  // 7
-    &launch_pn<4, 4>,  // 8
-    &launch_pn<4, 2, true>,  // 9: non-temporal stores of the flattened vectors
-    &launch_pn<8, 2, true>,  // 10
-    &launch_pn<8, 3, true>,  // 11: the default, 4.81 ms storing the flat vectors
+    &launch_pn<8, 3, true>,  // 0: the default, 4.81 ms storing the flat vectors
+    &launch_pn<4, 2>,        // 1: 4.33 ms on 129 ResNet-18 vectors, 5.12 storing the flat vectors
+    &launch_pn<4, 3>,        // 2: 4.45 ms
+    &launch_pn<8, 2, true>,  // 3
 };
 constexpr int kNumPnVariants = sizeof(kPnVariants) / sizeof(kPnVariants[0]);
 #endif

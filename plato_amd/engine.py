@@ -344,6 +344,16 @@ class FedAvgEngine:
             return None  # an entry was replaced or written after arrival: stage the current tensors
         return hit[3], hit[4]
 
+    def drop_arrival(self, payload) -> None:
+        """Return one payload's arrival slot (a multi-GPU prestage that failed on another device).
+
+        A copy still in flight into the row is ordered before any later copy into it (one copy stream)."""
+        hit = self._arrivals.pop(id(payload), None)
+        if hit is not None and hit[0] is payload:
+            self._arrival_free.setdefault(hit[1], []).append((hit[5], hit[6]))
+        elif hit is not None:
+            self._arrivals[id(payload)] = hit
+
     def release_arrivals(self) -> None:
         """Return every arrival slot (after the round that used them has completed, or failed)."""
         for payload, codec, _, _, _, slab, row, _ in self._arrivals.values():

@@ -808,6 +808,9 @@ class EntryShardedEngine:
         self.multi = multi
         self.devices = multi.devices
         self.variant = multi.variant
+        # shard 0 gets its own engine rather than the multi engine's primary: an engine keeps one
+        # staging layout, and the primary's (the whole model, for codecs staged on one GPU) and
+        # shard 0's (its entries) would evict each other's arenas and arrivals every round
         self._engines = [FedAvgEngine(d, variant=multi.variant) for d in self.devices]
         self._plans: dict = {}
         self._arrivals: dict = {}
@@ -865,11 +868,15 @@ class EntryShardedEngine:
             return False
         _, parts = self.plan(baseline_layout)
         subs = [_sub_payload(payload, names) for _, names in parts]
+        done = []
         for (g, names), sub in zip(parts, subs):
             lay = self._sub_layout(baseline_layout, names)
             with torch.cuda.device(self.devices[g]):
                 if not self._engines[g].prestage(sub, lay):
+                    for g0, sub0 in done:  # no half-staged payload keeps slots on the other shards
+                        self._engines[g0].drop_arrival(sub0)
                     return False
+            done.append((g, sub))
         self._arrivals[id(payload)] = (payload, payload_fingerprint(payload), subs)
         return True
 

@@ -301,7 +301,7 @@ def port_norms(dev, k, n, reps):
     chunk = torch.from_numpy(np.asarray([[0, 0, stride, 0]], dtype=np.uint32).view(np.int32)).to(dev)
     h = torch.cuda.current_stream(dev).cuda_stream
     ref = None
-    for v in (12, 9, 10, 11, 13, 14, 15, 16):
+    for v in range(_lib.tune().plato_agg_tune_num_entry_norms_variants()):
         out = torch.empty(k + 1, device=dev)
 
         def fn():
@@ -322,7 +322,7 @@ def port_norms(dev, k, n, reps):
         med = statistics.median(ts)
         print(json.dumps({"port_norms_variant": v, "vectors": k + 1, "n": stride, "ms_median": round(med, 4),
                           "cycles_per_step_at_2.4GHz": round(med * 1e-3 * 2.4e9 / (stride // 8), 2),
-                          "bitwise_equal_to_v12": got == ref}), flush=True)
+                          "bitwise_equal_to_v0": got == ref}), flush=True)
 
 
 def sdot_kernels(dev, k, n, reps):

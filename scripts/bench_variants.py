@@ -148,7 +148,7 @@ def main():
         for v in vlist:
             kernels[f"qsgd_v{v}"] = ((lambda v=v: run_qsgd(v)), kernels["qsgd"][1])
     if args.norm_variants:  # tuning: every plato_agg_tune_entry_norms variant
-        for v in range(17):
+        for v in range(_lib.tune().plato_agg_tune_num_entry_norms_variants()):
             kernels[f"norms_v{v}"] = ((lambda v=v: run_norms(v)), kernels["norms"][1])
     for name, (fn, nbytes) in kernels.items():
         if args.only and name.split("_v")[0] not in args.only.split(","):

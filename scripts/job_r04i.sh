@@ -1,0 +1,12 @@
+#!/bin/bash
+# round 4: register-staged FedAtt norms kernel shapes; QSGD software-pipelined / persistent shapes
+set -u
+mkdir -p gpurun_out/r04i
+timeout -k 10 900 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/test_gpu_kernels.py tests/test_qsgd_gpu.py > gpurun_out/r04i/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc"; grep -E "FAIL|Error|passed|failed" gpurun_out/r04i/pytest.log | tail -12; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -u scripts/bench_variants.py --only qsgd --qsgd-variants --clients 128 --reps 20 > gpurun_out/r04i/qsgd_k128.log 2>&1
+rc=$?; echo "qsgd rc=$rc"; grep qsgd gpurun_out/r04i/qsgd_k128.log; [ $rc -eq 0 ] || exit $rc
+for k in 128 32 4; do
+  timeout -k 10 300 python -u scripts/bench_variants.py --only norms --norm-variants --clients $k --reps 10 > gpurun_out/r04i/norms_k$k.log 2>&1
+  rc=$?; echo "norms k=$k rc=$rc"; grep norms gpurun_out/r04i/norms_k$k.log; [ $rc -eq 0 ] || exit $rc
+done

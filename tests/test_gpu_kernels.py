@@ -173,7 +173,7 @@ def test_split_launch_ranges_bit_exact(engine, groups):
     lib = _lib.tune()
     lib.plato_agg_tune_set_launch_groups(groups)
     try:
-        for v in (0, 14, 10):  # variant 0 = the default kernel, from the tuning library whose split is lowered
+        for v in (0, 6, 5):  # variant 0 = the default kernel, from the tuning library whose split is lowered
             got_f, got_i = _run(engine, layout, base, slab, k, weights, scales=scales, variant=v)
             exp_f, exp_i = ref.fedavg_numpy(bf, bi, xs_f, xs_i, weights, scales)
             assert bits_equal(got_f, exp_f), (v, first_mismatch(got_f, exp_f))

@@ -477,3 +477,23 @@ def test_entry_sharded_round_rejects_whole_model_reductions():
     with pytest.raises(ValueError, match="one GPU"):
         rnd.launch_entrywise(np.ones((len(layout.entries), recipe["k"])), add_base=False, device=True)
     assert not hasattr(rnd, "fedadp_dots") and not hasattr(rnd, "model_similarities")
+
+
+def test_entry_sharded_prestage_failure_keeps_no_slot():
+    """A payload whose prestage fails on one shard leaves no arrival slot on the shards before it."""
+    from tests.test_per_entry_gpu import CASES as PE, _host
+    from plato_amd.arena import ArenaLayout
+    from plato_amd.multi import MultiDeviceEngine
+
+    recipe = PE["fedadp_lenet5_k6"]["recipe"]
+    layout, base, pays, _, _ = _host(recipe)
+    eng = MultiDeviceEngine(_devices(2)).entries
+    lay = ArenaLayout.from_state_dict(base)
+    assert eng.prestage(pays[0], lay)
+    assert len(eng._engines[0]._arrivals) == 1 and len(eng._engines[1]._arrivals) == 1
+    eng._engines[1].prestage = lambda payload, layout: False
+    assert not eng.prestage(pays[1], lay)
+    assert len(eng._engines[0]._arrivals) == 1  # only the first payload's slot
+    assert id(pays[1]) not in eng._arrivals
+    eng._release()
+    assert eng._engines[0]._arrivals == {}

@@ -125,8 +125,8 @@ RING_SPEC = [("a", (5,), "f32"), ("w", (33333,), "f32"), ("n", (), "i64"), ("v",
 
 @pytest.mark.parametrize("k,deltas", [(5, False), (8, False), (3, True)])
 def test_entry_norm_kernels_agree_bitwise(engine, k, deltas):
-    """Ring kernel (default) == per-wave kernel == torch CPU order, across ring wrap-around,
-    unaligned entry starts, client groups with dead slots and both arena tails."""
+    """Every entry_norms kernel (LDS-DMA and register-staged producer / consumer shapes, per-wave) ==
+    torch CPU order, across ring wrap-around, unaligned entry starts and both arena tails."""
     from plato_amd import _lib
 
     for spec in (RING_SPEC, RING_SPEC[:-1] + [("z", (12291,), "f32")]):  # n_f32 % 4 == 0 / == 3
@@ -146,7 +146,7 @@ def test_entry_norm_kernels_agree_bitwise(engine, k, deltas):
         ef, ei = engine._norm_tables(layout)
         n_e = len(layout.entries)
         outs = []
-        for variant in (0, 1, 2, 3, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15, 16):
+        for variant in range(_lib.tune().plato_agg_tune_num_entry_norms_variants()):
             out = torch.full((k * n_e,), float("nan"), device=dev)
             _lib.tune_call("plato_agg_tune_entry_norms", variant, tf.data_ptr(), ti.data_ptr(), k,
                       None if deltas else b_f.data_ptr(), None if deltas else b_i.data_ptr(), ef.data_ptr(),
