@@ -90,6 +90,7 @@ struct AdpArgs {
   AdpDesc* desc;                 // [2][ngroups]
   uint32_t* bnd_at;              // [max_bnd]: (cg, group) of each boundary row
   uint32_t* n_bnd;               // number of boundary rows
+  uint32_t* cnt;                 // [ceil(2 ngroups / 256)]: boundary groups per descriptor block
   float* bnd;                    // [n_pairs][max_bnd][256]: process_grad's values of the boundary groups
   uint32_t n_segs;
   uint32_t ngroups;              // 8-block groups: ceil(nsteps / 8)
@@ -134,13 +135,16 @@ __device__ __forceinline__ uint32_t adp_find(const plato_agg_segment* segs, uint
   return lo;
 }
 
-// process_grad's value at any position of pair `pair` (the boundary groups and the epilogue)
-__device__ float adp_y_at(const AdpArgs& a, int pair, uint64_t p) {
-  const plato_agg_segment sg = a.segs[adp_find(a.segs, a.n_segs, p)];
+// process_grad's value at position p of pair `pair`, in segment sidx (the boundary groups and the epilogue)
+__device__ float adp_y_in(const AdpArgs& a, int pair, uint64_t p, uint32_t sidx) {
+  const plato_agg_segment sg = a.segs[sidx];
   const uint64_t e = sg.src_offset + (p - sg.flat_offset);
   const bool neg = sg.flags & PLATO_AGG_SEG_NEG_DIV;
   if (sg.region) return adp_i64(a.xi[pair][e], a.base_i[e], neg, a.lr);
   return adp_f32(a.xf[pair][e], a.base_f[e], neg, a.lr);
+}
+__device__ float adp_y_at(const AdpArgs& a, int pair, uint64_t p) {
+  return adp_y_in(a, pair, p, adp_find(a.segs, a.n_segs, p));
 }
 
 // Tuning flags (kF): client arenas read non-temporally, the division as a float64 product, x and
@@ -372,53 +376,59 @@ __global__ __launch_bounds__(64 * (kW + 2)) void fedadp_dots_kernel(AdpArgs a) {
 }
 
 // The descriptor of every (cg, group): fast if all its positions (whole blocks only) lie in one
-// fp32 entry, else a boundary group (its row in the table comes from fedadp_rows_kernel)
+// fp32 entry, else a boundary group (its row in the table comes from fedadp_rows_kernel); and the
+// boundary groups of each 256-descriptor block, for the rows' scan
 __global__ __launch_bounds__(256) void fedadp_desc_kernel(AdpArgs a) {
+  __shared__ uint32_t wave_cnt[4];
   const uint32_t j = blockIdx.x * 256u + threadIdx.x;
-  if (j >= 2 * a.ngroups) return;
-  const uint32_t cg = j / a.ngroups, grp = j % a.ngroups;
-  const uint64_t s_last = min(uint64_t(grp) * 8 + 7, a.nsteps - 1);
-  const uint64_t pf = uint64_t(grp) * 8 * 64 + cg * 32, pl = s_last * 64 + cg * 32 + 31;
-  const plato_agg_segment sg = a.segs[adp_find(a.segs, a.n_segs, pf)];
-  AdpDesc d;
-  if (!sg.region && pl < sg.flat_offset + sg.numel) {
-    d.off = uint32_t(sg.src_offset - sg.flat_offset);  // mod 2^32: position + off = arena element
-    d.flags = (sg.flags & PLATO_AGG_SEG_NEG_DIV) ? kDescNeg : 0u;
-  } else {
-    d.off = 0;
-    d.flags = kDescBoundary;
+  bool bnd = false;
+  if (j < 2 * a.ngroups) {
+    const uint32_t cg = j / a.ngroups, grp = j % a.ngroups;
+    const uint64_t s_last = min(uint64_t(grp) * 8 + 7, a.nsteps - 1);
+    const uint64_t pf = uint64_t(grp) * 8 * 64 + cg * 32, pl = s_last * 64 + cg * 32 + 31;
+    const plato_agg_segment sg = a.segs[adp_find(a.segs, a.n_segs, pf)];
+    AdpDesc d;
+    if (!sg.region && pl < sg.flat_offset + sg.numel) {
+      d.off = uint32_t(sg.src_offset - sg.flat_offset);  // mod 2^32: position + off = arena element
+      d.flags = (sg.flags & PLATO_AGG_SEG_NEG_DIV) ? kDescNeg : 0u;
+    } else {
+      d.off = 0;
+      d.flags = kDescBoundary;
+      bnd = true;
+    }
+    a.desc[j] = d;
   }
-  a.desc[j] = d;
+  const uint64_t m = __ballot(bnd);
+  if ((threadIdx.x & 63) == 0) wave_cnt[threadIdx.x >> 6] = uint32_t(__popcll(m));
+  __syncthreads();
+  if (threadIdx.x == 0) a.cnt[blockIdx.x] = wave_cnt[0] + wave_cnt[1] + wave_cnt[2] + wave_cnt[3];
 }
 
-// Rows of the boundary table, in (cg, group) order: one workgroup; thread t counts the boundary
-// groups of its contiguous run of descriptors, an exclusive scan of the 1,024 counts (wave
-// shuffles, then the 16 wave totals) gives each run its first row, and the run is numbered in order
-__global__ __launch_bounds__(1024) void fedadp_rows_kernel(AdpArgs a) {
-  __shared__ uint32_t wave_tot[16];
-  const uint32_t n = 2 * a.ngroups;
-  const uint32_t run = (n + 1023) / 1024;
-  const uint32_t j0 = min(threadIdx.x * run, n), j1 = min(j0 + run, n);
-  uint32_t cnt = 0;
-  for (uint32_t j = j0; j < j1; ++j) cnt += (a.desc[j].flags & kDescBoundary) ? 1u : 0u;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  uint32_t incl = cnt;  // inclusive scan within the wave
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t v = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += v;
+// Rows of the boundary table, in (cg, group) order: one workgroup per 256-descriptor block; the
+// block's first row is the sum of the earlier blocks' counts, each boundary descriptor's row within
+// the block its rank among the block's boundary descriptors (ballots); the last block writes the total
+__global__ __launch_bounds__(256) void fedadp_rows_kernel(AdpArgs a) {
+  __shared__ uint32_t part[4], wave_cnt[4];
+  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  uint32_t before = 0;
+  for (uint32_t b = threadIdx.x; b < blockIdx.x; b += 256) before += a.cnt[b];
+  for (int d = 32; d >= 1; d >>= 1) before += __shfl_xor(before, d, 64);
+  const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+  const bool bnd = j < 2 * a.ngroups && (a.desc[j].flags & kDescBoundary);
+  const uint64_t m = __ballot(bnd);
+  if (lane == 0) {
+    part[wave] = before;
+    wave_cnt[wave] = uint32_t(__popcll(m));
   }
-  if (lane == 63) wave_tot[wave] = incl;
   __syncthreads();
-  uint32_t row = incl - cnt;
-  for (int v = 0; v < wave; ++v) row += wave_tot[v];
-  for (uint32_t j = j0; j < j1; ++j) {
-    if (a.desc[j].flags & kDescBoundary) {
-      a.desc[j].off = row;
-      if (row < a.max_bnd) a.bnd_at[row] = j;
-      ++row;
-    }
+  uint32_t row = part[0] + part[1] + part[2] + part[3];
+  for (uint32_t w = 0; w < wave; ++w) row += wave_cnt[w];
+  row += uint32_t(__popcll(m & ((uint64_t(1) << lane) - 1)));
+  if (bnd) {
+    a.desc[j].off = row;
+    if (row < a.max_bnd) a.bnd_at[row] = j;
   }
-  if (threadIdx.x == 1023) *a.n_bnd = row;  // the last run ends at the total
+  if (blockIdx.x == gridDim.x - 1 && threadIdx.x == 255) *a.n_bnd = row + (bnd ? 1u : 0u);
 }
 
 // The boundary table: process_grad's values of every boundary group of every pair, in the lane
@@ -432,7 +442,18 @@ __global__ __launch_bounds__(256) void fedadp_boundary_kernel(AdpArgs a) {
   const uint32_t cg = j / a.ngroups, grp = j % a.ngroups;
   const uint32_t u = threadIdx.x / 32, v = threadIdx.x % 32;
   const uint64_t s = uint64_t(grp) * 8 + u;
-  const float val = s < a.nsteps ? adp_y_at(a, pair, s * 64 + cg * 32 + v) : 0.f;
+  // one segment search per workgroup (its first position), then short forward walks: the group's
+  // 512-position span crosses few segments
+  __shared__ uint32_t first;
+  if (threadIdx.x == 0) first = adp_find(a.segs, a.n_segs, uint64_t(grp) * 512 + cg * 32);
+  __syncthreads();
+  float val = 0.f;
+  if (s < a.nsteps) {
+    const uint64_t p = s * 64 + cg * 32 + v;
+    uint32_t idx = first;
+    while (idx + 1 < a.n_segs && a.segs[idx + 1].flat_offset <= p) ++idx;
+    val = adp_y_in(a, pair, p, idx);
+  }
   a.bnd[(uint64_t(pair) * a.max_bnd + row) * 256 + threadIdx.x] = val;
 }
 
@@ -560,14 +581,15 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
                uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
                float* d_out_xy, float* d_out_yy, hipStream_t stream);
 
-// workspace: [chain sums][descriptors][boundary rows + count][boundary table][xb], 256-byte aligned parts
+// workspace: [chain sums][descriptors][boundary rows + count][block counts][boundary table][xb],
+// 256-byte aligned parts
 size_t align256(size_t v) { return (v + 255) / 256 * 256; }
 // Boundary groups per chain group: one ends at (and so holds) each segment start — at most n_segs
 // — plus the groups that lie wholly inside int64 entries, each holding 256 of the chain group's
 // int64 positions: at most n_i64 / 256
 size_t adp_max_bnd(uint32_t n_segs, size_t n_i64) { return 2 * (size_t(n_segs) + n_i64 / 256 + 1); }
 struct AdpWs {
-  size_t chains, desc, bnd_at, bnd, xb, total;
+  size_t chains, desc, bnd_at, cnt, bnd, xb, total;
 };
 AdpWs adp_ws(int n_pairs, int with_xx, size_t n_i64, size_t n_flat, uint32_t n_segs) {
   const size_t k = size_t(n_pairs > 0 ? n_pairs : 0);
@@ -577,7 +599,8 @@ AdpWs adp_ws(int n_pairs, int with_xx, size_t n_i64, size_t n_flat, uint32_t n_s
   w.chains = 0;
   w.desc = align256((k + (with_xx ? 1 : 0)) * 128 * sizeof(float));
   w.bnd_at = align256(w.desc + 2 * ngroups * sizeof(AdpDesc));
-  w.bnd = align256(w.bnd_at + (max_bnd + 1) * sizeof(uint32_t));
+  w.cnt = align256(w.bnd_at + (max_bnd + 1) * sizeof(uint32_t));
+  w.bnd = align256(w.cnt + (2 * ngroups + 255) / 256 * sizeof(uint32_t));
   w.xb = align256(w.bnd + k * max_bnd * 256 * sizeof(float));
   w.total = w.xb + 2 * ngroups * 512 * sizeof(float);
   return w;
@@ -657,6 +680,7 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
   a.desc = reinterpret_cast<AdpDesc*>(ws + w.desc);
   a.bnd_at = reinterpret_cast<uint32_t*>(ws + w.bnd_at);
   a.n_bnd = a.bnd_at + a.max_bnd;
+  a.cnt = reinterpret_cast<uint32_t*>(ws + w.cnt);
   a.bnd = reinterpret_cast<float*>(ws + w.bnd);
   a.xb = reinterpret_cast<const float*>(ws + w.xb);
   a.n_i64 = n_i64;
@@ -666,7 +690,7 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
   if (a.nsteps) {
     hipLaunchKernelGGL(fedadp_desc_kernel, dim3((2 * a.ngroups + 255) / 256), dim3(256), 0, stream, a);
     if (int rc = check_launch("fedadp_desc launch")) return rc;
-    hipLaunchKernelGGL(fedadp_rows_kernel, dim3(1), dim3(1024), 0, stream, a);
+    hipLaunchKernelGGL(fedadp_rows_kernel, dim3((2 * a.ngroups + 255) / 256), dim3(256), 0, stream, a);
     if (int rc = check_launch("fedadp_rows launch")) return rc;
     hipLaunchKernelGGL(fedadp_boundary_kernel, dim3(a.max_bnd, uint32_t(n_pairs)), dim3(256), 0, stream, a);
     if (int rc = check_launch("fedadp_boundary launch")) return rc;
