@@ -91,11 +91,13 @@ int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const
                                hipStream_t stream);
 
 /* plato_agg_fedavg_qsgd kernel variants, workgroup size x clients per decode-table batch x
- * elements per lane: 0 = 512x4x8 pipelined (double-buffered tables, the next batch's codes loaded
- * before the current batch is summed, one barrier per batch; plato_agg_fedavg_qsgd), 1 = 1024x8x8
- * not pipelined (the round-1 default), 2-4 = timing probes of variant 0 (NOT the FedAvg: no code
- * loads / no table lookups / neither).  plato_agg_tune_qsgd_chunk gives the chunk capacity
- * (elements per workgroup pass) the variant is built for. */
+ * elements per lane: 0 = 1024x8x8, one barrier pair per table batch (plato_agg_fedavg_qsgd; the
+ * round-1 default, again since round 4), 1 = 512x4x8 pipelined (double-buffered tables, the next
+ * batch's codes loaded before the current batch is summed; the rounds 2-3 default), 2-4 = timing
+ * probes of variant 1 (NOT the FedAvg: no code loads / no table lookups / neither), 5-7 = variant 1
+ * with software-pipelined lookups and / or a persistent grid, 8-11 = plain shapes 1024x16x8,
+ * 1024x4x8, 512x8x8, 1024x8x4.  plato_agg_tune_qsgd_chunk gives the chunk capacity (elements per
+ * workgroup pass) the variant is built for. */
 int plato_agg_tune_num_qsgd_variants(void);
 int plato_agg_tune_qsgd_chunk(int variant);
 int plato_agg_tune_fedavg_qsgd(int variant, const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64,

@@ -978,49 +978,97 @@ __global__ __launch_bounds__(256) void np_sumsq_chunks_lds_kernel(SumsqArgs a) {
 constexpr int kLeafPitch = kPW + 8;
 __device__ __forceinline__ uint32_t np_pad8(uint64_t e) { return uint32_t(e + (e / kPW) * 8); }
 
-__global__ __launch_bounds__(256) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
-  __shared__ float sq[kNpBuf / kPW * kLeafPitch];
-  __shared__ float leaf_sum[kNpBuf / kPW];
-  constexpr int kQ = int(kNpBuf / 256);
-  // chunk-major: the K clients of a chunk are consecutive workgroups (dealt over the 8 XCDs
-  // together: each XCD's L2 serves the chunk's baseline to its share of them).  Client-major order
-  // (the K passes over the baseline a whole model apart) measured 1.61 ms against 1.26, all K
-  // clients of a chunk on one XCD 1.24.
-  const uint32_t k = blockIdx.x % uint32_t(a.K), c = blockIdx.x / uint32_t(a.K);
+
+// Task t of the chunk-major numbering: client t mod K of chunk t / K (the K clients of a chunk are
+// consecutive: each XCD's L2 serves the chunk's baseline to its share of them).  Client-major order
+// (the K passes over the baseline a whole model apart) measured 1.61 ms against 1.26, all K
+// clients of a chunk on one XCD 1.24.
+struct NpTask {
+  uint32_t k, c, n;
+  uint64_t begin;
+};
+__device__ __forceinline__ NpTask np_task(const SumsqArgs& a, uint64_t t) {
+  NpTask r;
+  r.k = uint32_t(t % uint64_t(a.K));
+  r.c = uint32_t(t / uint64_t(a.K));
   uint32_t lo = 0, hi = a.n_pieces;  // the piece holding chunk c
   while (hi - lo > 1) {
     const uint32_t mid = (lo + hi) >> 1;
-    if (a.first_chunk[mid] <= c) lo = mid; else hi = mid;
+    if (a.first_chunk[mid] <= r.c) lo = mid; else hi = mid;
   }
   const plato_agg_chunk p = a.pieces[lo];
-  const uint64_t begin = uint64_t(p.begin) + uint64_t(c - a.first_chunk[lo]) * kNpBuf;
-  const uint64_t end = begin + kNpBuf < uint64_t(p.end) ? begin + kNpBuf : uint64_t(p.end);
-  const uint32_t n = uint32_t(end - begin);
-  const float* x = a.x[k] + begin;
-  const float* b = a.base + begin;
-  const int tid = int(threadIdx.x);
-  {
-    float xv[kQ], bv[kQ];
+  r.begin = uint64_t(p.begin) + uint64_t(r.c - a.first_chunk[lo]) * kNpBuf;
+  const uint64_t end = r.begin + kNpBuf < uint64_t(p.end) ? r.begin + kNpBuf : uint64_t(p.end);
+  r.n = uint32_t(end - r.begin);
+  // workgroup-uniform: keep the task in SGPRs (scalar bases for the loads)
+  r.k = __builtin_amdgcn_readfirstlane(r.k);
+  r.c = __builtin_amdgcn_readfirstlane(r.c);
+  r.n = __builtin_amdgcn_readfirstlane(r.n);
+  r.begin = (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(r.begin >> 32))) << 32) |
+            __builtin_amdgcn_readfirstlane(uint32_t(r.begin));
+  return r;
+}
+
+// kT threads per workgroup, kNpBuf / kT elements per lane: element q * kT + tid.  kBuf: buffer
+// loads bounded by the chunk (positions past a partial chunk's end read as 0 and are never staged:
+// np_chunk stages i < n only; one lane offset plus a scalar offset per load, no address registers
+// per load — the persistent kernel's two register sets need that); else guarded global loads.
+template <int kT, bool kBuf = false>
+__device__ __forceinline__ void np_load(const SumsqArgs& a, const NpTask& t, float (&xv)[kNpBuf / kT],
+                                        float (&bv)[kNpBuf / kT]) {
+  const float* x = a.x[t.k] + t.begin;
+  const float* b = a.base + t.begin;
+  if constexpr (kBuf) {
+    const int bytes = int(t.n * 4u);
+    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, bytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), (short)0, bytes, 0x00020000);
+    const uint32_t lane_off = threadIdx.x * 4u;
 #pragma unroll
-    for (int q = 0; q < kQ; ++q) {
-      const uint32_t i = uint32_t(q * 256 + tid);
-      xv[q] = i < n ? __builtin_nontemporal_load(x + i) : 0.f;
-      bv[q] = i < n ? b[i] : 0.f;
+    for (int q = 0; q < int(kNpBuf / kT); ++q) {
+      xv[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, lane_off, q * kT * 4, 0));
+      bv[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, lane_off, q * kT * 4, 0));
     }
+  } else {
 #pragma unroll
-    for (int q = 0; q < kQ; ++q) {
-      const uint32_t i = uint32_t(q * 256 + tid);
-      const float d = xv[q] - bv[q];
-      if (i < n) sq[np_pad8(i)] = d * d;
+    for (int q = 0; q < int(kNpBuf / kT); ++q) {
+      const uint32_t i = uint32_t(q * kT) + threadIdx.x;
+      xv[q] = i < t.n ? __builtin_nontemporal_load(x + i) : 0.f;
+      bv[q] = i < t.n ? b[i] : 0.f;
     }
   }
-  __syncthreads();
-  float* dst = a.chunk_sums + uint64_t(k) * a.n_chunks + c;
-  if (n == kNpBuf) {
-    // 64 leaves x 8 accumulators = 512 lanes: two passes of the 256 threads
+}
+
+// A partial chunk (an entry's last), walked by one lane over the staged squares (the persistent
+// kernel calls it out of line, so that its recursion stack stays out of the register budget).
+__device__ __forceinline__ float np_partial_inl(const float* sq, uint32_t n) {
+  const auto v = [&](uint64_t e) { return sq[np_pad8(e)]; };
+  uint32_t so[16], sn[16], stage[16];
+  float sl[16];
+  return pw_walk([&](uint32_t o, uint32_t m) { return pw_leaf(v, o, m); }, 0, n, PwStack{so, sn, sl, stage});
+}
+__device__ __noinline__ float np_partial(const float* sq, uint32_t n) { return np_partial_inl(sq, n); }
+
+// The chunk's numpy sum of squares from this lane's values: squares staged in LDS, 64 leaves x 8
+// accumulators (numpy's r[0..7] over 16 steps), the 8 partials of a leaf by xor 1, 2, 4 shuffles,
+// the 64 leaves by a 6-level butterfly; a partial chunk walked by lane 0.  Ends with a barrier
+// (the next chunk may restage sq).
+template <int kT, bool kOutline = false>
+__device__ __forceinline__ void np_chunk(const SumsqArgs& a, const NpTask& t, const float (&xv)[kNpBuf / kT],
+                                         const float (&bv)[kNpBuf / kT], float* sq, float* leaf_sum) {
+  const int tid = int(threadIdx.x);
 #pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      const int slot = pass * 256 + tid, leaf = slot >> 3, j = slot & 7;
+  for (int q = 0; q < int(kNpBuf / kT); ++q) {
+    const uint32_t i = uint32_t(q * kT + tid);
+    const float d = xv[q] - bv[q];
+    if (i < t.n) sq[np_pad8(i)] = d * d;
+  }
+  __syncthreads();
+  float* dst = a.chunk_sums + uint64_t(t.k) * a.n_chunks + t.c;
+  if (t.n == kNpBuf) {
+    // 64 leaves x 8 accumulators = 512 lanes: 512 / kT passes
+#pragma unroll
+    for (int pass = 0; pass < 512 / kT; ++pass) {
+      const int slot = pass * kT + tid, leaf = slot >> 3, j = slot & 7;
       const float* l = sq + leaf * kLeafPitch + j;
       float r = l[0];
 #pragma unroll
@@ -1038,10 +1086,52 @@ __global__ __launch_bounds__(256) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
       if (tid == 0) *dst = s;
     }
   } else if (tid == 0) {
-    const auto v = [&](uint64_t e) { return sq[np_pad8(e)]; };
-    uint32_t so[16], sn[16], stage[16];
-    float sl[16];
-    *dst = pw_walk([&](uint32_t o, uint32_t m) { return pw_leaf(v, o, m); }, 0, n, PwStack{so, sn, sl, stage});
+    *dst = kOutline ? np_partial(sq, t.n) : np_partial_inl(sq, t.n);
+  }
+  __syncthreads();
+}
+
+// One workgroup per task, a full chunk's 64 loads per lane out before the first square is staged.
+__global__ __launch_bounds__(256) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
+  __shared__ float sq[kNpBuf / kPW * kLeafPitch];
+  __shared__ float leaf_sum[kNpBuf / kPW];
+  const NpTask t = np_task(a, blockIdx.x);
+  float xv[kNpBuf / 256], bv[kNpBuf / 256];
+  np_load<256>(a, t, xv, bv);
+  np_chunk<256>(a, t, xv, bv, sq, leaf_sum);
+}
+
+// Persistent and software-pipelined (round 4): a grid of a few workgroups per CU walks the tasks
+// (t = blockIdx.x + j * gridDim.x, still chunk-major across the grid), each holding two register
+// sets: the next task's 64 loads per lane go out before the current task's squares are staged and
+// summed, so a CU's loads stay in flight through the LDS phase instead of stopping per workgroup.
+template <int kT>
+__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void np_sumsq_persist_kernel(SumsqArgs a) {
+  constexpr int kQ = int(kNpBuf / kT);
+  __shared__ float sq[kNpBuf / kPW * kLeafPitch];
+  __shared__ float leaf_sum[kNpBuf / kPW];
+  const uint64_t total = uint64_t(a.n_chunks) * uint64_t(a.K), stride = gridDim.x;
+  float xa[kQ], ba[kQ], xb[kQ], bb[kQ];
+  uint64_t t = blockIdx.x;
+  if (t >= total) return;
+  NpTask ta = np_task(a, t), tb;
+  np_load<kT, true>(a, ta, xa, ba);
+  for (;;) {
+    const uint64_t t1 = t + stride;
+    if (t1 < total) {
+      tb = np_task(a, t1);
+      np_load<kT, true>(a, tb, xb, bb);
+    }
+    np_chunk<kT, true>(a, ta, xa, ba, sq, leaf_sum);
+    if (t1 >= total) break;
+    const uint64_t t2 = t1 + stride;
+    if (t2 < total) {
+      ta = np_task(a, t2);
+      np_load<kT, true>(a, ta, xa, ba);
+    }
+    np_chunk<kT, true>(a, tb, xb, bb, sq, leaf_sum);
+    if (t2 >= total) break;
+    t = t2;
   }
 }
 
@@ -1057,14 +1147,22 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
 }
 
 // variant 0: chunk-major, latency-shaped (np_sumsq_chunks_v2_kernel, the default); 1: the round-2
-// form (np_sumsq_chunks_lds_kernel, client-major, four memory round trips per workgroup).  G clients per
-// workgroup sharing the baseline (4.1-5.9 ms) were dropped after round 3.
+// form (np_sumsq_chunks_lds_kernel, client-major, four memory round trips per workgroup); 2, 3: the
+// persistent software-pipelined form, 512 threads, grids of 1 / 2 workgroups per CU.  G clients per workgroup sharing
+// the baseline (4.1-5.9 ms) were dropped after round 3.
 void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
-  const dim3 grid(uint32_t(uint64_t(a.n_chunks) * uint64_t(a.K)));
-  if (variant == 1) hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, grid, dim3(256), 0, st, a);
-  else hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel, grid, dim3(256), 0, st, a);
+  const uint64_t tasks = uint64_t(a.n_chunks) * uint64_t(a.K);
+  const dim3 grid{uint32_t(tasks)};
+  if (variant == 1) {
+    hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, grid, dim3(256), 0, st, a);
+  } else if (variant == 2 || variant == 3) {  // 512 threads, 1 / 2 workgroups per CU
+    const uint64_t g = uint64_t(variant == 2 ? 1 : 2) * 256;
+    hipLaunchKernelGGL(np_sumsq_persist_kernel<512>, dim3(uint32_t(tasks < g ? tasks : g)), dim3(512), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel, grid, dim3(256), 0, st, a);
+  }
 }
-[[maybe_unused]] constexpr int kNumSumsqVariants = 2;
+[[maybe_unused]] constexpr int kNumSumsqVariants = 4;
 constexpr int kSumsqDefault = 0;  // chunk-major v2: 1.24-1.27 ms vs 1.65 (variant 1) on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,

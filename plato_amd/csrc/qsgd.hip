@@ -42,10 +42,10 @@ typedef __attribute__((address_space(1))) const u1 gu1;
 // Kernel shape (tuning space, plato_agg_tune_fedavg_qsgd): B threads per
 // workgroup share each batch's decode tables, U clients per table batch, G
 // elements per lane (one 16/8/4-byte code load per client).  The default
-// (variant 0) is the pipelined form below at B = 512, U = 4, G = 8 (4,096-element
-// chunks); the round-1 default (B = 1024, U = 8, G = 8, not pipelined) is variant 1.
-// Every shape, pipelined, two-level or resident-table form measured lands within
-// 0.32-0.34 ms on C2-sized inputs; DESIGN.md §11 has the counters and probes.
+// (variant 0) is the plain form at B = 1024, U = 8, G = 8 (8,192-element chunks; the round-1
+// default, again since round 4: interleaved A/B on one box 0.331 against 0.373 ms for the
+// pipelined B = 512, U = 4 form of rounds 2-3, now variant 1).  Every shape, pipelined, two-level or
+// resident-table form measured lands within 0.32-0.38 ms on C2-sized inputs; DESIGN.md §11, §14.
 constexpr int kG = 16;      // elements per lane group of the plain kernel's template default
 
 template <class T>
@@ -479,22 +479,24 @@ struct QVariant {
 // the round-1 (non-pipelined) form and the default's timing probes remain.
 #ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so (scripts/bench_variants.py, tests/test_qsgd_gpu.py)
 const QVariant kQVariants[] = {
-    {512, 4, 8, {&launch_qp<512, 4, false, 8>, &launch_qp<512, 4, true, 8>}},        // 0 (default): pipelined
-    {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},       // 1: round-1 default
+    {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},       // 0 (default): plain
+    {512, 4, 8, {&launch_qp<512, 4, false, 8>, &launch_qp<512, 4, true, 8>}},        // 1: pipelined (rounds 2-3)
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 1>, &launch_qp<512, 4, true, 8, 1>}},  // 2: probe, no code loads
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 2>, &launch_qp<512, 4, true, 8, 2>}},  // 3: probe, no lookups
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 3>, &launch_qp<512, 4, true, 8, 3>}},  // 4: probe, neither
-    // round 4: software-pipelined lookups (SP) and a persistent grid (workgroups per CU)
+    // round 4: software-pipelined lookups (SP) and a persistent grid (workgroups per CU) on the
+    // pipelined form, then more shapes of the plain form
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 0, true>, &launch_qp<512, 4, true, 8, 0, true>}},         // 5: SP
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 0, false, 4>, &launch_qp<512, 4, true, 8, 0, false, 4>}},  // 6
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 0, true, 4>, &launch_qp<512, 4, true, 8, 0, true, 4>}},    // 7
-    {512, 8, 8, {&launch_qp<512, 8, false, 8, 0, true>, &launch_qp<512, 8, true, 8, 0, true>}},         // 8
-    {256, 4, 16, {&launch_qp<256, 4, false, 16, 0, true>, &launch_qp<256, 4, true, 16, 0, true>}},      // 9
-    {1024, 4, 8, {&launch_qp<1024, 4, false, 8, 0, true>, &launch_qp<1024, 4, true, 8, 0, true>}},      // 10
+    {1024, 16, 8, {&launch_q<1024, 16, false, 8>, &launch_q<1024, 16, true, 8>}},   // 8
+    {1024, 4, 8, {&launch_q<1024, 4, false, 8>, &launch_q<1024, 4, true, 8>}},      // 9
+    {512, 8, 8, {&launch_q<512, 8, false, 8>, &launch_q<512, 8, true, 8>}},         // 10
+    {1024, 8, 4, {&launch_q<1024, 8, false, 4>, &launch_q<1024, 8, true, 4>}},      // 11
 };
 #else  // libplato_agg.so: the default only
 const QVariant kQVariants[] = {
-    {512, 4, 8, {&launch_qp<512, 4, false, 8>, &launch_qp<512, 4, true, 8>}},  // 0 (default): pipelined
+    {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},  // 0 (default): plain
 };
 #endif
 constexpr int kNumQVariants = sizeof(kQVariants) / sizeof(kQVariants[0]);

@@ -39,6 +39,9 @@ def main():
     ap.add_argument("--norm-variants", action="store_true", help="also time each entry_norms kernel variant")
     ap.add_argument("--qsgd-variants", action="store_true", help="also time each fedavg_qsgd kernel variant")
     ap.add_argument("--qsgd-list", default=None, help="comma-separated fedavg_qsgd variants to time (instead of all)")
+    ap.add_argument("--interleave", type=int, default=0,
+                    help="time the selected kernels round-robin this many rounds (A/B on one box: clock and "
+                         "thermal drift hit every kernel alike); each round times each kernel --reps times")
     ap.add_argument("--norm-order", default="longest", choices=["longest", "layout"],
                     help="entry order of the norms launch (longest first = the engine's)")
     args = ap.parse_args()
@@ -150,25 +153,31 @@ def main():
     if args.norm_variants:  # tuning: every plato_agg_tune_entry_norms variant
         for v in range(_lib.tune().plato_agg_tune_num_entry_norms_variants()):
             kernels[f"norms_v{v}"] = ((lambda v=v: run_norms(v)), kernels["norms"][1])
-    for name, (fn, nbytes) in kernels.items():
-        if args.only and name.split("_v")[0] not in args.only.split(","):
-            continue
+    selected = [(name, fn, nbytes) for name, (fn, nbytes) in kernels.items()
+                if not args.only or name.split("_v")[0] in args.only.split(",")]
+
+    def timed(fn):
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
         fn()
-        torch.cuda.synchronize(dev)
-        times = []
-        for _ in range(args.reps):
-            e0 = torch.cuda.Event(enable_timing=True)
-            e1 = torch.cuda.Event(enable_timing=True)
-            e0.record(stream)
-            fn()
-            e1.record(stream)
-            e1.synchronize()
-            times.append(e0.elapsed_time(e1))
-        med = statistics.median(times)
+        e1.record(stream)
+        e1.synchronize()
+        return e0.elapsed_time(e1)
+
+    times = {name: [] for name, _, _ in selected}
+    for name, fn, _ in selected:  # warm every kernel first
+        fn()
+    torch.cuda.synchronize(dev)
+    for _ in range(max(1, args.interleave)):
+        for name, fn, _ in selected:
+            times[name].extend(timed(fn) for _ in range(args.reps))
+    for name, _, nbytes in selected:
+        med = statistics.median(times[name])
         gbs = nbytes / (med * 1e-3) / 1e9
-        print(json.dumps({"kernel": name, "clients": k, "ms_median": round(med, 4), "ms_min": round(min(times), 4),
+        print(json.dumps({"kernel": name, "clients": k, "ms_median": round(med, 4), "ms_min": round(min(times[name]), 4),
                           "algorithmic_bytes": int(nbytes), "GBps": round(gbs, 1),
-                          "frac_of_8TBps": round(gbs / PEAK, 4)}), flush=True)
+                          "frac_of_8TBps": round(gbs / PEAK, 4), "samples": len(times[name])}), flush=True)
 
 
 if __name__ == "__main__":

@@ -72,10 +72,10 @@ SPEC = [("a", (3,), "f32"), ("n0", (), "i64"), ("b", (17,), "f32"), ("c", (5, 7)
         ("e", (1000,), "f32"), ("g", (4099,), "f32"), ("h", (2,), "f32"), ("big", (3, 4097), "f32")]
 
 
-# the product default (libplato_agg.so) and the tuning library's FedAvg shapes: 0 the default's
-# pipelined form, 1 the round-1 (non-pipelined) default, 5-10 software-pipelined lookups / persistent
-# grids; 2-4 are timing probes (not the FedAvg)
-@pytest.mark.parametrize("variant", [None, 0, 1, 5, 6, 7, 8, 9, 10])
+# the product default (libplato_agg.so) and the tuning library's FedAvg shapes: 0 the default's plain
+# form, 1 the pipelined form of rounds 2-3, 5-7 software-pipelined lookups / persistent grids, 8-11
+# plain shapes; 2-4 are timing probes (not the FedAvg)
+@pytest.mark.parametrize("variant", [None, 0, 1, 5, 6, 7, 8, 9, 10, 11])
 @pytest.mark.parametrize("cap,k,two", [(8, 3, False), (20, 9, True), (4096, 17, False), (64, 16, True), (1 << 20, 5, False)])
 def test_qsgd_kernel_matches_oracle(engine, monkeypatch, cap, k, two, variant):
     """Chunk pieces of every alignment (caps 8/20: partial 16-byte groups everywhere;
