@@ -65,14 +65,16 @@ int plato_agg_tune_fedavg_bf16(int variant, const uint16_t* const* d_x_bf16,
 int plato_agg_tune_stream(int mode, const float* d_src, float* d_dst, size_t n,
                           int blocks, hipStream_t stream);
 
-/* plato_agg_entry_norms_f32 kernel variants (bitwise identical results; csrc/entrywise.hip):
- *   0, 1 = producer / consumer, one workgroup per (entry, client): a producer wave streams x and
- *       b into an LDS-DMA ring (1,024-element tiles x 5 stages / 2,048 x 3) and writes the delta
- *       tiles transposed, the chain wave walks the 8 chains (the long entries' chains at
- *       s_setprio 3); the round-3 defaults for grids of more / at most 6,144 pairs
- *   2 = one wavefront per (entry, client), one-tile register prefetch (the first version)
- *   3.. = register-staged producer / consumer (P producer waves hold D tiles of x and b in
- *       VGPRs; only the transposed delta ring is in LDS); shapes listed in entrywise.hip */
+/* plato_agg_entry_norms_f32 kernel variants (bitwise identical results; csrc/entrywise.hip), one
+ * workgroup per (entry, client):
+ *   0 = register-staged producer / consumer (the default): 2 producer waves hold 2 tiles of x and b
+ *       (2,048 elements) in VGPRs and write the delta tiles transposed into a two-slot LDS ring, the
+ *       chain wave walks the 8 chains (the long entries' chains at s_setprio 3)
+ *   1 = variant 0 with one producer wave; 2 = with 3 tiles in flight and the long entries' producers
+ *       at s_setprio 2
+ *   3, 4 = the round-3 defaults: one producer wave streams x and b into an LDS-DMA ring
+ *       (1,024-element tiles x 5 stages / 2,048 x 3)
+ *   5 = one wavefront per (entry, client), one-tile register prefetch (the first version) */
 int plato_agg_tune_num_entry_norms_variants(void);
 int plato_agg_tune_entry_norms(int variant, const float* const* d_x_f32, const int64_t* const* d_x_i64, int K,
                                const float* d_base_f32, const int64_t* d_base_i64,
@@ -94,10 +96,9 @@ int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const
  * elements per lane: 0 = 1024x8x8, one barrier pair per table batch (plato_agg_fedavg_qsgd; the
  * round-1 default, again since round 4), 1 = 512x4x8 pipelined (double-buffered tables, the next
  * batch's codes loaded before the current batch is summed; the rounds 2-3 default), 2-4 = timing
- * probes of variant 1 (NOT the FedAvg: no code loads / no table lookups / neither), 5-7 = variant 1
- * with software-pipelined lookups and / or a persistent grid, 8-11 = plain shapes 1024x16x8,
- * 1024x4x8, 512x8x8, 1024x8x4.  plato_agg_tune_qsgd_chunk gives the chunk capacity (elements per
- * workgroup pass) the variant is built for. */
+ * probes of variant 1 (NOT the FedAvg: no code loads / no table lookups / neither).
+ * plato_agg_tune_qsgd_chunk gives the chunk capacity (elements per workgroup pass) the variant is
+ * built for. */
 int plato_agg_tune_num_qsgd_variants(void);
 int plato_agg_tune_qsgd_chunk(int variant);
 int plato_agg_tune_fedavg_qsgd(int variant, const uint8_t* const* d_codes_f32, const uint8_t* const* d_codes_i64,

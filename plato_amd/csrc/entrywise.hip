@@ -838,10 +838,7 @@ __global__ __launch_bounds__(128) void entry_norms_pc_kernel(NormArgs a) {
 // the last reload the last tile (valid addresses, never read) and the chain wave
 // meets their barriers without reading.
 // ---------------------------------------------------------------------------
-// kL (lookahead): a three-slot d ring and one extra barrier at the end, so that at barrier tt + 1 the
-// tiles up to tt + 1 are complete and the chain wave can read tile tt + 1's first block while it
-// finishes tile tt (rs_chain); else the two-slot ring of pc_chain.
-template <int T, int P, int D, bool HAS_BASE, bool kL = false>
+template <int T, int P, int D, bool HAS_BASE>
 __device__ void rs_produce(const NormArgs& a, const Chunk ch, const float* x, int w, int lane, float* dtile,
                            int dstride, uint64_t ntiles, uint64_t nbar) {
   constexpr int kTS = DTile<T, true>::kTS;
@@ -870,7 +867,7 @@ __device__ void rs_produce(const NormArgs& a, const Chunk ch, const float* x, in
     for (int j = 0; j < D; ++j) {
       const uint64_t tt = t0 + j;
       wait_vmcnt<(D - 1) * kIt * kOps>();  // tile tt's loads (the oldest D - 1 trips stay in flight)
-      float* dt = dtile + (kL ? tt % 3 : tt & 1) * dstride;
+      float* dt = dtile + (tt & 1) * dstride;
 #pragma unroll
       for (int it = 0; it < kIt; ++it) {
         f4 dv = xr[j][it];
@@ -886,91 +883,14 @@ __device__ void rs_produce(const NormArgs& a, const Chunk ch, const float* x, in
       issue(xr[j], br[j], nt < ntiles ? nt : ntiles - 1);
       wait_lgkm0();  // d tile written (the loads stay in flight)
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
-      __builtin_amdgcn_s_barrier();  // tile tt ready; the chain wave is done with tile tt - 1 (kL: tt - 2)
+      __builtin_amdgcn_s_barrier();  // tile tt ready; the chain wave is done with tile tt - 1
       __atomic_signal_fence(__ATOMIC_SEQ_CST);
     }
   }
-  if (kL) __builtin_amdgcn_s_barrier();  // the chain's last tile
   wait_vmcnt<0>();
 }
 
-// Chain wave of the lookahead ring (kL producers): barrier 0, then per tile tt barrier tt + 1 (tiles
-// up to tt + 1 written) and the chains over tile tt, the last block's reads fetching the first block
-// of tile tt + 1 when that tile is a whole one too — no exposed LDS latency at tile starts.  Same
-// chains, same order as pc_chain.
-template <int T>
-__device__ float rs_chain(const Chunk ch, int lane, const float* dtile, int dstride, uint64_t nbar) {
-  constexpr int kRT = T, kTS = DTile<T, true>::kTS, kSteps = kRT / kNormLanes, kNB = kSteps / 16;
-  const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
-  const uint64_t ntiles = pc_ntiles<T>(ch);
-  const int c = lane & 7;
-  const uint32_t delta = ch.begin & 3u;
-  const int pj = int((uint32_t(c) + delta) & 7u);
-  const int64_t s_shift = (uint32_t(c) + delta) >= 8u ? -1 : 0;
-  const int64_t s_end = int64_t(m / kNormLanes);
-  auto whole = [&](uint64_t tt) { return tt >= 1 && tt < ntiles && int64_t(tt + 1) * kSteps <= s_end; };
-  float acc = 0.f;
-  f4 first[4];
-  bool have_first = false;
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  __builtin_amdgcn_s_barrier();
-  __atomic_signal_fence(__ATOMIC_SEQ_CST);
-  for (uint64_t tt = 0; tt < nbar; ++tt) {
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    __builtin_amdgcn_s_barrier();
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-    if (tt >= ntiles) continue;
-    const float* p = dtile + (tt % 3) * dstride + pj * kTS;
-    if (whole(tt)) {
-      const f4* q4 = reinterpret_cast<const f4*>(p);
-      const bool next = whole(tt + 1);
-      const f4* n4 = reinterpret_cast<const f4*>(dtile + ((tt + 1) % 3) * dstride + pj * kTS);
-      f4 cur[4], nxt[4];
-#pragma unroll
-      for (int q = 0; q < 4; ++q) cur[q] = have_first ? first[q] : q4[q];
-#pragma unroll
-      for (int blk = 0; blk < kNB; ++blk) {
-        if (blk + 1 < kNB) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) nxt[q] = q4[4 * (blk + 1) + q];
-        } else if (next) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) nxt[q] = n4[q];
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          acc = __builtin_fmaf(cur[q].x, cur[q].x, acc);
-          acc = __builtin_fmaf(cur[q].y, cur[q].y, acc);
-          acc = __builtin_fmaf(cur[q].z, cur[q].z, acc);
-          acc = __builtin_fmaf(cur[q].w, cur[q].w, acc);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) cur[q] = nxt[q];
-      }
-#pragma unroll
-      for (int q = 0; q < 4; ++q) first[q] = cur[q];
-      have_first = next;
-    } else {
-      have_first = false;
-      if (lane < kNormLanes) {
-        const int64_t s0 = int64_t(tt) * kSteps + s_shift;
-        for (int u = 0; u < kSteps; ++u) {
-          const int64_t st = s0 + u;
-          if (st >= 0 && st < s_end) {
-            const float v = p[u];
-            acc = __builtin_fmaf(v, v, acc);
-          }
-        }
-      }
-    }
-  }
-  return acc;
-}
-
-// One (entry, client) pair of the register-staged kernels, every wave of the workgroup.
-template <int T, int P, int D, bool HAS_BASE, int PRIO, bool kL = false>
+template <int T, int P, int D, bool HAS_BASE, int PRIO>
 __device__ __forceinline__ void rs_pair(const NormArgs& a, uint64_t pair, int wave, int lane, float* dbuf) {
   constexpr int kSize = DTile<T, true>::kSize;
   const uint32_t ent = uint32_t(pair / uint64_t(a.K));  // entry-major over the (longest-first) tables
@@ -987,26 +907,23 @@ __device__ __forceinline__ void rs_pair(const NormArgs& a, uint64_t pair, int wa
     if (wave > 0) {
       if (PRIO == -2 && pc_long(a, ch)) __builtin_amdgcn_s_setprio(2);  // long producers above short chains
       else __builtin_amdgcn_s_setprio(0);
-      if (ntiles) rs_produce<T, P, D, HAS_BASE, kL>(a, ch, x, wave - 1, lane, dbuf, kSize, ntiles, nbar);
+      if (ntiles) rs_produce<T, P, D, HAS_BASE>(a, ch, x, wave - 1, lane, dbuf, kSize, ntiles, nbar);
       return;
     }
     pc_chain_prio<PRIO>(a, ch);
-    const float acc = !ntiles ? 0.f
-                      : kL   ? rs_chain<T>(ch, lane, dbuf, kSize, nbar)
-                             : pc_chain<T, true>(ch, lane, dbuf, kSize, nbar);
-    pc_finish<HAS_BASE>(a, ch, i, x, lane, acc);
+    pc_finish<HAS_BASE>(a, ch, i, x, lane, pc_chain<T, true>(ch, lane, dbuf, kSize, nbar));
   } else if (ent < a.nef + a.nei) {
     if (wave == 0) norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows);
   }
 }
 
-template <int T, int P, int D, bool HAS_BASE, int PRIO, bool kL = false>
+template <int T, int P, int D, bool HAS_BASE, int PRIO>
 __global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rs_kernel(NormArgs a) {
   constexpr int kSize = DTile<T, true>::kSize;
   static_assert(2 * kSize >= kNormLanes * kNRow, "norm_pair's rows fit the d ring");
-  __shared__ __attribute__((aligned(16))) float dbuf[(kL ? 3 : 2) * kSize];
+  __shared__ __attribute__((aligned(16))) float dbuf[2 * kSize];
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-  rs_pair<T, P, D, HAS_BASE, PRIO, kL>(a, blockIdx.x, wave, lane, dbuf);
+  rs_pair<T, P, D, HAS_BASE, PRIO>(a, blockIdx.x, wave, lane, dbuf);
 }
 
 bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
@@ -1136,10 +1053,10 @@ void launch_pc(const NormArgs& a, bool hb, dim3 grid, hipStream_t st) {
   if (hb) hipLaunchKernelGGL((entry_norms_pc_kernel<T, PS, true, true, -1>), grid, dim3(128), 0, st, a);
   else hipLaunchKernelGGL((entry_norms_pc_kernel<T, PS, false, true, -1>), grid, dim3(128), 0, st, a);
 }
-template <int T, int P, int D, int PRIO = -1, bool L = false>
+template <int T, int P, int D, int PRIO = -1>
 void launch_rs(const NormArgs& a, bool hb, dim3 grid, hipStream_t st) {
-  if (hb) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, true, PRIO, L>), grid, dim3(64 * (1 + P)), 0, st, a);
-  else hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, false, PRIO, L>), grid, dim3(64 * (1 + P)), 0, st, a);
+  if (hb) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, true, PRIO>), grid, dim3(64 * (1 + P)), 0, st, a);
+  else hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, false, PRIO>), grid, dim3(64 * (1 + P)), 0, st, a);
 }
 #ifdef PLATO_AGG_TUNE
 void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
@@ -1149,36 +1066,23 @@ void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
   else hipLaunchKernelGGL(entry_norms_kernel<false>, grid, dim3(kBlock), 0, st, a);
 }
 #endif
-// Variants (include/plato_agg_tune.h; every one bitwise identical).  The rounds-1-3 sweep (natural
+// Variants (include/plato_agg_tune.h; every one bitwise identical).  The rounds 1-4 sweeps (natural
 // tiles, LDS-DMA ring kernels with 1-4 clients per workgroup, flat priorities, 256-1,024-element
-// tiles; DESIGN.md §11, profiles/r0*_norms*) is trimmed to the two round-3 defaults and the
-// per-wave first version; 3.. are the register-staged kernel's shapes (tile, producers, tiles in
-// flight).
-constexpr NormFn kNormDefaultLarge = &launch_pc<1024, 5>;
-constexpr NormFn kNormDefaultSmall = &launch_pc<2048, 3>;
+// tiles; round 4: 1-8 producer waves, 2-4 tiles in flight, a persistent long/short split, a
+// three-slot lookahead ring; DESIGN.md §11, §14, profiles/r0*_norms*) are trimmed to the round-4
+// default, two of its neighbours, the round-3 LDS-DMA defaults and the per-wave first version.
+// Interleaved on one box (K = 128 / 64 / 32 / 4 ResNet-18 clients, profiles/r04j-l_norms_k*.log):
+// <2048, 2, 2> 1.25-1.26 / 0.97 / 0.95 / 0.94 ms against the round-3 defaults' 1.29-1.37 / 1.01 /
+// 1.00 / 0.99.
+constexpr NormFn kNormDefault = &launch_rs<2048, 2, 2>;
 #ifdef PLATO_AGG_TUNE
 const NormFn kNormVariants[] = {
-    &launch_pc<1024, 5>,      // 0: LDS-DMA producer / consumer, 1,024-element tiles, 5 stages
-    &launch_pc<2048, 3>,      // 1: the same, 2,048-element tiles, 3 stages
-    &launch_per_wave,         // 2: one wavefront per (entry, client) (the first version)
-    // register-staged: tile, producer waves, tiles in flight (round 4, K = 128 / 32 / 4 on ResNet-18:
-    // <2048, 2, 3> 1.23 / 0.96 / 0.94 ms, <2048, 4, 3> 1.60 / 0.95 / 0.94, <2048, 8, 3> 2.72 / 0.94 /
-    // 0.93, <1024, 2, 4> 1.33 / 1.07 / 1.05; the LDS-DMA defaults 1.28 and 1.01 / 0.99)
-    &launch_rs<2048, 2, 3>,       // 3
-    &launch_rs<2048, 2, 3, -2>,   // 4: long producers at priority 2
-    &launch_rs<2048, 2, 2>,       // 5
-    &launch_rs<2048, 2, 4>,       // 6
-    &launch_rs<2048, 1, 2>,       // 7
-    &launch_rs<1024, 1, 4>,       // 8
-    &launch_rs<2048, 8, 3>,       // 9
-    &launch_rs<2048, 4, 3>,       // 10
-    &launch_rs<1024, 2, 4>,       // 11
-    &launch_rs<2048, 4, 3, -2>,   // 12
-    // lookahead ring: the chain reads the next tile's first block before its barrier
-    &launch_rs<2048, 2, 2, -1, true>,   // 13
-    &launch_rs<2048, 1, 2, -1, true>,   // 14
-    &launch_rs<2048, 2, 3, -2, true>,   // 15
-    &launch_rs<2048, 4, 3, -1, true>,   // 16
+    &launch_rs<2048, 2, 2>,      // 0: the default: register-staged, 2 producer waves, 2 tiles in flight
+    &launch_rs<2048, 1, 2>,      // 1: one producer wave
+    &launch_rs<2048, 2, 3, -2>,  // 2: 3 tiles in flight, the long entries' producers at priority 2
+    &launch_pc<1024, 5>,         // 3: LDS-DMA producer / consumer, 1,024-element tiles (round 3, > 6,144 pairs)
+    &launch_pc<2048, 3>,         // 4: the same, 2,048-element tiles (round 3, <= 6,144 pairs)
+    &launch_per_wave,            // 5: one wavefront per (entry, client) (the first version)
 };
 constexpr int kNumNormVariants = sizeof(kNormVariants) / sizeof(kNormVariants[0]);
 #endif
@@ -1223,14 +1127,9 @@ int plato_agg_entry_norms_f32(const float* const* d_x_f32, const int64_t* const*
                               const plato_agg_chunk* d_entries_f32, uint32_t n_entries_f32,
                               const plato_agg_chunk* d_entries_i64, uint32_t n_entries_i64, int n_entries,
                               size_t n_f32, size_t n_i64, float* d_out, hipStream_t stream) {
-  // Longer tiles halve the chain wave's barriers and exposed LDS latency per step but take more LDS
-  // per workgroup: 2,048-element tiles (3 stages, 2 workgroups per CU) win on small and medium grids
-  // (Port's K + 1 flattened vectors: 4.33 vs 5.22 ms; FedAtt on ResNet-18, 82 entries, K = 4-64:
-  // 4-6 % ahead of 1,024-element tiles), 1,024-element tiles (5 stages, 3 per CU) on large ones
-  // (FedAtt at K = 128, 10,496 pairs: 1.22 vs 1.48 ms).  DESIGN.md §11.
-  const uint64_t pairs = (uint64_t(n_entries_f32) + n_entries_i64) * uint64_t(K > 0 ? K : 0);
-  return run_norms(pairs <= 6144 ? kNormDefaultSmall : kNormDefaultLarge, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64,
-                   d_entries_f32, n_entries_f32, d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
+  // The register-staged producer / consumer kernel at every grid size.
+  return run_norms(kNormDefault, d_x_f32, d_x_i64, K, d_base_f32, d_base_i64, d_entries_f32, n_entries_f32,
+                   d_entries_i64, n_entries_i64, n_entries, n_f32, n_i64, d_out, stream);
 }
 
 #ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h

@@ -1009,50 +1009,33 @@ __device__ __forceinline__ NpTask np_task(const SumsqArgs& a, uint64_t t) {
   return r;
 }
 
-// kT threads per workgroup, kNpBuf / kT elements per lane: element q * kT + tid.  kBuf: buffer
-// loads bounded by the chunk (positions past a partial chunk's end read as 0 and are never staged:
-// np_chunk stages i < n only; one lane offset plus a scalar offset per load, no address registers
-// per load — the persistent kernel's two register sets need that); else guarded global loads.
-template <int kT, bool kBuf = false>
+// kT threads per workgroup, kNpBuf / kT elements per lane: element q * kT + tid.
+template <int kT>
 __device__ __forceinline__ void np_load(const SumsqArgs& a, const NpTask& t, float (&xv)[kNpBuf / kT],
                                         float (&bv)[kNpBuf / kT]) {
   const float* x = a.x[t.k] + t.begin;
   const float* b = a.base + t.begin;
-  if constexpr (kBuf) {
-    const int bytes = int(t.n * 4u);
-    const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(x), (short)0, bytes, 0x00020000);
-    const __amdgpu_buffer_rsrc_t rb = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(b), (short)0, bytes, 0x00020000);
-    const uint32_t lane_off = threadIdx.x * 4u;
 #pragma unroll
-    for (int q = 0; q < int(kNpBuf / kT); ++q) {
-      xv[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, lane_off, q * kT * 4, 0));
-      bv[q] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rb, lane_off, q * kT * 4, 0));
-    }
-  } else {
-#pragma unroll
-    for (int q = 0; q < int(kNpBuf / kT); ++q) {
-      const uint32_t i = uint32_t(q * kT) + threadIdx.x;
-      xv[q] = i < t.n ? __builtin_nontemporal_load(x + i) : 0.f;
-      bv[q] = i < t.n ? b[i] : 0.f;
-    }
+  for (int q = 0; q < int(kNpBuf / kT); ++q) {
+    const uint32_t i = uint32_t(q * kT) + threadIdx.x;
+    xv[q] = i < t.n ? __builtin_nontemporal_load(x + i) : 0.f;
+    bv[q] = i < t.n ? b[i] : 0.f;
   }
 }
 
-// A partial chunk (an entry's last), walked by one lane over the staged squares (the persistent
-// kernel calls it out of line, so that its recursion stack stays out of the register budget).
-__device__ __forceinline__ float np_partial_inl(const float* sq, uint32_t n) {
+// A partial chunk (an entry's last), walked by one lane over the staged squares.
+__device__ __forceinline__ float np_partial(const float* sq, uint32_t n) {
   const auto v = [&](uint64_t e) { return sq[np_pad8(e)]; };
   uint32_t so[16], sn[16], stage[16];
   float sl[16];
   return pw_walk([&](uint32_t o, uint32_t m) { return pw_leaf(v, o, m); }, 0, n, PwStack{so, sn, sl, stage});
 }
-__device__ __noinline__ float np_partial(const float* sq, uint32_t n) { return np_partial_inl(sq, n); }
 
 // The chunk's numpy sum of squares from this lane's values: squares staged in LDS, 64 leaves x 8
 // accumulators (numpy's r[0..7] over 16 steps), the 8 partials of a leaf by xor 1, 2, 4 shuffles,
 // the 64 leaves by a 6-level butterfly; a partial chunk walked by lane 0.  Ends with a barrier
 // (the next chunk may restage sq).
-template <int kT, bool kOutline = false>
+template <int kT>
 __device__ __forceinline__ void np_chunk(const SumsqArgs& a, const NpTask& t, const float (&xv)[kNpBuf / kT],
                                          const float (&bv)[kNpBuf / kT], float* sq, float* leaf_sum) {
   const int tid = int(threadIdx.x);
@@ -1086,7 +1069,7 @@ __device__ __forceinline__ void np_chunk(const SumsqArgs& a, const NpTask& t, co
       if (tid == 0) *dst = s;
     }
   } else if (tid == 0) {
-    *dst = kOutline ? np_partial(sq, t.n) : np_partial_inl(sq, t.n);
+    *dst = np_partial(sq, t.n);
   }
   __syncthreads();
 }
@@ -1099,40 +1082,6 @@ __global__ __launch_bounds__(256) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
   float xv[kNpBuf / 256], bv[kNpBuf / 256];
   np_load<256>(a, t, xv, bv);
   np_chunk<256>(a, t, xv, bv, sq, leaf_sum);
-}
-
-// Persistent and software-pipelined (round 4): a grid of a few workgroups per CU walks the tasks
-// (t = blockIdx.x + j * gridDim.x, still chunk-major across the grid), each holding two register
-// sets: the next task's 64 loads per lane go out before the current task's squares are staged and
-// summed, so a CU's loads stay in flight through the LDS phase instead of stopping per workgroup.
-template <int kT>
-__global__ __launch_bounds__(kT) __attribute__((amdgpu_waves_per_eu(2))) void np_sumsq_persist_kernel(SumsqArgs a) {
-  constexpr int kQ = int(kNpBuf / kT);
-  __shared__ float sq[kNpBuf / kPW * kLeafPitch];
-  __shared__ float leaf_sum[kNpBuf / kPW];
-  const uint64_t total = uint64_t(a.n_chunks) * uint64_t(a.K), stride = gridDim.x;
-  float xa[kQ], ba[kQ], xb[kQ], bb[kQ];
-  uint64_t t = blockIdx.x;
-  if (t >= total) return;
-  NpTask ta = np_task(a, t), tb;
-  np_load<kT, true>(a, ta, xa, ba);
-  for (;;) {
-    const uint64_t t1 = t + stride;
-    if (t1 < total) {
-      tb = np_task(a, t1);
-      np_load<kT, true>(a, tb, xb, bb);
-    }
-    np_chunk<kT, true>(a, ta, xa, ba, sq, leaf_sum);
-    if (t1 >= total) break;
-    const uint64_t t2 = t1 + stride;
-    if (t2 < total) {
-      ta = np_task(a, t2);
-      np_load<kT, true>(a, ta, xa, ba);
-    }
-    np_chunk<kT, true>(a, tb, xb, bb, sq, leaf_sum);
-    if (t2 >= total) break;
-    t = t2;
-  }
 }
 
 __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
@@ -1155,14 +1104,11 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
   const dim3 grid{uint32_t(tasks)};
   if (variant == 1) {
     hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, grid, dim3(256), 0, st, a);
-  } else if (variant == 2 || variant == 3) {  // 512 threads, 1 / 2 workgroups per CU
-    const uint64_t g = uint64_t(variant == 2 ? 1 : 2) * 256;
-    hipLaunchKernelGGL(np_sumsq_persist_kernel<512>, dim3(uint32_t(tasks < g ? tasks : g)), dim3(512), 0, st, a);
   } else {
     hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel, grid, dim3(256), 0, st, a);
   }
 }
-[[maybe_unused]] constexpr int kNumSumsqVariants = 4;
+[[maybe_unused]] constexpr int kNumSumsqVariants = 2;
 constexpr int kSumsqDefault = 0;  // chunk-major v2: 1.24-1.27 ms vs 1.65 (variant 1) on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,

@@ -282,29 +282,6 @@ __device__ __forceinline__ void sum_batch(int nu, const CodeOf<kG2> (&code)[kU],
   }
 }
 
-// Software-pipelined sum of a full batch (kSP): client u + 1's table lookups are issued before client
-// u's arithmetic, so each client's LDS latency (and bank-conflict replays) hides behind the previous
-// client's sums instead of a lgkmcnt(0) wait per client.  Same operations in the same order.
-template <int kU, int kG2, bool TWO>
-__device__ __forceinline__ void sum_batch_sp(const CodeOf<kG2> (&code)[kU], const float (&wu)[kU],
-                                             const float (&su)[kU], const float (*lut)[256], const float (&b)[kG2],
-                                             float (&acc)[kG2]) {
-  float x[2][kG2];
-#pragma unroll
-  for (int q = 0; q < kG2; ++q) x[0][q] = lut[0][(code[0][q >> 2] >> (8 * (q & 3))) & 255u];
-#pragma unroll
-  for (int u = 0; u < kU; ++u) {
-    if (u + 1 < kU) {
-#pragma unroll
-      for (int q = 0; q < kG2; ++q) x[(u + 1) & 1][q] = lut[u + 1][(code[u + 1][q >> 2] >> (8 * (q & 3))) & 255u];
-    }
-    __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-    for (int q = 0; q < kG2; ++q) acc[q] = acc[q] + term(x[u & 1][q], b[q], wu[u], su[u], TWO);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
 template <int kU, bool TWO>
 __device__ __forceinline__ void load_weights(const QArgs& a, int i0, float (&wu)[kU], float (&su)[kU]) {
   if (i0 + kU <= a.K) {
@@ -327,7 +304,7 @@ __device__ __forceinline__ void load_weights(const QArgs& a, int i0, float (&wu)
 // parity-tested): kP 1 without the code loads, 2 without the table lookups, 3 without either.
 // One batch of the pipelined loop: tables and codes of batch bi+1 go out, batch bi (codes in
 // `cur`, tables in lut[bi & 1]) is summed, then one barrier.
-template <int kBlock, int kU, bool TWO, int kG2, int kP, bool kSP>
+template <int kBlock, int kU, bool TWO, int kG2, int kP>
 __device__ __forceinline__ void pipe_step(const QArgs& a, const Chunk& ch, const float* mrow, int bi, int nb,
                                           bool full, bool have, uint64_t e0, const CodeOf<kG2> (&cur)[kU],
                                           CodeOf<kG2> (&nxt)[kU], float (*lut)[kU][256], const float (&b)[kG2],
@@ -349,9 +326,7 @@ __device__ __forceinline__ void pipe_step(const QArgs& a, const Chunk& ch, const
       }
     }
   }
-  if (full && kSP && nu == kU) {
-    sum_batch_sp<kU, kG2, TWO>(cur, wu, su, lut[bi & 1], b, acc);
-  } else if (full) {
+  if (full) {
     sum_batch<kU, kG2, TWO, (kP == 2 || kP == 3)>(nu, cur, wu, su, lut[bi & 1], b, acc);
   } else if (have) {
     for (int u = 0; u < nu; ++u) {
@@ -368,7 +343,7 @@ __device__ __forceinline__ void pipe_step(const QArgs& a, const Chunk& ch, const
   __syncthreads();  // batch bi+1's tables are written; batch bi's lookups are done
 }
 
-template <int kBlock, int kU, bool TWO, int kG2, int kP, bool kSP>
+template <int kBlock, int kU, bool TWO, int kG2, int kP>
 __device__ void qsgd_f32_chunk_pipe(const QArgs& a, uint32_t c, float (*lut)[kU][256]) {
   static_assert(kG2 == 16 || kG2 == 8 || kG2 == 4, "one 16-, 8- or 4-byte code load per lane");
   const Chunk ch = load_chunk(a.tf, c, a.n_f32);
@@ -410,9 +385,9 @@ __device__ void qsgd_f32_chunk_pipe(const QArgs& a, uint32_t c, float (*lut)[kU]
     if (full) load_codes<kU, kG2>(a, 0, K, e0, ca);
     __syncthreads();
     for (int bi = 0; bi < nb; bi += 2) {
-      pipe_step<kBlock, kU, TWO, kG2, kP, kSP>(a, ch, mrow, bi, nb, full, have, e0, ca, cb, lut, b, acc);
+      pipe_step<kBlock, kU, TWO, kG2, kP>(a, ch, mrow, bi, nb, full, have, e0, ca, cb, lut, b, acc);
       if (bi + 1 < nb)
-        pipe_step<kBlock, kU, TWO, kG2, kP, kSP>(a, ch, mrow, bi + 1, nb, full, have, e0, cb, ca, lut, b, acc);
+        pipe_step<kBlock, kU, TWO, kG2, kP>(a, ch, mrow, bi + 1, nb, full, have, e0, cb, ca, lut, b, acc);
     }
     if (full) {
 #pragma unroll
@@ -431,20 +406,15 @@ __device__ void qsgd_f32_chunk_pipe(const QArgs& a, uint32_t c, float (*lut)[kU]
   }
 }
 
-// kPersist > 0: a persistent grid of kPersist workgroups per CU walks the chunks (chunk c =
-// blockIdx.x + j * gridDim.x); every chunk ends with a barrier, so the next chunk's first table build
-// cannot overwrite tables still being read.
-template <int kBlock, int kU, bool TWO, int kGE, int kP, bool kSP, int kPersist>
+template <int kBlock, int kU, bool TWO, int kGE, int kP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) void fedavg_qsgd_pipe_kernel(
     QArgs a) {
   __shared__ float lut[2][kU][256];
-  const uint32_t nc = a.ncf + a.nci;
-  for (uint32_t c = blockIdx.x; c < nc; c += (kPersist ? gridDim.x : nc)) {
-    if (c < a.ncf) {
-      qsgd_f32_chunk_pipe<kBlock, kU, TWO, kGE, kP, kSP>(a, c, lut);
-    } else {
-      qsgd_i64_chunk<kBlock, TWO>(a, c - a.ncf);
-    }
+  const uint32_t c = blockIdx.x;
+  if (c < a.ncf) {
+    qsgd_f32_chunk_pipe<kBlock, kU, TWO, kGE, kP>(a, c, lut);
+  } else {
+    qsgd_i64_chunk<kBlock, TWO>(a, c - a.ncf);
   }
 }
 
@@ -464,19 +434,19 @@ template <int B, int U, bool TWO, int G = kG>
 void launch_q(const QArgs& a, hipStream_t st, uint32_t nc) {
   hipLaunchKernelGGL((fedavg_qsgd_kernel<B, U, TWO, G>), dim3(nc), dim3(B), 0, st, a);
 }
-template <int B, int U, bool TWO, int G, int P = 0, bool SP = false, int PERSIST = 0>
+template <int B, int U, bool TWO, int G, int P = 0>
 void launch_qp(const QArgs& a, hipStream_t st, uint32_t nc) {
-  const uint32_t grid = PERSIST && nc > 256u * PERSIST ? 256u * PERSIST : nc;
-  hipLaunchKernelGGL((fedavg_qsgd_pipe_kernel<B, U, TWO, G, P, SP, PERSIST>), dim3(grid), dim3(B), 0, st, a);
+  hipLaunchKernelGGL((fedavg_qsgd_pipe_kernel<B, U, TWO, G, P>), dim3(nc), dim3(B), 0, st, a);
 }
 struct QVariant {
   int block, u, g;  // threads, clients per table batch, elements per lane
   QFn fn[2];        // [TWO]
 };
-// The rounds-1-3 sweep (64 shapes: table-batch widths, two-level batching, resident tables, hybrid
-// arithmetic decode, sign-rotated tables, globally built tables) is recorded in DESIGN.md §11 and
-// profiles/r01_qsgd_*, r02d_qsgd_*, r02g_*, r03m_qsgd_*; none beat the default, so only the default,
-// the round-1 (non-pipelined) form and the default's timing probes remain.
+// The rounds 1-4 sweeps (table-batch widths, two-level batching, resident tables, hybrid arithmetic
+// decode, sign-rotated tables, globally built tables; round 4: software-pipelined lookups, a
+// persistent grid, the plain form with prefetched codes) are recorded in DESIGN.md §11, §14 and
+// profiles/r01_qsgd_*, r02d_qsgd_*, r02g_*, r03m_qsgd_*, r04*_qsgd_*; kept: the default, the pipelined
+// form of rounds 2-3 and its timing probes.
 #ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so (scripts/bench_variants.py, tests/test_qsgd_gpu.py)
 const QVariant kQVariants[] = {
     {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},       // 0 (default): plain
@@ -484,15 +454,6 @@ const QVariant kQVariants[] = {
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 1>, &launch_qp<512, 4, true, 8, 1>}},  // 2: probe, no code loads
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 2>, &launch_qp<512, 4, true, 8, 2>}},  // 3: probe, no lookups
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 3>, &launch_qp<512, 4, true, 8, 3>}},  // 4: probe, neither
-    // round 4: software-pipelined lookups (SP) and a persistent grid (workgroups per CU) on the
-    // pipelined form, then more shapes of the plain form
-    {512, 4, 8, {&launch_qp<512, 4, false, 8, 0, true>, &launch_qp<512, 4, true, 8, 0, true>}},         // 5: SP
-    {512, 4, 8, {&launch_qp<512, 4, false, 8, 0, false, 4>, &launch_qp<512, 4, true, 8, 0, false, 4>}},  // 6
-    {512, 4, 8, {&launch_qp<512, 4, false, 8, 0, true, 4>, &launch_qp<512, 4, true, 8, 0, true, 4>}},    // 7
-    {1024, 16, 8, {&launch_q<1024, 16, false, 8>, &launch_q<1024, 16, true, 8>}},   // 8
-    {1024, 4, 8, {&launch_q<1024, 4, false, 8>, &launch_q<1024, 4, true, 8>}},      // 9
-    {512, 8, 8, {&launch_q<512, 8, false, 8>, &launch_q<512, 8, true, 8>}},         // 10
-    {1024, 8, 4, {&launch_q<1024, 8, false, 4>, &launch_q<1024, 8, true, 4>}},      // 11
 };
 #else  // libplato_agg.so: the default only
 const QVariant kQVariants[] = {

@@ -1076,6 +1076,10 @@ class AggregationRound:
         eng, lay = self.engine, self.layout
         order = self._fedadp_order()
         segs, n_flat = self._flat_segments(order, True)
+        # plato_agg_fedadp_dots' limits (csrc/fedadp.hip run_fedadp); beyond them the round-2 path
+        if (len(order) >= self.FEDADP_MAX_SEGS or n_flat >= 1 << 30 or lay.n_f32 >= 1 << 30
+                or lay.n_i64 >= 1 << 30 or len(slots) > 65535):
+            return self.fedadp_dots_flat(grads, slots, lr)
         stream = torch.cuda.current_stream(eng.device)
         self.stager.fence(stream)
         g_flat, _ = self._flatten(_lib.PLATO_AGG_FLAT_RAW, segs, len(order), n_flat, [grads[0].data_ptr()],
@@ -1187,6 +1191,7 @@ class AggregationRound:
         return out
 
     PORT_NORMS_MAX_SEGS = 2048  # csrc/port.hip kMaxSegs
+    FEDADP_MAX_SEGS = 1 << 22   # csrc/fedadp.hip run_fedadp
 
     def model_similarities(self, reference: Mapping[str, torch.Tensor], slots: Sequence[int],
                            eps: float = 1e-8, threads: int | None = None, flat_norms: bool = False) -> list[np.float32]:

@@ -508,6 +508,13 @@ def test_fedadp_dots_many_entries_match_oracle(engine, n_entries):
     g_f, g_i = rnd.launch_entrywise(w1, add_base=False, device=True)
     inner, g_sq, l_sq = rnd.fedadp_dots((g_f, g_i), range(k), lr)
     flat = rnd.fedadp_dots_flat((g_f, g_i), range(k), lr)
+    # a layout past the fused kernel's limits routes to the flat path (limit lowered to force it)
+    calls = []
+    orig = rnd.fedadp_dots_flat
+    rnd.fedadp_dots_flat = lambda *a, **kw: calls.append(1) or orig(*a, **kw)
+    rnd.FEDADP_MAX_SEGS = n_entries
+    routed = rnd.fedadp_dots((g_f, g_i), range(k), lr)
+    assert calls and np.asarray(routed[0]).tobytes() == np.asarray(flat[0]).tobytes()
     assert np.asarray(inner).tobytes() == np.asarray(flat[0]).tobytes()
     assert np.float32(g_sq).tobytes() == np.float32(flat[1]).tobytes()
     assert np.asarray(l_sq).tobytes() == np.asarray(flat[2]).tobytes()
