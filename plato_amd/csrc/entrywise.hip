@@ -1068,8 +1068,8 @@ void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
 #endif
 // Variants (include/plato_agg_tune.h; every one bitwise identical).  The rounds 1-4 sweeps (natural
 // tiles, LDS-DMA ring kernels with 1-4 clients per workgroup, flat priorities, 256-1,024-element
-// tiles; round 4: 1-8 producer waves, 2-4 tiles in flight, a persistent long/short split, a
-// three-slot lookahead ring; DESIGN.md §11, §14, profiles/r0*_norms*) are trimmed to the round-4
+// tiles; round 4: 1-8 producer waves, 2-4 tiles in flight, 4,096-element tiles, a persistent
+// long/short split, a three-slot lookahead ring; DESIGN.md §11, §14, profiles/r0*_norms*) are trimmed to the round-4
 // default, two of its neighbours, the round-3 LDS-DMA defaults and the per-wave first version.
 // Interleaved on one box (K = 128 / 64 / 32 / 4 ResNet-18 clients, profiles/r04j-l_norms_k*.log):
 // <2048, 2, 2> 1.25-1.26 / 0.97 / 0.95 / 0.94 ms against the round-3 defaults' 1.29-1.37 / 1.01 /

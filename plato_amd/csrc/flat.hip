@@ -1048,10 +1048,11 @@ __device__ __forceinline__ void np_chunk(const SumsqArgs& a, const NpTask& t, co
   __syncthreads();
   float* dst = a.chunk_sums + uint64_t(t.k) * a.n_chunks + t.c;
   if (t.n == kNpBuf) {
-    // 64 leaves x 8 accumulators = 512 lanes: 512 / kT passes
+    // 64 leaves x 8 accumulators = 512 lanes: 512 / kT passes (kT = 1,024: waves 8-15 idle)
 #pragma unroll
-    for (int pass = 0; pass < 512 / kT; ++pass) {
+    for (int pass = 0; pass < (512 + kT - 1) / kT; ++pass) {
       const int slot = pass * kT + tid, leaf = slot >> 3, j = slot & 7;
+      if (kT > 512 && slot >= 512) break;  // wave-uniform
       const float* l = sq + leaf * kLeafPitch + j;
       float r = l[0];
 #pragma unroll
@@ -1074,14 +1075,16 @@ __device__ __forceinline__ void np_chunk(const SumsqArgs& a, const NpTask& t, co
   __syncthreads();
 }
 
-// One workgroup per task, a full chunk's 64 loads per lane out before the first square is staged.
-__global__ __launch_bounds__(256) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
+// One workgroup per task, a full chunk's loads (2 x 8,192 / kT per lane) out before the first square
+// is staged.
+template <int kT>
+__global__ __launch_bounds__(kT) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
   __shared__ float sq[kNpBuf / kPW * kLeafPitch];
   __shared__ float leaf_sum[kNpBuf / kPW];
   const NpTask t = np_task(a, blockIdx.x);
-  float xv[kNpBuf / 256], bv[kNpBuf / 256];
-  np_load<256>(a, t, xv, bv);
-  np_chunk<256>(a, t, xv, bv, sq, leaf_sum);
+  float xv[kNpBuf / kT], bv[kNpBuf / kT];
+  np_load<kT>(a, t, xv, bv);
+  np_chunk<kT>(a, t, xv, bv, sq, leaf_sum);
 }
 
 __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
@@ -1105,7 +1108,7 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
   if (variant == 1) {
     hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, grid, dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel<256>, grid, dim3(256), 0, st, a);
   }
 }
 [[maybe_unused]] constexpr int kNumSumsqVariants = 2;

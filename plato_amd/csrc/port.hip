@@ -42,11 +42,16 @@ __device__ __forceinline__ T sld(const T* p, int i) {
 }
 
 constexpr int kLanes = 8;                 // torch's 8-lane vectorised accumulation
-constexpr int kT = 2048;                  // positions per tile
-constexpr int kSteps = kT / kLanes;       // 256 steps per chain and tile
-constexpr int kR = kSteps + 4;            // row pitch: conflict-free writes (see pn_write) and reads
-constexpr int kSlot = kLanes * kR;        // one tile
-constexpr int kIts = kT / 256;            // gather iterations of 256 positions (4 per lane) per tile
+// Tile of kT positions (2,048 the default; 4,096 halves the chain wave's per-tile barrier and first
+// read): kSteps steps per chain, row pitch kR (conflict-free writes, see pn_write, and reads), kIts
+// gather iterations of 256 positions (4 per lane).
+template <int kT>
+struct PnTile {
+  static constexpr int kSteps = kT / kLanes;
+  static constexpr int kR = kSteps + 4;
+  static constexpr int kSlot = kLanes * kR;
+  static constexpr int kIts = kT / 256;
+};
 constexpr int kMaxSegs = 2048;
 constexpr uint32_t kSegI64 = 1u;
 
@@ -121,7 +126,7 @@ struct PnRegs {
   uint32_t fast;  // bit i: iteration i lies inside one fp32 entry and below m (wave-uniform)
 };
 
-template <int kWp, int kIt>
+template <int kT, int kWp, int kIt>
 __device__ __forceinline__ void pn_issue(const PnArgs& a, const PnSeg* S, PnCursor& cur, __amdgpu_buffer_rsrc_t rx,
                                          __amdgpu_buffer_rsrc_t rb, uint32_t t, int w, int lane, PnRegs<kIt>& r) {
   r.fast = 0;
@@ -146,11 +151,12 @@ __device__ __forceinline__ void pn_issue(const PnArgs& a, const PnSeg* S, PnCurs
 // 4 kR = 16 mod 32 apart, so each write's half-wave covers 32 banks (pitch 264 put lanes L and L ^ 1
 // on one bank: 45 M extra LDS cycles per 129-vector launch, profiles/r03x_pmc_paths.txt); the chain
 // wave's ds_read_b128 of rows 0..7 (banks mod 64) sit on 8 different 16-byte slots.
-template <int kWp, int kIt, bool kNT>
+template <int kT, int kWp, int kIt, bool kNT>
 __device__ __forceinline__ void pn_write(const PnArgs& a, const PnSeg* S, float* slot, float* flat, uint32_t t, int w,
                                          int lane, int v, const PnRegs<kIt>& r) {
 #pragma unroll
   for (int i = 0; i < kIt; ++i) {
+    constexpr int kR = PnTile<kT>::kR;
     const int q = i * kWp + w;
     float* dst = slot + (4 * (lane & 1)) * kR + q * 32 + (lane >> 1);
     const uint32_t p = t * kT + uint32_t(q) * 256 + uint32_t(4 * lane);
@@ -173,8 +179,10 @@ __device__ __forceinline__ void pn_write(const PnArgs& a, const PnSeg* S, float*
   }
 }
 
-template <int kWp, int kD, bool kNT = false>
+template <int kWp, int kD, bool kNT = false, int kT = 2048>
 __global__ __launch_bounds__(64 * (1 + kWp)) void port_norms_kernel(PnArgs a_in) {
+  using Tl = PnTile<kT>;
+  constexpr int kIts = Tl::kIts, kSlot = Tl::kSlot, kR = Tl::kR, kSteps = Tl::kSteps;
   constexpr int kIt = kIts / kWp;
   PnArgs a = a_in;
   if (a.lengths) {  // this vector's own length (FedAtt: one entry of one client)
@@ -202,14 +210,14 @@ __global__ __launch_bounds__(64 * (1 + kWp)) void port_norms_kernel(PnArgs a_in)
     float* flat = a.flat ? sld(a.flat, v) : nullptr;
     PnRegs<kIt> regs[kD];
 #pragma unroll
-    for (int j = 0; j < kD; ++j) pn_issue<kWp, kIt>(a, S, cur, rx, rb, uint32_t(j), w, lane, regs[j]);
+    for (int j = 0; j < kD; ++j) pn_issue<kT, kWp, kIt>(a, S, cur, rx, rb, uint32_t(j), w, lane, regs[j]);
     for (uint32_t t = 0; t < nbar; t += kD) {
 #pragma unroll
       for (int j = 0; j < kD; ++j) {
-        pn_write<kWp, kIt, kNT>(a, S, ring + ((t + j) & 1) * kSlot, flat, t + j, w, lane, v, regs[j]);
+        pn_write<kT, kWp, kIt, kNT>(a, S, ring + ((t + j) & 1) * kSlot, flat, t + j, w, lane, v, regs[j]);
         // past the last tile every load reads the arena's first elements: valid, never consumed
         const uint32_t nxt = t + j + kD;
-        pn_issue<kWp, kIt>(a, S, cur, rx, rb, nxt < ntiles ? nxt : ntiles, w, lane, regs[j]);
+        pn_issue<kT, kWp, kIt>(a, S, cur, rx, rb, nxt < ntiles ? nxt : ntiles, w, lane, regs[j]);
         __builtin_amdgcn_s_barrier();  // tile t + j published in slot (t + j) & 1
       }
     }
@@ -264,20 +272,23 @@ __global__ __launch_bounds__(64 * (1 + kWp)) void port_norms_kernel(PnArgs a_in)
 }
 
 using PnFn = void (*)(const PnArgs&, hipStream_t, int);
-template <int kWp, int kD, bool kNT = false>
+template <int kWp, int kD, bool kNT = false, int kT = 2048>
 void launch_pn(const PnArgs& a, hipStream_t st, int V) {
-  hipLaunchKernelGGL((port_norms_kernel<kWp, kD, kNT>), dim3(uint32_t(V)), dim3(64 * (1 + kWp)), 0, st, a);
+  hipLaunchKernelGGL((port_norms_kernel<kWp, kD, kNT, kT>), dim3(uint32_t(V)), dim3(64 * (1 + kWp)), 0, st, a);
 }
-// producer waves x tiles of loads in flight
-constexpr PnFn kPnDefault = &launch_pn<8, 3, true>;
+// producer waves x tiles of loads in flight (x non-temporal flat stores, x tile positions)
+constexpr PnFn kPnDefault = &launch_pn<8, 2, true, 4096>;
 #ifdef PLATO_AGG_TUNE
 // The round-3 sweep (1-8 producer waves x 2-4 tiles in flight, plain or non-temporal flat stores;
-// profiles/r03l_port.log) is in DESIGN.md §13; kept: the default and the runners-up.
+// profiles/r03l_port.log) and round 4's tile sizes (profiles/r04n_port_variants.log) are in DESIGN.md
+// §13-14; kept: the default, the round-3 default and the runners-up.
 const PnFn kPnVariants[] = {
-    &launch_pn<8, 3, true>,  // 0: the default, 4.81 ms storing the flat vectors
-    &launch_pn<4, 2>,        // 1: 4.33 ms on 129 ResNet-18 vectors, 5.12 storing the flat vectors
-    &launch_pn<4, 3>,        // 2: 4.45 ms
-    &launch_pn<8, 2, true>,  // 3
+    &launch_pn<8, 2, true, 4096>,  // 0: the default, 4.14 ms storing the flat vectors (4,096-position tiles)
+    &launch_pn<8, 3, true>,        // 1: the round-3 default (2,048), 4.70 ms
+    &launch_pn<4, 2>,              // 2: 4.25 ms without the stores
+    &launch_pn<8, 3, true, 4096>,  // 3: 4.17 ms
+    &launch_pn<8, 2, true, 8192>,  // 4
+    &launch_pn<8, 1, true, 4096>,  // 5
 };
 constexpr int kNumPnVariants = sizeof(kPnVariants) / sizeof(kPnVariants[0]);
 #endif

@@ -159,6 +159,7 @@ class FedAvgEngine:
 
     #: QSGD kernel variant (tuning / tests; None = the library default)
     qsgd_variant: int | None = None
+    port_variant: int | None = None  # plato_agg_tune_port_norms shape (tests / tuning), None = the default
     #: arena alignment of the layouts this engine builds (arena.ALIGNMENTS; FedAdp servers: "fedadp")
     layout_align: str | None = None
 
@@ -1270,9 +1271,13 @@ class AggregationRound:
             vt = torch.from_numpy(vec).to(eng.device)
             v8, n1 = vt.data_ptr(), 8 * (k + 1)
             scaled = torch.empty(stride, dtype=torch.float32, device=eng.device)
+            args = (v8, v8 + n1, v8 + 2 * n1, v8 + 3 * n1, k + 1, None, segs.data_ptr(), n_segs, n_flat, lay.n_f32,
+                    _lib.PLATO_AGG_PORT_CAST_FIRST, norms.data_ptr(), v8 + 4 * n1, h)
             with self._timed("port_norms", stream):
-                _lib.call("plato_agg_port_norms", v8, v8 + n1, v8 + 2 * n1, v8 + 3 * n1, k + 1, None, segs.data_ptr(),
-                          n_segs, n_flat, lay.n_f32, _lib.PLATO_AGG_PORT_CAST_FIRST, norms.data_ptr(), v8 + 4 * n1, h)
+                if eng.port_variant is None:
+                    _lib.call("plato_agg_port_norms", *args)
+                else:
+                    _lib.tune_call("plato_agg_tune_port_norms", eng.port_variant, *args)
             # current - previous over its norm once (not once per client), then the K cascade sums
             with self._timed("port_cosine", stream):
                 _lib.call("plato_agg_scale_by_norm", flat.data_ptr(), n_flat, norms.data_ptr(), float(eps),

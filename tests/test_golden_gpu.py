@@ -533,7 +533,7 @@ def test_he_plaintext_half_matches_reference(engine, case):
 
 
 # ragged layouts for the gathered Port norms: int64 counters first, between and last; entries shorter than a
-# 256-position gather iteration, entries straddling 2,048-position tiles, n % 8 tails of 0-7
+# 256-position gather iteration, entries straddling 2,048- / 4,096-position tiles, n % 8 tails of 0-7
 PORT_SPECS = {
     "i64_first_tail5": [("n0", (), "i64"), ("a", (3,), "f32"), ("b", (5000,), "f32"), ("n1", (2,), "i64"),
                         ("c", (7, 9), "f32"), ("d", (4099,), "f32"), ("n2", (), "i64")],
@@ -578,6 +578,15 @@ def test_port_norms_gathered_match_oracle(engine, spec):
     sims_staged = rnd.model_similarities(rnd.stage_reference(previous), range(k), threads=4)
     assert np.asarray(sims, np.float32).tobytes() == np.asarray(sims_staged, np.float32).tobytes()
     assert np.asarray(sims, np.float32).tobytes() == np.asarray(sims_flat, np.float32).tobytes()
+    from plato_amd import _lib
+    try:  # every tile / producer shape of the tuning library, bit for bit
+        for variant in range(_lib.tune().plato_agg_tune_num_port_norms_variants()):
+            engine.port_variant = variant
+            sims_v = rnd.model_similarities(previous, range(k), threads=4)
+            assert rnd.last_norms.tobytes() == got.tobytes(), variant
+            assert np.asarray(sims_v, np.float32).tobytes() == np.asarray(sims, np.float32).tobytes(), variant
+    finally:
+        engine.port_variant = None
     v = R.port_current_minus_previous(layout.entries, bf, bi, pf, pi)
     want = [R.torch_norm(v)] + [R.torch_norm(R.port_delta(layout.entries, bf, bi, xf, xi)) for xf, xi in clients]
     assert got.tobytes() == np.asarray(want, np.float32).tobytes()
