@@ -93,10 +93,11 @@ int plato_agg_tune_sdot_shared(int variant, const float* d_x, const float* const
                                hipStream_t stream);
 
 /* plato_agg_fedavg_qsgd kernel variants, workgroup size x clients per decode-table batch x
- * elements per lane: 0 = 1024x8x8, one barrier pair per table batch (plato_agg_fedavg_qsgd; the
- * round-1 default, again since round 4), 1 = 512x4x8 pipelined (double-buffered tables, the next
- * batch's codes loaded before the current batch is summed; the rounds 2-3 default), 2-4 = timing
- * probes of variant 1 (NOT the FedAvg: no code loads / no table lookups / neither).
+ * elements per lane: 0 = 512x8x8 plain form (two barriers per table batch, max_v by scalar loads,
+ * the batch's codes issued before its table build; plato_agg_fedavg_qsgd), 1 = 512x4x8 pipelined
+ * (double-buffered tables, the next batch's codes loaded before the current batch is summed; the
+ * rounds 2-3 default), 2-4 = timing probes of variant 1 (NOT the FedAvg: no code loads / no table
+ * lookups / neither), 5 = 1024x8x8 plain form of round 1, 6 = variant 0 at 256 threads.
  * plato_agg_tune_qsgd_chunk gives the chunk capacity (elements per workgroup pass) the variant is
  * built for. */
 int plato_agg_tune_num_qsgd_variants(void);

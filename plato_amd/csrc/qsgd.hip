@@ -42,10 +42,11 @@ typedef __attribute__((address_space(1))) const u1 gu1;
 // Kernel shape (tuning space, plato_agg_tune_fedavg_qsgd): B threads per
 // workgroup share each batch's decode tables, U clients per table batch, G
 // elements per lane (one 16/8/4-byte code load per client).  The default
-// (variant 0) is the plain form at B = 1024, U = 8, G = 8 (8,192-element chunks; the round-1
-// default, again since round 4: interleaved A/B on one box 0.331 against 0.373 ms for the
-// pipelined B = 512, U = 4 form of rounds 2-3, now variant 1).  Every shape, pipelined, two-level or
-// resident-table form measured lands within 0.32-0.38 ms on C2-sized inputs; DESIGN.md §11, §14.
+// (variant 0) is the plain form (two barriers per table batch) at B = 512, U = 8, G = 8 (4,096-element
+// chunks) with max_v by scalar loads and each batch's codes issued before its table build: 0.306 ms
+// interleaved on one box against 0.333 for the round-1 plain form (B = 1,024, vector max_v loads,
+// codes after the barrier; variant 5) and 0.373 for the pipelined form of rounds 2-3 (variant 1);
+// DESIGN.md §11, §14.
 constexpr int kG = 16;      // elements per lane group of the plain kernel's template default
 
 template <class T>
@@ -95,7 +96,7 @@ __device__ __forceinline__ float term(float x, float b, float w, float s, bool t
   return t;
 }
 
-template <int kBlock, int kU, bool TWO, int kG = ::kG>
+template <int kBlock, int kU, bool TWO, int kG = ::kG, bool kSM = false>
 __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
   static_assert(kG == 16 || kG == 8 || kG == 4, "one 16-, 8- or 4-byte code load per lane");
   const Chunk ch = load_chunk(a.tf, c, a.n_f32);
@@ -129,13 +130,24 @@ __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
         if (e >= ch.begin && e < ch.end) b[q] = a.base_f[e];
       }
     }
+    using CodeT = std::conditional_t<kG == 16, u4, std::conditional_t<kG == 8, u2, u1>>;
+    using GCodeT = std::conditional_t<kG == 16, gu4, std::conditional_t<kG == 8, gu2, gu1>>;
     for (int i0 = 0; i0 < K; i0 += kU) {
       const int nu = K - i0 < kU ? K - i0 : kU;
       __syncthreads();  // previous batch's lookups are done
+      CodeT code[kU];
+      if (kSM && full) {  // the batch's codes in flight during its table build and barrier
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          const int i = i0 + u < K ? i0 + u : K - 1;
+          code[u] = __builtin_nontemporal_load((GCodeT*)(sld(a.cf, i) + e0));
+        }
+      }
       // codes 128 + z decode to exactly -decode(z) (round-to-nearest is sign-symmetric),
       // except 128 itself: zeta = -0 is the integer 0
       for (int t = threadIdx.x; t < kU * 128; t += kBlock) {
-        const int u = t >> 7, z = t & 127;
+            // kSM: u is wave-uniform (128 table slots per client, 64 lanes per wave): max_v by a scalar load
+        const int u = kSM ? __builtin_amdgcn_readfirstlane(t >> 7) : t >> 7, z = t & 127;
         if (u < nu) {
           const float v = decode(uint32_t(z), sld(mrow, i0 + u), a.divisor);
           lut[u][z] = v;
@@ -144,13 +156,12 @@ __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
       }
       __syncthreads();
       if (full) {
-        using CodeT = std::conditional_t<kG == 16, u4, std::conditional_t<kG == 8, u2, u1>>;
-        using GCodeT = std::conditional_t<kG == 16, gu4, std::conditional_t<kG == 8, gu2, gu1>>;
-        CodeT code[kU];
+        if (!kSM) {
 #pragma unroll
-        for (int u = 0; u < kU; ++u) {
-          const int i = i0 + u < K ? i0 + u : K - 1;
-          code[u] = __builtin_nontemporal_load((GCodeT*)(sld(a.cf, i) + e0));
+          for (int u = 0; u < kU; ++u) {
+            const int i = i0 + u < K ? i0 + u : K - 1;
+            code[u] = __builtin_nontemporal_load((GCodeT*)(sld(a.cf, i) + e0));
+          }
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u) {
@@ -418,21 +429,21 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) 
   }
 }
 
-template <int kBlock, int kU, bool TWO, int kGE = kG>
+template <int kBlock, int kU, bool TWO, int kGE = kG, bool kSM = false>
 __global__ __launch_bounds__(kBlock) void fedavg_qsgd_kernel(QArgs a) {
   __shared__ float lut[kU][256];
   const uint32_t c = blockIdx.x;
   if (c < a.ncf) {
-    qsgd_f32_chunk<kBlock, kU, TWO, kGE>(a, c, lut);
+    qsgd_f32_chunk<kBlock, kU, TWO, kGE, kSM>(a, c, lut);
   } else {
     qsgd_i64_chunk<kBlock, TWO>(a, c - a.ncf);
   }
 }
 
 using QFn = void (*)(const QArgs&, hipStream_t, uint32_t);
-template <int B, int U, bool TWO, int G = kG>
+template <int B, int U, bool TWO, int G = kG, bool SM = false>
 void launch_q(const QArgs& a, hipStream_t st, uint32_t nc) {
-  hipLaunchKernelGGL((fedavg_qsgd_kernel<B, U, TWO, G>), dim3(nc), dim3(B), 0, st, a);
+  hipLaunchKernelGGL((fedavg_qsgd_kernel<B, U, TWO, G, SM>), dim3(nc), dim3(B), 0, st, a);
 }
 template <int B, int U, bool TWO, int G, int P = 0>
 void launch_qp(const QArgs& a, hipStream_t st, uint32_t nc) {
@@ -449,15 +460,17 @@ struct QVariant {
 // form of rounds 2-3 and its timing probes.
 #ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so (scripts/bench_variants.py, tests/test_qsgd_gpu.py)
 const QVariant kQVariants[] = {
-    {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},       // 0 (default): plain
+    {512, 8, 8, {&launch_q<512, 8, false, 8, true>, &launch_q<512, 8, true, 8, true>}},  // 0 (default)
     {512, 4, 8, {&launch_qp<512, 4, false, 8>, &launch_qp<512, 4, true, 8>}},        // 1: pipelined (rounds 2-3)
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 1>, &launch_qp<512, 4, true, 8, 1>}},  // 2: probe, no code loads
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 2>, &launch_qp<512, 4, true, 8, 2>}},  // 3: probe, no lookups
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 3>, &launch_qp<512, 4, true, 8, 3>}},  // 4: probe, neither
+    {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},       // 5: round 1 (vector max_v loads)
+    {256, 8, 8, {&launch_q<256, 8, false, 8, true>, &launch_q<256, 8, true, 8, true>}},  // 6
 };
 #else  // libplato_agg.so: the default only
 const QVariant kQVariants[] = {
-    {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},  // 0 (default): plain
+    {512, 8, 8, {&launch_q<512, 8, false, 8, true>, &launch_q<512, 8, true, 8, true>}},  // 0 (default)
 };
 #endif
 constexpr int kNumQVariants = sizeof(kQVariants) / sizeof(kQVariants[0]);

@@ -222,7 +222,7 @@ class FedAvgEngine:
 
     # per-entry kernels: chunk capacity (elements) per workgroup
     STATS_CHUNK = 4096      # entry_stats: 256 lanes x 4 float4 groups
-    QSGD_CHUNK = 8192       # fedavg_qsgd: 1,024 lanes x 8 one-byte codes (plato_agg_tune_qsgd_chunk(0))
+    QSGD_CHUNK = 4096       # fedavg_qsgd: 512 lanes x 8 one-byte codes (plato_agg_tune_qsgd_chunk(0))
     ENTRYWISE_CHUNK = 1024  # fedavg_entrywise: 256 lanes x 1 float4 group
 
     def _chunks(self, layout: ArenaLayout, cap: int):
