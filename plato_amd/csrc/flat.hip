@@ -1077,13 +1077,33 @@ __device__ __forceinline__ void np_chunk(const SumsqArgs& a, const NpTask& t, co
 
 // One workgroup per task, a full chunk's loads (2 x 8,192 / kT per lane) out before the first square
 // is staged.
-template <int kT>
+// kProbe (timing probes, wrong results by design, never a default): 1 no baseline loads (b = 0),
+// 2 no LDS staging or leaf sums (a lane's own squares summed in registers).
+template <int kT, int kProbe = 0>
 __global__ __launch_bounds__(kT) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
   __shared__ float sq[kNpBuf / kPW * kLeafPitch];
   __shared__ float leaf_sum[kNpBuf / kPW];
   const NpTask t = np_task(a, blockIdx.x);
-  float xv[kNpBuf / kT], bv[kNpBuf / kT];
-  np_load<kT>(a, t, xv, bv);
+  constexpr int kQ = int(kNpBuf / kT);
+  float xv[kQ], bv[kQ];
+  if (kProbe == 1) {
+    const float* x = a.x[t.k] + t.begin;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+      const uint32_t i = uint32_t(q * kT) + threadIdx.x;
+      xv[q] = i < t.n ? __builtin_nontemporal_load(x + i) : 0.f;
+      bv[q] = 0.f;
+    }
+  } else {
+    np_load<kT>(a, t, xv, bv);
+  }
+  if (kProbe == 2) {
+    float r = 0.f;
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) r += (xv[q] - bv[q]) * (xv[q] - bv[q]);
+    if (r == 12345.f) a.chunk_sums[blockIdx.x] = r;  // keeps the loads; practically never stores
+    return;
+  }
   np_chunk<kT>(a, t, xv, bv, sq, leaf_sum);
 }
 
@@ -1107,11 +1127,15 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
   const dim3 grid{uint32_t(tasks)};
   if (variant == 1) {
     hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, grid, dim3(256), 0, st, a);
+  } else if (variant == 2) {
+    hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256, 1>), grid, dim3(256), 0, st, a);
+  } else if (variant == 3) {
+    hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256, 2>), grid, dim3(256), 0, st, a);
   } else {
     hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel<256>, grid, dim3(256), 0, st, a);
   }
 }
-[[maybe_unused]] constexpr int kNumSumsqVariants = 2;
+[[maybe_unused]] constexpr int kNumSumsqVariants = 4;
 constexpr int kSumsqDefault = 0;  // chunk-major v2: 1.24-1.27 ms vs 1.65 (variant 1) on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
