@@ -1107,6 +1107,61 @@ __global__ __launch_bounds__(kT) void np_sumsq_chunks_v2_kernel(SumsqArgs a) {
   np_chunk<kT>(a, t, xv, bv, sq, leaf_sum);
 }
 
+// Full chunks staged in two halves (round 4): 32 leaves' squares at a time, so the LDS per workgroup
+// halves (17.4 KB) and more workgroups share a CU; same leaves, same order.  Partial chunks (an entry's
+// last) take np_sumsq_tail_kernel.
+__global__ __launch_bounds__(256) void np_sumsq_half_kernel(SumsqArgs a) {
+  __shared__ float sq[kNpBuf / kPW / 2 * kLeafPitch];
+  __shared__ float leaf_sum[kNpBuf / kPW];
+  const NpTask t = np_task(a, blockIdx.x);
+  if (t.n != kNpBuf) return;  // workgroup-uniform
+  constexpr int kQ = int(kNpBuf / 256), kHalfQ = kQ / 2;
+  float xv[kQ], bv[kQ];
+  np_load<256>(a, t, xv, bv);
+  const int tid = int(threadIdx.x), leaf = tid >> 3, j = tid & 7;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h) __syncthreads();  // the first half's leaf reads are done
+#pragma unroll
+    for (int q = 0; q < kHalfQ; ++q) {
+      const uint32_t i = uint32_t(q * 256 + tid);  // element h * 4096 + i
+      const float d = xv[h * kHalfQ + q] - bv[h * kHalfQ + q];
+      sq[np_pad8(i)] = d * d;
+    }
+    __syncthreads();
+    // 32 leaves x 8 accumulators = the 256 threads
+    const float* l = sq + leaf * kLeafPitch + j;
+    float r = l[0];
+#pragma unroll
+    for (int i = 8; i < kPW; i += 8) r += l[i];
+    r = r + __shfl_xor(r, 1);
+    r = r + __shfl_xor(r, 2);
+    r = r + __shfl_xor(r, 4);
+    if (j == 0) leaf_sum[h * 32 + leaf] = r;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float s = leaf_sum[tid];
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) s = s + __shfl_xor(s, m);
+    if (tid == 0) a.chunk_sums[uint64_t(t.k) * a.n_chunks + t.c] = s;
+  }
+}
+
+// The partial last chunk of every (piece, client), through the full-staging path.
+__global__ __launch_bounds__(256) void np_sumsq_tail_kernel(SumsqArgs a) {
+  __shared__ float sq[kNpBuf / kPW * kLeafPitch];
+  __shared__ float leaf_sum[kNpBuf / kPW];
+  const uint32_t k = blockIdx.x % uint32_t(a.K), pc = blockIdx.x / uint32_t(a.K);
+  const uint32_t c_end = pc + 1 < a.n_pieces ? a.first_chunk[pc + 1] : a.n_chunks;
+  if (c_end == a.first_chunk[pc]) return;
+  const NpTask t = np_task(a, uint64_t(c_end - 1) * uint64_t(a.K) + k);
+  if (t.n == kNpBuf) return;  // workgroup-uniform: a whole last chunk went through the half kernel
+  float xv[kNpBuf / 256], bv[kNpBuf / 256];
+  np_load<256>(a, t, xv, bv);
+  np_chunk<256>(a, t, xv, bv, sq, leaf_sum);
+}
+
 __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   if (t >= uint64_t(a.n_pieces) * uint64_t(a.K)) return;
@@ -1118,10 +1173,15 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   a.out[uint64_t(k) * a.n_pieces + pc] = out;
 }
 
-// variant 0: chunk-major, latency-shaped (np_sumsq_chunks_v2_kernel, the default); 1: the round-2
-// form (np_sumsq_chunks_lds_kernel, client-major, four memory round trips per workgroup); 2, 3: the
-// persistent software-pipelined form, 512 threads, grids of 1 / 2 workgroups per CU.  G clients per workgroup sharing
-// the baseline (4.1-5.9 ms) were dropped after round 3.
+// variant 0 (the default): full chunks staged in two halves (np_sumsq_half_kernel: 17.4 KB of LDS, six
+// workgroups per CU instead of four; 1.25 against 1.39 ms interleaved) plus the partial last chunks
+// (np_sumsq_tail_kernel); 1: the round-2 form (np_sumsq_chunks_lds_kernel, client-major, four memory
+// round trips per workgroup); 2, 3: timing probes of variant 4 (wrong results by design: no baseline
+// loads / no LDS phase); 4: the round-3 default (np_sumsq_chunks_v2_kernel, every chunk staged whole).
+// G clients per workgroup sharing the baseline (4.1-5.9 ms) were dropped after round 3; a persistent
+// software-pipelined form (2.9 ms: its two register sets left one workgroup per CU), 512 / 1,024
+// threads per chunk (1.70 / 2.79 ms against 1.38) and an LDS-free form loading each accumulator's
+// stride-8 elements directly (2.20 ms) in round 4.
 void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
   const uint64_t tasks = uint64_t(a.n_chunks) * uint64_t(a.K);
   const dim3 grid{uint32_t(tasks)};
@@ -1131,12 +1191,15 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256, 1>), grid, dim3(256), 0, st, a);
   } else if (variant == 3) {
     hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256, 2>), grid, dim3(256), 0, st, a);
+  } else if (variant == 4) {
+    hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256>), grid, dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL(np_sumsq_chunks_v2_kernel<256>, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(np_sumsq_half_kernel, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   }
 }
-[[maybe_unused]] constexpr int kNumSumsqVariants = 4;
-constexpr int kSumsqDefault = 0;  // chunk-major v2: 1.24-1.27 ms vs 1.65 (variant 1) on 128 ResNet-18 clients
+[[maybe_unused]] constexpr int kNumSumsqVariants = 5;
+constexpr int kSumsqDefault = 0;  // half-staged + tail: 1.25 ms vs 1.39 (variant 4) on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
                  float* d_out, hipStream_t stream);

@@ -124,8 +124,8 @@ def test_cosine_of_a_zero_vector_uses_eps():
 
 @pytest.mark.parametrize("k", [3, 11])
 def test_np_sumsq_variants_agree_bitwise(k):
-    """Both np_sumsq kernels (chunk-major latency-shaped default, the round-2 client-major form) equal the
-    product default, which the test below pins to numpy."""
+    """Every np_sumsq kernel (half-staged default, round-3 whole-chunk form, round-2 client-major form;
+    not the timing probes) equals the product default, which the test below pins to numpy."""
     from plato_amd.arena import ArenaLayout
     from plato_amd.engine import FedAvgEngine
 
