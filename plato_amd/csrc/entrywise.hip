@@ -542,7 +542,9 @@ __device__ void norm_pair(const NormArgs& a, const Chunk ch, int i, int lane, fl
   if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
 }
 
-template <bool HAS_BASE>
+// kRest: only the pairs the split register-staged launch leaves out (int64 entries, and the fp32 entry
+// that reaches the arena's partial last float4 group).
+template <bool HAS_BASE, bool kRest = false>
 __global__ __launch_bounds__(kBlock) void entry_norms_kernel(NormArgs a) {
   // one wavefront per (entry, client), entry-major
   __shared__ __attribute__((aligned(16))) float rows[kBlock / 64][kNormLanes][kNRow];
@@ -553,7 +555,9 @@ __global__ __launch_bounds__(kBlock) void entry_norms_kernel(NormArgs a) {
   const uint32_t ent = uint32_t(pair / a.K);
   const int i = int(pair % a.K);
   if (ent < a.nef) {
-    norm_pair<HAS_BASE, false>(a, load_chunk(a.ef, ent, a.n_f32), i, lane, rows[wave]);
+    const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
+    if (kRest && uint64_t(ch.end) <= (a.n_f32 & ~3ull)) return;
+    norm_pair<HAS_BASE, false>(a, ch, i, lane, rows[wave]);
   } else {
     norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows[wave]);
   }
@@ -890,7 +894,7 @@ __device__ void rs_produce(const NormArgs& a, const Chunk ch, const float* x, in
   wait_vmcnt<0>();
 }
 
-template <int T, int P, int D, bool HAS_BASE, int PRIO>
+template <int T, int P, int D, bool HAS_BASE, int PRIO, bool kSplit = false>
 __device__ __forceinline__ void rs_pair(const NormArgs& a, uint64_t pair, int wave, int lane, float* dbuf) {
   constexpr int kSize = DTile<T, true>::kSize;
   const uint32_t ent = uint32_t(pair / uint64_t(a.K));  // entry-major over the (longest-first) tables
@@ -899,7 +903,7 @@ __device__ __forceinline__ void rs_pair(const NormArgs& a, uint64_t pair, int wa
   if (ent < a.nef) {
     const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
     if (uint64_t(ch.end) > (a.n_f32 & ~3ull)) {  // the arena's partial last float4 group: per-wave path
-      if (wave == 0) norm_pair<HAS_BASE, false>(a, ch, i, lane, rows);
+      if (!kSplit && wave == 0) norm_pair<HAS_BASE, false>(a, ch, i, lane, rows);
       return;
     }
     const uint64_t ntiles = pc_ntiles<T>(ch), nbar = (ntiles + D - 1) / D * D;
@@ -912,18 +916,21 @@ __device__ __forceinline__ void rs_pair(const NormArgs& a, uint64_t pair, int wa
     }
     pc_chain_prio<PRIO>(a, ch);
     pc_finish<HAS_BASE>(a, ch, i, x, lane, pc_chain<T, true>(ch, lane, dbuf, kSize, nbar));
-  } else if (ent < a.nef + a.nei) {
+  } else if (!kSplit && ent < a.nef + a.nei) {
     if (wave == 0) norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows);
   }
 }
 
-template <int T, int P, int D, bool HAS_BASE, int PRIO>
+// kSplit: the per-wave pairs (int64 entries, the partial-last-group fp32 entry) are left to a second
+// launch (entry_norms_kernel<., true>), so that norm_pair's 64 registers of tile prefetch do not set
+// this kernel's register count and with it how many pairs share a CU.
+template <int T, int P, int D, bool HAS_BASE, int PRIO, bool kSplit = false>
 __global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rs_kernel(NormArgs a) {
   constexpr int kSize = DTile<T, true>::kSize;
   static_assert(2 * kSize >= kNormLanes * kNRow, "norm_pair's rows fit the d ring");
   __shared__ __attribute__((aligned(16))) float dbuf[2 * kSize];
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-  rs_pair<T, P, D, HAS_BASE, PRIO>(a, blockIdx.x, wave, lane, dbuf);
+  rs_pair<T, P, D, HAS_BASE, PRIO, kSplit>(a, blockIdx.x, wave, lane, dbuf);
 }
 
 bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
@@ -1058,6 +1065,19 @@ void launch_rs(const NormArgs& a, bool hb, dim3 grid, hipStream_t st) {
   if (hb) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, true, PRIO>), grid, dim3(64 * (1 + P)), 0, st, a);
   else hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, false, PRIO>), grid, dim3(64 * (1 + P)), 0, st, a);
 }
+template <int T, int P, int D, int PRIO = -1>
+void launch_rs_split(const NormArgs& a, bool hb, dim3, hipStream_t st) {
+  const dim3 g1{uint32_t(uint64_t(a.nef) * uint64_t(a.K))};  // the fp32 pairs; int64 pairs come after them
+  const uint64_t waves = (uint64_t(a.nef) + a.nei) * uint64_t(a.K);
+  const dim3 g2{uint32_t((waves + kBlock / 64 - 1) / (kBlock / 64))};
+  if (hb) {
+    if (a.nef) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, true, PRIO, true>), g1, dim3(64 * (1 + P)), 0, st, a);
+    hipLaunchKernelGGL((entry_norms_kernel<true, true>), g2, dim3(kBlock), 0, st, a);
+  } else {
+    if (a.nef) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, false, PRIO, true>), g1, dim3(64 * (1 + P)), 0, st, a);
+    hipLaunchKernelGGL((entry_norms_kernel<false, true>), g2, dim3(kBlock), 0, st, a);
+  }
+}
 #ifdef PLATO_AGG_TUNE
 void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
   const uint64_t threads = (uint64_t(a.nef) + a.nei) * uint64_t(a.K) * 64;  // a wave per pair
@@ -1073,16 +1093,22 @@ void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
 // default, two of its neighbours, the round-3 LDS-DMA defaults and the per-wave first version.
 // Interleaved on one box (K = 128 / 64 / 32 / 4 ResNet-18 clients, profiles/r04j-l_norms_k*.log):
 // <2048, 2, 2> 1.25-1.26 / 0.97 / 0.95 / 0.94 ms against the round-3 defaults' 1.29-1.37 / 1.01 /
-// 1.00 / 0.99.
-constexpr NormFn kNormDefault = &launch_rs<2048, 2, 2>;
+// 1.00 / 0.99; with the per-wave pairs in a second launch (64 VGPRs at 4 producer waves), <2048, 4,
+// 2> 1.20 / 0.98 / - / 0.94 (profiles/r04s_norms_k*.log).
+constexpr NormFn kNormDefault = &launch_rs_split<2048, 4, 2>;
 #ifdef PLATO_AGG_TUNE
 const NormFn kNormVariants[] = {
-    &launch_rs<2048, 2, 2>,      // 0: the default: register-staged, 2 producer waves, 2 tiles in flight
-    &launch_rs<2048, 1, 2>,      // 1: one producer wave
-    &launch_rs<2048, 2, 3, -2>,  // 2: 3 tiles in flight, the long entries' producers at priority 2
-    &launch_pc<1024, 5>,         // 3: LDS-DMA producer / consumer, 1,024-element tiles (round 3, > 6,144 pairs)
-    &launch_pc<2048, 3>,         // 4: the same, 2,048-element tiles (round 3, <= 6,144 pairs)
-    &launch_per_wave,            // 5: one wavefront per (entry, client) (the first version)
+    &launch_rs_split<2048, 4, 2>,  // 0: the default: register-staged, 4 producer waves, 2 tiles in flight,
+                                   //    the per-wave pairs (int64, partial last group) in a second launch
+    &launch_rs<2048, 2, 2>,        // 1: 2 producer waves, one launch (the first round-4 default)
+    &launch_rs<2048, 2, 3, -2>,    // 2: 3 tiles in flight, the long entries' producers at priority 2
+    &launch_pc<1024, 5>,           // 3: LDS-DMA producer / consumer, 1,024-element tiles (round 3, > 6,144 pairs)
+    &launch_pc<2048, 3>,           // 4: the same, 2,048-element tiles (round 3, <= 6,144 pairs)
+    &launch_per_wave,              // 5: one wavefront per (entry, client) (the first version)
+    &launch_rs_split<2048, 2, 2>,  // 6
+    &launch_rs_split<2048, 2, 1>,  // 7
+    &launch_rs_split<2048, 4, 1>,  // 8
+    &launch_rs_split<2048, 4, 3>,  // 9
 };
 constexpr int kNumNormVariants = sizeof(kNormVariants) / sizeof(kNormVariants[0]);
 #endif
