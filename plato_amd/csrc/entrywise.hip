@@ -1094,7 +1094,9 @@ void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
 // Interleaved on one box (K = 128 / 64 / 32 / 4 ResNet-18 clients, profiles/r04j-l_norms_k*.log):
 // <2048, 2, 2> 1.25-1.26 / 0.97 / 0.95 / 0.94 ms against the round-3 defaults' 1.29-1.37 / 1.01 /
 // 1.00 / 0.99; with the per-wave pairs in a second launch (64 VGPRs at 4 producer waves), <2048, 4,
-// 2> 1.20 / 0.98 / - / 0.94 (profiles/r04s_norms_k*.log).
+// 2> 1.13-1.20 / 0.97 / - / 0.94 (profiles/r04s_norms_k*.log).  Split shapes measured and dropped
+// (K = 128 / 64, interleaved): <2048, 2, 2> 1.31 / 1.01, <2048, 2, 1> 1.29 / 1.02, <2048, 4, 1> 1.21 /
+// 1.00, <2048, 4, 3> 1.16 / 0.97 against the default's 1.13 / 0.97.
 constexpr NormFn kNormDefault = &launch_rs_split<2048, 4, 2>;
 #ifdef PLATO_AGG_TUNE
 const NormFn kNormVariants[] = {
@@ -1105,10 +1107,6 @@ const NormFn kNormVariants[] = {
     &launch_pc<1024, 5>,           // 3: LDS-DMA producer / consumer, 1,024-element tiles (round 3, > 6,144 pairs)
     &launch_pc<2048, 3>,           // 4: the same, 2,048-element tiles (round 3, <= 6,144 pairs)
     &launch_per_wave,              // 5: one wavefront per (entry, client) (the first version)
-    &launch_rs_split<2048, 2, 2>,  // 6
-    &launch_rs_split<2048, 2, 1>,  // 7
-    &launch_rs_split<2048, 4, 1>,  // 8
-    &launch_rs_split<2048, 4, 3>,  // 9
 };
 constexpr int kNumNormVariants = sizeof(kNormVariants) / sizeof(kNormVariants[0]);
 #endif

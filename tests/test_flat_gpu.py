@@ -105,6 +105,30 @@ def test_norms_and_cosine_sum_equal_torch_order(n):
             assert got[j].tobytes() == R.torch_cosine(a, bs[j], threads).tobytes(), (n, threads, j)
 
 
+@pytest.mark.parametrize("n", [1000, (1 << 20) + 3])
+def test_scaled_cosine_equals_torch_order(n):
+    """plato_agg_scale_by_norm + the scaled cascade cosine sum (Port's path) over ragged chunkings."""
+    rng = np.random.default_rng(n + 7)
+    a = (rng.standard_normal(n) * 1e-2).astype(np.float32)
+    bs = [(rng.standard_normal(n) * 3e-2).astype(np.float32) + a for _ in range(3)]
+    buf, ptrs = _rows([a] + bs)
+    chunk = torch.from_numpy(np.asarray([[0, 0, n, 0]], dtype=np.uint32).view(np.int32)).to(DEV)
+    norms = torch.empty(4, dtype=torch.float32, device=DEV)
+    h = torch.cuda.current_stream().cuda_stream
+    _lib.call("plato_agg_entry_norms_f32", ptrs.data_ptr(), None, 4, None, None, chunk.data_ptr(), 1, None, 0, 1,
+              n, 0, norms.data_ptr(), h)
+    scaled = torch.empty(n, device=DEV)
+    _lib.call("plato_agg_scale_by_norm", buf.data_ptr(), n, norms.data_ptr(), 1e-8, scaled.data_ptr(), h)
+    for threads in (1, 5, 16):
+        want = [R.torch_cosine(a, b, threads).tobytes() for b in bs]
+        ws = torch.empty(_lib.lib().plato_agg_torch_cosine_workspace(3, threads) // 4 + 1, device=DEV)
+        out = torch.full((3,), float("nan"), device=DEV)
+        _lib.call("plato_agg_torch_cosine_sum_scaled", scaled.data_ptr(), ptrs.data_ptr() + 8, 3, n,
+                  norms.data_ptr() + 4, 1e-8, threads, ws.data_ptr(), out.data_ptr(), h)
+        got = out.cpu().numpy()
+        assert [got[j].tobytes() for j in range(3)] == want, (n, threads)
+
+
 def test_cosine_of_a_zero_vector_uses_eps():
     n = 1000
     a = np.zeros(n, np.float32)
