@@ -128,6 +128,14 @@ int plato_agg_tune_np_sumsq(int variant, const float* const* d_x, int K, const f
                             const plato_agg_chunk* d_pieces, const uint32_t* d_first_chunk, uint32_t n_pieces,
                             uint32_t n_chunks, void* d_workspace, float* d_out, hipStream_t stream);
 
+/* plato_agg_torch_cosine_sum_scaled with an explicit cascade form: 0 = two alternating LDS
+ * buffers, one barrier per level-1 group (the default), 1 = one buffer, two barriers (round 3)
+ * (csrc/flat.hip chunk_cascade).  Bitwise identical results. */
+int plato_agg_tune_num_cosine_variants(void);
+int plato_agg_tune_torch_cosine_sum_scaled(int variant, const float* d_a_scaled, const float* const* d_b, int K,
+                                           size_t n, const float* d_norm_b, float eps, int threads,
+                                           void* d_workspace, float* d_out, hipStream_t stream);
+
 /* plato_agg_port_norms with an explicit shape (see csrc/port.hip). */
 int plato_agg_tune_num_port_norms_variants(void);
 int plato_agg_tune_port_norms(int variant, const void* const* d_x_f32, const void* const* d_x_i64,

@@ -190,6 +190,10 @@ TUNE_SIGNATURES = {
     "plato_agg_tune_fedadp_is_probe": (_c_int, [_c_int]),
     "plato_agg_tune_num_port_norms_variants": (_c_int, []),
     "plato_agg_tune_num_np_sumsq_variants": (_c_int, []),
+    "plato_agg_tune_num_cosine_variants": (_c_int, []),
+    "plato_agg_tune_torch_cosine_sum_scaled": (
+        _c_int, [_c_int, _c_void_p, _c_void_p, _c_int, _c_size_t, _c_void_p, _c_float, _c_int, _c_void_p, _c_void_p,
+                 _c_void_p]),
     "plato_agg_tune_num_entry_norms_variants": (_c_int, []),
     "plato_agg_tune_np_sumsq": (
         _c_int,

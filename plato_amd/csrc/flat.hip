@@ -624,7 +624,10 @@ using QSrc = QSrcT<false>;
 // One chunk [b0, b0+size0) -> final_acc of vectorized_inner_sum (size0 >= 8).
 // Level-0 groups (L rows of 32 values: 4 ILP rows x 8 lanes) are summed in
 // parallel by the workgroup, the higher levels in order by lanes 0..31 of wave 0.
-template <class Q>
+// kDB: common-case level-0 sums into two alternating LDS buffers, one barrier per level-1 group (the
+// buffer a pass writes was last read two passes ago, before the barrier between); else one buffer
+// and a second barrier after lanes 0..31 have read it
+template <class Q, bool kDB = true>
 __device__ float chunk_cascade(const Q& q, uint64_t b0, uint64_t size0, float* lds_s0) {
   const uint64_t vec_size = size0 / 8;
   const uint64_t size_ilp = vec_size / 4;
@@ -644,6 +647,8 @@ __device__ float chunk_cascade(const Q& q, uint64_t b0, uint64_t size0, float* l
     return s;
   };
   for (uint64_t g1 = 0; g1 < G1; ++g1) {
+    // L == 16 uses 16 x 32 floats of the 64 x 32: with kDB, passes alternate between the halves
+    float* const s0 = (kDB && L == 16) ? lds_s0 + (g1 & 1) * 1024 : lds_s0;
     if (L == 16) {
       // the common case (chunks of 2^14 .. 2^22 elements): both of this thread's level-0 groups with
       // all 64 loads issued before the first add (the generic loop waits on each row's loads in turn)
@@ -664,7 +669,7 @@ __device__ float chunk_cascade(const Q& q, uint64_t b0, uint64_t size0, float* l
         float s = 0.f;
 #pragma unroll
         for (int i = 0; i < kL; ++i) s += q.av(av[jj][i]) * (bv[jj][i] / q.nb);
-        lds_s0[uint64_t(gslot + jj * (kSumThreads / 32)) * 32 + uint64_t(acc_id)] = s;
+        s0[uint64_t(gslot + jj * (kSumThreads / 32)) * 32 + uint64_t(acc_id)] = s;
       }
     } else {
       for (uint64_t j = uint64_t(gslot); j < L; j += kSumThreads / 32)
@@ -673,15 +678,16 @@ __device__ float chunk_cascade(const Q& q, uint64_t b0, uint64_t size0, float* l
     __syncthreads();
     if (tid < 32) {
       float s1 = 0.f;
-      for (uint64_t j = 0; j < L; ++j) s1 += lds_s0[j * 32 + uint64_t(tid)];
+      for (uint64_t j = 0; j < L; ++j) s1 += s0[j * 32 + uint64_t(tid)];
       acc2 += s1;
       if ((g1 + 1) % L == 0) {
         acc3 += acc2;
         acc2 = 0.f;
       }
     }
-    __syncthreads();
+    if (!kDB || L != 16) __syncthreads();
   }
+  if (kDB && L == 16) __syncthreads();  // lanes 0..31 have read the last pass
   // the partial level-1 group: its complete level-0 groups, in order
   const uint64_t rem0 = G0 - G1 * L;
   for (uint64_t j = uint64_t(gslot); j < rem0; j += kSumThreads / 32)
@@ -768,7 +774,7 @@ __device__ float small_inner_sum(const float* in, int n) {
   return ps[0][0];
 }
 
-template <bool kScaled>
+template <bool kScaled, bool kDB = true>
 __global__ __launch_bounds__(kSumThreads) void cosine_chunks_kernel(CosArgs a) {
   __shared__ float lds_s0[64 * 32];  // L <= 64 level-0 groups of 32 values
   // the K clients of a chunk are consecutive workgroups (dealt over the 8 XCDs together): the XCD L2s
@@ -787,7 +793,7 @@ __global__ __launch_bounds__(kSumThreads) void cosine_chunks_kernel(CosArgs a) {
   const uint64_t size0 = e0 - b0;
   float r;
   if (size0 >= 8) {
-    r = chunk_cascade(q, b0, size0, lds_s0);
+    r = chunk_cascade<QSrcT<kScaled>, kDB>(q, b0, size0, lds_s0);
   } else {
     r = 0.f;
     if (threadIdx.x == 0) {
@@ -1265,7 +1271,8 @@ int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_bas
 
 namespace {
 int run_cosine(bool scaled, const float* d_a, const float* const* d_b, int K, size_t n, const float* d_norm_a,
-               const float* d_norm_b, float eps, int threads, void* d_workspace, float* d_out, hipStream_t stream) {
+               const float* d_norm_b, float eps, int threads, void* d_workspace, float* d_out, hipStream_t stream,
+               int variant = 0) {
   if (K <= 0 || K > 65535) return set_error(PLATO_AGG_EINVAL, "K must be in [1, 65535]");
   if (threads < 1 || threads > 1024) return set_error(PLATO_AGG_EINVAL, "threads must be in [1, 1024]");
   if (!d_a || !d_b || (!scaled && !d_norm_a) || !d_norm_b || !d_workspace || !d_out)
@@ -1302,8 +1309,15 @@ int run_cosine(bool scaled, const float* d_a, const float* const* d_b, int K, si
     while ((uint64_t(1) << r) < size_ilp) ++r;
     if (r / 4 > 6) return set_error(PLATO_AGG_EINVAL, "thread chunk too long (> 2^33 elements)");
   }
-  if (scaled) hipLaunchKernelGGL(cosine_chunks_kernel<true>, dim3(uint32_t(K), uint32_t(a.nt)), dim3(kSumThreads), 0, stream, a);
-  else hipLaunchKernelGGL(cosine_chunks_kernel<false>, dim3(uint32_t(K), uint32_t(a.nt)), dim3(kSumThreads), 0, stream, a);
+  // variant (tuning only): 1 = one LDS buffer, two barriers per level-1 group (round 3)
+  const dim3 grid{uint32_t(K), uint32_t(a.nt)};
+  if (variant == 1) {
+    if (scaled) hipLaunchKernelGGL((cosine_chunks_kernel<true, false>), grid, dim3(kSumThreads), 0, stream, a);
+    else hipLaunchKernelGGL((cosine_chunks_kernel<false, false>), grid, dim3(kSumThreads), 0, stream, a);
+  } else {
+    if (scaled) hipLaunchKernelGGL(cosine_chunks_kernel<true>, grid, dim3(kSumThreads), 0, stream, a);
+    else hipLaunchKernelGGL(cosine_chunks_kernel<false>, grid, dim3(kSumThreads), 0, stream, a);
+  }
   if (int rc = check_launch("cosine chunks launch")) return rc;
   hipLaunchKernelGGL(cosine_combine_kernel, dim3(uint32_t((K + 63) / 64)), dim3(64), 0, stream, a, K);
   return check_launch("cosine combine launch");
@@ -1386,6 +1400,18 @@ int plato_agg_torch_cosine_sum_scaled(const float* d_a_scaled, const float* cons
                                       hipStream_t stream) {
   return run_cosine(true, d_a_scaled, d_b, K, n, nullptr, d_norm_b, eps, threads, d_workspace, d_out, stream);
 }
+
+#ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
+int plato_agg_tune_num_cosine_variants(void) { return 2; }
+
+int plato_agg_tune_torch_cosine_sum_scaled(int variant, const float* d_a_scaled, const float* const* d_b, int K,
+                                           size_t n, const float* d_norm_b, float eps, int threads,
+                                           void* d_workspace, float* d_out, hipStream_t stream) {
+  if (variant < 0 || variant > 1) return set_error(PLATO_AGG_EINVAL, "bad cosine variant");
+  return run_cosine(true, d_a_scaled, d_b, K, n, nullptr, d_norm_b, eps, threads, d_workspace, d_out, stream,
+                    variant);
+}
+#endif  // PLATO_AGG_TUNE
 
 int plato_agg_scale_by_norm(const float* d_a, size_t n, const float* d_norm, float eps, float* d_out,
                             hipStream_t stream) {

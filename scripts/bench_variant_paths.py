@@ -56,6 +56,9 @@ def main():
                     help="HIP-event time of every plato_agg_tune_port_norms variant on the arenas")
     ap.add_argument("--port-norms", action="store_true",
                     help="time the entry_norms variants on Port's K+1 flattened vectors (one entry each)")
+    ap.add_argument("--cosine-variants", action="store_true",
+                    help="HIP-event time of every plato_agg_tune_torch_cosine_sum_scaled variant, interleaved")
+    ap.add_argument("--threads", type=int, default=None, help="torch threads of the cosine chunking (default: this host's)")
     args = ap.parse_args()
     args.sdot = args.sdot or args.sdot_only
     args.fedadp_kernel = args.fedadp_kernel or args.fedadp_only
@@ -134,7 +137,7 @@ def main():
     }
     for name, (fn, nbytes, chain, what) in paths.items():
         if (args.sdot_only or args.fedadp_only or args.port_gathered
-                or args.polaris_variants):
+                or args.polaris_variants or args.cosine_variants):
             break
         if args.port_only and not name.startswith("port"):
             continue
@@ -163,6 +166,8 @@ def main():
         port_gathered(dev, rnd, slots, layout, previous, args.reps)
     if args.polaris_variants:
         polaris_variants(dev, rnd, slots, layout, args.reps)
+    if args.cosine_variants:
+        cosine_variants(dev, k, n_f + n_i, args.reps, args.threads or torch.get_num_threads())
 
 
 def fedadp_kernel(dev, rnd, slots, layout, reps):
@@ -288,6 +293,46 @@ def port_gathered(dev, rnd, slots, layout, previous, reps):
                           "ms_median": round(med, 4),
                           "cycles_per_step_at_2.4GHz": round(med * 1e-3 * 2.4e9 / (n_flat // 8), 2),
                           "bitwise_equal_to_flat_path": ok}), flush=True)
+
+
+def cosine_variants(dev, k, n, reps, threads):
+    """Port's cascade cosine sums (a already divided by its norm) per tuning variant, interleaved
+    rep by rep so that box drift hits every variant alike, bitwise compared."""
+    from plato_amd import _lib
+
+    stride = -(-n // 64) * 64
+    a = torch.randn(stride, device=dev)
+    bs = torch.randn((k, stride), device=dev) * 1e-2
+    tab = torch.tensor([bs.data_ptr() + r * stride * 4 for r in range(k)], dtype=torch.int64, device=dev)
+    nb = torch.linalg.vector_norm(bs, dim=1)
+    ws = torch.empty(max(1, _lib.lib().plato_agg_torch_cosine_workspace(k, threads) // 4), device=dev)
+    h = torch.cuda.current_stream(dev).cuda_stream
+    nv = _lib.tune().plato_agg_tune_num_cosine_variants()
+    outs = [torch.empty(k, device=dev) for _ in range(nv)]
+
+    def fn(v):
+        _lib.tune_call("plato_agg_tune_torch_cosine_sum_scaled", v, a.data_ptr(), tab.data_ptr(), k, n, nb.data_ptr(),
+                       1e-8, threads, ws.data_ptr(), outs[v].data_ptr(), h)
+    for v in range(nv):
+        fn(v)
+    torch.cuda.synchronize(dev)
+    ref = outs[0].cpu().numpy().tobytes()
+    same = [o.cpu().numpy().tobytes() == ref for o in outs]
+    ts = [[] for _ in range(nv)]
+    for _ in range(reps):
+        for v in range(nv):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            fn(v)
+            e1.record()
+            e1.synchronize()
+            ts[v].append(e0.elapsed_time(e1))
+    uniq = (k + 1) * n * 4
+    for v in range(nv):
+        med = statistics.median(ts[v])
+        print(json.dumps({"cosine_variant": v, "clients": k, "n": n, "threads": threads, "ms_median": round(med, 4),
+                          "ms_min": round(min(ts[v]), 4), "GBps_unique_bytes": round(uniq / (med * 1e-3) / 1e9, 1),
+                          "bitwise_equal_to_v0": same[v]}), flush=True)
 
 
 def port_norms(dev, k, n, reps):

@@ -107,7 +107,7 @@ def test_norms_and_cosine_sum_equal_torch_order(n):
 
 @pytest.mark.parametrize("n", [1000, (1 << 20) + 3])
 def test_scaled_cosine_equals_torch_order(n):
-    """plato_agg_scale_by_norm + the scaled cascade cosine sum (Port's path) over ragged chunkings."""
+    """plato_agg_scale_by_norm + every form of the scaled cascade cosine sum (Port's path), ragged chunkings."""
     rng = np.random.default_rng(n + 7)
     a = (rng.standard_normal(n) * 1e-2).astype(np.float32)
     bs = [(rng.standard_normal(n) * 3e-2).astype(np.float32) + a for _ in range(3)]
@@ -122,11 +122,16 @@ def test_scaled_cosine_equals_torch_order(n):
     for threads in (1, 5, 16):
         want = [R.torch_cosine(a, b, threads).tobytes() for b in bs]
         ws = torch.empty(_lib.lib().plato_agg_torch_cosine_workspace(3, threads) // 4 + 1, device=DEV)
-        out = torch.full((3,), float("nan"), device=DEV)
-        _lib.call("plato_agg_torch_cosine_sum_scaled", scaled.data_ptr(), ptrs.data_ptr() + 8, 3, n,
-                  norms.data_ptr() + 4, 1e-8, threads, ws.data_ptr(), out.data_ptr(), h)
-        got = out.cpu().numpy()
-        assert [got[j].tobytes() for j in range(3)] == want, (n, threads)
+        for v in [None] + list(range(_lib.tune().plato_agg_tune_num_cosine_variants())):
+            out = torch.full((3,), float("nan"), device=DEV)
+            args = (scaled.data_ptr(), ptrs.data_ptr() + 8, 3, n, norms.data_ptr() + 4, 1e-8, threads, ws.data_ptr(),
+                    out.data_ptr(), h)
+            if v is None:
+                _lib.call("plato_agg_torch_cosine_sum_scaled", *args)
+            else:
+                _lib.tune_call("plato_agg_tune_torch_cosine_sum_scaled", v, *args)
+            got = out.cpu().numpy()
+            assert [got[j].tobytes() for j in range(3)] == want, (n, threads, v)
 
 
 def test_cosine_of_a_zero_vector_uses_eps():
