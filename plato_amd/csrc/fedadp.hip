@@ -557,7 +557,9 @@ constexpr AdpLaunch adp_launch() {
 
 // The product's shape: 192-step stages of 12 producer waves x 2 iterations, x and b from the
 // chain-group-major buffer, the client arenas read non-temporally (once-read, kept out of the L2
-// the re-read x and b live in), the division as a float64 product
+// the re-read x and b live in), the division as a float64 product.  On aligned
+// arenas the buffer still pays for its prep launch: without it (x from the flat gradient, b from
+// the baseline arena) the whole call took 1.381 ms against 1.355 (profiles/r04v_fedadp.log).
 constexpr AdpLaunch kAdpDefault = adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB>();
 #ifdef PLATO_AGG_TUNE
 const AdpLaunch kAdpVariants[] = {

@@ -199,20 +199,24 @@ def fedadp_kernel(dev, rnd, slots, layout, reps):
                                                     yy.data_ptr(), h))
     # unique bytes: each client's fp32 arena + int64 counters once, the baseline and g_flat once
     uniq = k * (layout.n_f32 * 4 + layout.n_i64 * 8) + 2 * layout.n_f32 * 4 + n_flat * 4
+    oks = {}
     for name, fn in runs.items():
         fn()
         torch.cuda.synchronize(dev)
-        ok = (xy.cpu().numpy()[:k].tobytes() == np.asarray(want[0]).tobytes()
-              and xy.cpu().numpy()[k:].tobytes() == np.float32(want[1]).tobytes()
-              and yy.cpu().numpy()[:k].tobytes() == np.asarray(want[2]).tobytes())
-        ts = []
-        for _ in range(reps):
+        oks[name] = (xy.cpu().numpy()[:k].tobytes() == np.asarray(want[0]).tobytes()
+                     and xy.cpu().numpy()[k:].tobytes() == np.float32(want[1]).tobytes()
+                     and yy.cpu().numpy()[:k].tobytes() == np.asarray(want[2]).tobytes())
+    tss = {name: [] for name in runs}
+    for _ in range(reps):  # interleaved: box drift hits every variant alike
+        for name, fn in runs.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             fn()
             e1.record()
             e1.synchronize()
-            ts.append(e0.elapsed_time(e1))
+            tss[name].append(e0.elapsed_time(e1))
+    for name in runs:
+        ok, ts = oks[name], tss[name]
         med = statistics.median(ts)
         print(json.dumps({"fedadp_dots": name, "pairs": k + 1, "n_flat": n_flat, "ms_median": round(med, 4),
                           "ms_min": round(min(ts), 4), "GBps_unique_bytes": round(uniq / (med * 1e-3) / 1e9, 1),
