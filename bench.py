@@ -40,8 +40,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--config", default="C2", choices=sorted(CONFIGS),
                    help="BASELINE.json configuration (C2 = the headline metric's workload)")
     p.add_argument("--clients", type=int, default=None, help="override K")

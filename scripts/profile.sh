@@ -14,7 +14,7 @@ EXTRA="$*"
 cd /tmp && export TMPDIR=/tmp
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
-B="python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-host-inclusive $EXTRA"
+B="python3 $R/bench.py --steps 100 --warmup 10 --no-cpu-baseline --no-host-inclusive $EXTRA"
 timeout -k 10 300 $B > $OUT/bench.json 2> $OUT/bench.err
 rc=$?; echo "bench (unprofiled) rc=$rc"; tail -c 400 $OUT/bench.json
 [ $rc -ne 0 ] && exit $rc

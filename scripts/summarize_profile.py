@@ -34,7 +34,7 @@ def last_json(path):
     return json.loads(lines[-1]) if lines else None
 
 
-def main(tag, alg_bytes, label, steps=20):
+def main(tag, alg_bytes, label, steps=None):
     src = os.path.join(ROOT, "gpurun_out", f"prof_{tag}")
     dst = os.path.join(ROOT, "profiles")
     os.makedirs(dst, exist_ok=True)
@@ -51,9 +51,11 @@ def main(tag, alg_bytes, label, steps=20):
              if r["Kernel_Name"] == row["Name"]]
     trace.sort(key=lambda r: int(r["Start_Timestamp"]))
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in trace]
-    timed = durs[-steps:]
     run = last_json(os.path.join(src, "bench.json"))
     prof_run = last_json(os.path.join(src, "kt.log"))
+    if steps is None:  # the profiled bench's own timed-step count
+        steps = (prof_run or run or {}).get("steps", 20)
+    timed = durs[-steps:]
     sys.path.insert(0, ROOT)
     import bench  # noqa: E402  (source stamp of the profiled kernel)
     out = {
