@@ -17,7 +17,7 @@
 // which need the norms first: the store rides in the shadow of the serial chain.
 //
 // Shape: one workgroup per vector (V = K + 1: vector 0 = current - previous, vectors 1..K the
-// client deltas), 1 chain wave + kWp producer waves, 2,048-position tiles (256 steps per chain),
+// client deltas), 1 chain wave + kWp producer waves, kT-position tiles (kT / 8 steps per chain),
 // a two-slot tile ring and one s_barrier per tile; each producer keeps kD tiles of loads in flight.
 // The launch is bound by the serial chain (n / 8 dependent fmas), not by HBM; DESIGN.md §13.
 // Compiled with -ffp-contract=off; the chain fma is an explicit fma (torch's vfmadd231ps).
@@ -277,17 +277,19 @@ void launch_pn(const PnArgs& a, hipStream_t st, int V) {
   hipLaunchKernelGGL((port_norms_kernel<kWp, kD, kNT, kT>), dim3(uint32_t(V)), dim3(64 * (1 + kWp)), 0, st, a);
 }
 // producer waves x tiles of loads in flight (x non-temporal flat stores, x tile positions)
-constexpr PnFn kPnDefault = &launch_pn<8, 2, true, 4096>;
+// 8,192-position tiles: 4.098 against 4.156 ms for 4,096 interleaved (profiles/r04zz_port.log; 4.12 against
+// 4.17 in round 4's first sweep)
+constexpr PnFn kPnDefault = &launch_pn<8, 2, true, 8192>;
 #ifdef PLATO_AGG_TUNE
 // The round-3 sweep (1-8 producer waves x 2-4 tiles in flight, plain or non-temporal flat stores;
 // profiles/r03l_port.log) and round 4's tile sizes (profiles/r04n_port_variants.log) are in DESIGN.md
 // §13-14; kept: the default, the round-3 default and the runners-up.
 const PnFn kPnVariants[] = {
-    &launch_pn<8, 2, true, 4096>,  // 0: the default, 4.14 ms storing the flat vectors (4,096-position tiles)
+    &launch_pn<8, 2, true, 8192>,  // 0: the default, 4.10 ms storing the flat vectors (8,192-position tiles)
     &launch_pn<8, 3, true>,        // 1: the round-3 default (2,048), 4.70 ms
     &launch_pn<4, 2>,              // 2: 4.25 ms without the stores
     &launch_pn<8, 3, true, 4096>,  // 3: 4.17 ms
-    &launch_pn<8, 2, true, 8192>,  // 4
+    &launch_pn<8, 2, true, 4096>,  // 4: the first round-4 default (4,096-position tiles), 4.16 ms
     &launch_pn<8, 1, true, 4096>,  // 5
 };
 constexpr int kNumPnVariants = sizeof(kPnVariants) / sizeof(kPnVariants[0]);

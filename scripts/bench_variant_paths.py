@@ -276,22 +276,30 @@ def port_gathered(dev, rnd, slots, layout, previous, reps):
     v8 = vt.data_ptr()
     out = torch.empty(k + 1, device=dev)
     h = torch.cuda.current_stream(dev).cuda_stream
-    for v, store in [(v, st) for v in range(_lib.tune().plato_agg_tune_num_port_norms_variants()) for st in (False, True)]:
+    def make(v, store):
         def fn():
             _lib.tune_call("plato_agg_tune_port_norms", v, v8, v8 + 8 * (k + 1), v8 + 16 * (k + 1), v8 + 24 * (k + 1),
                            k + 1, None, segs.data_ptr(), len(layout.entries), n_flat, layout.n_f32,
                            _lib.PLATO_AGG_PORT_CAST_FIRST, out.data_ptr(), v8 + 32 * (k + 1) if store else None, h)
+        return fn
+    # the stores-flat form (the product's) of every variant, interleaved rep by rep
+    runs = {(v, True): make(v, True) for v in range(_lib.tune().plato_agg_tune_num_port_norms_variants())}
+    oks = {}
+    for key, fn in runs.items():
         fn()
         torch.cuda.synchronize(dev)
-        ok = out.cpu().numpy().tobytes() == want.tobytes()
-        ts = []
-        for _ in range(reps):
+        oks[key] = out.cpu().numpy().tobytes() == want.tobytes()
+    tss = {key: [] for key in runs}
+    for _ in range(reps):
+        for key, fn in runs.items():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             fn()
             e1.record()
             e1.synchronize()
-            ts.append(e0.elapsed_time(e1))
+            tss[key].append(e0.elapsed_time(e1))
+    for (v, store), ts in tss.items():
+        ok = oks[(v, store)]
         med = statistics.median(ts)
         print(json.dumps({"port_norms_gathered_variant": v, "stores_flat": store, "vectors": k + 1, "n": n_flat,
                           "ms_median": round(med, 4),
