@@ -587,6 +587,12 @@ __device__ __forceinline__ void wait_vmcnt() {
 __device__ __forceinline__ void wait_lgkm0() {
   __builtin_amdgcn_s_waitcnt((63 & 15) | (7 << 4) | (0 << 8) | ((63 >> 4) << 14));
 }
+// s_waitcnt lgkmcnt(N) alone
+template <int N>
+__device__ __forceinline__ void wait_lgkm() {
+  static_assert(N >= 0 && N < 16, "lgkmcnt range");
+  __builtin_amdgcn_s_waitcnt((63 & 15) | (7 << 4) | (N << 8) | ((63 >> 4) << 14));
+}
 
 template <int T, bool HAS_BASE>
 __device__ __forceinline__ void pc_issue(const float* x, const float* b, float (*raw)[2][T], uint32_t slot,
@@ -681,7 +687,11 @@ __device__ __forceinline__ uint64_t pc_ntiles(const Chunk ch) {
 
 // nbar >= the tile count: barriers past the last tile (a producer that runs whole trips of D
 // tiles, entry_norms_rs_kernel) are met without reading a tile.
-template <int T, bool TR>
+// kOW (transposed tiles): 0 = the compiler's waits (one s_waitcnt per ds_read_b128 of a 16-step block);
+// 1 / 2 = one s_waitcnt per 16- / 32-step block (4 / 8 reads), the next block's reads in flight.  Each
+// ds_read_b128 costs the chain wave ~5 issue cycles and each s_waitcnt ~3.7 beside the 4 of a
+// dependent v_fmac_f32 (scripts/micro/chain_b128.hip, profiles/r04_micro_chain_b128.log).
+template <int T, bool TR, int kOW = 0>
 __device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstride, uint64_t nbar) {
   constexpr int kRT = T, kTS = DTile<T, TR>::kTS;
   const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
@@ -701,7 +711,33 @@ __device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstr
     const float* p = TR ? tile + pj * kTS : tile + pj;
     constexpr int kStep = TR ? 1 : 8;  // floats between a chain's consecutive steps
     const int64_t s0 = int64_t(tt) * (kRT / kNormLanes) + s_shift;
-    if (TR && tt >= 1 && int64_t(tt + 1) * (kRT / kNormLanes) <= s_end) {
+    if (TR && kOW > 0 && tt >= 1 && int64_t(tt + 1) * (kRT / kNormLanes) <= s_end) {
+      constexpr int kQ = 4 * (kOW > 0 ? kOW : 1), kNB = kRT / kNormLanes / (4 * kQ);
+      const f4* q4 = reinterpret_cast<const f4*>(p);
+      f4 buf[2][kQ];
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) buf[0][q] = q4[q];
+#pragma unroll
+      for (int blk = 0; blk < kNB; ++blk) {
+        const int cb = blk & 1;
+        if (blk + 1 < kNB) {
+#pragma unroll
+          for (int q = 0; q < kQ; ++q) buf[cb ^ 1][q] = q4[kQ * (blk + 1) + q];
+          wait_lgkm<kQ>();  // this block's reads have landed; the next block's stay in flight
+        } else {
+          wait_lgkm<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+          acc = __builtin_fmaf(buf[cb][q].x, buf[cb][q].x, acc);
+          acc = __builtin_fmaf(buf[cb][q].y, buf[cb][q].y, acc);
+          acc = __builtin_fmaf(buf[cb][q].z, buf[cb][q].z, acc);
+          acc = __builtin_fmaf(buf[cb][q].w, buf[cb][q].w, acc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if (TR && tt >= 1 && int64_t(tt + 1) * (kRT / kNormLanes) <= s_end) {
       // 16 steps per block as 4 ds_read_b128, the next block's in flight
       constexpr int kNB = kRT / kNormLanes / 16;
       const f4* q4 = reinterpret_cast<const f4*>(p);
@@ -894,7 +930,7 @@ __device__ void rs_produce(const NormArgs& a, const Chunk ch, const float* x, in
   wait_vmcnt<0>();
 }
 
-template <int T, int P, int D, bool HAS_BASE, int PRIO, bool kSplit = false>
+template <int T, int P, int D, bool HAS_BASE, int PRIO, bool kSplit = false, int kOW = 0>
 __device__ __forceinline__ void rs_pair(const NormArgs& a, uint64_t pair, int wave, int lane, float* dbuf) {
   constexpr int kSize = DTile<T, true>::kSize;
   const uint32_t ent = uint32_t(pair / uint64_t(a.K));  // entry-major over the (longest-first) tables
@@ -915,7 +951,7 @@ __device__ __forceinline__ void rs_pair(const NormArgs& a, uint64_t pair, int wa
       return;
     }
     pc_chain_prio<PRIO>(a, ch);
-    pc_finish<HAS_BASE>(a, ch, i, x, lane, pc_chain<T, true>(ch, lane, dbuf, kSize, nbar));
+    pc_finish<HAS_BASE>(a, ch, i, x, lane, pc_chain<T, true, kOW>(ch, lane, dbuf, kSize, nbar));
   } else if (!kSplit && ent < a.nef + a.nei) {
     if (wave == 0) norm_pair<HAS_BASE, true>(a, load_chunk(a.ei, ent - a.nef, a.n_i64), i, lane, rows);
   }
@@ -924,13 +960,13 @@ __device__ __forceinline__ void rs_pair(const NormArgs& a, uint64_t pair, int wa
 // kSplit: the per-wave pairs (int64 entries, the partial-last-group fp32 entry) are left to a second
 // launch (entry_norms_kernel<., true>), so that norm_pair's 64 registers of tile prefetch do not set
 // this kernel's register count and with it how many pairs share a CU.
-template <int T, int P, int D, bool HAS_BASE, int PRIO, bool kSplit = false>
+template <int T, int P, int D, bool HAS_BASE, int PRIO, bool kSplit = false, int kOW = 0>
 __global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rs_kernel(NormArgs a) {
   constexpr int kSize = DTile<T, true>::kSize;
   static_assert(2 * kSize >= kNormLanes * kNRow, "norm_pair's rows fit the d ring");
   __shared__ __attribute__((aligned(16))) float dbuf[2 * kSize];
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
-  rs_pair<T, P, D, HAS_BASE, PRIO, kSplit>(a, blockIdx.x, wave, lane, dbuf);
+  rs_pair<T, P, D, HAS_BASE, PRIO, kSplit, kOW>(a, blockIdx.x, wave, lane, dbuf);
 }
 
 bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
@@ -1065,16 +1101,16 @@ void launch_rs(const NormArgs& a, bool hb, dim3 grid, hipStream_t st) {
   if (hb) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, true, PRIO>), grid, dim3(64 * (1 + P)), 0, st, a);
   else hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, false, PRIO>), grid, dim3(64 * (1 + P)), 0, st, a);
 }
-template <int T, int P, int D, int PRIO = -1>
+template <int T, int P, int D, int PRIO = -1, int kOW = 0>
 void launch_rs_split(const NormArgs& a, bool hb, dim3, hipStream_t st) {
   const dim3 g1{uint32_t(uint64_t(a.nef) * uint64_t(a.K))};  // the fp32 pairs; int64 pairs come after them
   const uint64_t waves = (uint64_t(a.nef) + a.nei) * uint64_t(a.K);
   const dim3 g2{uint32_t((waves + kBlock / 64 - 1) / (kBlock / 64))};
   if (hb) {
-    if (a.nef) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, true, PRIO, true>), g1, dim3(64 * (1 + P)), 0, st, a);
+    if (a.nef) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, true, PRIO, true, kOW>), g1, dim3(64 * (1 + P)), 0, st, a);
     hipLaunchKernelGGL((entry_norms_kernel<true, true>), g2, dim3(kBlock), 0, st, a);
   } else {
-    if (a.nef) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, false, PRIO, true>), g1, dim3(64 * (1 + P)), 0, st, a);
+    if (a.nef) hipLaunchKernelGGL((entry_norms_rs_kernel<T, P, D, false, PRIO, true, kOW>), g1, dim3(64 * (1 + P)), 0, st, a);
     hipLaunchKernelGGL((entry_norms_kernel<false, true>), g2, dim3(kBlock), 0, st, a);
   }
 }
@@ -1097,16 +1133,22 @@ void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
 // 2> 1.13-1.20 / 0.97 / - / 0.94 (profiles/r04s_norms_k*.log).  Split shapes measured and dropped
 // (K = 128 / 64, interleaved): <2048, 2, 2> 1.31 / 1.01, <2048, 2, 1> 1.29 / 1.02, <2048, 4, 1> 1.21 /
 // 1.00, <2048, 4, 3> 1.16 / 0.97 against the default's 1.13 / 0.97.
-constexpr NormFn kNormDefault = &launch_rs_split<2048, 4, 2>;
+// One s_waitcnt per 32 chain steps (kOW = 2): 0.832 against 0.939 ms at K = 4 and 1.139 against 1.157
+// at K = 128, interleaved (profiles/r04za_norms_k*.log; 76 VGPRs, six waves per SIMD).
+constexpr NormFn kNormDefault = &launch_rs_split<2048, 4, 2, -1, 2>;
 #ifdef PLATO_AGG_TUNE
 const NormFn kNormVariants[] = {
-    &launch_rs_split<2048, 4, 2>,  // 0: the default: register-staged, 4 producer waves, 2 tiles in flight,
-                                   //    the per-wave pairs (int64, partial last group) in a second launch
+    &launch_rs_split<2048, 4, 2, -1, 2>,  // 0: the default: register-staged, 4 producer waves, 2 tiles in
+                                          //    flight, the per-wave pairs (int64, partial last group) in a
+                                          //    second launch, one s_waitcnt per 32 chain steps
     &launch_rs<2048, 2, 2>,        // 1: 2 producer waves, one launch (the first round-4 default)
     &launch_rs<2048, 2, 3, -2>,    // 2: 3 tiles in flight, the long entries' producers at priority 2
     &launch_pc<1024, 5>,           // 3: LDS-DMA producer / consumer, 1,024-element tiles (round 3, > 6,144 pairs)
     &launch_pc<2048, 3>,           // 4: the same, 2,048-element tiles (round 3, <= 6,144 pairs)
     &launch_per_wave,              // 5: one wavefront per (entry, client) (the first version)
+    &launch_rs_split<2048, 4, 2, -1, 1>,  // 6: one s_waitcnt per 16 chain steps (64 VGPRs)
+    &launch_rs_split<2048, 4, 2>,         // 7: the compiler's waits, one per ds_read_b128 (the first round-4
+                                          //    split default)
 };
 constexpr int kNumNormVariants = sizeof(kNormVariants) / sizeof(kNormVariants[0]);
 #endif

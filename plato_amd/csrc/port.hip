@@ -179,7 +179,18 @@ __device__ __forceinline__ void pn_write(const PnArgs& a, const PnSeg* S, float*
   }
 }
 
-template <int kWp, int kD, bool kNT = false, int kT = 2048>
+// s_waitcnt lgkmcnt(N) alone (gfx9 encoding; vmcnt and expcnt at their maxima)
+template <int N>
+__device__ __forceinline__ void pn_wait_lgkm() {
+  static_assert(N >= 0 && N < 16, "lgkmcnt range");
+  __builtin_amdgcn_s_waitcnt(15 | (7 << 4) | (N << 8) | (3 << 14));
+}
+
+// kOW: the chain's LDS reads per wait.  0: the compiler's waits, one s_waitcnt per ds_read_b128 of
+// a 16-step block; 1: one s_waitcnt per 16-step block (4 reads), 2: per 32-step block (8 reads).
+// scripts/micro/chain_b128.hip: each ds_read_b128 costs the chain wave ~5 issue cycles and each
+// s_waitcnt ~3.7 on top of the 4 of a dependent v_fmac_f32 (profiles/r04_micro_chain_b128.log).
+template <int kWp, int kD, bool kNT = false, int kT = 2048, int kOW = 0>
 __global__ __launch_bounds__(64 * (1 + kWp)) void port_norms_kernel(PnArgs a_in) {
   using Tl = PnTile<kT>;
   constexpr int kIts = Tl::kIts, kSlot = Tl::kSlot, kR = Tl::kR, kSteps = Tl::kSteps;
@@ -233,6 +244,34 @@ __global__ __launch_bounds__(64 * (1 + kWp)) void port_norms_kernel(PnArgs a_in)
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
     if (t >= ntiles) continue;
     const f4* row = reinterpret_cast<const f4*>(ring + (t & 1) * kSlot + j * kR);
+    if constexpr (kOW > 0) {
+      // kQ reads (4 kQ steps) per block, the next block's reads in flight, one wait per block
+      constexpr int kQ = 4 * kOW, kNB = kSteps / (4 * kQ);
+      f4 buf[2][kQ];
+#pragma unroll
+      for (int q = 0; q < kQ; ++q) buf[0][q] = row[q];
+#pragma unroll
+      for (int blk = 0; blk < kNB; ++blk) {
+        const int cb = blk & 1;
+        if (blk + 1 < kNB) {
+#pragma unroll
+          for (int q = 0; q < kQ; ++q) buf[cb ^ 1][q] = row[kQ * (blk + 1) + q];
+          pn_wait_lgkm<kQ>();  // this block's reads have landed; the next block's stay in flight
+        } else {
+          pn_wait_lgkm<0>();
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < kQ; ++q) {
+          acc = __builtin_fmaf(buf[cb][q].x, buf[cb][q].x, acc);
+          acc = __builtin_fmaf(buf[cb][q].y, buf[cb][q].y, acc);
+          acc = __builtin_fmaf(buf[cb][q].z, buf[cb][q].z, acc);
+          acc = __builtin_fmaf(buf[cb][q].w, buf[cb][q].w, acc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      continue;
+    }
     // 16 steps per block as 4 ds_read_b128, the next block's reads in flight (positions past m are +0:
     // fma(0, 0, acc) leaves the non-negative sum unchanged)
     f4 cur4[4], nxt4[4];
@@ -272,25 +311,29 @@ __global__ __launch_bounds__(64 * (1 + kWp)) void port_norms_kernel(PnArgs a_in)
 }
 
 using PnFn = void (*)(const PnArgs&, hipStream_t, int);
-template <int kWp, int kD, bool kNT = false, int kT = 2048>
+template <int kWp, int kD, bool kNT = false, int kT = 2048, int kOW = 0>
 void launch_pn(const PnArgs& a, hipStream_t st, int V) {
-  hipLaunchKernelGGL((port_norms_kernel<kWp, kD, kNT, kT>), dim3(uint32_t(V)), dim3(64 * (1 + kWp)), 0, st, a);
+  hipLaunchKernelGGL((port_norms_kernel<kWp, kD, kNT, kT, kOW>), dim3(uint32_t(V)), dim3(64 * (1 + kWp)), 0, st, a);
 }
 // producer waves x tiles of loads in flight (x non-temporal flat stores, x tile positions)
 // 8,192-position tiles: 4.098 against 4.156 ms for 4,096 interleaved (profiles/r04zz_port.log; 4.12 against
-// 4.17 in round 4's first sweep)
-constexpr PnFn kPnDefault = &launch_pn<8, 2, true, 8192>;
+// 4.17 in round 4's first sweep); one s_waitcnt per 32-step block: 3.536 against 4.099 ms
+// (6.07 cycles per chain step; profiles/r04zz_port_onewait.log)
+constexpr PnFn kPnDefault = &launch_pn<8, 2, true, 8192, 2>;
 #ifdef PLATO_AGG_TUNE
 // The round-3 sweep (1-8 producer waves x 2-4 tiles in flight, plain or non-temporal flat stores;
 // profiles/r03l_port.log) and round 4's tile sizes (profiles/r04n_port_variants.log) are in DESIGN.md
 // §13-14; kept: the default, the round-3 default and the runners-up.
 const PnFn kPnVariants[] = {
-    &launch_pn<8, 2, true, 8192>,  // 0: the default, 4.10 ms storing the flat vectors (8,192-position tiles)
+    &launch_pn<8, 2, true, 8192, 2>,  // 0: the default, 3.54 ms storing the flat vectors (8,192-position
+                                      //    tiles, one s_waitcnt per 32 chain steps)
     &launch_pn<8, 3, true>,        // 1: the round-3 default (2,048), 4.70 ms
     &launch_pn<4, 2>,              // 2: 4.25 ms without the stores
     &launch_pn<8, 3, true, 4096>,  // 3: 4.17 ms
     &launch_pn<8, 2, true, 4096>,  // 4: the first round-4 default (4,096-position tiles), 4.16 ms
     &launch_pn<8, 1, true, 4096>,  // 5
+    &launch_pn<8, 2, true, 8192, 1>,  // 6: one s_waitcnt per 16-step block, 3.67 ms
+    &launch_pn<8, 2, true, 8192>,     // 7: the compiler's waits (one per ds_read_b128), 4.10 ms
 };
 constexpr int kNumPnVariants = sizeof(kPnVariants) / sizeof(kPnVariants[0]);
 #endif
