@@ -573,7 +573,10 @@ def main():
         dist.destroy_process_group()
 
 
-CHAIN_CYCLES = 6.0   # one dependent v_fma_f32 step on MI355X (scripts/micro/fma_chain.hip)
+# one dependent v_fmac_f32 step on MI355X: 4.04 shader cycles back to back from registers
+# (scripts/micro/chain_b128.hip, profiles/r04_micro_chain_b128.log), the wave64 issue rate; the
+# round-1 micro's 6.0 (scripts/micro/fma_chain.hip) included a taken loop branch every 16 steps
+CHAIN_CYCLES = 4.0
 CLOCK_HZ = 2.4e9
 
 
@@ -634,7 +637,7 @@ def variant_legs(dev, k: int, reps: int) -> dict:
 
     out = {"clients": k, "model": "resnet18", "reps": reps,
            "note": "HIP events around each engine launch (AggregationRound.timings); outside the headline's timed "
-                   "region; floor = max(algorithmic bytes at 8 TB/s, serial fma chain at 6 cycles/step, 2.4 GHz)"}
+                   "region; floor = max(algorithmic bytes at 8 TB/s, serial fma chain at 4 cycles/step, 2.4 GHz)"}
     lay, base, rnd = make_round(None)
     n_f, n_i = lay.n_f32_data, lay.n_i64
     model_bytes = n_f * 4 + n_i * 8
