@@ -1134,7 +1134,9 @@ void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
 // (K = 128 / 64, interleaved): <2048, 2, 2> 1.31 / 1.01, <2048, 2, 1> 1.29 / 1.02, <2048, 4, 1> 1.21 /
 // 1.00, <2048, 4, 3> 1.16 / 0.97 against the default's 1.13 / 0.97.
 // One s_waitcnt per 32 chain steps (kOW = 2): 0.832 against 0.939 ms at K = 4 and 1.139 against 1.157
-// at K = 128, interleaved (profiles/r04za_norms_k*.log; 76 VGPRs, six waves per SIMD).
+// at K = 128, interleaved (profiles/r04za_norms_k*.log; 76 VGPRs, six waves per SIMD); on a second box
+// 1.101 / 0.873 ms at K = 128 / 64 against 1.198 / 0.973, and neither long producers at priority 2,
+// 2 producers nor 3 tiles in flight beat it (1.12-1.20 / 0.88-0.89; profiles/r04zc_norms_k*.log).
 constexpr NormFn kNormDefault = &launch_rs_split<2048, 4, 2, -1, 2>;
 #ifdef PLATO_AGG_TUNE
 const NormFn kNormVariants[] = {
