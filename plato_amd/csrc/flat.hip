@@ -722,7 +722,85 @@ __device__ float chunk_cascade(const Q& q, uint64_t b0, uint64_t size0, float* l
   return result;
 }
 
-// scalar_inner_sum / vectorized_inner_sum of a short array (single thread)
+// scalar_inner_sum / vectorized_inner_sum of a short array (single thread), W = 8 (n >= 8) or 1 lanes;
+// every accumulator index is a compile-time constant (unrolled k, l and level loops), so the 4 x 4 x 8
+// cascade stays in registers (the runtime-indexed form spilled 656 bytes per lane to scratch and took
+// 28 us for the K cosine combines)
+template <int W>
+__device__ float small_inner_sum_w(const float* in, int n) {
+  const int vec_size = n / W;
+  const int size_ilp = vec_size / 4;
+  int lp = ceil_log2_u64(uint64_t(size_ilp)) / 4;
+  if (lp < 4) lp = 4;
+  const int L = 1 << lp;
+  float acc[4][4][W];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < W; ++l) acc[j][k][l] = 0.f;
+  int i = 0;
+  for (; i + L <= size_ilp;) {
+    for (int jj = 0; jj < L; ++jj, ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int l = 0; l < W; ++l) acc[0][k][l] += in[(i * 4 + k) * W + l];
+#pragma unroll
+    for (int j = 1; j < 4; ++j) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int l = 0; l < W; ++l) {
+          acc[j][k][l] += acc[j - 1][k][l];
+          acc[j - 1][k][l] = 0.f;
+        }
+      if ((uint64_t(i) & (uint64_t(L - 1) << (j * lp))) != 0) break;
+    }
+  }
+  for (; i < size_ilp; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < W; ++l) acc[0][k][l] += in[(i * 4 + k) * W + l];
+#pragma unroll
+  for (int j = 1; j < 4; ++j)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < W; ++l) acc[0][k][l] += acc[j][k][l];
+  if constexpr (W == 8) {
+    float ps0[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) ps0[l] = acc[0][0][l];
+    for (int v = size_ilp * 4; v < vec_size; ++v)
+#pragma unroll
+      for (int l = 0; l < 8; ++l) ps0[l] += in[v * 8 + l];
+#pragma unroll
+    for (int k = 1; k < 4; ++k)
+#pragma unroll
+      for (int l = 0; l < 8; ++l) ps0[l] += acc[0][k][l];
+    float final_acc = 0.f;
+    for (int e = vec_size * 8; e < n; ++e) final_acc += in[e];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) final_acc += ps0[l];
+    return final_acc;
+  } else {
+    float ps0 = acc[0][0][0];
+    for (int v = size_ilp * 4; v < n; ++v) ps0 += in[v];
+#pragma unroll
+    for (int k = 1; k < 4; ++k) ps0 += acc[0][k][0];
+    return ps0;
+  }
+}
+
+__device__ float small_inner_sum_reg(const float* in, int n) {
+  return n >= 8 ? small_inner_sum_w<8>(in, n) : small_inner_sum_w<1>(in, n);
+}
+
+// the same sum with runtime-indexed accumulators: the cascade chunk kernel's rare < 8-element chunk
+// (the register form above would raise that streaming kernel's register count, 62 -> 87 VGPRs)
 __device__ float small_inner_sum(const float* in, int n) {
   float ps[4][8];
   for (int k = 0; k < 4; ++k)
@@ -822,7 +900,7 @@ __global__ void cosine_combine_kernel(CosArgs a, int K) {
     return;
   }
   for (int t = a.nt; t < a.T; ++t) buf[t] = 0.f;
-  a.out[k] = 0.f + small_inner_sum(buf, a.T);
+  a.out[k] = 0.f + small_inner_sum_reg(buf, a.T);
 }
 
 // ------------------------------------------------- numpy pairwise sum of squares
@@ -1309,7 +1387,9 @@ int run_cosine(bool scaled, const float* d_a, const float* const* d_b, int K, si
     while ((uint64_t(1) << r) < size_ilp) ++r;
     if (r / 4 > 6) return set_error(PLATO_AGG_EINVAL, "thread chunk too long (> 2^33 elements)");
   }
-  // variant (tuning only): 1 = one LDS buffer, two barriers per level-1 group (round 3)
+  // variant (tuning only): 1 = one LDS buffer, two barriers per level-1 group (round 3).  Held to 64
+  // VGPRs (eight waves per SIMD, the 2,048-workgroup grid in one round) the default spilled (2.23 ms)
+  // and, loading one level-0 group at a time, ran 1.070 against 1.044 (profiles/r04zh_cosine.log)
   const dim3 grid{uint32_t(K), uint32_t(a.nt)};
   if (variant == 1) {
     if (scaled) hipLaunchKernelGGL((cosine_chunks_kernel<true, false>), grid, dim3(kSumThreads), 0, stream, a);
