@@ -42,6 +42,8 @@ def main():
     ap.add_argument("--interleave", type=int, default=0,
                     help="time the selected kernels round-robin this many rounds (A/B on one box: clock and "
                          "thermal drift hit every kernel alike); each round times each kernel --reps times")
+    ap.add_argument("--ew-chunks", default=None,
+                    help="comma-separated fedavg_entrywise chunk sizes to time besides the engine's (tuning)")
     ap.add_argument("--norm-order", default="longest", choices=["longest", "layout"],
                     help="entry order of the norms launch (longest first = the engine's)")
     args = ap.parse_args()
@@ -114,8 +116,8 @@ def main():
                   None, _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(out_f),
                   _ptr(out_i), n_f, n_i, h)
 
-    def run_entrywise():
-        cf, ci = chunks(engine.ENTRYWISE_CHUNK)
+    def run_entrywise(cap=None):
+        cf, ci = chunks(cap or engine.ENTRYWISE_CHUNK)
         _lib.call("plato_agg_fedavg_entrywise", _ptr(tf), _ptr(ti), k, _ptr(w_ek), n_e, _ptr(cf), cf.shape[0],
                   _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(noise), _ptr(noise_i), -1.2, 0.001,
                   _lib.PLATO_AGG_ADD_BASE, _ptr(out_f), _ptr(out_i), n_f, n_i, h)
@@ -150,6 +152,9 @@ def main():
                  else range(_lib.tune().plato_agg_tune_num_qsgd_variants()))
         for v in vlist:
             kernels[f"qsgd_v{v}"] = ((lambda v=v: run_qsgd(v)), kernels["qsgd"][1])
+    if args.ew_chunks:  # tuning: fedavg_entrywise at other chunk sizes
+        for cap in [int(x) for x in args.ew_chunks.split(",")]:
+            kernels[f"entrywise_v{cap}"] = ((lambda cap=cap: run_entrywise(cap)), kernels["entrywise"][1])
     if args.norm_variants:  # tuning: every plato_agg_tune_entry_norms variant
         for v in range(_lib.tune().plato_agg_tune_num_entry_norms_variants()):
             kernels[f"norms_v{v}"] = ((lambda v=v: run_norms(v)), kernels["norms"][1])

@@ -54,7 +54,7 @@ def _random_round(engine, k, seed):
     return layout, rnd, bf, bi, xs_f, xs_i, rng
 
 
-@pytest.mark.parametrize("cap", [8, 20, 1024])
+@pytest.mark.parametrize("cap", [8, 20, 1024, 2048])
 @pytest.mark.parametrize("noise,add_base", [(False, True), (True, True), (False, False)])
 def test_entrywise_matches_oracle(engine, monkeypatch, cap, noise, add_base):
     monkeypatch.setattr(FedAvgEngine, "ENTRYWISE_CHUNK", cap)
