@@ -318,7 +318,8 @@ void launch_pn(const PnArgs& a, hipStream_t st, int V) {
 // producer waves x tiles of loads in flight (x non-temporal flat stores, x tile positions)
 // 8,192-position tiles: 4.098 against 4.156 ms for 4,096 interleaved (profiles/r04zz_port.log; 4.12 against
 // 4.17 in round 4's first sweep); one s_waitcnt per 32-step block: 3.536 against 4.099 ms
-// (6.07 cycles per chain step; profiles/r04zz_port_onewait.log)
+// (6.07 cycles per chain step; profiles/r04zz_port_onewait.log); with it, 4 producer waves (3.83 ms) and 3
+// tiles of loads in flight (3.56) lose to the default's 3.51 (profiles/r04zz_port_producers.log)
 constexpr PnFn kPnDefault = &launch_pn<8, 2, true, 8192, 2>;
 #ifdef PLATO_AGG_TUNE
 // The round-3 sweep (1-8 producer waves x 2-4 tiles in flight, plain or non-temporal flat stores;
