@@ -88,8 +88,9 @@ class ArenaLayout:
         self.n_f32 = n_f32  # fp32 region length, padding included
         self.n_i64 = n_i64
         self.align = align
-        # model elements of the fp32 region (algorithmic bytes count these, not the padding)
-        self.n_f32_data = sum(e.numel for e in entries if e.region == F32)
+        # model elements of the fp32 region (algorithmic bytes count these, not the padding); a raw
+        # arena without an entry map (bench pieces, distributed buckets) is all data
+        self.n_f32_data = sum(e.numel for e in entries if e.region == F32) if entries else n_f32
         self.row_f32 = _round_up(max(n_f32, 1), ROW_ALIGN)
         self.row_i64 = max(n_i64, 1)
         self._by_name = {e.name: e for e in entries}

@@ -87,6 +87,27 @@ def test_gloo_piece_sharding_bit_exact(tmp_path, world):
     assert all(o["bit_exact"] for o in outs)
 
 
+@pytest.mark.parametrize("world,pieces", [(2, 4), (8, 4)])
+def test_piece_layouts_count_their_bytes(world, pieces):
+    """bench.py's per-rank piece layouts (entry-less arenas) count every element as model data, so a
+    rank's algorithmic bytes sum to the job's (the N > 1 roofline's numerator)."""
+    from plato_amd import workloads
+    from plato_amd.arena import ArenaLayout
+    from plato_amd.distributed import PiecePlan
+
+    full = ArenaLayout.from_shapes(workloads.resnet(18, 10))
+    plan = PiecePlan.for_layout(full, world, pieces)
+    k = 128
+    total = 0
+    for r in range(world):
+        lays = [ArenaLayout([], plan.piece_elements(r, p), full.n_i64 if (p == 0 and r == 0) else 0)
+                for p in range(pieces)]
+        got = sum(lay.algorithmic_bytes(k) for lay in lays)
+        assert got > 0
+        total += got
+    assert total == full.algorithmic_bytes(k)
+
+
 @pytest.mark.parametrize("n_f32,world,pieces", [(61706, 2, 4), (11183562, 8, 4), (100, 8, 3), (0, 2, 2)])
 def test_piece_plan_covers_arena_once(n_f32, world, pieces):
     from plato_amd.distributed import PiecePlan
