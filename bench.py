@@ -57,9 +57,18 @@ def parse():
                    help="also time arrival staging and the trigger-to-result latency (C4, examples/async)")
     p.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                    help="strong: one job bucket-sharded over the ranks (+ all-gather); weak: a job per rank")
-    p.add_argument("--pieces", type=int, default=4,
+    p.add_argument("--pieces", type=int, default=None,
                    help="strong scaling, N>1: each rank's bucket in this many pieces, the all-gather of "
-                        "piece p running on RCCL's stream while the kernels of the later pieces run")
+                        "piece p running on RCCL's stream while the kernels of the later pieces run "
+                        "(default: PIECES_BY_WORLD, chosen from the one-GPU anchor, DESIGN.md §6)")
+    p.add_argument("--anchor", action="store_true",
+                   help="one process, one GPU, no collective: time one rank's piece kernels for N = 1, 2, 4, 8 "
+                        "(C2 and C3) and the grid-tail shapes of the headline kernel; JSON lines, not the metric")
+    p.add_argument("--client-split", action="store_true",
+                   help="with --engine-devices N: also time the client-split round (FedAdp / Port over N devices): "
+                        "the assembly of each device's client arenas, and FedAdp's dots")
+    p.add_argument("--probe-launch", action="store_true",
+                   help="launcher check without a GPU: every rank joins a gloo group, rank 0 prints one JSON line")
     p.add_argument("--no-variants", action="store_true",
                    help="skip the variant servers' reductions leg (SURVEY.md §8(f), N=1 only)")
     p.add_argument("--variant-reps", type=int, default=5)
@@ -92,6 +101,51 @@ def model_spec(name):
         "vit_large": lambda: workloads.vit_large(),
         "gpt2_medium": lambda: workloads.gpt2_medium(),
     }[name]()
+
+
+def self_launch(n: int, argv: list[str]) -> int:
+    """``bench.py --gpus N`` started plainly: run it under torch.distributed.run, one rank per GPU.
+
+    Called before anything touches the GPU (no torch.cuda call in this process): the N ranks are
+    a child process tree (never an exec of this one).  Rank 0's JSON line is forwarded to this
+    process's stdout; anything else the child writes on stdout goes to stderr, so the result line
+    stays the only stdout line.  Returns the child's exit code.
+    """
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
+    progress(f"--gpus {n} without a torch.distributed world: launching {n} ranks (port {port})")
+    child = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in child.stdout:
+        if line.startswith("{"):
+            sys.stdout.write(line)
+            sys.stdout.flush()
+        else:
+            sys.stderr.write(line)
+    return child.wait()
+
+
+def probe_launch(args) -> None:
+    """The launcher's plumbing on CPU: every rank joins a gloo group and sums its rank; rank 0 prints."""
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    t = torch.tensor([float(rank)])
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({"probe": "launch", "n_gpus": world, "requested": args.gpus,
+                          "rank_sum": float(t.item())}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def dist_setup(args):
@@ -148,7 +202,7 @@ def kernel_signature(variant: int) -> str:
     f = fl.value
     b = lambda x: "true" if x else "false"  # noqa: E731
     return (f"fedavg_kernel<(anonymous namespace)::Cfg<{bs.value}, {v.value}, {u.value}, {b(f & 1)}, {b(f & 2)}, "
-            f"{b(f & 4)}, {b(f & 8)}, {(f >> 4) & 255}, {b(f & (1 << 12))}>, true, false>")
+            f"{b(f & 4)}, {b(f & 8)}, {(f >> 4) & 255}, {b(f & (1 << 12))}, {b(f & (1 << 13))}>, true, false>")
 
 
 def source_stamp() -> str:
@@ -251,6 +305,12 @@ def cpu_model():
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args.gpus, sys.argv[1:]))
+    if args.probe_launch:
+        return probe_launch(args)
+    if args.anchor:
+        return anchor_bench(args)
     world, rank, local = dist_setup(args)
     dev = torch.device("cuda", local)
 
@@ -273,7 +333,9 @@ def main():
         # the model and one all-gather per p assembles them in place
         from plato_amd.distributed import PiecePlan
 
-        pieces = max(1, args.pieces)
+        pieces = max(1, args.pieces or pieces_for(args.config, world))
+        progress(f"rank {rank}: {pieces} pieces per rank "
+                 + ("(--pieces)" if args.pieces else "(PIECES_BY_WORLD, from the one-GPU anchor)"))
         plan = PiecePlan.for_layout(full_layout, world, pieces)
         piece_n = [plan.piece_elements(rank, p) for p in range(pieces)]
         n_i64_loc = full_layout.n_i64 if rank == 0 else 0
@@ -726,6 +788,126 @@ def variant_legs(dev, k: int, reps: int) -> dict:
     return out
 
 
+# Strong scaling, N > 1: pieces per rank, chosen from the one-GPU anchor (``--anchor``).
+# More pieces overlap more of the all-gather with the kernels but make each piece kernel smaller.
+# C2: pieces=1 kernels are the fastest at every N (profiles/r05a_anchor.log: N8 0.138 ms vs 0.189 ms in 4
+# pieces), but the all-gather then runs wholly exposed; with RCCL's all-gather at ~330 GB/s bus bandwidth
+# on the 8-GPU mesh (one ~76 GB/s link between 2 GPUs) the sum kernel + exposed gather is smallest at 4
+# pieces for N = 2 and 4 and at 2 for N = 8.  C3's rank kernels are flat in the
+# piece count (ms-long), so its 84 MB gathers take 4.
+PIECES_BY_WORLD = {"C2": {2: 4, 4: 4, 8: 2}, "C3": {2: 4, 4: 4, 8: 4}}
+
+
+def pieces_for(config: str, world: int) -> int:
+    table = PIECES_BY_WORLD.get(config, PIECES_BY_WORLD["C2"])
+    return table.get(world, table[max(table)])
+
+
+def anchor_bench(args):
+    """One rank's share of the strong-scaling job, timed on ONE GPU with no collective.
+
+    For C2 and C3 and N = 1, 2, 4, 8 with 1, 2, 4, 8 pieces per rank: rank 0's pieces (the largest
+    rank: it also carries the int64 entries) are launched back to back on one stream, exactly as
+    ``main`` launches them at N > 1, over a slab laid out as the rank's (rows of pieces x piece
+    length); HIP events around each piece and around the rank's whole step.  Also the headline
+    kernel on C2-like arenas whose grids are 2 to 12 resident rounds (the grid-tail study of
+    DESIGN.md §4).  Kernel variants from libplato_agg_tune.so (``--variant`` picks one), median of
+    ``--steps`` interleaved repetitions.  Prints JSON lines; the all-gather a rank would add is
+    reported as bytes (RCCL needs N distinct GPUs).
+    """
+    from plato_amd import _lib
+    from plato_amd.arena import ArenaLayout
+    from plato_amd.distributed import PiecePlan
+
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    stream = torch.cuda.current_stream(dev)
+    nv = _lib.tune().plato_agg_tune_num_variants()
+    variants = [args.variant] if args.variant is not None else [v for v in (0, 5, 7, 9, 10, 11) if v < nv]
+    reps = max(3, args.steps)
+
+    def describe(v):
+        import ctypes
+
+        bs, a, b, c = ctypes.c_int(), ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _lib.tune().plato_agg_tune_describe(v, ctypes.byref(bs), ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return {"B": bs.value, "V": a.value, "U": b.value, "persist": (c.value >> 4) & 255,
+                "balanced": bool(c.value >> 13 & 1)}
+
+    def run_shapes(label, k, shapes, row):
+        """shapes: [(name, [(piece offset in the row, fp32 elements, int64 entries)], extra)] over one slab."""
+        slab = torch.empty((k, row), dtype=torch.float32, device=dev)
+        slab.uniform_(-1.0, 1.0)
+        slab_i = torch.zeros((k, 64), dtype=torch.int64, device=dev)
+        base = torch.empty(row, dtype=torch.float32, device=dev).uniform_(-1.0, 1.0)
+        base_i = torch.zeros(64, dtype=torch.int64, device=dev)
+        out = torch.empty(row, dtype=torch.float32, device=dev)
+        out_i = torch.empty(64, dtype=torch.float32, device=dev)
+        w = torch.full((k,), 1.0 / k, dtype=torch.float32, device=dev)
+        rows = slab.data_ptr() + np.arange(k, dtype=np.int64) * row * 4
+        ti = torch.from_numpy(slab_i.data_ptr() + np.arange(k, dtype=np.int64) * 64 * 8).to(dev)
+        tables = {}
+
+        def launch(v, pieces):
+            for off, n, ni in pieces:
+                tf = tables.setdefault(off, torch.from_numpy(rows + off * 4).to(dev))
+                _lib.tune_call("plato_agg_tune_fedavg", v, 1, tf.data_ptr(), ti.data_ptr() if ni else None,
+                               w.data_ptr(), None, k, base.data_ptr() + off * 4, base_i.data_ptr() if ni else None,
+                               out.data_ptr() + off * 4, out_i.data_ptr() if ni else None, n, ni, stream.cuda_stream)
+
+        for name, pieces, extra in shapes:
+            nbytes = sum((k + 2) * (n * 4 + ni * 8) for _, n, ni in pieces)
+            times = {v: [] for v in variants}
+            for v in variants:
+                launch(v, pieces)
+            torch.cuda.synchronize(dev)
+            for _ in range(reps):
+                for v in variants:
+                    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    e0.record(stream)
+                    launch(v, pieces)
+                    e1.record(stream)
+                    e1.synchronize()
+                    times[v].append(e0.elapsed_time(e1))
+            for v in variants:
+                med = statistics.median(times[v])
+                print(json.dumps({"anchor": label, "shape": name, "clients": k, "variant": v, **describe(v),
+                                  "piece_elements": [n for _, n, _ in pieces], "algorithmic_bytes": nbytes,
+                                  "kernel_ms": round(med, 4), "kernel_ms_min": round(min(times[v]), 4),
+                                  "GBps": round(nbytes / (med * 1e-3) / 1e9, 1),
+                                  "frac": round(nbytes / (med * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), **extra}),
+                      flush=True)
+        del slab, slab_i, base, out
+        torch.cuda.empty_cache()
+
+    # grid-tail study: C2's K on arenas of r resident rounds (256 CUs x 8 workgroups of 1,024 elements)
+    per_round = 2048 * 1024
+    c2 = ArenaLayout.from_shapes(model_spec("resnet18"))
+    rounds = [2, 4, 5, c2.n_f32 / per_round, 5.5, 6, 8, 12]
+    shapes = [(f"rounds_{r:.3f}", [(0, int(r * per_round) // 64 * 64, 0)], {"rounds": round(r, 3)}) for r in rounds]
+    run_shapes("grid_tail", 128, shapes, max(n for _, ((_, n, _),), _ in shapes))
+
+    # one rank's pieces at N GPUs (rank 0: the largest bucket, with the int64 entries)
+    for config in ("C2", "C3"):
+        model, k = CONFIGS[config]
+        full = ArenaLayout.from_shapes(model_spec(model))
+        shapes, row = [], 0
+        for world in (1, 2, 4, 8):
+            for pieces in ((1,) if world == 1 else (1, 2, 4, 8)):
+                plan = PiecePlan.for_layout(full, world, pieces)
+                L = plan.length
+                ps = [(p * L, plan.piece_elements(0, p), full.n_i64 if p == 0 else 0) for p in range(pieces)]
+                ps = [x for x in ps if x[1] or x[2]]
+                row = max(row, pieces * L)
+                gather = world * (pieces * L + 64) * 4
+                shapes.append((f"N{world}_p{pieces}", ps, {
+                    "world": world, "pieces": pieces, "config": config,
+                    "job_bytes": full.algorithmic_bytes(k),
+                    "allgather_bytes_received_per_rank": (world - 1) * gather // world if world > 1 else 0}))
+        progress(f"anchor {config}: {len(shapes)} layouts, slab {k} x {row} fp32 ({k * row * 4 / 1e9:.1f} GB)")
+        run_shapes(config, k, shapes, row)
+
+
 def engine_devices_bench(args):
     """The server's own multi-GPU path in one process (plato_amd.multi.MultiDeviceEngine).
 
@@ -794,8 +976,50 @@ def engine_devices_bench(args):
         "device_resident_gathered": {"GBps": round(bytes_ / med(gath) / 1e9, 1), "ms": round(med(gath) * 1e3, 3)},
         "note": "median over --steps rounds after --warmup; repeated devices share one GPU",
     }
+    if args.client_split:
+        out["client_split"] = client_split_leg(eng, baseline, payloads, k, args.steps)
     print(json.dumps(out), flush=True)
     eng.close()
+
+
+def client_split_leg(eng, baseline, payloads, k: int, reps: int) -> dict:
+    """FedAdp over the multi engine's devices split by client (``ClientRound``): the asynchronous assembly of
+    each device's client arenas from the bucket shards, then the global gradient and the dots."""
+    asm_wall, asm_dev, dots = [], [], []
+    w1 = None
+    for r in range(reps + 1):
+        rnd = eng.clients.begin(baseline, k)
+        rnd.put_baseline(baseline)
+        for slot, p in enumerate(payloads):
+            rnd.put_client(slot, p)
+        for d in dict.fromkeys(eng.devices):
+            torch.cuda.synchronize(d)
+        t0 = time.perf_counter()
+        rnd._client_rounds()
+        for d in dict.fromkeys(eng.devices):
+            torch.cuda.synchronize(d)
+        t1 = time.perf_counter()
+        rnd._resolve_assembly()
+        if w1 is None:
+            w1 = np.full((len(rnd.layout.entries), k), 1.0 / k)
+        t2 = time.perf_counter()
+        grads = rnd.launch_entrywise(w1, add_base=False, device=True)
+        rnd.fedadp_dots(grads, list(range(k)), 0.01)
+        t3 = time.perf_counter()
+        if r:
+            asm_wall.append((t1 - t0) * 1e3)
+            asm_dev.append(rnd.timings["client_assembly_ms"])
+            dots.append((t3 - t2) * 1e3)
+        del rnd
+    per_dev = eng.world
+    moved = sum(p_.numel() * p_.element_size() for p_ in payloads[0].values()) * k
+    med = statistics.median
+    return {"clients": k, "devices": per_dev, "client_bytes_moved": moved,
+            "client_assembly_ms": round(med(asm_dev), 3), "client_assembly_wall_ms": round(med(asm_wall), 3),
+            "client_assembly_GBps": round(moved / (med(asm_dev) * 1e-3) / 1e9, 1),
+            "fedadp_entrywise_and_dots_wall_ms": round(med(dots), 3),
+            "note": "one strided device-to-device copy per (device, bucket); repeated devices share one GPU, so the "
+                    "copies are HBM-to-HBM on it (xGMI on a real node); median of --steps after one warm-up"}
 
 
 def _host_state_dicts(layout, base, slab, k):

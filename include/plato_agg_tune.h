@@ -37,7 +37,8 @@ void plato_agg_tune_set_launch_groups(uint64_t groups);
  * batch) and flags: bit 0 non-temporal loads, bit 1 non-temporal stores,
  * bit 2 software-pipelined batches, bit 3 buffer loads, bits 4..11 persistent
  * workgroups per CU (0 = one workgroup per chunk), bit 12 XCD-contiguous chunk
- * order (each of the 8 XCDs streams one contiguous eighth of the arena). */
+ * order (each of the 8 XCDs streams one contiguous eighth of the arena), bit 13
+ * balanced grid (occupancy x CUs workgroups, one equal contiguous share each). */
 int plato_agg_tune_describe(int variant, int* block, int* v, int* u, int* flags);
 
 /* has_base != 0: plato_agg_fedavg_weights; == 0: plato_agg_fedavg_deltas. */

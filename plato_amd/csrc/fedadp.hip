@@ -662,6 +662,9 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
   if (n_flat == 0 || n_flat >= (size_t(1) << 30)) return set_error(PLATO_AGG_EINVAL, "flat length must be in [1, 2^30)");
   if (n_f32 >= (size_t(1) << 30)) return set_error(PLATO_AGG_EINVAL, "fp32 arena must be < 2^30 elements");
   if (n_i64 >= (size_t(1) << 30)) return set_error(PLATO_AGG_EINVAL, "int64 region must be < 2^30 elements");
+  // boundary-table rows are 1 KiB, addressed by 32-bit byte offsets within a pair's table (adp_issue)
+  if (adp_max_bnd(n_segs, n_i64) >= (size_t(1) << 22))
+    return set_error(PLATO_AGG_EINVAL, "boundary table needs >= 2^22 rows (too many segments / int64 entries)");
   const AdpWs w = adp_ws(n_pairs, with_xx, n_i64, n_flat, n_segs);
   char* ws = static_cast<char*>(d_workspace);
   AdpArgs a{};

@@ -130,6 +130,7 @@ struct AggArgs {
   uint32_t nb_vec_full;        // of which fully in range (no bounds checks)
   uint32_t nb_grid;            // PERSIST: workgroups striding over the chunks; XCD: vector blocks in the grid
   uint32_t xcd_per;            // XCD: chunks per XCD (contiguous range)
+  uint32_t nb_scalar;          // workgroups of scalar items: the FIRST blocks of the grid
   uint64_t x_off;              // element offset of this launch's range in every client arena
   int K;
 };
@@ -143,13 +144,16 @@ struct AggArgs {
 //            over the chunks (grid = min(chunks, 256*N))
 //   XCD   workgroups are dealt to the 8 XCDs round-robin by blockIdx; remap so
 //         that each XCD streams one contiguous eighth of the arena
+//   BAL   balanced grid: as many workgroups as the chip holds at once (occupancy x CUs), each
+//         owning one contiguous, equal share of the f4 groups, so every workgroup finishes at the
+//         same time instead of a partial last round draining on part of the chip
 template <int B_, int V_, int U_, bool NTL_, bool NTS_, bool PIPE_, bool BUF_ = false, int PERSIST_ = 0,
-          bool XCD_ = false>
+          bool XCD_ = false, bool BAL_ = false>
 struct Cfg {
   static constexpr int B = B_, V = V_, U = U_;
   static constexpr bool NTL = NTL_, NTS = NTS_, PIPE = PIPE_, BUF = BUF_;
   static constexpr int PERSIST = PERSIST_;
-  static constexpr bool XCD = XCD_;
+  static constexpr bool XCD = XCD_, BAL = BAL_;
 };
 
 template <bool NT>
@@ -207,11 +211,12 @@ __device__ __forceinline__ void load_batch(f4 (&x)[C::U][C::V], const AggArgs& a
   }
 }
 
+// The lanes of one workgroup own f4 groups g0 + threadIdx.x + v*B (v < V); groups at or past `lim`
+// (CHECK only) are clamped loads with no store.
 template <class C, bool HAS_BASE, bool TWO, bool CHECK>
-__device__ __forceinline__ void vec_body(const AggArgs& a, uint32_t blk) {
+__device__ __forceinline__ void vec_at(const AggArgs& a, uint64_t g0, uint64_t lim) {
   constexpr int V = C::V, U = C::U;
-  constexpr uint64_t kChunk = uint64_t(C::B) * V;
-  const uint64_t first = uint64_t(blk) * kChunk + threadIdx.x;
+  const uint64_t first = g0 + threadIdx.x;
 
   // Element groups this lane owns, as 32-bit byte offsets (host guarantees an
   // fp32 arena < 4 GiB per launch).  In the (single) partial workgroup the
@@ -225,8 +230,8 @@ __device__ __forceinline__ void vec_body(const AggArgs& a, uint32_t blk) {
 #pragma unroll
   for (int v = 0; v < V; ++v) {
     const uint64_t e = first + uint64_t(v) * C::B;
-    live[v] = !CHECK || e < a.n4;
-    off[v] = uint32_t((CHECK ? (e < a.n4 ? e : a.n4 - 1) : e) * 16u);
+    live[v] = !CHECK || e < lim;
+    off[v] = uint32_t((CHECK ? (e < lim ? e : lim - 1) : e) * 16u);
     acc[v] = f4_zero();
     b[v] = HAS_BASE ? ld4_off<false>(a.base_f, off[v]) : f4_zero();
   }
@@ -275,7 +280,17 @@ __device__ __forceinline__ void vec_body(const AggArgs& a, uint32_t blk) {
   }
 }
 
-// One scalar work item: the fp32 tail element or an int64 entry.
+template <class C, bool HAS_BASE, bool TWO, bool CHECK>
+__device__ __forceinline__ void vec_body(const AggArgs& a, uint32_t blk) {
+  vec_at<C, HAS_BASE, TWO, CHECK>(a, uint64_t(blk) * (uint64_t(C::B) * C::V), a.n4);
+}
+
+// One scalar work item: the fp32 tail element or an int64 entry.  These lanes walk the same K clients
+// as the vector lanes, so their loads are batched kSU clients at a time (kSU independent loads in
+// flight, then the in-order adds): a one-load-at-a-time walk is K round trips to HBM under the full
+// stream's queueing, which outlasted the vector part of the grid (C2: +23 us per launch).
+constexpr int kSU = 16;
+
 template <bool HAS_BASE, bool TWO>
 __device__ __forceinline__ void scalar_item(const AggArgs& a, uint64_t j) {
   const uint64_t tail = a.n_f32 - 4 * a.n4;
@@ -284,8 +299,21 @@ __device__ __forceinline__ void scalar_item(const AggArgs& a, uint64_t j) {
     const uint64_t e = 4 * a.n4 + j;
     const float b = HAS_BASE ? a.base_f[e] : 0.f;
     float acc = 0.f;
-    for (int i = 0; i < K; ++i) {
-      const float x = sld(a.xf, i)[a.x_off + e];
+    int i = 0;
+    for (; i + kSU <= K; i += kSU) {
+      float x[kSU];
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) x[u] = ((gfloat*)(sld(a.xf, i + u) + a.x_off))[e];
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) {
+        const float d = HAS_BASE ? x[u] - b : x[u];
+        float t = d * sld(a.w, i + u);
+        if constexpr (TWO) t = t * sld(a.s, i + u);
+        acc = acc + t;
+      }
+    }
+    for (; i < K; ++i) {
+      const float x = ((gfloat*)(sld(a.xf, i) + a.x_off))[e];
       const float d = HAS_BASE ? x - b : x;
       float t = d * sld(a.w, i);
       if constexpr (TWO) t = t * sld(a.s, i);
@@ -296,12 +324,26 @@ __device__ __forceinline__ void scalar_item(const AggArgs& a, uint64_t j) {
   }
   const uint64_t e = j - tail;
   if (e >= a.n_i64) return;
+  typedef __attribute__((address_space(1))) const int64_t gi64;
   const int64_t b = HAS_BASE ? a.base_i[e] : 0;
   float acc = 0.f;
-  for (int i = 0; i < K; ++i) {
-    const int64_t x = sld(a.xi, i)[e];
-    // int64 subtraction wraps like torch's; the promotion to fp32 happens at
-    // the scalar multiply (servers/fedavg.py:154, int tensor * Python float).
+  // int64 subtraction wraps like torch's; the promotion to fp32 happens at the scalar multiply
+  // (servers/fedavg.py:154, int tensor * Python float).
+  int i = 0;
+  for (; i + kSU <= K; i += kSU) {
+    int64_t x[kSU];
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) x[u] = ((gi64*)sld(a.xi, i + u))[e];
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) {
+      const int64_t d = HAS_BASE ? (int64_t)((uint64_t)x[u] - (uint64_t)b) : x[u];
+      float t = (float)d * sld(a.w, i + u);
+      if constexpr (TWO) t = t * sld(a.s, i + u);
+      acc = acc + t;
+    }
+  }
+  for (; i < K; ++i) {
+    const int64_t x = ((gi64*)sld(a.xi, i))[e];
     const int64_t d = HAS_BASE ? (int64_t)((uint64_t)x - (uint64_t)b) : x;
     float t = (float)d * sld(a.w, i);
     if constexpr (TWO) t = t * sld(a.s, i);
@@ -313,8 +355,28 @@ __device__ __forceinline__ void scalar_item(const AggArgs& a, uint64_t j) {
 
 template <class C, bool HAS_BASE, bool TWO>
 __global__ __launch_bounds__(C::B) void fedavg_kernel(AggArgs a) {
-  const uint32_t blk = blockIdx.x;
-  if constexpr (C::XCD) {
+  // the scalar items (fp32 tail, int64 entries) are the first blocks: dispatched first, they run beside
+  // the stream from its start instead of after its last round
+  if (blockIdx.x < a.nb_scalar) {
+    scalar_item<HAS_BASE, TWO>(a, uint64_t(blockIdx.x) * C::B + threadIdx.x);
+    return;
+  }
+  const uint32_t blk = blockIdx.x - a.nb_scalar;
+  if constexpr (C::BAL) {
+    if (blk < a.nb_grid) {
+      // workgroup blk owns f4 groups [lo, hi): equal shares (to one group) of the arena
+      const uint64_t lo = uint64_t(blk) * a.n4 / a.nb_grid;
+      const uint64_t hi = uint64_t(blk + 1) * a.n4 / a.nb_grid;
+      constexpr uint64_t kChunk = uint64_t(C::B) * C::V;
+      for (uint64_t g0 = lo; g0 < hi; g0 += kChunk) {
+        if (g0 + kChunk <= hi) {
+          vec_at<C, HAS_BASE, TWO, false>(a, g0, hi);
+        } else {
+          vec_at<C, HAS_BASE, TWO, true>(a, g0, hi);
+        }
+      }
+    }
+  } else if constexpr (C::XCD) {
     if (blk < a.nb_grid) {
       const uint32_t c = (blk % 8) * a.xcd_per + blk / 8;
       if (c < a.nb_vec_full) {
@@ -322,12 +384,9 @@ __global__ __launch_bounds__(C::B) void fedavg_kernel(AggArgs a) {
       } else if (c < a.nb_vec) {
         vec_body<C, HAS_BASE, TWO, true>(a, c);
       }
-    } else {
-      const uint64_t j = uint64_t(blk - a.nb_grid) * C::B + threadIdx.x;
-      scalar_item<HAS_BASE, TWO>(a, j);
     }
   } else if constexpr (C::PERSIST > 0) {
-    // a.nb_grid workgroups stride over the nb_vec chunks; the rest do scalars
+    // a.nb_grid workgroups stride over the nb_vec chunks
     if (blk < a.nb_grid) {
       for (uint32_t c = blk; c < a.nb_vec; c += a.nb_grid) {
         if (c < a.nb_vec_full) {
@@ -336,18 +395,12 @@ __global__ __launch_bounds__(C::B) void fedavg_kernel(AggArgs a) {
           vec_body<C, HAS_BASE, TWO, true>(a, c);
         }
       }
-    } else {
-      const uint64_t j = uint64_t(blk - a.nb_grid) * C::B + threadIdx.x;
-      scalar_item<HAS_BASE, TWO>(a, j);
     }
   } else {
     if (blk < a.nb_vec_full) {
       vec_body<C, HAS_BASE, TWO, false>(a, blk);
     } else if (blk < a.nb_vec) {
       vec_body<C, HAS_BASE, TWO, true>(a, blk);
-    } else {
-      const uint64_t j = uint64_t(blk - a.nb_vec) * C::B + threadIdx.x;
-      scalar_item<HAS_BASE, TWO>(a, j);
     }
   }
 }
@@ -359,6 +412,21 @@ using LaunchFn = void (*)(const AggArgs&, dim3, hipStream_t);
 
 template <class C, bool HAS_BASE, bool TWO>
 void launch_one(const AggArgs& a, dim3 grid, hipStream_t st) {
+  if constexpr (C::BAL) {
+    // the grid the chip holds at once: occupancy of this instantiation x CUs (queried once)
+    static int resident = [] {
+      int per_cu = 0, cus = 0, dev = 0;
+      const bool ok = hipGetDevice(&dev) == hipSuccess &&
+                      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
+                      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fedavg_kernel<C, HAS_BASE, TWO>, C::B,
+                                                                   0) == hipSuccess;
+      return ok && per_cu > 0 && cus > 0 ? per_cu * cus : 2048;
+    }();
+    AggArgs b = a;
+    b.nb_grid = a.nb_vec < uint32_t(resident) ? a.nb_vec : uint32_t(resident);
+    hipLaunchKernelGGL((fedavg_kernel<C, HAS_BASE, TWO>), dim3(b.nb_grid + a.nb_scalar), dim3(C::B), 0, st, b);
+    return;
+  }
   hipLaunchKernelGGL((fedavg_kernel<C, HAS_BASE, TWO>), grid, dim3(C::B), 0, st, a);
 }
 
@@ -366,13 +434,13 @@ struct Variant {
   int B, V, U;
   bool NTL, NTS, PIPE, BUF;
   int PERSIST;
-  bool XCD;
+  bool XCD, BAL;
   LaunchFn fn[2][2];  // [HAS_BASE][TWO]
 };
 
 template <class C>
 constexpr Variant make_variant() {
-  return Variant{C::B, C::V, C::U, C::NTL, C::NTS, C::PIPE, C::BUF, C::PERSIST, C::XCD,
+  return Variant{C::B, C::V, C::U, C::NTL, C::NTS, C::PIPE, C::BUF, C::PERSIST, C::XCD, C::BAL,
                  {{&launch_one<C, false, false>, &launch_one<C, false, true>},
                   {&launch_one<C, true, false>, &launch_one<C, true, true>}}};
 }
@@ -390,6 +458,11 @@ const Variant kVariants[] = {
     make_variant<Cfg<256, 1, 8, true, true, false, true>>(),             // 4 buffer loads (nt)
     make_variant<Cfg<256, 1, 8, true, true, false, false, 8>>(),         // 5 persistent 8/CU
     make_variant<Cfg<256, 1, 8, true, true, false, false, 0, true>>(),   // 6 XCD-contiguous chunks
+    make_variant<Cfg<256, 1, 16, true, true, false>>(),                  // 7 16 clients per batch
+    make_variant<Cfg<256, 1, 32, true, true, false>>(),                  // 8 32 clients per batch
+    make_variant<Cfg<256, 1, 8, true, true, false, false, 0, false, true>>(),   // 9 balanced grid
+    make_variant<Cfg<256, 1, 16, true, true, false, false, 0, false, true>>(),  // 10 balanced, U=16
+    make_variant<Cfg<64, 1, 8, true, true, false>>(),                    // 11 one wave per workgroup
 };
 #else  // libplato_agg.so: the default only
 const Variant kVariants[] = {
@@ -482,6 +555,7 @@ int run_agg_range(const Variant& vr, bool has_base, const float* const* xf, cons
     const uint64_t cap = uint64_t(256) * vr.PERSIST;  // 256 CUs on MI355X
     a.nb_grid = uint32_t(nb_vec < cap ? nb_vec : cap);
   }
+  a.nb_scalar = uint32_t(nb_scalar);
   dim3 grid(uint32_t(a.nb_grid + nb_scalar));
   vr.fn[has_base ? 1 : 0][s ? 1 : 0](a, grid, st);
   return check_launch("fedavg kernel launch");
@@ -1142,7 +1216,7 @@ int plato_agg_tune_describe(int variant, int* block, int* v, int* u, int* flags)
   *v = vr.V;
   *u = vr.U;
   *flags = (vr.NTL ? 1 : 0) | (vr.NTS ? 2 : 0) | (vr.PIPE ? 4 : 0) | (vr.BUF ? 8 : 0) | (vr.PERSIST << 4) |
-           (vr.XCD ? 1 << 12 : 0);
+           (vr.XCD ? 1 << 12 : 0) | (vr.BAL ? 1 << 13 : 0);
   return PLATO_AGG_OK;
 }
 

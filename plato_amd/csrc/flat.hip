@@ -1232,6 +1232,57 @@ __global__ __launch_bounds__(256) void np_sumsq_half_kernel(SumsqArgs a) {
   }
 }
 
+// np_sumsq_half_kernel with 16-byte loads and stores: lane tid holds elements q * 1,024 + 4 tid .. + 3
+// (q < 8) of the chunk, x read non-temporally, and stages its 4 squares with one ds_write_b128 (4
+// consecutive elements never cross a 128-element leaf, and the padded layout keeps them 16-byte
+// aligned).  A quarter of the load and LDS-write instructions of the dword form; the same leaves, the
+// same accumulators, the same order.
+typedef __attribute__((address_space(1))) const f4 gcf4;
+__global__ __launch_bounds__(256) void np_sumsq_half4_kernel(SumsqArgs a) {
+  __shared__ __attribute__((aligned(16))) float sq[kNpBuf / kPW / 2 * kLeafPitch];
+  __shared__ float leaf_sum[kNpBuf / kPW];
+  const NpTask t = np_task(a, blockIdx.x);
+  if (t.n != kNpBuf) return;  // workgroup-uniform
+  constexpr int kQ = int(kNpBuf / 1024), kHalfQ = kQ / 2;
+  const int tid = int(threadIdx.x);
+  f4 xv[kQ], bv[kQ];
+  const gcf4* x = (const gcf4*)(a.x[t.k] + t.begin) + tid;
+  const gcf4* b = (const gcf4*)(a.base + t.begin) + tid;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+    xv[q] = __builtin_nontemporal_load(x + q * 256);
+    bv[q] = b[q * 256];
+  }
+  const int leaf = tid >> 3, j = tid & 7;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    if (h) __syncthreads();  // the first half's leaf reads are done
+#pragma unroll
+    for (int q = 0; q < kHalfQ; ++q) {
+      const uint32_t i = uint32_t(q * 1024 + 4 * tid);  // element h * 4096 + i
+      const f4 d = xv[h * kHalfQ + q] - bv[h * kHalfQ + q];
+      *reinterpret_cast<f4*>(sq + np_pad8(i)) = d * d;
+    }
+    __syncthreads();
+    // 32 leaves x 8 accumulators = the 256 threads
+    const float* l = sq + leaf * kLeafPitch + j;
+    float r = l[0];
+#pragma unroll
+    for (int i = 8; i < kPW; i += 8) r += l[i];
+    r = r + __shfl_xor(r, 1);
+    r = r + __shfl_xor(r, 2);
+    r = r + __shfl_xor(r, 4);
+    if (j == 0) leaf_sum[h * 32 + leaf] = r;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float s = leaf_sum[tid];
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) s = s + __shfl_xor(s, m);
+    if (tid == 0) a.chunk_sums[uint64_t(t.k) * a.n_chunks + t.c] = s;
+  }
+}
+
 // The partial last chunk of every (piece, client), through the full-staging path.
 __global__ __launch_bounds__(256) void np_sumsq_tail_kernel(SumsqArgs a) {
   __shared__ float sq[kNpBuf / kPW * kLeafPitch];
@@ -1261,7 +1312,8 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
 // workgroups per CU instead of four; 1.25 against 1.39 ms interleaved) plus the partial last chunks
 // (np_sumsq_tail_kernel); 1: the round-2 form (np_sumsq_chunks_lds_kernel, client-major, four memory
 // round trips per workgroup); 2, 3: timing probes of variant 4 (wrong results by design: no baseline
-// loads / no LDS phase); 4: the round-3 default (np_sumsq_chunks_v2_kernel, every chunk staged whole).
+// loads / no LDS phase); 4: the round-3 default (np_sumsq_chunks_v2_kernel, every chunk staged whole);
+// 5: variant 0 with 16-byte loads and LDS writes (np_sumsq_half4_kernel).
 // G clients per workgroup sharing the baseline (4.1-5.9 ms) were dropped after round 3; a persistent
 // software-pipelined form (2.9 ms: its two register sets left one workgroup per CU), 512 / 1,024
 // threads per chunk (1.70 / 2.79 ms against 1.38) and an LDS-free form loading each accumulator's
@@ -1277,12 +1329,15 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256, 2>), grid, dim3(256), 0, st, a);
   } else if (variant == 4) {
     hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256>), grid, dim3(256), 0, st, a);
+  } else if (variant == 5) {
+    hipLaunchKernelGGL(np_sumsq_half4_kernel, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   } else {
     hipLaunchKernelGGL(np_sumsq_half_kernel, grid, dim3(256), 0, st, a);
     hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   }
 }
-[[maybe_unused]] constexpr int kNumSumsqVariants = 5;
+[[maybe_unused]] constexpr int kNumSumsqVariants = 6;
 constexpr int kSumsqDefault = 0;  // half-staged + tail: 1.25 ms vs 1.39 (variant 4) on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,

@@ -1079,7 +1079,8 @@ class AggregationRound:
         segs, n_flat = self._flat_segments(order, True)
         # plato_agg_fedadp_dots' limits (csrc/fedadp.hip run_fedadp); beyond them the round-2 path
         if (len(order) >= self.FEDADP_MAX_SEGS or n_flat >= 1 << 30 or lay.n_f32 >= 1 << 30
-                or lay.n_i64 >= 1 << 30 or len(slots) > 65535):
+                or lay.n_i64 >= 1 << 30 or len(slots) > 65535
+                or self.fedadp_boundary_rows(len(order), lay.n_i64) >= self.FEDADP_MAX_BND):
             return self.fedadp_dots_flat(grads, slots, lr)
         stream = torch.cuda.current_stream(eng.device)
         self.stager.fence(stream)
@@ -1193,6 +1194,12 @@ class AggregationRound:
 
     PORT_NORMS_MAX_SEGS = 2048  # csrc/port.hip kMaxSegs
     FEDADP_MAX_SEGS = 1 << 22   # csrc/fedadp.hip run_fedadp
+    FEDADP_MAX_BND = 1 << 22    # boundary-table rows (32-bit byte offsets of 1 KiB rows)
+
+    @staticmethod
+    def fedadp_boundary_rows(n_segs: int, n_i64: int) -> int:
+        """csrc/fedadp.hip adp_max_bnd: boundary-table rows the kernel reserves per pair."""
+        return 2 * (n_segs + n_i64 // 256 + 1)
 
     def model_similarities(self, reference: Mapping[str, torch.Tensor], slots: Sequence[int],
                            eps: float = 1e-8, threads: int | None = None, flat_norms: bool = False) -> list[np.float32]:

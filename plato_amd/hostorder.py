@@ -147,22 +147,27 @@ def host_port_value(models: dict, threads: int) -> np.float32:
 
 
 # ---------------------------------------------------------------- device halves
-def _probe_round(device, models: dict):
-    """A one-client round of the probe model on a private engine (the server's engine keeps its layout)."""
+def _probe_round(device, models: dict, align: str | None = None, port_variant: int | None = None):
+    """A one-client round of the probe model on a private engine (the server's engine keeps its layout).
+
+    ``align`` / ``port_variant``: the server engine's arena alignment and Port kernel shape, so the probe
+    takes the same descriptor / offset path as the rounds (FedAdp's servers run on aligned arenas)."""
     from .engine import FedAvgEngine
 
     eng = FedAvgEngine(device)
+    eng.layout_align = align
+    eng.port_variant = port_variant
     rnd = eng.begin(models["baseline"], 1)
     rnd.put_baseline(models["baseline"])
     rnd.put_client(0, models["client"])
     return rnd
 
 
-def device_fedadp_values(device, models: dict, lr: float) -> np.ndarray:
+def device_fedadp_values(device, models: dict, lr: float, align: str | None = None) -> np.ndarray:
     """The same three dots through ``AggregationRound.fedadp_dots`` (the product's ``plato_agg_fedadp_dots``)."""
     from .arena import F32
 
-    rnd = _probe_round(device, models)
+    rnd = _probe_round(device, models, align)
     lay = rnd.layout
     gf = torch.zeros(lay.row_f32, dtype=torch.float32)
     gi = torch.zeros(max(1, lay.row_i64), dtype=torch.float32)
@@ -174,9 +179,10 @@ def device_fedadp_values(device, models: dict, lr: float) -> np.ndarray:
     return np.asarray([inner[0], l_sq[0], g_sq], dtype=np.float32)
 
 
-def device_port_value(device, models: dict, threads: int) -> np.float32:
+def device_port_value(device, models: dict, threads: int, align: str | None = None,
+                      port_variant: int | None = None) -> np.float32:
     """The cosine through ``AggregationRound.model_similarities`` (port_norms + scale_by_norm + cosine sums)."""
-    rnd = _probe_round(device, models)
+    rnd = _probe_round(device, models, align, port_variant)
     return np.float32(rnd.model_similarities(models["previous"], [0], threads=threads)[0])
 
 
@@ -190,38 +196,40 @@ def _report(key, ok: bool, msg: str, strict: bool) -> bool:
     return ok
 
 
-def check_fedadp(device, lr: float = PROBE_LR, strict: bool = False) -> bool:
-    """True if this host's numpy dots equal the device's bit for bit (checked once per device and lr).
+def check_fedadp(device, lr: float = PROBE_LR, strict: bool = False, align: str | None = None) -> bool:
+    """True if this host's numpy dots equal the device's bit for bit (checked once per device, lr and alignment).
 
-    A mismatch is logged once (``strict``: raises :class:`HostOrderError`).
+    ``align``: the server engine's arena alignment (FedAdp servers use "fedadp").  A mismatch is logged
+    once (``strict``: raises :class:`HostOrderError`).
     """
-    key = ("fedadp", str(device), float(lr))
+    key = ("fedadp", str(device), float(lr), align)
     with _lock:
         if key in _checked and (_checked[key] or not strict):
             return _checked[key]
         models = probe_models(PROBE_N)
         want = host_fedadp_values(models, lr)
-        got = device_fedadp_values(device, models, lr)
+        got = device_fedadp_values(device, models, lr, align)
         msg = ("FedAdp: this host's numpy float32 dot order differs from the one the device reproduces "
                f"(OpenBLAS sdot_k_SKYLAKEX); probe np.inner/dot = {want.tolist()}, device {got.tolist()}. "
                f"{host_description()}. The reference's FedAdp weights on this host would differ in the last bits.")
         return _report(key, want.tobytes() == got.tobytes(), msg, strict)
 
 
-def check_port(device, threads: int, strict: bool = False) -> bool:
+def check_port(device, threads: int, strict: bool = False, align: str | None = None,
+               port_variant: int | None = None) -> bool:
     """True if F.cosine_similarity at ``threads`` equals the device's bit for bit (checked once per device and count).
 
     The probe is long enough (:func:`probe_size`) that ATen splits its sum over all
     ``threads`` chunks, as it does for a real model.  A mismatch is logged once
     (``strict``: raises :class:`HostOrderError`).
     """
-    key = ("port", str(device), int(threads))
+    key = ("port", str(device), int(threads), align, port_variant)
     with _lock:
         if key in _checked and (_checked[key] or not strict):
             return _checked[key]
         models = probe_models(probe_size(threads))
         want = host_port_value(models, threads)
-        got = device_port_value(device, models, threads)
+        got = device_port_value(device, models, threads, align, port_variant)
         msg = (f"Port: this host's F.cosine_similarity order at {threads} threads differs from the one the "
                f"device reproduces (ATen vector_norm + cascade sum); probe {float(want)!r}, device {float(got)!r}. "
                f"{host_description()}. The reference's Port similarities on this host would differ in the last bits.")

@@ -110,6 +110,22 @@ def _row_ptr(t: torch.Tensor, row: int) -> int:
     return t.data_ptr() + row * t.stride(0) * t.element_size()
 
 
+def _copy_rows(dst: torch.Tensor, rows: Sequence[torch.Tensor]) -> None:
+    """``dst[i] = rows[i]`` (stream-ordered): one strided copy when the rows are equally spaced in one storage
+    (a slab's rows, the common case), else one copy per row (rows adopted from several arrival slabs)."""
+    r0 = rows[0]
+    step = rows[1].data_ptr() - r0.data_ptr() if len(rows) > 1 else r0.numel() * r0.element_size()
+    one = step > 0 and step % r0.element_size() == 0 and r0.is_contiguous() and all(
+        b.untyped_storage().data_ptr() == r0.untyped_storage().data_ptr() and b.shape == r0.shape
+        and b.data_ptr() - a.data_ptr() == step for a, b in zip(rows, rows[1:]))
+    if one:
+        src = r0.as_strided((len(rows), r0.numel()), (step // r0.element_size(), 1), r0.storage_offset())
+        dst.copy_(src, non_blocking=True)
+        return
+    for i, row in enumerate(rows):
+        dst[i].copy_(row, non_blocking=True)
+
+
 class MultiDeviceEngine:
     """Bucket-sharded FedAvg over several GPUs of one node, driven from one process."""
 
@@ -243,8 +259,10 @@ class MultiDeviceEngine:
         layout = self._prepare(template)
         for shard in self._shards:
             shard.slab(codec, capacity)
-            # the previous round's kernel may still read this round's rows
+            # the previous round's kernel (and a client-split assembly, on the current stream) may still
+            # read this round's rows
             shard.copy_stream.wait_stream(shard.stream)
+            shard.copy_stream.wait_stream(torch.cuda.current_stream(shard.device))
         return (ClientRound if client_split else MultiRound)(self, layout, capacity, codec)
 
     def prestage(self, payload: Mapping[str, torch.Tensor], baseline_layout: ArenaLayout) -> bool:
@@ -597,7 +615,19 @@ class ClientRound(MultiRound):
 
     # ------------------------------------------------------------ client split
     def _client_rounds(self):
-        """Per device g: a single-GPU round holding the whole arenas of the staged slots j = g mod N."""
+        """Per device g: a single-GPU round holding the whole arenas of the staged slots j = g mod N.
+
+        Enqueued, never waited for on the host.  Each bucket's current stream first waits for its copy
+        stream (the H2D of the buckets); then, per (destination, bucket), ONE strided device-to-device
+        copy moves that bucket of every client the destination owns (their rows are equally spaced in
+        the bucket's slab; rows adopted from arrival slabs fall back to a copy per row).  torch orders a
+        cross-device copy after the current streams of both devices and makes the destination's current
+        stream wait for it, so the reductions that follow on each device's current stream see the
+        assembled arenas without a host synchronisation.  Destination device g then holds its clients'
+        whole arenas next to its bucket shard (memory: one extra copy of the clients, split over the GPUs).
+        ``timings["client_assembly_ms"]``: the longest destination's span (HIP events), filled once the
+        reductions have synchronised.
+        """
         if self._split is not None:
             return self._split
         if self._baseline_sd is None:
@@ -605,8 +635,8 @@ class ClientRound(MultiRound):
         eng = self.engine
         world = eng.world
         staged = [j for j in range(self.capacity) if self.staged[j]]
-        for d in dict.fromkeys(eng.devices):  # the buckets' H2D copies (copy streams) are done
-            torch.cuda.synchronize(d)
+        for sh in eng._shards:  # this round's bucket copies (copy streams) before any read of them
+            torch.cuda.current_stream(sh.device).wait_stream(sh.copy_stream)
 
         def build(g):
             mine = [j for j in staged if j % world == g]
@@ -616,27 +646,42 @@ class ClientRound(MultiRound):
                 r = e.begin(self._baseline_sd, max(1, len(mine)), "native")
                 if r.layout.signature != self.layout.signature:
                     raise RuntimeError("client engine built another arena layout")
+                here = torch.cuda.current_stream(dev)
+                here.wait_stream(e._copy_stream)  # the previous round's copies into this engine's slab
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(here)
                 for sh in eng._shards:  # the baseline, bucket by bucket
                     if sh.n:
-                        e._base.f32[sh.lo:sh.hi].copy_(sh.base_f[: sh.n])
+                        e._base.f32[sh.lo:sh.hi].copy_(sh.base_f[: sh.n], non_blocking=True)
                     if sh.ni:
-                        e._base.i64[sh.ilo:sh.ihi].copy_(sh.base_i[: sh.ni])
+                        e._base.i64[sh.ilo:sh.ihi].copy_(sh.base_i[: sh.ni], non_blocking=True)
                 r.has_baseline = True
-                for local, j in enumerate(mine):
-                    dst_f, dst_i = r.slab.f32[local], r.slab.i64[local]
-                    for sh, (src_f, src_i) in zip(eng._shards, self._rows[j]):
+                if mine:
+                    for sh in eng._shards:
                         if sh.n:
-                            dst_f[sh.lo:sh.hi].copy_(src_f[: sh.n])
+                            _copy_rows(r.slab.f32[: len(mine), sh.lo:sh.hi],
+                                       [self._rows[j][sh.index][0][: sh.n] for j in mine])
                         if sh.ni:
-                            dst_i[sh.ilo:sh.ihi].copy_(src_i[: sh.ni])
-                    pf, pi = r.slab.row_pointers([local])
-                    r._pf[local], r._pi[local] = int(pf[0]), int(pi[0])
+                            _copy_rows(r.slab.i64[: len(mine), sh.ilo:sh.ihi],
+                                       [self._rows[j][sh.index][1][: sh.ni] for j in mine])
+                e1.record(here)
+                pf, pi = r.slab.row_pointers(range(len(mine)))
+                for local in range(len(mine)):
+                    r._pf[local], r._pi[local] = int(pf[local]), int(pi[local])
                     r.staged[local] = True
-                torch.cuda.synchronize(dev)
-            return r, {j: local for local, j in enumerate(mine)}
+            return r, {j: local for local, j in enumerate(mine)}, (e0, e1)
 
-        self._split = eng.each(build, range(world))
+        built = eng.each(build, range(world))
+        self._assembly_events = [b[2] for b in built]
+        self._split = [(b[0], b[1]) for b in built]
         return self._split
+
+    def _resolve_assembly(self) -> None:
+        """``timings["client_assembly_ms"]`` once the devices have passed the assembly (after a reduction's sync)."""
+        evs = getattr(self, "_assembly_events", None)
+        if evs and all(e1.query() for _, e1 in evs):
+            self.timings["client_assembly_ms"] = max(e0.elapsed_time(e1) for e0, e1 in evs)
+            self._assembly_events = None
 
     def _by_device(self, slots):
         """[(device g, [local slots], [positions in ``slots``])] for the devices holding some of ``slots``."""
@@ -694,9 +739,9 @@ class ClientRound(MultiRound):
                 outs.append((out_f, out_i))
                 keep.append((tf, ti, dw, dcf, dci))
         fulls = self._gather(outs)
-        for d in dict.fromkeys(eng.devices):
-            torch.cuda.synchronize(d)
-        del keep
+        for s in eng._shards:  # the reductions run on each device's current stream: order them after the gather
+            torch.cuda.current_stream(s.device).wait_stream(s.stream)
+        self._keep_entrywise = keep  # stream-ordered inputs: alive until the next launch
         return fulls
 
     def _bucket_chunks(self):
@@ -738,6 +783,7 @@ class ClientRound(MultiRound):
                 return split[g][0].fedadp_dots(grads[g], local, lr)
 
         parts = self.engine.each(run, groups)
+        self._resolve_assembly()
         inner = np.zeros(len(slots), dtype=np.float32)
         l_sq = np.zeros(len(slots), dtype=np.float32)
         for (g, _, pos), (xy, gg, yy) in zip(groups, parts):
@@ -765,6 +811,7 @@ class ClientRound(MultiRound):
                 return sims, rnd.last_norms
 
         parts = self.engine.each(run, groups)
+        self._resolve_assembly()
         sims = [None] * len(slots)
         norms = np.zeros(len(slots) + 1, dtype=np.float32)
         for (g, _, pos), (vals, dev_norms) in zip(groups, parts):

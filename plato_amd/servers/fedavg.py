@@ -51,6 +51,11 @@ class _EngineHolder:
     #: reduction order is the one the device reproduces (plato_amd.hostorder):
     #: "warn" logs a mismatch once and goes on, "strict" (or True) raises, False skips
     host_order_check = "warn"
+    #: FedAdp / Port over several ``aggregation_devices``: split the whole-model reductions by client
+    #: (``MultiDeviceEngine.clients``, every GPU reduces its own clients' chains).  Opt-in: the split's
+    #: cross-device copies and RCCL all-gather have only run with repeated devices on a one-GPU box, so
+    #: its parity on distinct GPUs is unpinned; the default runs such rounds on the first GPU.
+    client_split_rounds = False
     #: arena alignment of the round layouts (plato_amd.arena.ALIGNMENTS): FedAdp's servers align
     #: every fp32 entry to its flattened position so the dot kernel reads whole lines
     arena_alignment = None
@@ -79,16 +84,16 @@ class _EngineHolder:
         native / bf16 payloads; whole-entry shards (``MultiDeviceEngine.entries``)
         for QSGD payloads (per-entry scales) and entry-local staged weights
         (Polaris); for weights that reduce the whole flattened model serially
-        per client (Port's similarity, FedAdp's dots) bucket-sharded staging with
-        the reductions split by client (``MultiDeviceEngine.clients``), or the
-        first GPU for coded payloads.
+        per client (Port's similarity, FedAdp's dots) the first GPU, or, with
+        ``client_split_rounds``, bucket-sharded staging with the reductions split
+        by client (``MultiDeviceEngine.clients``; native payloads only).
         """
         eng = self.aggregation_engine()
         primary = getattr(eng, "primary", None)
         if primary is None:
             return eng
         if self.needs_staged_round and not self.entry_local_weights:
-            return eng.clients if codec == "native" else primary
+            return eng.clients if (codec == "native" and self.client_split_rounds) else primary
         if self.needs_staged_round or codec not in ("native", "bf16"):
             return eng.entries
         return eng
@@ -128,6 +133,9 @@ class _EngineHolder:
         (HIP events, max over GPUs), ``aggregation_d2h_ms``, ``aggregation_total_ms``
         (hook entry to result), ``aggregation_GBps`` (algorithmic bytes / kernel time)
         and ``aggregation_gpus``; list them in ``results.types`` to record them.
+        ``aggregation_host_order_ok`` (FedAdp / Port): whether this host's numpy / torch reduction order
+        matched the device's on the probe (False: the weights may differ from this host's reference in
+        the last bits; None: not checked), so a "warn"-mode mismatch shows in the results, not only the log.
         """
         items = super().get_logged_items() if hasattr(super(), "get_logged_items") else {}
         t = getattr(self, "_plato_amd_timings", None) or {}
@@ -139,6 +147,7 @@ class _EngineHolder:
             "aggregation_total_ms": t.get("total_ms"),
             "aggregation_GBps": (t["bytes"] / (kernel * 1e-3) / 1e9) if kernel else None,
             "aggregation_gpus": t.get("gpus"),
+            "aggregation_host_order_ok": getattr(self, "_plato_amd_host_order_ok", None),
         })
         return items
 

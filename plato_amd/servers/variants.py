@@ -74,7 +74,9 @@ class PortWeights(_EngineHolder):
         threads = torch.get_num_threads() if self.port_threads is None else int(self.port_threads)
         check = hostorder.mode(self.host_order_check)
         if check:  # this host's F.cosine_similarity order (a mismatch warns; "strict" refuses)
-            hostorder.check_port(rnd.engine.device, threads, strict=check == "strict")
+            self._plato_amd_host_order_ok = hostorder.check_port(
+                rnd.engine.device, threads, strict=check == "strict", align=getattr(rnd.engine, "layout_align", None),
+                port_variant=getattr(rnd.engine, "port_variant", None))
         # coded payloads: the per-entry reductions run on the dequantized rows (model_dequantize semantics)
         sims = rnd.decoded().model_similarities(previous, need, threads=threads)
         out = [1.0] * len(updates)
@@ -252,7 +254,8 @@ class FedAdpWeights(_EngineHolder):
         alpha = self.fedadp_alpha if self.fedadp_alpha is not None else _config_attr("algorithm", "alpha", 5)
         check = hostorder.mode(self.host_order_check)
         if check:  # this host's numpy sdot order (a mismatch warns; "strict" refuses)
-            hostorder.check_fedadp(rnd.engine.device, lr, strict=check == "strict")
+            self._plato_amd_host_order_ok = hostorder.check_fedadp(
+                rnd.engine.device, lr, strict=check == "strict", align=getattr(rnd.engine, "layout_align", None))
         inner, g_sq, l_sq = rnd.fedadp_dots(grads, range(k), lr)
         angles = W.fedadp_angles_from_dots(inner, g_sq, l_sq)
         contribs = W.fedadp_contributions(angles, self.selected_clients, self.local_angles,

@@ -87,6 +87,15 @@ def test_argument_errors_are_raised_without_gpu_work():
         _lib.call("plato_agg_fedavg_weights", 8, None, 8, None, 2, 4, None, 4, None, 16, 0, None)
     with pytest.raises(ValueError, match="modulus"):
         _lib.call("plato_agg_fill_synth_i64", 8, None, 4, 0, 0, 0, None)
+    # FedAdp's boundary table is addressed with 32-bit byte offsets of 1 KiB rows: a segment count whose
+    # table would reach 2^22 rows is refused, not wrapped
+    a = 1 << 12  # any 256-byte-aligned non-null address: nothing is dereferenced on this path
+    with pytest.raises(ValueError, match="boundary table"):
+        _lib.call("plato_agg_fedadp_dots", a, a, a, 1, a, None, a, (1 << 21) - 1, 1 << 20, 1 << 20, 0, 0.01, 1,
+                  a, a, a, None)
+    from plato_amd.engine import AggregationRound
+
+    assert AggregationRound.fedadp_boundary_rows((1 << 21) - 1, 0) >= AggregationRound.FEDADP_MAX_BND
 
 
 def test_engine_refuses_without_gpu():

@@ -155,3 +155,36 @@ def test_rccl_collectives_one_rank_per_gpu(tmp_path):
     for o in outs:
         assert o["f32_match"] and o["i64_match"] and o["reduce_scatter_on_gpu"], o
         assert o["normwise"] <= 1e-6, o
+
+
+def _bench_lines(args, env_extra, timeout):
+    env = dict(os.environ, OMP_NUM_THREADS="2", PLATO_BENCH_BACKEND="gloo", **env_extra)
+    env.pop("WORLD_SIZE", None)
+    proc = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
+                          text=True, timeout=timeout)
+    assert proc.returncode == 0, proc.stdout[-3000:] + proc.stderr[-3000:]
+    lines = [ln for ln in proc.stdout.splitlines() if ln.strip()]
+    return lines, proc.stderr
+
+
+def test_bench_self_launches_its_ranks():
+    """``python bench.py --gpus 2`` from a plain invocation spawns torch.distributed.run itself (before any GPU
+    call) and forwards rank 0's single JSON line: the launcher plumbing, with gloo and no GPU work."""
+    lines, err = _bench_lines(["--gpus", "2", "--probe-launch"], {}, 300)
+    assert len(lines) == 1, (lines, err[-2000:])
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["requested"] == 2 and out["rank_sum"] == 1.0
+    assert "launching 2 ranks" in err
+
+
+@pytest.mark.gpu
+def test_bench_self_launch_two_ranks_on_gpu():
+    """The N > 1 bench from a plain ``python bench.py --gpus 2`` on the one-GPU box (gloo rehearsal: the ranks share
+    the GPU): one parsed line with n_gpus == 2 and the per-rank algorithmic bytes counted."""
+    lines, err = _bench_lines(["--gpus", "2", "--steps", "3", "--warmup", "1"], {}, 600)
+    assert len(lines) == 1, (lines, err[-2000:])
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["value"] > 0
+    cfg = out["config"]
+    assert cfg["algorithmic_bytes_per_step_per_gpu"] > 0 and cfg["pieces_per_rank"] >= 1
+    assert out["roofline"]["frac"] > 0

@@ -94,8 +94,10 @@ def test_multi_device_deltas_and_variants(n):
         assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"], name
 
 
-def test_multi_device_routes_staged_round_variants():
-    """Port / FedAdp rounds of native payloads split their reductions by client; coded ones stay on GPU 0."""
+@pytest.mark.parametrize("split", [False, True])
+def test_multi_device_routes_staged_round_variants(split):
+    """Port / FedAdp rounds run on GPU 0 by default; with client_split_rounds native payloads split their
+    reductions by client, coded ones stay on GPU 0."""
     from plato_amd.servers import variants as V
 
     case = _case("port_resnet18_k16")
@@ -106,6 +108,7 @@ def test_multi_device_routes_staged_round_variants():
     class Server(V.PortServerMixin):
         aggregation_devices = _devices(4)
         staleness_weight = 3
+        client_split_rounds = split
 
         def __init__(self):
             self.current_round = 0
@@ -113,9 +116,10 @@ def test_multi_device_routes_staged_round_variants():
     server = Server()
     updated = asyncio.run(server.aggregate_weights(updates, baseline, [u.payload for u in updates]))
     eng = server.aggregation_engine()
-    assert server.round_engine("native") is eng.clients and server.round_engine("qsgd") is eng.primary
+    assert server.round_engine("native") is (eng.clients if split else eng.primary)
+    assert server.round_engine("qsgd") is eng.primary
     assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
-    assert server.get_logged_items()["aggregation_gpus"] == 4
+    assert server.get_logged_items()["aggregation_gpus"] == (4 if split else 1)
 
 
 @pytest.mark.parametrize("n", [2, 3, 8])
@@ -133,6 +137,7 @@ def test_client_split_fedadp_matches_reference(name, n):
 
     class Server(FedAdpServerMixin):
         aggregation_devices = _devices(n)
+        client_split_rounds = True
         fedadp_lr = 0.01
 
     server = Server()
@@ -166,6 +171,7 @@ def test_client_split_port_matches_reference(tmp_path, name, n):
 
     class Server(PortServerMixin):
         aggregation_devices = _devices(n)
+        client_split_rounds = True
         staleness_weight = 3
         current_round = recipe["current_round"]
         port_threads = FIXTURE_TORCH_THREADS
