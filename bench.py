@@ -536,22 +536,39 @@ def main():
     torch.cuda.synchronize(dev)
     barrier(world)
     torch.cuda.synchronize(dev)
-    # HIP events on the launch stream around every kernel and every assembly
-    marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    t0 = time.perf_counter()
-    for m in marks:
-        m[0].record(stream)
-        kernel()
-        m[1].record(stream)
-        assemble()
-        m[2].record(stream)
+    # HIP events on the launch stream.  N = 1: one event per step boundary, so a step's kernel time is
+    # the span between consecutive events (the launch gap included); each recorded event costs the
+    # stream ~3-4 us (profiles/r05c_anchor.log "launch_gaps": 0.9064 ms per launch with none, 0.9097
+    # with one, 0.9182 with the three per step of rounds 1-4).  N > 1: events around the kernels and
+    # around the assembly, which are timed apart.
+    if plan is None:
+        bounds = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        t0 = time.perf_counter()
+        bounds[0].record(stream)
+        for i in range(args.steps):
+            kernel()
+            assemble()
+            bounds[i + 1].record(stream)
+    else:
+        marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        t0 = time.perf_counter()
+        for m in marks:
+            m[0].record(stream)
+            kernel()
+            m[1].record(stream)
+            assemble()
+            m[2].record(stream)
     torch.cuda.synchronize(dev)
     barrier(world)
     torch.cuda.synchronize(dev)
     t1 = time.perf_counter()
     wall = max_over_ranks(t1 - t0, world)
-    kernel_ms = statistics.fmean(m[0].elapsed_time(m[1]) for m in marks)
-    assembly_ms = statistics.fmean(m[1].elapsed_time(m[2]) for m in marks)
+    if plan is None:
+        kernel_ms = statistics.fmean(a.elapsed_time(b) for a, b in zip(bounds, bounds[1:]))
+        assembly_ms = 0.0
+    else:
+        kernel_ms = statistics.fmean(m[0].elapsed_time(m[1]) for m in marks)
+        assembly_ms = statistics.fmean(m[1].elapsed_time(m[2]) for m in marks)
     kernel_ms_max = max_over_ranks(kernel_ms, world)
     assembly_ms_max = max_over_ranks(assembly_ms, world)
 
@@ -823,7 +840,7 @@ def anchor_bench(args):
     torch.cuda.set_device(dev)
     stream = torch.cuda.current_stream(dev)
     nv = _lib.tune().plato_agg_tune_num_variants()
-    variants = [args.variant] if args.variant is not None else [v for v in (0, 5, 7, 9, 10, 11) if v < nv]
+    variants = [args.variant] if args.variant is not None else [v for v in (0, 5, 11, 12, 13) if v < nv]
     reps = max(3, args.steps)
 
     def describe(v):
@@ -844,28 +861,56 @@ def anchor_bench(args):
         out = torch.empty(row, dtype=torch.float32, device=dev)
         out_i = torch.empty(64, dtype=torch.float32, device=dev)
         w = torch.full((k,), 1.0 / k, dtype=torch.float32, device=dev)
-        rows = slab.data_ptr() + np.arange(k, dtype=np.int64) * row * 4
         ti = torch.from_numpy(slab_i.data_ptr() + np.arange(k, dtype=np.int64) * 64 * 8).to(dev)
         tables = {}
 
-        def launch(v, pieces):
+        def launch(v, pieces, stride=row):
+            """``stride``: the client rows' pitch in floats (<= row: the slab's own, or a denser view of it)."""
             for off, n, ni in pieces:
-                tf = tables.setdefault(off, torch.from_numpy(rows + off * 4).to(dev))
+                tf = tables.get((off, stride))
+                if tf is None:
+                    tf = tables[(off, stride)] = torch.from_numpy(
+                        slab.data_ptr() + np.arange(k, dtype=np.int64) * stride * 4 + off * 4).to(dev)
                 _lib.tune_call("plato_agg_tune_fedavg", v, 1, tf.data_ptr(), ti.data_ptr() if ni else None,
                                w.data_ptr(), None, k, base.data_ptr() + off * 4, base_i.data_ptr() if ni else None,
                                out.data_ptr() + off * 4, out_i.data_ptr() if ni else None, n, ni, stream.cuda_stream)
 
+        if label == "grid_tail":  # what the timed loop's per-step HIP events cost (C2-sized launches)
+            c2_pieces = next(p for name, p, _ in shapes if name.startswith("rounds_5.3"))
+            gaps = {}
+            for mode in ("none", "one", "three", "none"):
+                marks = []
+                launch(0, c2_pieces)
+                torch.cuda.synchronize(dev)
+                t0 = time.perf_counter()
+                for _ in range(reps * 5):
+                    for _ in range({"none": 0, "one": 1, "three": 2}[mode]):
+                        ev = torch.cuda.Event(enable_timing=True)
+                        ev.record(stream)
+                        marks.append(ev)
+                    launch(0, c2_pieces)
+                    if mode == "three":
+                        ev = torch.cuda.Event(enable_timing=True)
+                        ev.record(stream)
+                        marks.append(ev)
+                torch.cuda.synchronize(dev)
+                gaps[mode] = min(gaps.get(mode, 1e9), (time.perf_counter() - t0) * 1e3 / (reps * 5))
+            print(json.dumps({"anchor": "launch_gaps", "shape": "rounds_5.333", "clients": k,
+                              "ms_per_launch_by_events_per_step": {m: round(v, 4) for m, v in gaps.items()},
+                              "note": "wall clock over back-to-back launches; 'three' = bench.py's timed loop"}),
+                  flush=True)
         for name, pieces, extra in shapes:
             nbytes = sum((k + 2) * (n * 4 + ni * 8) for _, n, ni in pieces)
             times = {v: [] for v in variants}
+            stride = extra.get("row_stride", row)
             for v in variants:
-                launch(v, pieces)
+                launch(v, pieces, stride)
             torch.cuda.synchronize(dev)
             for _ in range(reps):
                 for v in variants:
                     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     e0.record(stream)
-                    launch(v, pieces)
+                    launch(v, pieces, stride)
                     e1.record(stream)
                     e1.synchronize()
                     times[v].append(e0.elapsed_time(e1))
@@ -885,7 +930,15 @@ def anchor_bench(args):
     c2 = ArenaLayout.from_shapes(model_spec("resnet18"))
     rounds = [2, 4, 5, c2.n_f32 / per_round, 5.5, 6, 8, 12]
     shapes = [(f"rounds_{r:.3f}", [(0, int(r * per_round) // 64 * 64, 0)], {"rounds": round(r, 3)}) for r in rounds]
-    run_shapes("grid_tail", 128, shapes, max(n for _, ((_, n, _),), _ in shapes))
+    row = max(n for _, ((_, n, _),), _ in shapes)
+    # C2 itself (with and without its int64 entries) at several client-row pitches: the bench's slab pitch
+    # (the arena rounded to 64 floats), padded pitches and the power-of-two-multiple pitches above
+    pitch = -(-c2.n_f32 // 64) * 64
+    for stride in (pitch, pitch + 64, pitch + 1024, pitch + 4096, pitch + 32768, 12 * 2**20, 16 * 2**20, row):
+        for ni in (c2.n_i64, 0):
+            shapes.append((f"c2_pitch_{stride}_i64_{ni}", [(0, c2.n_f32, ni)],
+                           {"row_stride": stride, "pitch_bytes": stride * 4, "int64_entries": ni}))
+    run_shapes("grid_tail", 128, shapes, row)
 
     # one rank's pieces at N GPUs (rank 0: the largest bucket, with the int64 entries)
     for config in ("C2", "C3"):

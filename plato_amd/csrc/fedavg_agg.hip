@@ -445,13 +445,16 @@ constexpr Variant make_variant() {
                   {&launch_one<C, true, false>, &launch_one<C, true, true>}}};
 }
 
-// Variant 0 is the default of the public entry points (fastest in the
-// interleaved sweep on MI355X).
+// Variant 0 is the default of the public entry points: one-wave (64-thread) workgroups, NT loads and
+// stores.  256-thread workgroups were the default of rounds 1-4; with the scalar items
+// moved to the front of the grid the one-wave form ran 1-2.5 % faster on every C2 / C3 shape and up to
+// 9 % on the small per-rank pieces of N > 1, on two boxes (profiles/r05b_anchor.log, r05c_anchor.log;
+// DESIGN.md §15).
 #ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so: every variant (bench.py --sweep, scripts/)
 // The round-1 sweep of 18 shapes (profiles/r01_sweep.log) is trimmed to one of each
 // kind; bench.py --sweep interleaves these.
 const Variant kVariants[] = {
-    make_variant<Cfg<256, 1, 8, true, true, false>>(),                   // 0 (default): NT loads + NT stores
+    make_variant<Cfg<64, 1, 8, true, true, false>>(),                    // 0 (default): one wave, NT loads + stores
     make_variant<Cfg<256, 2, 8, false, false, false>>(),                 // 1 first version
     make_variant<Cfg<256, 1, 8, false, false, false>>(),                 // 2 plain loads
     make_variant<Cfg<256, 1, 8, true, true, true>>(),                    // 3 pipelined
@@ -462,11 +465,13 @@ const Variant kVariants[] = {
     make_variant<Cfg<256, 1, 32, true, true, false>>(),                  // 8 32 clients per batch
     make_variant<Cfg<256, 1, 8, true, true, false, false, 0, false, true>>(),   // 9 balanced grid
     make_variant<Cfg<256, 1, 16, true, true, false, false, 0, false, true>>(),  // 10 balanced, U=16
-    make_variant<Cfg<64, 1, 8, true, true, false>>(),                    // 11 one wave per workgroup
+    make_variant<Cfg<256, 1, 8, true, true, false>>(),                   // 11 the rounds 1-4 default (4 waves)
+    make_variant<Cfg<64, 1, 16, true, true, false>>(),                   // 12 one wave, 16 clients per batch
+    make_variant<Cfg<128, 1, 8, true, true, false>>(),                   // 13 two waves
 };
 #else  // libplato_agg.so: the default only
 const Variant kVariants[] = {
-    make_variant<Cfg<256, 1, 8, true, true, false>>(),              // 0 (default): NT loads + NT stores
+    make_variant<Cfg<64, 1, 8, true, true, false>>(),               // 0 (default): one wave, NT loads + stores
 };
 #endif
 constexpr int kNumVariants = sizeof(kVariants) / sizeof(kVariants[0]);

@@ -14,7 +14,8 @@
 #   variants           scripts/bench_variants.py (variant-server kernels)
 #   profile            scripts/profile.sh <tag>: unprofiled bench + kernel trace + FETCH_SIZE + WRITE_SIZE passes
 #   profile_variants   scripts/profile_variants.sh <tag>
-#   pmc=<counters>     one rocprofv3 --pmc pass (comma-separated counters) over scripts/bench_variants.py
+#   pmc=<counters>@<script+args>   one rocprofv3 --pmc pass (comma-separated counters) over python3 <script> <args>
+#                      (default script: scripts/bench_variants.py --reps 3)
 #   py=<script+args>   python <script> <args> (spaces as '+')
 # Libraries are built in-tree before the call (never on the GPU box).
 set -u
@@ -53,10 +54,15 @@ for step in "$@"; do
     variants) run variants 600 python -u scripts/bench_variants.py ;;
     profile) run profile 900 bash scripts/profile.sh "$tag" ;;
     profile_variants) run profile_variants 900 bash scripts/profile_variants.sh "$tag" ;;
-    pmc=*) (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc ${arg//,/ } --output-format csv \
-              -d "$GRAFT_REPO_ROOT/$out/pmc_$n" -o pmc -- python3 "$GRAFT_REPO_ROOT/scripts/bench_variants.py" --reps 3) \
+    pmc=*) ctrs=${arg%%@*}
+           prog="scripts/bench_variants.py --reps 3"
+           [ "$ctrs" != "$arg" ] && prog=${arg#*@} && prog=${prog//+/ }
+           set -- $prog
+           script=$1; shift
+           (cd /tmp && export TMPDIR=/tmp && timeout -s KILL 180 rocprofv3 --pmc ${ctrs//,/ } --output-format csv \
+              -d "$GRAFT_REPO_ROOT/$out/pmc_$n" -o pmc -- python3 "$GRAFT_REPO_ROOT/$script" "$@") \
              > "$out/pmc_$n.log" 2>&1 || { rc=$?; echo "pmc pass $n rc=$rc"; tail -4 "$out/pmc_$n.log"; exit $rc; }
-           echo "=== pmc_$n ok" ;;
+           echo "=== pmc_$n ok ($ctrs over $script $*)" ;;
     py=*) run py_$n 600 python -u $args ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
