@@ -471,6 +471,7 @@ int plato_agg_scale_by_norm(const float* d_a, size_t n, const float* d_norm, flo
  * Polaris' per-layer squared deltas (examples/client_selection/polaris/
  * polaris_server.py:78-81).  d_first_chunk[p] = sum over earlier pieces of
  * ceil(len / 8192); n_chunks the total.  d_out: [K][n_pieces] floats.
+ * d_workspace: plato_agg_np_sumsq_workspace(K, n_chunks) bytes (the per-chunk sums).
  */
 size_t plato_agg_np_sumsq_workspace(int K, uint32_t n_chunks);
 int plato_agg_np_sumsq(const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,

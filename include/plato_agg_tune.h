@@ -121,9 +121,10 @@ int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const*
                                float* d_out_yy, hipStream_t stream);
 
 /* plato_agg_np_sumsq with an explicit kernel (csrc/flat.hip): 0 = full chunks staged in two halves
- * plus a tail kernel for the partial last chunks (the default); 1 = the round-2 client-major kernel;
- * 2, 3 = timing probes of variant 4 (wrong results by design: no baseline loads / no LDS phase);
- * 4 = the round-3 default (chunk-major, every chunk staged whole). */
+ * with 16-byte loads plus a tail kernel for the partial last chunks (the default); 1 = the round-2
+ * client-major kernel; 2, 3 = timing probes of variant 4 (wrong results by design: no baseline loads /
+ * no LDS phase); 4 = the round-3 default (chunk-major, every chunk staged whole); 5 = the round-4
+ * default (variant 0 with dword loads). */
 int plato_agg_tune_num_np_sumsq_variants(void);
 int plato_agg_tune_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base,
                             const plato_agg_chunk* d_pieces, const uint32_t* d_first_chunk, uint32_t n_pieces,

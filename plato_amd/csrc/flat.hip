@@ -1071,7 +1071,7 @@ struct NpTask {
   uint32_t k, c, n;
   uint64_t begin;
 };
-__device__ __forceinline__ NpTask np_task(const SumsqArgs& a, uint64_t t) {
+__device__ __forceinline__ NpTask np_task_lane(const SumsqArgs& a, uint64_t t) {  // any t per lane
   NpTask r;
   r.k = uint32_t(t % uint64_t(a.K));
   r.c = uint32_t(t / uint64_t(a.K));
@@ -1084,6 +1084,10 @@ __device__ __forceinline__ NpTask np_task(const SumsqArgs& a, uint64_t t) {
   r.begin = uint64_t(p.begin) + uint64_t(r.c - a.first_chunk[lo]) * kNpBuf;
   const uint64_t end = r.begin + kNpBuf < uint64_t(p.end) ? r.begin + kNpBuf : uint64_t(p.end);
   r.n = uint32_t(end - r.begin);
+  return r;
+}
+__device__ __forceinline__ NpTask np_task(const SumsqArgs& a, uint64_t t) {  // t workgroup-uniform
+  NpTask r = np_task_lane(a, t);
   // workgroup-uniform: keep the task in SGPRs (scalar bases for the loads)
   r.k = __builtin_amdgcn_readfirstlane(r.k);
   r.c = __builtin_amdgcn_readfirstlane(r.c);
@@ -1283,85 +1287,6 @@ __global__ __launch_bounds__(256) void np_sumsq_half4_kernel(SumsqArgs a) {
   }
 }
 
-// Streaming form (round 5): persistent workgroups of 4 loader waves and 1 summer wave.  The loaders
-// keep the next task's x and b loads in flight (two register sets, 16-byte loads) while they write the
-// current task's squares into one of two LDS slots; the summer wave sums the slot the loaders filled
-// one step earlier, lane = leaf: each lane runs its leaf's 8 accumulators over the leaf's 16 steps
-// (numpy's r[j], 16-byte LDS reads, a 132-float leaf pitch keeps a 16-lane read group on 64 distinct
-// banks), ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)), then the 64 leaves by the same xor
-// butterfly.  One s_barrier per task; the loads never wait for an LDS phase (the half kernel's
-// workgroups, all in the same phase, left the CU without loads in flight during it: DESIGN.md §14-15).
-// Full chunks only; partial chunks take np_sumsq_tail_kernel.  Same sums, same order.
-constexpr int kStreamPitch = kPW + 4;
-constexpr int kStreamSlot = kNpBuf / kPW * kStreamPitch;  // floats per LDS slot
-constexpr int kStreamLoaders = 4;
-
-__device__ __forceinline__ void np_stream_issue(const SumsqArgs& a, uint64_t t, f4 (&xv)[8], f4 (&bv)[8], int tid) {
-  const NpTask k = np_task(a, t);
-  if (k.n != kNpBuf) return;  // workgroup-uniform: a partial chunk (the tail kernel's)
-  const gcf4* x = (const gcf4*)(a.x[k.k] + k.begin) + tid;
-  const gcf4* b = (const gcf4*)(a.base + k.begin) + tid;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    xv[q] = __builtin_nontemporal_load(x + q * 256);
-    bv[q] = b[q * 256];
-  }
-}
-
-__device__ __forceinline__ void np_stream_write(const SumsqArgs& a, uint64_t t, const f4 (&xv)[8], const f4 (&bv)[8],
-                                                float* slot, int tid) {
-  if (np_task(a, t).n != kNpBuf) return;
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const uint32_t e = uint32_t(q * 1024 + 4 * tid);  // 4 elements of one leaf
-    const f4 d = xv[q] - bv[q];
-    *reinterpret_cast<f4*>(slot + (e / kPW) * kStreamPitch + e % kPW) = d * d;
-  }
-}
-
-__global__ __launch_bounds__(64 * (kStreamLoaders + 1)) void np_sumsq_stream_kernel(SumsqArgs a, uint64_t n_tasks) {
-  __shared__ __attribute__((aligned(16))) float ring[2 * kStreamSlot];
-  const uint64_t G = gridDim.x;
-  if (blockIdx.x >= n_tasks) return;  // (workgroup-uniform, before any barrier)
-  const uint64_t n_it = (n_tasks - blockIdx.x + G - 1) / G;  // this workgroup's tasks: blockIdx.x + s G
-  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  if (wave < kStreamLoaders) {
-    const int tid = int(threadIdx.x);
-    f4 xa[8], ba[8], xb[8], bb[8];
-    np_stream_issue(a, blockIdx.x, xa, ba, tid);
-    for (uint64_t s = 0; s < n_it; s += 2) {
-      const uint64_t t = blockIdx.x + s * G;
-      if (s + 1 < n_it) np_stream_issue(a, t + G, xb, bb, tid);
-      np_stream_write(a, t, xa, ba, ring, tid);
-      __syncthreads();  // task s staged in slot 0
-      if (s + 1 >= n_it) break;
-      if (s + 2 < n_it) np_stream_issue(a, t + 2 * G, xa, ba, tid);
-      np_stream_write(a, t + G, xb, bb, ring + kStreamSlot, tid);
-      __syncthreads();  // task s + 1 staged in slot 1
-    }
-    return;
-  }
-  // the summer wave: task s from slot s & 1, between barrier s and barrier s + 1 (the loaders fill the
-  // other slot meanwhile)
-  const int leaf = int(threadIdx.x & 63);
-  for (uint64_t s = 0; s < n_it; ++s) {
-    __syncthreads();
-    const NpTask k = np_task(a, blockIdx.x + s * G);
-    if (k.n != kNpBuf) continue;
-    const f4* l = reinterpret_cast<const f4*>(ring + (s & 1) * kStreamSlot + leaf * kStreamPitch);
-    f4 lo = l[0], hi = l[1];
-#pragma unroll
-    for (int i = 1; i < kPW / 8; ++i) {
-      lo = lo + l[2 * i];
-      hi = hi + l[2 * i + 1];
-    }
-    float v = ((lo.x + lo.y) + (lo.z + lo.w)) + ((hi.x + hi.y) + (hi.z + hi.w));
-#pragma unroll
-    for (int m = 1; m < 64; m <<= 1) v = v + __shfl_xor(v, m);
-    if (leaf == 0) a.chunk_sums[uint64_t(k.k) * a.n_chunks + k.c] = v;
-  }
-}
-
 // The partial last chunk of every (piece, client), through the full-staging path.
 __global__ __launch_bounds__(256) void np_sumsq_tail_kernel(SumsqArgs a) {
   __shared__ float sq[kNpBuf / kPW * kLeafPitch];
@@ -1387,13 +1312,15 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   a.out[uint64_t(k) * a.n_pieces + pc] = out;
 }
 
-// variant 0 (the default): full chunks staged in two halves (np_sumsq_half_kernel: 17.4 KB of LDS, six
-// workgroups per CU instead of four; 1.25 against 1.39 ms interleaved) plus the partial last chunks
-// (np_sumsq_tail_kernel); 1: the round-2 form (np_sumsq_chunks_lds_kernel, client-major, four memory
-// round trips per workgroup); 2, 3: timing probes of variant 4 (wrong results by design: no baseline
-// loads / no LDS phase); 4: the round-3 default (np_sumsq_chunks_v2_kernel, every chunk staged whole);
-// 5: variant 0 with 16-byte loads and LDS writes (np_sumsq_half4_kernel); 6: persistent loader / summer
-// workgroups (np_sumsq_stream_kernel).
+// variant 0 (the default): full chunks staged in two halves with 16-byte loads and LDS writes
+// (np_sumsq_half4_kernel: 17.4 KB of LDS; 1.5-1.8 % under variant 5 in three interleaved runs,
+// profiles/r05b_polaris_variants.log, r05e-h) plus the partial last chunks (np_sumsq_tail_kernel);
+// 1: the round-2 form (np_sumsq_chunks_lds_kernel, client-major, four memory round trips per
+// workgroup); 2, 3: timing probes of variant 4 (wrong results by design: no baseline loads / no LDS
+// phase); 4: the round-3 default (np_sumsq_chunks_v2_kernel, every chunk staged whole); 5: the round-4
+// default (np_sumsq_half_kernel, dword loads and LDS writes).  A persistent loader / summer form (four
+// loader waves keeping the next chunk's loads in flight, one summer wave per chunk, lane = leaf)
+// measured 1.51 ms against 1.25 and was removed.
 // G clients per workgroup sharing the baseline (4.1-5.9 ms) were dropped after round 3; a persistent
 // software-pipelined form (2.9 ms: its two register sets left one workgroup per CU), 512 / 1,024
 // threads per chunk (1.70 / 2.79 ms against 1.38) and an LDS-free form loading each accumulator's
@@ -1410,28 +1337,15 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
   } else if (variant == 4) {
     hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256>), grid, dim3(256), 0, st, a);
   } else if (variant == 5) {
-    hipLaunchKernelGGL(np_sumsq_half4_kernel, grid, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
-  } else if (variant == 6) {
-    // persistent: as many workgroups as the chip holds at once (queried once), at most one per task
-    static int resident = [] {
-      int per_cu = 0, cus = 0, dev = 0;
-      const bool ok = hipGetDevice(&dev) == hipSuccess &&
-                      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess &&
-                      hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, np_sumsq_stream_kernel,
-                                                                   64 * (kStreamLoaders + 1), 0) == hipSuccess;
-      return ok && per_cu > 0 && cus > 0 ? per_cu * cus : 256;
-    }();
-    const uint32_t g = uint32_t(tasks < uint64_t(resident) ? tasks : uint64_t(resident));
-    hipLaunchKernelGGL(np_sumsq_stream_kernel, dim3(g), dim3(64 * (kStreamLoaders + 1)), 0, st, a, tasks);
+    hipLaunchKernelGGL(np_sumsq_half_kernel, grid, dim3(256), 0, st, a);
     hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL(np_sumsq_half_kernel, grid, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(np_sumsq_half4_kernel, grid, dim3(256), 0, st, a);
     hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   }
 }
-[[maybe_unused]] constexpr int kNumSumsqVariants = 7;
-constexpr int kSumsqDefault = 0;  // half-staged + tail: 1.25 ms vs 1.39 (variant 4) on 128 ResNet-18 clients
+[[maybe_unused]] constexpr int kNumSumsqVariants = 6;
+constexpr int kSumsqDefault = 0;  // half-staged (16-byte) + tail: 1.23-1.27 ms on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
                  float* d_out, hipStream_t stream);

@@ -177,6 +177,7 @@ def test_np_sumsq_variants_agree_bitwise(k):
     ws = torch.empty(max(1, eng.lib.plato_agg_np_sumsq_workspace(k, n_chunks) // 4), dtype=torch.float32, device=DEV)
     for v in [v for v in range(_lib.tune().plato_agg_tune_num_np_sumsq_variants()) if v not in (2, 3)]:  # probes
         out = torch.full((k, int(entry_of.size)), float("nan"), device=DEV)
+        ws.fill_(float("nan"))  # a variant that leaves a chunk sum unwritten must not inherit the previous one's
         _lib.tune_call("plato_agg_tune_np_sumsq", v, tf.data_ptr(), k, rnd._base.f32.data_ptr(), pieces.data_ptr(),
                        first.data_ptr(), int(entry_of.size), n_chunks, ws.data_ptr(), out.data_ptr(),
                        torch.cuda.current_stream().cuda_stream)
