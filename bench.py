@@ -807,12 +807,12 @@ def variant_legs(dev, k: int, reps: int) -> dict:
 
 # Strong scaling, N > 1: pieces per rank, chosen from the one-GPU anchor (``--anchor``).
 # More pieces overlap more of the all-gather with the kernels but make each piece kernel smaller.
-# C2: pieces=1 kernels are the fastest at every N (profiles/r05a_anchor.log: N8 0.138 ms vs 0.189 ms in 4
-# pieces), but the all-gather then runs wholly exposed; with RCCL's all-gather at ~330 GB/s bus bandwidth
-# on the 8-GPU mesh (one ~76 GB/s link between 2 GPUs) the sum kernel + exposed gather is smallest at 4
-# pieces for N = 2 and 4 and at 2 for N = 8.  C3's rank kernels are flat in the
-# piece count (ms-long), so its 84 MB gathers take 4.
-PIECES_BY_WORLD = {"C2": {2: 4, 4: 4, 8: 2}, "C3": {2: 4, 4: 4, 8: 4}}
+# From the one-GPU anchor with the one-wave kernel (profiles/r05d_anchor.log): a rank's
+# kernels lose little to more pieces (C2 at N = 8: 0.116 ms in 1 piece, 0.123 in 4, 0.151 in 8), while
+# each piece lets the all-gather of the one before it run under the kernels; with RCCL's all-gather
+# modelled at one ~64 GB/s xGMI link for N = 2 and ~192 / ~330 GB/s of bus bandwidth for N = 4 / 8, plus
+# ~15 us per collective, 4 pieces give the shortest step at every N for C2 and C3.
+PIECES_BY_WORLD = {"C2": {2: 4, 4: 4, 8: 4}, "C3": {2: 4, 4: 4, 8: 4}}
 
 
 def pieces_for(config: str, world: int) -> int:

@@ -50,6 +50,10 @@ int plato_agg_tune_fedavg(int variant, int has_base,
                           float* d_out_f32, float* d_out_i64f,
                           size_t n_f32, size_t n_i64, hipStream_t stream);
 
+/* Threads per plato_agg_fedavg_entrywise workgroup: 64, 128 or 256 (0 restores the default, 64; any
+ * other value too).  Process-wide, for A/B timings of the tuning library's entry point. */
+void plato_agg_tune_set_entrywise_block(int threads);
+
 /* bf16-payload kernel variants (plato_agg_fedavg_weights_bf16 uses 0). */
 int plato_agg_tune_num_bf16_variants(void);
 int plato_agg_tune_fedavg_bf16(int variant, const uint16_t* const* d_x_bf16,

@@ -162,6 +162,7 @@ SIGNATURES = {
 TUNE_SIGNATURES = {
     "plato_agg_tune_num_variants": (_c_int, []),
     "plato_agg_tune_set_launch_groups": (None, [_c_u64]),
+    "plato_agg_tune_set_entrywise_block": (None, [_c_int]),
     "plato_agg_tune_describe": (
         _c_int,
         [_c_int, ctypes.POINTER(_c_int), ctypes.POINTER(_c_int), ctypes.POINTER(_c_int),

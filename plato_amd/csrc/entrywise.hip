@@ -345,7 +345,31 @@ __device__ __forceinline__ f4 ew_post(const EwArgs& a, f4 acc, f4 b, f4 noise, b
   return u;
 }
 
+// One element of a chunk's partial float4 group, or of an int64 entry: its K clients walked in order
+// with kEwSU independent loads per round trip (a one-load-at-a-time walk is K round trips to HBM).
+constexpr int kEwSU = 16;
+
 template <bool HAS_BASE>
+__device__ __forceinline__ float ew_f32_scalar(const EwArgs& a, const float* wrow, uint64_t e) {
+  const float b = HAS_BASE ? a.base_f[e] : 0.f;
+  const int K = a.K;
+  float acc = 0.f;
+  int i = 0;
+  for (; i + kEwSU <= K; i += kEwSU) {
+    float x[kEwSU];
+#pragma unroll
+    for (int u = 0; u < kEwSU; ++u) x[u] = sld(a.xf, i + u)[e];
+#pragma unroll
+    for (int u = 0; u < kEwSU; ++u) acc = acc + (HAS_BASE ? x[u] - b : x[u]) * sld(wrow, i + u);
+  }
+  for (; i < K; ++i) {
+    const float x = sld(a.xf, i)[e];
+    acc = acc + (HAS_BASE ? x - b : x) * sld(wrow, i);
+  }
+  return acc;
+}
+
+template <bool HAS_BASE, int B>
 __device__ void ew_f32_chunk(const EwArgs& a, uint32_t c) {
   const Chunk ch = load_chunk(a.cf, c, a.n_f32);
   const uint64_t n4 = a.n_f32 / 4;
@@ -353,7 +377,7 @@ __device__ void ew_f32_chunk(const EwArgs& a, uint32_t c) {
   const float* wrow = a.w + uint64_t(ch.entry) * a.K;
   const int K = a.K;
   const bool has_noise = a.noise_f != nullptr;
-  for (uint64_t g = g0 + threadIdx.x; g < g1; g += kBlock) {
+  for (uint64_t g = g0 + threadIdx.x; g < g1; g += B) {
     const uint64_t e0 = 4 * g;
     const bool full = e0 >= ch.begin && e0 + 4 <= ch.end;  // all 4 elements in the chunk (=> in range)
     if (full && g < n4) {
@@ -382,31 +406,41 @@ __device__ void ew_f32_chunk(const EwArgs& a, uint32_t c) {
       for (int q = 0; q < 4; ++q) {
         const uint64_t e = e0 + q;
         if (e < ch.begin || e >= ch.end) continue;
-        const float b = HAS_BASE ? a.base_f[e] : 0.f;
-        float acc = 0.f;
-        for (int i = 0; i < K; ++i) {
-          const float x = sld(a.xf, i)[e];
-          const float d = HAS_BASE ? x - b : x;
-          acc = acc + d * sld(wrow, i);
-        }
+        const float acc = ew_f32_scalar<HAS_BASE>(a, wrow, e);
         float u = acc * a.scale;
         if (has_noise) u = u + a.noise_f[e] * a.noise_scale;
-        if (HAS_BASE && (a.flags & PLATO_AGG_ADD_BASE)) u = b + u;
+        if (HAS_BASE && (a.flags & PLATO_AGG_ADD_BASE)) u = a.base_f[e] + u;
         a.out_f[e] = u;
       }
     }
   }
 }
 
-template <bool HAS_BASE>
+template <bool HAS_BASE, int B>
 __device__ void ew_i64_chunk(const EwArgs& a, uint32_t cc) {
+  typedef __attribute__((address_space(1))) const int64_t gi64;
   const Chunk ch = load_chunk(a.ci, cc, a.n_i64);
   const float* wrow = a.w + uint64_t(ch.entry) * a.K;
-  for (uint64_t e = ch.begin + threadIdx.x; e < ch.end; e += kBlock) {
+  const int K = a.K;
+  for (uint64_t e = ch.begin + threadIdx.x; e < ch.end; e += B) {
+    // torch's int64 subtraction wraps; the promotion to fp32 happens after (i64_delta)
+    const int64_t bv = HAS_BASE ? a.base_i[e] : 0;
     float acc = 0.f;
-    for (int i = 0; i < a.K; ++i) {
-      const float d = i64_delta(sld(a.xi, i), HAS_BASE ? a.base_i : nullptr, e);
-      acc = acc + d * sld(wrow, i);
+    int i = 0;
+    for (; i + kEwSU <= K; i += kEwSU) {
+      int64_t x[kEwSU];
+#pragma unroll
+      for (int u = 0; u < kEwSU; ++u) x[u] = ((gi64*)sld(a.xi, i + u))[e];
+#pragma unroll
+      for (int u = 0; u < kEwSU; ++u) {
+        const int64_t d = HAS_BASE ? (int64_t)((uint64_t)x[u] - (uint64_t)bv) : x[u];
+        acc = acc + (float)d * sld(wrow, i + u);
+      }
+    }
+    for (; i < K; ++i) {
+      const int64_t x = ((gi64*)sld(a.xi, i))[e];
+      const int64_t d = HAS_BASE ? (int64_t)((uint64_t)x - (uint64_t)bv) : x;
+      acc = acc + (float)d * sld(wrow, i);
     }
     float u = acc * a.scale;
     if (a.noise_if) u = u + a.noise_if[e] * a.noise_scale;
@@ -416,13 +450,37 @@ __device__ void ew_i64_chunk(const EwArgs& a, uint32_t cc) {
   }
 }
 
-template <bool HAS_BASE>
-__global__ __launch_bounds__(kBlock) void fedavg_entrywise_kernel(EwArgs a) {
+// The int64 chunks are the grid's first blocks (dispatched first, their K-client walks run beside the
+// stream instead of after it), the fp32 chunks follow.  B threads per chunk; the engine's chunk size is
+// B x 2 float4 groups (FedAvgEngine.ENTRYWISE_CHUNK).
+template <bool HAS_BASE, int B>
+__global__ __launch_bounds__(B) void fedavg_entrywise_kernel(EwArgs a) {
   const uint32_t c = blockIdx.x;
-  if (c < a.ncf) {
-    ew_f32_chunk<HAS_BASE>(a, c);
+  if (c < a.nci) {
+    ew_i64_chunk<HAS_BASE, B>(a, c);
   } else {
-    ew_i64_chunk<HAS_BASE>(a, c - a.ncf);
+    ew_f32_chunk<HAS_BASE, B>(a, c - a.nci);
+  }
+}
+
+// threads per fedavg_entrywise workgroup: one wave, as the FedAvg kernel
+constexpr int kEwBlock = 64;
+#ifdef PLATO_AGG_TUNE
+int g_ew_block = 0;  // plato_agg_tune_set_entrywise_block: 0 = kEwBlock
+#endif
+
+template <bool HAS_BASE>
+void launch_entrywise(const EwArgs& a, uint32_t nc, hipStream_t stream) {
+  int blk = kEwBlock;
+#ifdef PLATO_AGG_TUNE
+  if (g_ew_block) blk = g_ew_block;
+#endif
+  if (blk == 256) {
+    hipLaunchKernelGGL((fedavg_entrywise_kernel<HAS_BASE, 256>), dim3(nc), dim3(256), 0, stream, a);
+  } else if (blk == 128) {
+    hipLaunchKernelGGL((fedavg_entrywise_kernel<HAS_BASE, 128>), dim3(nc), dim3(128), 0, stream, a);
+  } else {
+    hipLaunchKernelGGL((fedavg_entrywise_kernel<HAS_BASE, 64>), dim3(nc), dim3(64), 0, stream, a);
   }
 }
 
@@ -1080,12 +1138,18 @@ int plato_agg_fedavg_entrywise(const float* const* d_x_f32, const int64_t* const
   a.K = K;
   a.flags = flags;
   if (d_base_f32) {
-    hipLaunchKernelGGL(fedavg_entrywise_kernel<true>, dim3(uint32_t(nc)), dim3(kBlock), 0, stream, a);
+    launch_entrywise<true>(a, uint32_t(nc), stream);
   } else {
-    hipLaunchKernelGGL(fedavg_entrywise_kernel<false>, dim3(uint32_t(nc)), dim3(kBlock), 0, stream, a);
+    launch_entrywise<false>(a, uint32_t(nc), stream);
   }
   return launch_error("fedavg_entrywise launch");
 }
+
+#ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
+void plato_agg_tune_set_entrywise_block(int threads) {
+  g_ew_block = (threads == 64 || threads == 128 || threads == 256) ? threads : 0;
+}
+#endif
 
 }  // extern "C"
 

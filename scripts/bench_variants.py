@@ -44,6 +44,9 @@ def main():
                          "thermal drift hit every kernel alike); each round times each kernel --reps times")
     ap.add_argument("--ew-chunks", default=None,
                     help="comma-separated fedavg_entrywise chunk sizes to time besides the engine's (tuning)")
+    ap.add_argument("--ew-shapes", default=None,
+                    help="comma-separated chunk:threads pairs of fedavg_entrywise to time through the tuning "
+                         "library (plato_agg_tune_set_entrywise_block), e.g. 2048:256,512:64")
     ap.add_argument("--norm-order", default="longest", choices=["longest", "layout"],
                     help="entry order of the norms launch (longest first = the engine's)")
     args = ap.parse_args()
@@ -116,8 +119,14 @@ def main():
                   None, _ptr(cf), cf.shape[0], _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(out_f),
                   _ptr(out_i), n_f, n_i, h)
 
-    def run_entrywise(cap=None):
+    def run_entrywise(cap=None, threads=None):
         cf, ci = chunks(cap or engine.ENTRYWISE_CHUNK)
+        if threads is not None:  # the tuning library's copy of the entry point, at this workgroup size
+            _lib.tune().plato_agg_tune_set_entrywise_block(threads)
+            _lib.tune_call("plato_agg_fedavg_entrywise", _ptr(tf), _ptr(ti), k, _ptr(w_ek), n_e, _ptr(cf),
+                           cf.shape[0], _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(noise),
+                           _ptr(noise_i), -1.2, 0.001, _lib.PLATO_AGG_ADD_BASE, _ptr(out_f), _ptr(out_i), n_f, n_i, h)
+            return
         _lib.call("plato_agg_fedavg_entrywise", _ptr(tf), _ptr(ti), k, _ptr(w_ek), n_e, _ptr(cf), cf.shape[0],
                   _ptr(ci), ci.shape[0], _ptr(base.f32), _ptr(base.i64), _ptr(noise), _ptr(noise_i), -1.2, 0.001,
                   _lib.PLATO_AGG_ADD_BASE, _ptr(out_f), _ptr(out_i), n_f, n_i, h)
@@ -155,6 +164,11 @@ def main():
     if args.ew_chunks:  # tuning: fedavg_entrywise at other chunk sizes
         for cap in [int(x) for x in args.ew_chunks.split(",")]:
             kernels[f"entrywise_v{cap}"] = ((lambda cap=cap: run_entrywise(cap)), kernels["entrywise"][1])
+    if args.ew_shapes:  # tuning: fedavg_entrywise at other (chunk, workgroup size) pairs
+        for pair in args.ew_shapes.split(","):
+            cap, thr = (int(x) for x in pair.split(":"))
+            kernels[f"entrywise_v{cap}x{thr}"] = ((lambda cap=cap, thr=thr: run_entrywise(cap, thr)),
+                                                  kernels["entrywise"][1])
     if args.norm_variants:  # tuning: every plato_agg_tune_entry_norms variant
         for v in range(_lib.tune().plato_agg_tune_num_entry_norms_variants()):
             kernels[f"norms_v{v}"] = ((lambda v=v: run_norms(v)), kernels["norms"][1])
