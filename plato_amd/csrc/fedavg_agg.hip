@@ -597,13 +597,14 @@ struct Bf16Args {
   float* out_if;
   uint64_t n8, n_f32, n_i64;
   uint32_t nb_vec, nb_vec_full;
+  uint32_t nb_scalar;  // workgroups of scalar items: the FIRST blocks of the grid
   uint64_t x_off;  // element offset of this launch's range in every client arena
   int K;
 };
 
-template <bool TWO, bool CHECK, int U>
+template <bool TWO, bool CHECK, int U, int B>
 __device__ __forceinline__ void bf16_body(const Bf16Args& a, uint32_t blk) {
-  const uint64_t e8 = uint64_t(blk) * 256 + threadIdx.x;
+  const uint64_t e8 = uint64_t(blk) * B + threadIdx.x;
   const bool live = !CHECK || e8 < a.n8;
   const uint64_t g = CHECK ? (e8 < a.n8 ? e8 : a.n8 - 1) : e8;
   const uint32_t xoff = uint32_t(g * 16u);   // bf16 bytes
@@ -664,10 +665,10 @@ __device__ __forceinline__ void bf16_body(const Bf16Args& a, uint32_t blk) {
 typedef unsigned int u2 __attribute__((ext_vector_type(2)));
 typedef __attribute__((address_space(1))) const u2 gu2;
 
-template <bool TWO, bool CHECK, int U>
+template <bool TWO, bool CHECK, int U, int B>
 __device__ __forceinline__ void bf16_body4(const Bf16Args& a, uint32_t blk) {
   const uint64_t n4 = a.n8 * 2;  // groups of 4 (n8 counts groups of 8 in this mode: see launcher)
-  const uint64_t e4 = uint64_t(blk) * 256 + threadIdx.x;
+  const uint64_t e4 = uint64_t(blk) * B + threadIdx.x;
   const bool live = !CHECK || e4 < n4;
   const uint64_t g = CHECK ? (e4 < n4 ? e4 : n4 - 1) : e4;
   const uint32_t xoff = uint32_t(g * 8u);
@@ -703,66 +704,79 @@ __device__ __forceinline__ void bf16_body4(const Bf16Args& a, uint32_t blk) {
   if (live) st4_off<true>(a.out_f, foff, b + acc);
 }
 
+// One scalar item (fp32 tail element or int64 entry): K clients in order, kSU loads per round trip.
 template <bool TWO>
 __device__ __forceinline__ void bf16_scalar(const Bf16Args& a, uint64_t j) {
   const uint64_t tail = a.n_f32 - 8 * a.n8;
   const int K = a.K;
-  if (j < tail) {
-    const uint64_t e = 8 * a.n8 + j;
-    const float b = a.base_f[e];
-    float acc = 0.f;
-    for (int i = 0; i < K; ++i) {
-      float t = (bf16_at(sld(a.xf, i), a.x_off + e) - b) * sld(a.w, i);
-      if constexpr (TWO) t = t * sld(a.s, i);
+  const bool f32 = j < tail;
+  const uint64_t e = f32 ? 8 * a.n8 + j : j - tail;
+  if (!f32 && e >= a.n_i64) return;
+  const uint16_t* const* xs = f32 ? a.xf : a.xi;
+  const uint64_t xe = f32 ? a.x_off + e : e;
+  const float b = f32 ? a.base_f[e] : (float)a.base_i[e];
+  float acc = 0.f;
+  int i = 0;
+  for (; i + kSU <= K; i += kSU) {
+    float x[kSU];
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) x[u] = bf16_at(sld(xs, i + u), xe);
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) {
+      float t = (x[u] - b) * sld(a.w, i + u);
+      if constexpr (TWO) t = t * sld(a.s, i + u);
       acc = acc + t;
     }
-    a.out_f[e] = b + acc;
-    return;
   }
-  const uint64_t e = j - tail;
-  if (e >= a.n_i64) return;
-  const float b = (float)a.base_i[e];
-  float acc = 0.f;
-  for (int i = 0; i < K; ++i) {
-    float t = (bf16_at(sld(a.xi, i), e) - b) * sld(a.w, i);
+  for (; i < K; ++i) {
+    float t = (bf16_at(sld(xs, i), xe) - b) * sld(a.w, i);
     if constexpr (TWO) t = t * sld(a.s, i);
     acc = acc + t;
   }
-  a.out_if[e] = b + acc;
+  if (f32) {
+    a.out_f[e] = b + acc;
+  } else {
+    a.out_if[e] = b + acc;
+  }
 }
 
-template <bool TWO, int LANE, int U>
-__global__ __launch_bounds__(256) void fedavg_bf16_kernel(Bf16Args a) {
-  const uint32_t blk = blockIdx.x;
+template <bool TWO, int LANE, int U, int B>
+__global__ __launch_bounds__(B) void fedavg_bf16_kernel(Bf16Args a) {
+  // scalar items first (dispatched first, beside the stream: see fedavg_kernel)
+  if (blockIdx.x < a.nb_scalar) {
+    bf16_scalar<TWO>(a, uint64_t(blockIdx.x) * B + threadIdx.x);
+    return;
+  }
+  const uint32_t blk = blockIdx.x - a.nb_scalar;
   if (blk < a.nb_vec_full) {
-    if constexpr (LANE == 8) bf16_body<TWO, false, U>(a, blk); else bf16_body4<TWO, false, U>(a, blk);
+    if constexpr (LANE == 8) bf16_body<TWO, false, U, B>(a, blk); else bf16_body4<TWO, false, U, B>(a, blk);
   } else if (blk < a.nb_vec) {
-    if constexpr (LANE == 8) bf16_body<TWO, true, U>(a, blk); else bf16_body4<TWO, true, U>(a, blk);
-  } else {
-    bf16_scalar<TWO>(a, uint64_t(blk - a.nb_vec) * 256 + threadIdx.x);
+    if constexpr (LANE == 8) bf16_body<TWO, true, U, B>(a, blk); else bf16_body4<TWO, true, U, B>(a, blk);
   }
 }
 
 using Bf16Fn = void (*)(const Bf16Args&, dim3, hipStream_t);
-template <bool TWO, int LANE, int U>
+template <bool TWO, int LANE, int U, int B>
 void launch_bf16(const Bf16Args& a, dim3 g, hipStream_t st) {
-  hipLaunchKernelGGL((fedavg_bf16_kernel<TWO, LANE, U>), g, dim3(256), 0, st, a);
+  hipLaunchKernelGGL((fedavg_bf16_kernel<TWO, LANE, U, B>), g, dim3(B), 0, st, a);
 }
 struct Bf16Variant {
-  int lane, u;
+  int lane, u, block;
   Bf16Fn fn[2];
 };
-// variant 0 is the default of plato_agg_fedavg_weights_bf16
+// variant 0 is the default of plato_agg_fedavg_weights_bf16: one-wave workgroups, as fedavg_kernel's
 #ifdef PLATO_AGG_TUNE
 const Bf16Variant kBf16Variants[] = {
-    {4, 8, {&launch_bf16<false, 4, 8>, &launch_bf16<true, 4, 8>}},
-    {8, 8, {&launch_bf16<false, 8, 8>, &launch_bf16<true, 8, 8>}},
-    {4, 16, {&launch_bf16<false, 4, 16>, &launch_bf16<true, 4, 16>}},
-    {8, 4, {&launch_bf16<false, 8, 4>, &launch_bf16<true, 8, 4>}},
+    {4, 8, 64, {&launch_bf16<false, 4, 8, 64>, &launch_bf16<true, 4, 8, 64>}},
+    {8, 8, 256, {&launch_bf16<false, 8, 8, 256>, &launch_bf16<true, 8, 8, 256>}},
+    {4, 16, 256, {&launch_bf16<false, 4, 16, 256>, &launch_bf16<true, 4, 16, 256>}},
+    {8, 4, 256, {&launch_bf16<false, 8, 4, 256>, &launch_bf16<true, 8, 4, 256>}},
+    {4, 8, 256, {&launch_bf16<false, 4, 8, 256>, &launch_bf16<true, 4, 8, 256>}},  // the rounds 2-4 default
+    {8, 8, 64, {&launch_bf16<false, 8, 8, 64>, &launch_bf16<true, 8, 8, 64>}},
 };
 #else
 const Bf16Variant kBf16Variants[] = {
-    {4, 8, {&launch_bf16<false, 4, 8>, &launch_bf16<true, 4, 8>}},
+    {4, 8, 64, {&launch_bf16<false, 4, 8, 64>, &launch_bf16<true, 4, 8, 64>}},
 };
 #endif
 constexpr int kNumBf16Variants = sizeof(kBf16Variants) / sizeof(kBf16Variants[0]);
@@ -1179,13 +1193,14 @@ int run_bf16_range(const Bf16Variant& vr, const uint16_t* const* d_x_bf16, const
   a.n_i64 = n_i64;
   a.K = K;
   const uint64_t groups = vr.lane == 8 ? a.n8 : 2 * a.n8;
-  const uint64_t nb_vec = (groups + 255) / 256;
+  const uint64_t nb_vec = (groups + vr.block - 1) / vr.block;
   const uint64_t n_scalar = (n_f32 - 8 * a.n8) + n_i64;
-  const uint64_t nb_scalar = (n_scalar + 255) / 256;
+  const uint64_t nb_scalar = (n_scalar + vr.block - 1) / vr.block;
   if (nb_vec + nb_scalar > 0x7fffffffull || a.n8 * 32ull > 0xffffffffull)
     return fail(PLATO_AGG_EINVAL, "launch range exceeds 4 GiB (internal split error)");
   a.nb_vec = uint32_t(nb_vec);
-  a.nb_vec_full = uint32_t(groups / 256);
+  a.nb_vec_full = uint32_t(groups / vr.block);
+  a.nb_scalar = uint32_t(nb_scalar);
   vr.fn[d_s ? 1 : 0](a, dim3(uint32_t(nb_vec + nb_scalar)), stream);
   return check_launch("fedavg_bf16 kernel launch");
 }
