@@ -991,13 +991,14 @@ struct W64Args {
   float* out_if;
   uint64_t n4, n_f32, n_i64;
   uint32_t nb_vec;
+  uint32_t nb_scalar;  // workgroups of scalar items: the FIRST blocks of the grid (see fedavg_kernel)
   int K;
 };
 
 template <bool HAS_BASE>
 __global__ __launch_bounds__(256) void fedavg_w64_kernel(W64Args a) {
-  const uint32_t blk = blockIdx.x;
-  if (blk < a.nb_vec) {
+  const uint32_t blk = blockIdx.x - a.nb_scalar;
+  if (blockIdx.x >= a.nb_scalar) {
     const uint64_t g = uint64_t(blk) * 256 + threadIdx.x;
     if (g >= a.n4) return;
     const uint32_t off = uint32_t(g * 16u);
@@ -1030,13 +1031,26 @@ __global__ __launch_bounds__(256) void fedavg_w64_kernel(W64Args a) {
     st4_off<true>(a.out_f, off, HAS_BASE ? f4_add(b, acc) : acc);
     return;
   }
-  const uint64_t j = uint64_t(blk - a.nb_vec) * 256 + threadIdx.x;
+  // scalar items: kSU client loads per round trip, then the in-order adds
+  const uint64_t j = uint64_t(blockIdx.x) * 256 + threadIdx.x;
   const uint64_t tail = a.n_f32 - 4 * a.n4;
+  const int K = a.K;
   if (j < tail) {
     const uint64_t e = 4 * a.n4 + j;
     const float b = HAS_BASE ? a.base_f[e] : 0.f;
     float acc = 0.f;
-    for (int i = 0; i < a.K; ++i) {
+    int i = 0;
+    for (; i + kSU <= K; i += kSU) {
+      float x[kSU];
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) x[u] = ((gfloat*)sld(a.xf, i + u))[e];
+#pragma unroll
+      for (int u = 0; u < kSU; ++u) {
+        const float d = HAS_BASE ? x[u] - b : x[u];
+        acc = float(double(acc) + double(d) * sld(a.w64, i + u));
+      }
+    }
+    for (; i < K; ++i) {
       const float x = sld(a.xf, i)[e];
       const float d = HAS_BASE ? x - b : x;
       acc = float(double(acc) + double(d) * sld(a.w64, i));
@@ -1046,9 +1060,21 @@ __global__ __launch_bounds__(256) void fedavg_w64_kernel(W64Args a) {
   }
   const uint64_t e = j - tail;
   if (e >= a.n_i64) return;
+  typedef __attribute__((address_space(1))) const int64_t gi64;
   const int64_t b = HAS_BASE ? a.base_i[e] : 0;
   float acc = 0.f;
-  for (int i = 0; i < a.K; ++i) {
+  int i = 0;
+  for (; i + kSU <= K; i += kSU) {
+    int64_t x[kSU];
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) x[u] = ((gi64*)sld(a.xi, i + u))[e];
+#pragma unroll
+    for (int u = 0; u < kSU; ++u) {
+      const int64_t d = HAS_BASE ? (int64_t)((uint64_t)x[u] - (uint64_t)b) : x[u];
+      acc = acc + (float)d * sld(a.wi, i + u);
+    }
+  }
+  for (; i < K; ++i) {
     const int64_t x = sld(a.xi, i)[e];
     const int64_t d = HAS_BASE ? (int64_t)((uint64_t)x - (uint64_t)b) : x;
     acc = acc + (float)d * sld(a.wi, i);
@@ -1130,6 +1156,7 @@ int plato_agg_fedavg_w64(const float* const* d_x_f32, const int64_t* const* d_x_
   const uint64_t nb_vec = (a.n4 + 255) / 256;
   const uint64_t nb_scalar = ((n_f32 - 4 * a.n4) + n_i64 + 255) / 256;
   a.nb_vec = uint32_t(nb_vec);
+  a.nb_scalar = uint32_t(nb_scalar);
   const dim3 grid(uint32_t(nb_vec + nb_scalar));
   if (has_base) {
     hipLaunchKernelGGL(fedavg_w64_kernel<true>, grid, dim3(256), 0, stream, a);

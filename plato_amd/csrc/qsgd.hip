@@ -206,6 +206,10 @@ __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
   }
 }
 
+// The int64 entries' codes: K clients in order, one code load at a time.  Their chunks are the grid's
+// first blocks, so these K round trips run beside the stream from its start (at the end of the grid they
+// outlasted it).  Batching the loads, as the FedAvg kernel does, raised the kernel's VGPR count past the
+// 64 that keep two 512-thread workgroups per CU (0.353 against 0.311 ms, profiles/r05k_qsgd.log).
 template <int kBlock, bool TWO>
 __device__ void qsgd_i64_chunk(const QArgs& a, uint32_t cc) {
   const Chunk ch = load_chunk(a.ti, cc, a.n_i64);
@@ -421,22 +425,22 @@ template <int kBlock, int kU, bool TWO, int kGE, int kP>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) void fedavg_qsgd_pipe_kernel(
     QArgs a) {
   __shared__ float lut[2][kU][256];
-  const uint32_t c = blockIdx.x;
-  if (c < a.ncf) {
-    qsgd_f32_chunk_pipe<kBlock, kU, TWO, kGE, kP>(a, c, lut);
+  const uint32_t c = blockIdx.x;  // the int64 chunks first (qsgd_i64_chunk)
+  if (c >= a.nci) {
+    qsgd_f32_chunk_pipe<kBlock, kU, TWO, kGE, kP>(a, c - a.nci, lut);
   } else {
-    qsgd_i64_chunk<kBlock, TWO>(a, c - a.ncf);
+    qsgd_i64_chunk<kBlock, TWO>(a, c);
   }
 }
 
 template <int kBlock, int kU, bool TWO, int kGE = kG, bool kSM = false>
 __global__ __launch_bounds__(kBlock) void fedavg_qsgd_kernel(QArgs a) {
   __shared__ float lut[kU][256];
-  const uint32_t c = blockIdx.x;
-  if (c < a.ncf) {
-    qsgd_f32_chunk<kBlock, kU, TWO, kGE, kSM>(a, c, lut);
+  const uint32_t c = blockIdx.x;  // the int64 chunks first (qsgd_i64_chunk)
+  if (c >= a.nci) {
+    qsgd_f32_chunk<kBlock, kU, TWO, kGE, kSM>(a, c - a.nci, lut);
   } else {
-    qsgd_i64_chunk<kBlock, TWO>(a, c - a.ncf);
+    qsgd_i64_chunk<kBlock, TWO>(a, c);
   }
 }
 
@@ -460,17 +464,18 @@ struct QVariant {
 // form of rounds 2-3 and its timing probes.
 #ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so (scripts/bench_variants.py, tests/test_qsgd_gpu.py)
 const QVariant kQVariants[] = {
-    {512, 8, 8, {&launch_q<512, 8, false, 8, true>, &launch_q<512, 8, true, 8, true>}},  // 0 (default)
+    {256, 8, 8, {&launch_q<256, 8, false, 8, true>, &launch_q<256, 8, true, 8, true>}},  // 0 (default, round 5)
     {512, 4, 8, {&launch_qp<512, 4, false, 8>, &launch_qp<512, 4, true, 8>}},        // 1: pipelined (rounds 2-3)
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 1>, &launch_qp<512, 4, true, 8, 1>}},  // 2: probe, no code loads
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 2>, &launch_qp<512, 4, true, 8, 2>}},  // 3: probe, no lookups
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 3>, &launch_qp<512, 4, true, 8, 3>}},  // 4: probe, neither
     {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},       // 5: round 1 (vector max_v loads)
-    {256, 8, 8, {&launch_q<256, 8, false, 8, true>, &launch_q<256, 8, true, 8, true>}},  // 6
+    {512, 8, 8, {&launch_q<512, 8, false, 8, true>, &launch_q<512, 8, true, 8, true>}},  // 6: the round-4 default
 };
 #else  // libplato_agg.so: the default only
+// 256 threads: 0.309 against 0.320 ms for the round-4 512-thread form, interleaved (profiles/r05l_qsgd.log)
 const QVariant kQVariants[] = {
-    {512, 8, 8, {&launch_q<512, 8, false, 8, true>, &launch_q<512, 8, true, 8, true>}},  // 0 (default)
+    {256, 8, 8, {&launch_q<256, 8, false, 8, true>, &launch_q<256, 8, true, 8, true>}},  // 0 (default)
 };
 #endif
 constexpr int kNumQVariants = sizeof(kQVariants) / sizeof(kQVariants[0]);
