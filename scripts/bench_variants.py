@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--qsgd-codes", default="qsgd", choices=["qsgd", "uniform"])
     ap.add_argument("--norm-variants", action="store_true", help="also time each entry_norms kernel variant")
+    ap.add_argument("--norm-list", default=None, help="comma-separated entry_norms variants to time (instead of all)")
     ap.add_argument("--qsgd-variants", action="store_true", help="also time each fedavg_qsgd kernel variant")
     ap.add_argument("--qsgd-list", default=None, help="comma-separated fedavg_qsgd variants to time (instead of all)")
     ap.add_argument("--interleave", type=int, default=0,
@@ -169,8 +170,9 @@ def main():
             cap, thr = (int(x) for x in pair.split(":"))
             kernels[f"entrywise_v{cap}x{thr}"] = ((lambda cap=cap, thr=thr: run_entrywise(cap, thr)),
                                                   kernels["entrywise"][1])
-    if args.norm_variants:  # tuning: every plato_agg_tune_entry_norms variant
-        for v in range(_lib.tune().plato_agg_tune_num_entry_norms_variants()):
+    if args.norm_variants or args.norm_list:  # tuning: every (or the listed) plato_agg_tune_entry_norms variant
+        for v in ([int(x) for x in args.norm_list.split(",")] if args.norm_list
+                  else range(_lib.tune().plato_agg_tune_num_entry_norms_variants())):
             kernels[f"norms_v{v}"] = ((lambda v=v: run_norms(v)), kernels["norms"][1])
     selected = [(name, fn, nbytes) for name, (fn, nbytes) in kernels.items()
                 if not args.only or name.split("_v")[0] in args.only.split(",")]
