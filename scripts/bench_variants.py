@@ -87,17 +87,17 @@ def main():
     # "uniform": every byte equally likely (worst case for the LDS decode tables).
     qslab = ClientSlab(layout, k, dev, codec="qsgd")
 
-    def codes(shape):
+    def codes(shape, r):
         if args.qsgd_codes == "uniform":
             return torch.randint(0, 256, shape, dtype=torch.uint8, device=dev)
-        g = torch.Generator(device=dev).manual_seed(1)
+        g = torch.Generator(device=dev).manual_seed(1 + r)  # every client its own codes
         mag = torch.floor(torch.randn(shape, device=dev, generator=g).abs() * (63 / 5)
                           + torch.rand(shape, device=dev, generator=g)).clamp_(0, 127)
         sign = (torch.rand(shape, device=dev, generator=g) < 0.5).to(torch.float32) * 128
         return (mag + sign).to(torch.uint8)
 
     for r in range(k):
-        qslab.f32[r].copy_(codes(qslab.f32[r].shape))
+        qslab.f32[r].copy_(codes(qslab.f32[r].shape, r))
     qslab.i64.copy_(codes(qslab.i64.shape))
     qpf, qpi = qslab.row_pointers(range(k))
     qtf = torch.from_numpy(qpf).to(dev)
