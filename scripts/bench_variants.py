@@ -98,7 +98,7 @@ def main():
 
     for r in range(k):
         qslab.f32[r].copy_(codes(qslab.f32[r].shape, r))
-    qslab.i64.copy_(codes(qslab.i64.shape))
+    qslab.i64.copy_(codes(qslab.i64.shape, k))
     qpf, qpi = qslab.row_pointers(range(k))
     qtf = torch.from_numpy(qpf).to(dev)
     qti = torch.from_numpy(qpi).to(dev)
