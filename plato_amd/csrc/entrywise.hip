@@ -1027,6 +1027,98 @@ __global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rs_kernel(NormArgs a
   rs_pair<T, P, D, HAS_BASE, PRIO, kSplit, kOW>(a, blockIdx.x, wave, lane, dbuf);
 }
 
+// ---------------------------------------------------------------------------
+// entry_norms, C clients of one entry per workgroup (register-staged, split launch only).  The
+// one-pair kernel above streams the baseline b once per (entry, client): at K = 128 the L2-served b
+// re-reads take as many of a CU's ~110 in-flight read slots as the client bytes themselves
+// ("What bounds the streams").  Here C chain waves (one per client, the same chains
+// and order as pc_chain) share P producer waves that load each b tile once and the C clients' x
+// tiles beside it, and write C transposed d tiles; everyone meets at one s_barrier per tile (the C
+// pairs of one entry have the same tile count).  A ragged last group (K mod C) recomputes client
+// K - 1 in its idle chain waves and does not store it.
+// ---------------------------------------------------------------------------
+template <int T, int P, int D, int C, bool HAS_BASE>
+__device__ void rsc_produce(const NormArgs& a, const Chunk ch, const gf4* const (&xs)[C], int w, int lane,
+                            float* dbuf, uint64_t ntiles, uint64_t nbar) {
+  constexpr int kTS = DTile<T, true>::kTS, kSize = DTile<T, true>::kSize;
+  constexpr int kIt = T / 256 / P;
+  static_assert(kIt >= 1 && kIt * P * 256 == T, "whole iterations per producer");
+  constexpr int kOps = C + (HAS_BASE ? 1 : 0);
+  static_assert((D - 1) * kIt * kOps < 64, "vmcnt range");
+  const uint64_t g_first = ch.begin >> 2;
+  const uint64_t gmax = (a.n_f32 >> 2) - 1;
+  const gf4* bs = (const gf4*)(a.base_f);
+  f4 xr[D][kIt][C], br[D][kIt];
+  auto issue = [&](f4(&xv)[kIt][C], f4(&bv)[kIt], uint64_t t) {
+#pragma unroll
+    for (int it = 0; it < kIt; ++it) {
+      uint64_t g = g_first + t * (T / 4) + uint64_t(it * P + w) * 64 + lane;
+      g = g < gmax ? g : gmax;
+#pragma unroll
+      for (int c = 0; c < C; ++c) xv[it][c] = __builtin_nontemporal_load(xs[c] + g);
+      if (HAS_BASE) bv[it] = bs[g];
+    }
+  };
+#pragma unroll
+  for (int j = 0; j < D; ++j) issue(xr[j], br[j], uint64_t(j) < ntiles ? uint64_t(j) : ntiles - 1);
+  for (uint64_t t0 = 0; t0 < nbar; t0 += D) {
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      const uint64_t tt = t0 + j;
+      wait_vmcnt<(D - 1) * kIt * kOps>();  // tile tt's loads (the later trips stay in flight)
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        float* dt = dbuf + (2 * c + int(tt & 1)) * kSize;
+#pragma unroll
+        for (int it = 0; it < kIt; ++it) {
+          f4 dv = xr[j][it][c];
+          if (HAS_BASE) dv = dv - br[j][it];  // fp32, as compute_weight_deltas
+          // tile elements 256 r + 4 lane + k: chain 4 (lane & 1) + k, step 32 r + lane / 2
+          float* col = dt + 32 * (it * P + w) + (lane >> 1) + 4 * (lane & 1) * kTS;
+          col[0] = dv.x;
+          col[kTS] = dv.y;
+          col[2 * kTS] = dv.z;
+          col[3 * kTS] = dv.w;
+        }
+      }
+      const uint64_t nt = tt + D;
+      issue(xr[j], br[j], nt < ntiles ? nt : ntiles - 1);
+      wait_lgkm0();  // d tiles written (the loads stay in flight)
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+      __builtin_amdgcn_s_barrier();  // tile tt ready; the chain waves are done with tile tt - 1
+      __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    }
+  }
+  wait_vmcnt<0>();
+}
+
+template <int T, int P, int D, int C, bool HAS_BASE, int PRIO, int kOW>
+__global__ __launch_bounds__(64 * (C + P)) void entry_norms_rsc_kernel(NormArgs a) {
+  constexpr int kSize = DTile<T, true>::kSize;
+  __shared__ __attribute__((aligned(16))) float dbuf[2 * C * kSize];
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  const uint32_t groups = uint32_t((a.K + C - 1) / C);
+  const uint32_t ent = blockIdx.x / groups;  // entry-major over the (longest-first) fp32 table
+  const int i0 = int(blockIdx.x % groups) * C;
+  const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
+  if (uint64_t(ch.end) > (a.n_f32 & ~3ull)) return;  // the arena's partial last float4 group: per-wave launch
+  const uint64_t ntiles = pc_ntiles<T>(ch), nbar = (ntiles + D - 1) / D * D;
+  if (wave >= C) {
+    __builtin_amdgcn_s_setprio(0);
+    if (!ntiles) return;
+    const gf4* xs[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) xs[c] = (const gf4*)sld(a.xf, i0 + c < a.K ? i0 + c : a.K - 1);
+    rsc_produce<T, P, D, C, HAS_BASE>(a, ch, xs, wave - C, lane, dbuf, ntiles, nbar);
+    return;
+  }
+  const int i = i0 + wave;
+  const float* x = sld(a.xf, i < a.K ? i : a.K - 1);
+  pc_chain_prio<PRIO>(a, ch);
+  const float acc = pc_chain<T, true, kOW>(ch, lane, dbuf + 2 * wave * kSize, kSize, nbar);
+  if (i < a.K) pc_finish<HAS_BASE>(a, ch, i, x, lane, acc);
+}
+
 bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
 
 int launch_error(const char* what) {
@@ -1178,6 +1270,19 @@ void launch_rs_split(const NormArgs& a, bool hb, dim3, hipStream_t st) {
     hipLaunchKernelGGL((entry_norms_kernel<false, true>), g2, dim3(kBlock), 0, st, a);
   }
 }
+template <int T, int P, int D, int C, int PRIO = -1, int kOW = 2>
+void launch_rsc_split(const NormArgs& a, bool hb, dim3, hipStream_t st) {
+  const dim3 g1{uint32_t(uint64_t(a.nef) * uint64_t((a.K + C - 1) / C))};
+  const uint64_t waves = (uint64_t(a.nef) + a.nei) * uint64_t(a.K);
+  const dim3 g2{uint32_t((waves + kBlock / 64 - 1) / (kBlock / 64))};
+  if (hb) {
+    if (a.nef) hipLaunchKernelGGL((entry_norms_rsc_kernel<T, P, D, C, true, PRIO, kOW>), g1, dim3(64 * (C + P)), 0, st, a);
+    hipLaunchKernelGGL((entry_norms_kernel<true, true>), g2, dim3(kBlock), 0, st, a);
+  } else {
+    if (a.nef) hipLaunchKernelGGL((entry_norms_rsc_kernel<T, P, D, C, false, PRIO, kOW>), g1, dim3(64 * (C + P)), 0, st, a);
+    hipLaunchKernelGGL((entry_norms_kernel<false, true>), g2, dim3(kBlock), 0, st, a);
+  }
+}
 #ifdef PLATO_AGG_TUNE
 void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
   const uint64_t threads = (uint64_t(a.nef) + a.nei) * uint64_t(a.K) * 64;  // a wave per pair
@@ -1201,12 +1306,23 @@ void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
 // at K = 128, interleaved (profiles/r04za_norms_k*.log; 76 VGPRs, six waves per SIMD); on a second box
 // 1.101 / 0.873 ms at K = 128 / 64 against 1.198 / 0.973, and neither long producers at priority 2,
 // 2 producers nor 3 tiles in flight beat it (1.12-1.20 / 0.88-0.89; profiles/r04zc_norms_k*.log).
-constexpr NormFn kNormDefault = &launch_rs_split<2048, 4, 2, -1, 2>;
+// Round 5, two clients of one entry per workgroup sharing the baseline tiles (entry_norms_rsc_kernel,
+// profiles/r05s-u_norms.log, interleaved, K = 32 / 64 / 96 / 128 / 256): <2048, 8, 2, C = 2> 0.93 / 0.94 /
+// 0.995 / 1.044-1.065 / 2.005 ms against the one-client default's 0.839 / 0.870 / 1.002 / 1.100-1.106 /
+// 2.228.  Where the 10,000 short pairs' traffic binds (K >= 96) the halved b reads win; below it the
+// long entries' serial chains bind, and a chain that shares its tile barrier with a second client's
+// runs ~10 % slower.  The default picks by K.  Measured and dropped: four clients per workgroup (1.18-1.26
+// at K = 128), three (1.19), and the long entries kept at one client per workgroup (1.18 at K = 128:
+// their ten-wave workgroups crowd the short pairs out; 0.86 at K = 32).
+constexpr int kNormShareK = 96;
+void launch_norms_default(const NormArgs& a, bool hb, dim3 g, hipStream_t st) {
+  if (a.K >= kNormShareK) launch_rsc_split<2048, 8, 2, 2>(a, hb, g, st);
+  else launch_rs_split<2048, 4, 2, -1, 2>(a, hb, g, st);
+}
+constexpr NormFn kNormDefault = &launch_norms_default;
 #ifdef PLATO_AGG_TUNE
 const NormFn kNormVariants[] = {
-    &launch_rs_split<2048, 4, 2, -1, 2>,  // 0: the default: register-staged, 4 producer waves, 2 tiles in
-                                          //    flight, the per-wave pairs (int64, partial last group) in a
-                                          //    second launch, one s_waitcnt per 32 chain steps
+    &launch_norms_default,         // 0: the default: one client per workgroup below K = 96, two from 96
     &launch_rs<2048, 2, 2>,        // 1: 2 producer waves, one launch (the first round-4 default)
     &launch_rs<2048, 2, 3, -2>,    // 2: 3 tiles in flight, the long entries' producers at priority 2
     &launch_pc<1024, 5>,           // 3: LDS-DMA producer / consumer, 1,024-element tiles (round 3, > 6,144 pairs)
@@ -1215,6 +1331,14 @@ const NormFn kNormVariants[] = {
     &launch_rs_split<2048, 4, 2, -1, 1>,  // 6: one s_waitcnt per 16 chain steps (64 VGPRs)
     &launch_rs_split<2048, 4, 2>,         // 7: the compiler's waits, one per ds_read_b128 (the first round-4
                                           //    split default)
+    &launch_rs_split<2048, 4, 2, -1, 2>,  // 8: the one-client shape (register-staged, 4 producer waves, 2 tiles
+                                          //    in flight, the per-wave pairs (int64, partial last group) in a
+                                          //    second launch, one s_waitcnt per 32 chain steps): the default below
+                                          //    K = 96, rounds 4-5's default at every K
+    &launch_rsc_split<2048, 8, 2, 2>,     // 9: two clients per workgroup, 8 producer waves: the default from K = 96
+    &launch_rsc_split<2048, 4, 2, 2>,     // 10: two clients, 4 producer waves
+    &launch_rsc_split<2048, 8, 3, 2>,     // 11: two clients, 3 tiles of loads in flight
+    &launch_rsc_split<2048, 8, 2, 4>,     // 12: four clients, 8 producer waves
 };
 constexpr int kNumNormVariants = sizeof(kNormVariants) / sizeof(kNormVariants[0]);
 #endif

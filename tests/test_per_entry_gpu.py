@@ -167,6 +167,44 @@ def test_entry_norm_kernels_agree_bitwise(engine, k, deltas):
             assert outs[0][:, e_i].tobytes() == ref.torch_cpu_norm_f32(np.ascontiguousarray(rows)).tobytes(), e.name
 
 
+@pytest.mark.parametrize("k,deltas", [(96, False), (97, False), (129, True)])
+def test_entry_norms_default_from_k96_matches_oracle(engine, k, deltas):
+    """The product entry point at K >= 96 (two clients of one entry per workgroup sharing the baseline
+    tiles; an odd K leaves a one-client last group) == torch CPU order, both arena tails."""
+    from plato_amd import _lib
+
+    for spec in (RING_SPEC, RING_SPEC[:-1] + [("z", (12291,), "f32")]):
+        layout = ArenaLayout.from_shapes(spec)
+        rng = np.random.default_rng(k)
+        dev = torch.device(DEV)
+        bf = rng.standard_normal(layout.row_f32).astype(np.float32)
+        bi = rng.integers(-1000, 1000, max(layout.row_i64, 1))
+        xs_f = (bf + 0.01 * rng.standard_normal((k, layout.row_f32))).astype(np.float32)
+        xs_i = bi + rng.integers(0, 9, (k, bi.size))
+        xf = torch.from_numpy(xs_f).to(dev)
+        xi = torch.from_numpy(xs_i).to(dev)
+        tf = torch.tensor([xf[i].data_ptr() for i in range(k)], dtype=torch.int64, device=dev)
+        ti = torch.tensor([xi[i].data_ptr() for i in range(k)], dtype=torch.int64, device=dev)
+        b_f = torch.from_numpy(bf).to(dev)
+        b_i = torch.from_numpy(bi).to(dev)
+        ef, ei = engine._norm_tables(layout)
+        n_e = len(layout.entries)
+        out = torch.full((k * n_e,), float("nan"), device=dev)
+        _lib.call("plato_agg_entry_norms_f32", tf.data_ptr(), ti.data_ptr(), k, None if deltas else b_f.data_ptr(),
+                  None if deltas else b_i.data_ptr(), ef.data_ptr(), ef.shape[0], ei.data_ptr(), ei.shape[0], n_e,
+                  layout.n_f32, layout.n_i64, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        got = out.cpu().numpy().reshape(k, n_e)
+        for e_i, e in enumerate(layout.entries):
+            if e.region == "f32":
+                rows = xs_f[:, e.offset:e.offset + e.numel]
+                if not deltas:
+                    rows = np.subtract(rows, bf[e.offset:e.offset + e.numel], dtype=np.float32)
+            else:
+                rows = xs_i[:, e.offset:e.offset + e.numel]
+                rows = (rows if deltas else rows - bi[e.offset:e.offset + e.numel]).astype(np.float32)
+            assert got[:, e_i].tobytes() == ref.torch_cpu_norm_f32(np.ascontiguousarray(rows)).tobytes(), e.name
+
+
 # ------------------------------------------------------------------ hooks vs reference
 def _host(recipe):
     layout, base, pays, arenas = G.host_state_dicts(recipe)
