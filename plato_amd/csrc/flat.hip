@@ -1287,6 +1287,67 @@ __global__ __launch_bounds__(256) void np_sumsq_half4_kernel(SumsqArgs a) {
   }
 }
 
+// np_sumsq_half4_kernel for C clients of one chunk: the baseline's 16-byte loads are issued once for
+// all of them (the L2-served b re-reads take as many of a CU's in-flight read slots as the client
+// bytes), the clients' squares staged and summed one after the other through the same
+// half-chunk buffer.  A ragged last group (K mod C) loads and stores only its own clients.
+template <int C>
+__global__ __launch_bounds__(256) void np_sumsq_half4xc_kernel(SumsqArgs a) {
+  __shared__ __attribute__((aligned(16))) float sq[kNpBuf / kPW / 2 * kLeafPitch];
+  __shared__ float leaf_sum[C][kNpBuf / kPW];
+  const uint32_t groups = (uint32_t(a.K) + C - 1) / C;
+  const NpTask t = np_task(a, uint64_t(blockIdx.x / groups) * uint64_t(a.K) + (blockIdx.x % groups) * C);
+  if (t.n != kNpBuf) return;  // workgroup-uniform
+  const int nc = a.K - int(t.k) < C ? a.K - int(t.k) : C;  // clients in this group
+  constexpr int kQ = int(kNpBuf / 1024), kHalfQ = kQ / 2;
+  const int tid = int(threadIdx.x);
+  f4 xv[C][kQ], bv[kQ];
+  const gcf4* b = (const gcf4*)(a.base + t.begin) + tid;
+#pragma unroll
+  for (int q = 0; q < kQ; ++q) {
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const gcf4* x = (const gcf4*)(a.x[c < nc ? t.k + c : t.k] + t.begin) + tid;
+      xv[c][q] = c < nc ? __builtin_nontemporal_load(x + q * 256) : f4{0.f, 0.f, 0.f, 0.f};  // nc is uniform
+    }
+    bv[q] = b[q * 256];
+  }
+  const int leaf = tid >> 3, j = tid & 7;
+#pragma unroll
+  for (int s = 0; s < 2 * C; ++s) {  // (client, half) in order
+    const int c = s >> 1, h = s & 1;
+    if (s) __syncthreads();  // the previous pass's leaf reads are done
+#pragma unroll
+    for (int q = 0; q < kHalfQ; ++q) {
+      const uint32_t i = uint32_t(q * 1024 + 4 * tid);  // element h * 4096 + i
+      const f4 d = xv[c][h * kHalfQ + q] - bv[h * kHalfQ + q];
+      *reinterpret_cast<f4*>(sq + np_pad8(i)) = d * d;
+    }
+    __syncthreads();
+    // 32 leaves x 8 accumulators = the 256 threads
+    const float* l = sq + leaf * kLeafPitch + j;
+    float r = l[0];
+#pragma unroll
+    for (int i = 8; i < kPW; i += 8) r += l[i];
+    r = r + __shfl_xor(r, 1);
+    r = r + __shfl_xor(r, 2);
+    r = r + __shfl_xor(r, 4);
+    if (j == 0) leaf_sum[c][h * 32 + leaf] = r;
+  }
+  __syncthreads();
+  // wave w: client w's 64 leaves (clients 4 .. C - 1 on a second pass)
+#pragma unroll
+  for (int c0 = 0; c0 < C; c0 += 4) {
+    const int c = c0 + (tid >> 6);
+    if (c < C) {
+      float s = leaf_sum[c][tid & 63];
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) s = s + __shfl_xor(s, m);
+      if ((tid & 63) == 0 && c < nc) a.chunk_sums[uint64_t(t.k + c) * a.n_chunks + t.c] = s;
+    }
+  }
+}
+
 // The partial last chunk of every (piece, client), through the full-staging path.
 __global__ __launch_bounds__(256) void np_sumsq_tail_kernel(SumsqArgs a) {
   __shared__ float sq[kNpBuf / kPW * kLeafPitch];
@@ -1312,22 +1373,27 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   a.out[uint64_t(k) * a.n_pieces + pc] = out;
 }
 
-// variant 0 (the default): full chunks staged in two halves with 16-byte loads and LDS writes
-// (np_sumsq_half4_kernel: 17.4 KB of LDS; 1.5-1.8 % under variant 5 in three interleaved runs,
-// profiles/r05b_polaris_variants.log, r05e-h) plus the partial last chunks (np_sumsq_tail_kernel);
+// variant 0 (the default): two clients of a chunk per workgroup sharing the baseline loads
+// (np_sumsq_half4xc_kernel<2>; one client when K = 1) plus the partial last chunks
+// (np_sumsq_tail_kernel): 1.153 against 1.256 ms for the one-client form, interleaved, bitwise equal
+// (profiles/r05w_polaris_variants.log, r05x_polaris_variants.log; three and four clients 1.169);
+// 6: the one-client form (np_sumsq_half4_kernel, full chunks staged in two halves with 16-byte loads
+// and LDS writes, 17.4 KB of LDS; the first round-5 default, 1.5-1.8 % under variant 5,
+// profiles/r05b_polaris_variants.log, r05e-h); 7, 8: three / four clients per workgroup;
 // 1: the round-2 form (np_sumsq_chunks_lds_kernel, client-major, four memory round trips per
 // workgroup); 2, 3: timing probes of variant 4 (wrong results by design: no baseline loads / no LDS
 // phase); 4: the round-3 default (np_sumsq_chunks_v2_kernel, every chunk staged whole); 5: the round-4
 // default (np_sumsq_half_kernel, dword loads and LDS writes).  A persistent loader / summer form (four
 // loader waves keeping the next chunk's loads in flight, one summer wave per chunk, lane = leaf)
 // measured 1.51 ms against 1.25 and was removed.
-// G clients per workgroup sharing the baseline (4.1-5.9 ms) were dropped after round 3; a persistent
-// software-pipelined form (2.9 ms: its two register sets left one workgroup per CU), 512 / 1,024
-// threads per chunk (1.70 / 2.79 ms against 1.38) and an LDS-free form loading each accumulator's
-// stride-8 elements directly (2.20 ms) in round 4.
+// Round 3's G clients per workgroup (4.1-5.9 ms: baseline staged through LDS, one load at a time) were
+// dropped; a persistent software-pipelined form (2.9 ms: its two register sets left one workgroup per
+// CU), 512 / 1,024 threads per chunk (1.70 / 2.79 ms against 1.38) and an LDS-free form loading each
+// accumulator's stride-8 elements directly (2.20 ms) in round 4.
 void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
   const uint64_t tasks = uint64_t(a.n_chunks) * uint64_t(a.K);
   const dim3 grid{uint32_t(tasks)};
+  if (variant == 0 && a.K == 1) variant = 6;  // one client: nothing to share
   if (variant == 1) {
     hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, grid, dim3(256), 0, st, a);
   } else if (variant == 2) {
@@ -1339,13 +1405,20 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
   } else if (variant == 5) {
     hipLaunchKernelGGL(np_sumsq_half_kernel, grid, dim3(256), 0, st, a);
     hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
+  } else if (variant == 0 || variant == 7 || variant == 8) {
+    const int c = variant == 0 ? 2 : variant - 4;  // 2, 3, 4 clients per workgroup
+    const dim3 gc{uint32_t(uint64_t(a.n_chunks) * uint64_t((a.K + c - 1) / c))};
+    if (c == 2) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<2>, gc, dim3(256), 0, st, a);
+    else if (c == 3) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<3>, gc, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL(np_sumsq_half4xc_kernel<4>, gc, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   } else {
     hipLaunchKernelGGL(np_sumsq_half4_kernel, grid, dim3(256), 0, st, a);
     hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   }
 }
-[[maybe_unused]] constexpr int kNumSumsqVariants = 6;
-constexpr int kSumsqDefault = 0;  // half-staged (16-byte) + tail: 1.23-1.27 ms on 128 ResNet-18 clients
+[[maybe_unused]] constexpr int kNumSumsqVariants = 9;
+constexpr int kSumsqDefault = 0;  // two clients per workgroup + tail: 1.15 ms on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
                  float* d_out, hipStream_t stream);

@@ -151,10 +151,11 @@ def test_cosine_of_a_zero_vector_uses_eps():
     assert out.item() == float(R.torch_cosine(a, b, 8)) == 0.0
 
 
-@pytest.mark.parametrize("k", [3, 11])
+@pytest.mark.parametrize("k", [1, 2, 3, 11])
 def test_np_sumsq_variants_agree_bitwise(k):
-    """Every np_sumsq kernel (half-staged default, round-3 whole-chunk form, round-2 client-major form;
-    not the timing probes) equals the product default, which the test below pins to numpy."""
+    """Every np_sumsq kernel (the default's two clients per workgroup, three and four with ragged last
+    groups, the one-client half-staged form, round-3 whole-chunk form, round-2 client-major form; not the
+    timing probes) equals the product default, which the test below pins to numpy."""
     from plato_amd.arena import ArenaLayout
     from plato_amd.engine import FedAvgEngine
 
