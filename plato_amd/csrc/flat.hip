@@ -1524,7 +1524,9 @@ int run_cosine(bool scaled, const float* d_a, const float* const* d_b, int K, si
   }
   // variant (tuning only): 1 = one LDS buffer, two barriers per level-1 group (round 3).  Held to 64
   // VGPRs (eight waves per SIMD, the 2,048-workgroup grid in one round) the default spilled (2.23 ms)
-  // and, loading one level-0 group at a time, ran 1.070 against 1.044 (profiles/r04zh_cosine.log)
+  // and, loading one level-0 group at a time, ran 1.070 against 1.044 (profiles/r04zh_cosine.log).  Two
+  // clients of a chunk per workgroup sharing the loads of a (118 VGPRs, lanes 32c.. of wave 0 running client
+  // c's higher levels) ran 1.117 against 1.083, bitwise equal (profiles/r05z_cosine_variants.log); removed
   const dim3 grid{uint32_t(K), uint32_t(a.nt)};
   if (variant == 1) {
     if (scaled) hipLaunchKernelGGL((cosine_chunks_kernel<true, false>), grid, dim3(kSumThreads), 0, stream, a);
