@@ -9,6 +9,10 @@
 //   3: global loads streaming a buffer (the producers' loads)   4: modes 1 + 2 + 3 together
 // and mode 5 runs the chain with its operands from registers only (no LDS reads) with no noise;
 // kNarrow runs the chain (reads and fmas) on lanes 0..7 only (exec mask 0xff).
+// Modes 8-10 (round 5) feed the chain from global memory instead of LDS: the same transposed rows in a
+// per-CU 33 KB buffer (L1 / L2 resident), 8 buffer_load_dwordx4 per 32-step block with the next block's
+// in flight and one s_waitcnt vmcnt per block; cache policy aux 0 (8), sc0 (9), sc0 | sc1 (10: agent
+// scope, past the CU's L1 — what producer-written rows would need).
 // Build: hipcc --offload-arch=gfx950 -O3 -o chain_b128 chain_b128.hip; run: ./chain_b128
 #include <hip/hip_runtime.h>
 
@@ -32,7 +36,7 @@ __global__ void chain_b128(const float* in, float* out, long long* cyc, const fl
   __syncthreads();
   if (wave > 0) {  // noise
     if (kMode == 0 || kMode == 5 || kMode == 7) return;
-    constexpr int nm = kMode == 6 ? 4 : kMode;  // mode 6's noise: everything
+    constexpr int nm = (kMode == 6 || kMode >= 8) ? 4 : kMode;  // modes 6, 8-10: all the noise
     float a0 = lane, a1 = lane + 1, a2 = lane + 2, a3 = lane + 3;
     unsigned long long g = (unsigned long long)(blockIdx.x * 1024 + wave * 64 + lane) * 4;
     float sink = 0.f;
@@ -116,6 +120,39 @@ __global__ void chain_b128(const float* in, float* out, long long* cyc, const fl
         if (kMode == 7) keep.x += buf[cb][0].x * 0.f;  // the reads stay live
       }
     }
+  } else if (kMode >= 8 && kMode <= 10) {
+    constexpr int kAux = kMode == 8 ? 0 : kMode == 9 ? 1 : 17;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(big + (unsigned long long)blockIdx.x * 8 * kR), (short)0, 8 * kR * 4, 0x00020000);
+    const unsigned rowb = unsigned(j * kR) * 4u;
+    for (int t = 0; t < kTiles; ++t) {
+      f4 buf[2][8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        buf[0][q] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, rowb + 16u * q, 0, kAux));
+#pragma unroll
+      for (int blk = 0; blk < kSteps / 32; ++blk) {
+        const int cb = blk & 1;
+        if (blk + 1 < kSteps / 32) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q)
+            buf[cb ^ 1][q] = __builtin_bit_cast(
+                f4, __builtin_amdgcn_raw_buffer_load_b128(rs, rowb + 16u * (8 * (blk + 1) + q), 0, kAux));
+          __builtin_amdgcn_s_waitcnt(8 | (7 << 4) | (15 << 8));  // vmcnt(8): this block's loads landed
+        } else {
+          __builtin_amdgcn_s_waitcnt(0 | (7 << 4) | (15 << 8));  // vmcnt(0)
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          acc = __builtin_fmaf(buf[cb][q].x, buf[cb][q].x, acc);
+          acc = __builtin_fmaf(buf[cb][q].y, buf[cb][q].y, acc);
+          acc = __builtin_fmaf(buf[cb][q].z, buf[cb][q].z, acc);
+          acc = __builtin_fmaf(buf[cb][q].w, buf[cb][q].w, acc);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
   } else if (!kNarrow || lane < 8) {  // kNarrow: the chain (reads and fmas) on lanes 0..7 only
     for (int t = 0; t < kTiles; ++t) {
       const f4* row = reinterpret_cast<const f4*>(tile + j * kR);
@@ -172,6 +209,9 @@ int main() {
   hipMemset(in, 0, 4096 * sizeof(float));
   hipMemset(big, 0, nbig * sizeof(float));
   for (int rep = 0; rep < 2; ++rep) {
+    printf("global rows (aux 0 / sc0 / sc0|sc1), no noise: %.2f / %.2f / %.2f; P=8 all: %.2f / %.2f / %.2f cycles/step\n",
+           run<8>(0, in, out, cyc, big, nbig), run<9>(0, in, out, cyc, big, nbig), run<10>(0, in, out, cyc, big, nbig),
+           run<8>(8, in, out, cyc, big, nbig), run<9>(8, in, out, cyc, big, nbig), run<10>(8, in, out, cyc, big, nbig));
     printf("registers only, no noise: %.2f cycles/step\n", run<5>(0, in, out, cyc, big, nbig));
     printf("one s_waitcnt per block, no noise: %.2f; P=8 all: %.2f cycles/step\n", run<6>(0, in, out, cyc, big, nbig),
            run<6>(8, in, out, cyc, big, nbig));
