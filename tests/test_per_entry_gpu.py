@@ -96,13 +96,13 @@ def test_entry_stats_match_oracle(engine, monkeypatch, cap):
     assert none_dv is None and none_vv is None and dd2.tobytes() == dd.tobytes()
 
 
-@pytest.mark.parametrize("long_threshold", [None, 1 << 17, 8, 1])
-def test_entry_norms_follow_torch_cpu_order(engine, monkeypatch, long_threshold):
+@pytest.mark.parametrize("long_threshold,k", [(None, 7), (1 << 17, 7), (8, 7), (1, 7), (None, 97)])
+def test_entry_norms_follow_torch_cpu_order(engine, monkeypatch, long_threshold, k):
     """Every entry's norm in torch's CPU order, whichever kernel takes it: the long entries through
     plato_agg_port_norms on the side stream (threshold 8 / 1: nearly every fp32 entry, ragged lengths,
-    n % 8 tails, unaligned arena offsets), the rest through plato_agg_entry_norms_f32."""
+    n % 8 tails, unaligned arena offsets), the rest through plato_agg_entry_norms_f32 (K = 97: two clients
+    per workgroup, a one-client last group; empty and int64 entries)."""
     monkeypatch.setattr(engine, "norms_long_threshold", long_threshold)
-    k = 7
     layout, rnd, bf, bi, xs_f, xs_i, _ = _random_round(engine, k, 5)
     got = rnd.entry_norms(range(k))
     for e_i, e in enumerate(layout.entries):
