@@ -1291,7 +1291,7 @@ __global__ __launch_bounds__(256) void np_sumsq_half4_kernel(SumsqArgs a) {
 // all of them (the L2-served b re-reads take as many of a CU's in-flight read slots as the client
 // bytes), the clients' squares staged and summed one after the other through the same
 // half-chunk buffer.  A ragged last group (K mod C) loads and stores only its own clients.
-template <int C>
+template <int C, bool kFirstThenRest = false>
 __global__ __launch_bounds__(256) void np_sumsq_half4xc_kernel(SumsqArgs a) {
   __shared__ __attribute__((aligned(16))) float sq[kNpBuf / kPW / 2 * kLeafPitch];
   __shared__ float leaf_sum[C][kNpBuf / kPW];
@@ -1303,14 +1303,30 @@ __global__ __launch_bounds__(256) void np_sumsq_half4xc_kernel(SumsqArgs a) {
   const int tid = int(threadIdx.x);
   f4 xv[C][kQ], bv[kQ];
   const gcf4* b = (const gcf4*)(a.base + t.begin) + tid;
+  if constexpr (kFirstThenRest) {  // the first client and b, then the others: client 0's squares can be
+                                   // staged while the later clients' loads are still in flight
 #pragma unroll
-  for (int q = 0; q < kQ; ++q) {
-#pragma unroll
-    for (int c = 0; c < C; ++c) {
-      const gcf4* x = (const gcf4*)(a.x[c < nc ? t.k + c : t.k] + t.begin) + tid;
-      xv[c][q] = c < nc ? __builtin_nontemporal_load(x + q * 256) : f4{0.f, 0.f, 0.f, 0.f};  // nc is uniform
+    for (int q = 0; q < kQ; ++q) {
+      xv[0][q] = __builtin_nontemporal_load((const gcf4*)(a.x[t.k] + t.begin) + tid + q * 256);
+      bv[q] = b[q * 256];
     }
-    bv[q] = b[q * 256];
+#pragma unroll
+    for (int c = 1; c < C; ++c) {
+      const gcf4* x = (const gcf4*)(a.x[c < nc ? t.k + c : t.k] + t.begin) + tid;
+#pragma unroll
+      for (int q = 0; q < kQ; ++q)
+        xv[c][q] = c < nc ? __builtin_nontemporal_load(x + q * 256) : f4{0.f, 0.f, 0.f, 0.f};  // nc is uniform
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kQ; ++q) {
+#pragma unroll
+      for (int c = 0; c < C; ++c) {
+        const gcf4* x = (const gcf4*)(a.x[c < nc ? t.k + c : t.k] + t.begin) + tid;
+        xv[c][q] = c < nc ? __builtin_nontemporal_load(x + q * 256) : f4{0.f, 0.f, 0.f, 0.f};  // nc is uniform
+      }
+      bv[q] = b[q * 256];
+    }
   }
   const int leaf = tid >> 3, j = tid & 7;
 #pragma unroll
@@ -1373,10 +1389,12 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   a.out[uint64_t(k) * a.n_pieces + pc] = out;
 }
 
-// variant 0 (the default): two clients of a chunk per workgroup sharing the baseline loads
-// (np_sumsq_half4xc_kernel<2>; one client when K = 1) plus the partial last chunks
-// (np_sumsq_tail_kernel): 1.153 against 1.256 ms for the one-client form, interleaved, bitwise equal
-// (profiles/r05w_polaris_variants.log, r05x_polaris_variants.log; three and four clients 1.169);
+// variant 0 (the default): two clients of a chunk per workgroup sharing the baseline loads, the first
+// client's and the baseline's loads issued before the second client's (np_sumsq_half4xc_kernel<2, true>;
+// one client when K = 1) plus the partial last chunks (np_sumsq_tail_kernel): 1.145-1.149 ms against
+// 1.249-1.256 for the one-client form, interleaved, bitwise equal; 9: the same with the clients' loads
+// interleaved, 1.153-1.174 (profiles/r05w-y, r05zh, r05zi_polaris_variants.log; three and four clients
+// 1.165-1.177);
 // 6: the one-client form (np_sumsq_half4_kernel, full chunks staged in two halves with 16-byte loads
 // and LDS writes, 17.4 KB of LDS; the first round-5 default, 1.5-1.8 % under variant 5,
 // profiles/r05b_polaris_variants.log, r05e-h); 7, 8: three / four clients per workgroup;
@@ -1405,10 +1423,11 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
   } else if (variant == 5) {
     hipLaunchKernelGGL(np_sumsq_half_kernel, grid, dim3(256), 0, st, a);
     hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
-  } else if (variant == 0 || variant == 7 || variant == 8) {
-    const int c = variant == 0 ? 2 : variant - 4;  // 2, 3, 4 clients per workgroup
+  } else if (variant == 0 || variant == 7 || variant == 8 || variant == 9) {
+    const int c = (variant == 0 || variant == 9) ? 2 : variant - 4;  // 2, 3, 4 clients per workgroup
     const dim3 gc{uint32_t(uint64_t(a.n_chunks) * uint64_t((a.K + c - 1) / c))};
-    if (c == 2) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<2>, gc, dim3(256), 0, st, a);
+    if (variant == 0) hipLaunchKernelGGL((np_sumsq_half4xc_kernel<2, true>), gc, dim3(256), 0, st, a);
+    else if (c == 2) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<2>, gc, dim3(256), 0, st, a);
     else if (c == 3) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<3>, gc, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(np_sumsq_half4xc_kernel<4>, gc, dim3(256), 0, st, a);
     hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
@@ -1417,8 +1436,8 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   }
 }
-[[maybe_unused]] constexpr int kNumSumsqVariants = 9;
-constexpr int kSumsqDefault = 0;  // two clients per workgroup + tail: 1.15 ms on 128 ResNet-18 clients
+[[maybe_unused]] constexpr int kNumSumsqVariants = 10;
+constexpr int kSumsqDefault = 0;  // two clients per workgroup + tail: 1.145-1.149 ms on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
                  float* d_out, hipStream_t stream);
