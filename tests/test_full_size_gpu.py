@@ -89,3 +89,52 @@ def test_full_size_sampled_exact_and_variant_invariant(engine, name):
     assert got_i.tobytes() == exp_i.tobytes()
     del slab, base, outs
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("k", [128, 256])
+def test_shared_baseline_kernels_match_one_client_forms_at_full_size(engine, k):
+    """FedAtt norms and Polaris sums on K ResNet-18 clients: the product kernels (two clients per
+    workgroup sharing the baseline loads; FedAtt from K = 96) equal, bit for bit on every (client, entry),
+    the one-client forms that the small-size tests pin to the oracle (tuning variants 8 / 6)."""
+    from plato_amd import _lib
+
+    layout = ArenaLayout.from_shapes(workloads.resnet(18, 10))
+    base = DeviceArena(layout, DEV)
+    slab = ClientSlab(layout, k, DEV)
+    fill_baseline(base, 23)
+    fill_clients(slab, base, 23, k)
+    pf, pi = slab.row_pointers(range(k))
+    tf = torch.from_numpy(pf).to(DEV)
+    ti = torch.from_numpy(pi).to(DEV)
+    h = torch.cuda.current_stream(DEV).cuda_stream
+    n_e = len(layout.entries)
+    ef, ei = engine._norm_tables(layout)
+    norm_args = (tf.data_ptr(), ti.data_ptr(), k, base.f32.data_ptr(), base.i64.data_ptr(), ef.data_ptr(), ef.shape[0],
+                 ei.data_ptr(), ei.shape[0], n_e, layout.n_f32, layout.n_i64)
+    prod = torch.full((k * n_e,), float("nan"), device=DEV)
+    one = torch.full((k * n_e,), float("nan"), device=DEV)
+    _lib.call("plato_agg_entry_norms_f32", *norm_args, prod.data_ptr(), h)
+    _lib.tune_call("plato_agg_tune_entry_norms", 8, *norm_args, one.data_ptr(), h)
+    torch.cuda.synchronize()
+    assert not torch.isnan(prod).any()
+    assert prod.cpu().numpy().tobytes() == one.cpu().numpy().tobytes()
+
+    rows, first, n_chunks = [], [], 0
+    for idx, e in enumerate(layout.entries):
+        if e.region == "f32" and e.numel:
+            rows.append((idx, e.offset, e.offset + e.numel, 0))
+            first.append(n_chunks)
+            n_chunks += -(-e.numel // 8192)
+    pieces = torch.from_numpy(np.asarray(rows, dtype=np.uint32).view(np.int32).copy()).to(DEV)
+    firsts = torch.from_numpy(np.asarray(first, dtype=np.uint32).view(np.int32)).to(DEV)
+    ws = torch.empty(max(1, engine.lib.plato_agg_np_sumsq_workspace(k, n_chunks) // 4), device=DEV)
+    sq_args = (tf.data_ptr(), k, base.f32.data_ptr(), pieces.data_ptr(), firsts.data_ptr(), len(rows), n_chunks,
+               ws.data_ptr())
+    sq_prod = torch.full((k, len(rows)), float("nan"), device=DEV)
+    sq_one = torch.full((k, len(rows)), float("nan"), device=DEV)
+    _lib.call("plato_agg_np_sumsq", *sq_args, sq_prod.data_ptr(), h)
+    ws.fill_(float("nan"))
+    _lib.tune_call("plato_agg_tune_np_sumsq", 6, *sq_args, sq_one.data_ptr(), h)
+    torch.cuda.synchronize()
+    assert not torch.isnan(sq_prod).any()
+    assert sq_prod.cpu().numpy().tobytes() == sq_one.cpu().numpy().tobytes()
