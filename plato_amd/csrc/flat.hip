@@ -1119,11 +1119,51 @@ __device__ __forceinline__ float np_partial(const float* sq, uint32_t n) {
   return pw_walk([&](uint32_t o, uint32_t m) { return pw_leaf(v, o, m); }, 0, n, PwStack{so, sn, sl, stage});
 }
 
+// The same sum with the leaves in parallel (every thread of the workgroup calls it): lane 0 lists the
+// recursion's leaves left to right (offsets and lengths only), the threads sum one leaf each (pw_leaf,
+// as np_partial), and lane 0 walks the recursion again adding the leaf values in post-order — the same
+// additions in the same order as np_partial, which ran every leaf's ~128 dependent adds on one lane
+// (an entry's partial last chunk: up to 8,191 of them; 0.33 of the 1.15 ms Polaris launch,
+// profiles/r05zz_kernel_stats.csv).  Leaves hold more than 56 elements unless the chunk is shorter, so a
+// chunk below 8,192 has fewer than 150.  Returns the sum on lane 0.
+constexpr int kNpMaxLeaves = 256;
+__device__ float np_partial_par(const float* sq, uint32_t n) {
+  __shared__ uint32_t leaf_off[kNpMaxLeaves], leaf_n[kNpMaxLeaves];
+  __shared__ float leaf_val[kNpMaxLeaves];
+  __shared__ int n_leaves;
+  const int tid = int(threadIdx.x);
+  if (tid == 0) {
+    int cnt = 0;
+    uint32_t so[16], sn[16], stage[16];
+    float sl[16];
+    pw_walk([&](uint32_t o, uint32_t m) {
+      leaf_off[cnt] = o;
+      leaf_n[cnt] = m;
+      ++cnt;
+      return 0.f;
+    }, 0, n, PwStack{so, sn, sl, stage});
+    n_leaves = cnt;
+  }
+  __syncthreads();
+  const int nl = n_leaves;
+  const auto v = [&](uint64_t e) { return sq[np_pad8(e)]; };
+  for (int i = tid; i < nl; i += int(blockDim.x)) leaf_val[i] = pw_leaf(v, leaf_off[i], leaf_n[i]);
+  __syncthreads();
+  float r = 0.f;
+  if (tid == 0) {
+    int idx = 0;
+    uint32_t so[16], sn[16], stage[16];
+    float sl[16];
+    r = pw_walk([&](uint32_t, uint32_t) { return leaf_val[idx++]; }, 0, n, PwStack{so, sn, sl, stage});
+  }
+  return r;
+}
+
 // The chunk's numpy sum of squares from this lane's values: squares staged in LDS, 64 leaves x 8
 // accumulators (numpy's r[0..7] over 16 steps), the 8 partials of a leaf by xor 1, 2, 4 shuffles,
 // the 64 leaves by a 6-level butterfly; a partial chunk walked by lane 0.  Ends with a barrier
 // (the next chunk may restage sq).
-template <int kT>
+template <int kT, bool kParLeaves = false>
 __device__ __forceinline__ void np_chunk(const SumsqArgs& a, const NpTask& t, const float (&xv)[kNpBuf / kT],
                                          const float (&bv)[kNpBuf / kT], float* sq, float* leaf_sum) {
   const int tid = int(threadIdx.x);
@@ -1157,8 +1197,9 @@ __device__ __forceinline__ void np_chunk(const SumsqArgs& a, const NpTask& t, co
       for (int m = 1; m < 64; m <<= 1) s = s + __shfl_xor(s, m);
       if (tid == 0) *dst = s;
     }
-  } else if (tid == 0) {
-    *dst = np_partial(sq, t.n);
+  } else {  // workgroup-uniform
+    const float r = kParLeaves ? np_partial_par(sq, t.n) : (tid == 0 ? np_partial(sq, t.n) : 0.f);
+    if (tid == 0) *dst = r;
   }
   __syncthreads();
 }
@@ -1364,7 +1405,9 @@ __global__ __launch_bounds__(256) void np_sumsq_half4xc_kernel(SumsqArgs a) {
   }
 }
 
-// The partial last chunk of every (piece, client), through the full-staging path.
+// The partial last chunk of every (piece, client), through the full-staging path (kPar: its leaves
+// summed in parallel, np_partial_par).
+template <bool kPar = true>
 __global__ __launch_bounds__(256) void np_sumsq_tail_kernel(SumsqArgs a) {
   __shared__ float sq[kNpBuf / kPW * kLeafPitch];
   __shared__ float leaf_sum[kNpBuf / kPW];
@@ -1375,7 +1418,7 @@ __global__ __launch_bounds__(256) void np_sumsq_tail_kernel(SumsqArgs a) {
   if (t.n == kNpBuf) return;  // workgroup-uniform: a whole last chunk went through the half kernel
   float xv[kNpBuf / 256], bv[kNpBuf / 256];
   np_load<256>(a, t, xv, bv);
-  np_chunk<256>(a, t, xv, bv, sq, leaf_sum);
+  np_chunk<256, kPar>(a, t, xv, bv, sq, leaf_sum);
 }
 
 __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
@@ -1391,10 +1434,11 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
 
 // variant 0 (the default): two clients of a chunk per workgroup sharing the baseline loads, the first
 // client's and the baseline's loads issued before the second client's (np_sumsq_half4xc_kernel<2, true>;
-// one client when K = 1) plus the partial last chunks (np_sumsq_tail_kernel): 1.145-1.149 ms against
-// 1.249-1.256 for the one-client form, interleaved, bitwise equal; 9: the same with the clients' loads
-// interleaved, 1.153-1.174 (profiles/r05w-y, r05zh, r05zi_polaris_variants.log; three and four clients
-// 1.165-1.177);
+// one client when K = 1) plus the partial last chunks with their leaves summed in parallel
+// (np_sumsq_tail_kernel<true>): 1.053 ms against 1.148 for the same with the partial chunks walked by one
+// lane (variant 10) and 1.249-1.256 for the one-client form, interleaved, bitwise equal
+// (profiles/r05zza_polaris_variants.log); 9: variant 10 with the clients' loads interleaved, 1.153-1.174
+// (profiles/r05w-y, r05zh, r05zi_polaris_variants.log; three and four clients 1.165-1.177);
 // 6: the one-client form (np_sumsq_half4_kernel, full chunks staged in two halves with 16-byte loads
 // and LDS writes, 17.4 KB of LDS; the first round-5 default, 1.5-1.8 % under variant 5,
 // profiles/r05b_polaris_variants.log, r05e-h); 7, 8: three / four clients per workgroup;
@@ -1412,6 +1456,14 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
   const uint64_t tasks = uint64_t(a.n_chunks) * uint64_t(a.K);
   const dim3 grid{uint32_t(tasks)};
   if (variant == 0 && a.K == 1) variant = 6;  // one client: nothing to share
+  if (variant == 10) {  // the default with the partial chunks walked by one lane (rounds 2-5)
+    const dim3 gc{uint32_t(uint64_t(a.n_chunks) * uint64_t((a.K + 1) / 2))};
+    if (a.K == 1) hipLaunchKernelGGL(np_sumsq_half4_kernel, grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((np_sumsq_half4xc_kernel<2, true>), gc, dim3(256), 0, st, a);
+    hipLaunchKernelGGL(np_sumsq_tail_kernel<false>, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0,
+                       st, a);
+    return;
+  }
   if (variant == 1) {
     hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, grid, dim3(256), 0, st, a);
   } else if (variant == 2) {
@@ -1422,7 +1474,7 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256>), grid, dim3(256), 0, st, a);
   } else if (variant == 5) {
     hipLaunchKernelGGL(np_sumsq_half_kernel, grid, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(np_sumsq_tail_kernel<true>, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   } else if (variant == 0 || variant == 7 || variant == 8 || variant == 9) {
     const int c = (variant == 0 || variant == 9) ? 2 : variant - 4;  // 2, 3, 4 clients per workgroup
     const dim3 gc{uint32_t(uint64_t(a.n_chunks) * uint64_t((a.K + c - 1) / c))};
@@ -1430,14 +1482,14 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
     else if (c == 2) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<2>, gc, dim3(256), 0, st, a);
     else if (c == 3) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<3>, gc, dim3(256), 0, st, a);
     else hipLaunchKernelGGL(np_sumsq_half4xc_kernel<4>, gc, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(np_sumsq_tail_kernel<true>, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   } else {
     hipLaunchKernelGGL(np_sumsq_half4_kernel, grid, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(np_sumsq_tail_kernel, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(np_sumsq_tail_kernel<true>, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
   }
 }
-[[maybe_unused]] constexpr int kNumSumsqVariants = 10;
-constexpr int kSumsqDefault = 0;  // two clients per workgroup + tail: 1.145-1.149 ms on 128 ResNet-18 clients
+[[maybe_unused]] constexpr int kNumSumsqVariants = 11;
+constexpr int kSumsqDefault = 0;  // two clients per workgroup + parallel-leaf tail: 1.05 ms on 128 ResNet-18 clients
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
                  float* d_out, hipStream_t stream);

@@ -150,12 +150,29 @@ def main():
     def run_fedavg():
         engine.launch_fedavg(layout, tf, ti, w, None, k, base.f32, base.i64, out_f, out_i, stream)
 
+    # Polaris: numpy-order sums of squares per fp32 entry (plato_agg_np_sumsq, the product kernels)
+    sq_rows, sq_first, sq_chunks = [], [], 0
+    for idx, e in enumerate(layout.entries):
+        if e.region == "f32" and e.numel:
+            sq_rows.append((idx, e.offset, e.offset + e.numel, 0))
+            sq_first.append(sq_chunks)
+            sq_chunks += -(-e.numel // 8192)
+    sq_pieces = torch.from_numpy(np.asarray(sq_rows, dtype=np.uint32).view(np.int32).copy()).to(dev)
+    sq_firsts = torch.from_numpy(np.asarray(sq_first, dtype=np.uint32).view(np.int32)).to(dev)
+    sq_ws = torch.empty(max(1, engine.lib.plato_agg_np_sumsq_workspace(k, sq_chunks) // 4), device=dev)
+    sq_out = torch.empty((k, len(sq_rows)), device=dev)
+
+    def run_sumsq():
+        _lib.call("plato_agg_np_sumsq", _ptr(tf), k, _ptr(base.f32), _ptr(sq_pieces), _ptr(sq_firsts), len(sq_rows),
+                  sq_chunks, _ptr(sq_ws), _ptr(sq_out), h)
+
     kernels = {
         "qsgd": (run_qsgd, k * (n_f + n_i) + n_f * 8 + n_i * 12),
         "entrywise": (run_entrywise, (k + 3) * n_f * 4 + (k + 2) * n_i * 8),
         "stats": (run_stats, (k + 2) * n_f * 4 + (k + 1) * n_i * 8),
         "norms": (run_norms, (k + 1) * n_f * 4 + (k + 1) * n_i * 8),
         "fedavg": (run_fedavg, layout.algorithmic_bytes(k)),
+        "sumsq": (run_sumsq, (k + 1) * n_f * 4),
     }
     if args.qsgd_variants or args.qsgd_list:  # tuning: every (or the listed) plato_agg_tune_fedavg_qsgd variant
         vlist = ([int(x) for x in args.qsgd_list.split(",")] if args.qsgd_list

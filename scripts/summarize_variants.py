@@ -15,18 +15,16 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KERNELS = {"qsgd": "fedavg_qsgd_", "entrywise": "fedavg_entrywise_kernel",
-           "stats": "entry_stats_partial", "norms": "entry_norms", "fedavg": "fedavg_kernel"}
+           "stats": "entry_stats_partial", "norms": "entry_norms", "fedavg": "fedavg_kernel",
+           "sumsq": "np_sumsq_half4"}
 
 
 def per_kernel(path, name):
+    """Median counter value per kernel name (the kernel trace's Name, e.g. one entry_norms instantiation)."""
     out = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] != name:
-            continue
-        for key, sym in KERNELS.items():
-            if sym in r["Kernel_Name"] and not (key == "fedavg" and "qsgd" in r["Kernel_Name"]) \
-                    and not (key == "fedavg" and "entrywise" in r["Kernel_Name"]):
-                out.setdefault(key, []).append(float(r["Counter_Value"]))
+        if r["Counter_Name"] == name:
+            out.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     return {k: statistics.median(v) for k, v in out.items()}
 
 
@@ -49,10 +47,10 @@ def main(tag):
             cand = [r for r in cand if "qsgd" not in r["Name"] and "entrywise" not in r["Name"]]
         if not cand or key not in alg:
             continue
-        row = max(cand, key=lambda r: int(r["Calls"]))
+        row = max(cand, key=lambda r: float(r["TotalDurationNs"]))  # the path's main kernel (norms, sumsq: 2 each)
         avg_ns = float(row["AverageNs"])
-        rd = fetch.get(key, 0) * 1024 * 2
-        wr = write.get(key, 0) * 1024
+        rd = fetch.get(row["Name"], 0) * 1024 * 2
+        wr = write.get(row["Name"], 0) * 1024
         out["kernels"][key] = {
             "kernel": row["Name"], "calls": int(row["Calls"]), "avg_duration_ms": avg_ns / 1e6,
             "algorithmic_bytes": alg[key], "achieved_GBps": alg[key] / avg_ns,
