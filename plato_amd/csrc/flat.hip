@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <map>
+#include <mutex>
 #include <string>
 
 #include "common.h"
@@ -1432,16 +1434,20 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   a.out[uint64_t(k) * a.n_pieces + pc] = out;
 }
 
-// variant 0 (the default): two clients of a chunk per workgroup sharing the baseline loads, the first
-// client's and the baseline's loads issued before the second client's (np_sumsq_half4xc_kernel<2, true>;
-// one client when K = 1) plus the partial last chunks with their leaves summed in parallel
-// (np_sumsq_tail_kernel<true>): 1.053 ms against 1.148 for the same with the partial chunks walked by one
-// lane (variant 10) and 1.249-1.256 for the one-client form, interleaved, bitwise equal
-// (profiles/r05zza_polaris_variants.log); 9: variant 10 with the clients' loads interleaved, 1.153-1.174
-// (profiles/r05w-y, r05zh, r05zi_polaris_variants.log; three and four clients 1.165-1.177);
-// 6: the one-client form (np_sumsq_half4_kernel, full chunks staged in two halves with 16-byte loads
-// and LDS writes, 17.4 KB of LDS; the first round-5 default, 1.5-1.8 % under variant 5,
-// profiles/r05b_polaris_variants.log, r05e-h); 7, 8: three / four clients per workgroup;
+// variant 0 (the default): four clients of a chunk per workgroup sharing the baseline loads
+// (np_sumsq_half4xc_kernel<4>; two when K = 2-3, one when K = 1) plus the partial last chunks with their
+// leaves summed in parallel (np_sumsq_tail_kernel<true>) on a side stream beside the full chunks
+// (run_np_sumsq): 0.979-0.985 ms against 1.004-1.032 for two clients (variant 14, the form before) in two
+// interleaved runs (profiles/r05zzc, r05zzd_polaris_variants.log), bitwise equal.  With the partial chunks
+// serialised after the full ones, four clients had lost to two (1.169 / 1.153): the shapes trade against
+// the partial chunks' overlap.  14: two clients, the first client's and the baseline's loads issued first
+// (np_sumsq_half4xc_kernel<2, true>); 11: variant 14 with both launches on one stream, 1.060-1.086;
+// 10: variant 14 with the partial chunks walked by one lane, 1.033-1.048 (on one stream: 1.148, against
+// 1.053 leaf-parallel, profiles/r05zza_polaris_variants.log); 9: two clients, loads interleaved; 7, 8:
+// three / four clients, loads interleaved; 12, 13: three / four clients, the first client's loads first;
+// 6: the one-client form (np_sumsq_half4_kernel, full chunks staged in two halves with 16-byte loads and
+// LDS writes, 17.4 KB of LDS; the first round-5 default, 1.5-1.8 % under variant 5,
+// profiles/r05b_polaris_variants.log, r05e-h);
 // 1: the round-2 form (np_sumsq_chunks_lds_kernel, client-major, four memory round trips per
 // workgroup); 2, 3: timing probes of variant 4 (wrong results by design: no baseline loads / no LDS
 // phase); 4: the round-3 default (np_sumsq_chunks_v2_kernel, every chunk staged whole); 5: the round-4
@@ -1452,47 +1458,64 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
 // dropped; a persistent software-pipelined form (2.9 ms: its two register sets left one workgroup per
 // CU), 512 / 1,024 threads per chunk (1.70 / 2.79 ms against 1.38) and an LDS-free form loading each
 // accumulator's stride-8 elements directly (2.20 ms) in round 4.
-void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st) {
+void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st, hipStream_t tail_st) {
   const uint64_t tasks = uint64_t(a.n_chunks) * uint64_t(a.K);
-  const dim3 grid{uint32_t(tasks)};
-  if (variant == 0 && a.K == 1) variant = 6;  // one client: nothing to share
-  if (variant == 10) {  // the default with the partial chunks walked by one lane (rounds 2-5)
-    const dim3 gc{uint32_t(uint64_t(a.n_chunks) * uint64_t((a.K + 1) / 2))};
-    if (a.K == 1) hipLaunchKernelGGL(np_sumsq_half4_kernel, grid, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((np_sumsq_half4xc_kernel<2, true>), gc, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(np_sumsq_tail_kernel<false>, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0,
-                       st, a);
+  const dim3 grid{uint32_t(tasks)}, tail_grid{uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))};
+  if ((variant == 0 || variant == 11 || variant == 14) && a.K == 1) variant = 6;  // one client: nothing to share
+  if (variant == 0 && a.K < 4) variant = 14;  // two or three clients: two per workgroup
+  if (variant >= 1 && variant <= 4) {  // whole-chunk forms: no separate partial-chunk launch
+    if (variant == 1) hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, grid, dim3(256), 0, st, a);
+    else if (variant == 2) hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256, 1>), grid, dim3(256), 0, st, a);
+    else if (variant == 3) hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256, 2>), grid, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256>), grid, dim3(256), 0, st, a);
     return;
   }
-  if (variant == 1) {
-    hipLaunchKernelGGL(np_sumsq_chunks_lds_kernel, grid, dim3(256), 0, st, a);
-  } else if (variant == 2) {
-    hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256, 1>), grid, dim3(256), 0, st, a);
-  } else if (variant == 3) {
-    hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256, 2>), grid, dim3(256), 0, st, a);
-  } else if (variant == 4) {
-    hipLaunchKernelGGL((np_sumsq_chunks_v2_kernel<256>), grid, dim3(256), 0, st, a);
-  } else if (variant == 5) {
-    hipLaunchKernelGGL(np_sumsq_half_kernel, grid, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(np_sumsq_tail_kernel<true>, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
-  } else if (variant == 0 || variant == 7 || variant == 8 || variant == 9) {
-    const int c = (variant == 0 || variant == 9) ? 2 : variant - 4;  // 2, 3, 4 clients per workgroup
-    const dim3 gc{uint32_t(uint64_t(a.n_chunks) * uint64_t((a.K + c - 1) / c))};
-    if (variant == 0) hipLaunchKernelGGL((np_sumsq_half4xc_kernel<2, true>), gc, dim3(256), 0, st, a);
-    else if (c == 2) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<2>, gc, dim3(256), 0, st, a);
-    else if (c == 3) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<3>, gc, dim3(256), 0, st, a);
-    else hipLaunchKernelGGL(np_sumsq_half4xc_kernel<4>, gc, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(np_sumsq_tail_kernel<true>, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
-  } else {
-    hipLaunchKernelGGL(np_sumsq_half4_kernel, grid, dim3(256), 0, st, a);
-    hipLaunchKernelGGL(np_sumsq_tail_kernel<true>, dim3(uint32_t(uint64_t(a.n_pieces) * uint64_t(a.K))), dim3(256), 0, st, a);
-  }
+  // the partial last chunks first (on tail_st: beside the full chunks), then the full chunks
+  if (variant == 10) hipLaunchKernelGGL(np_sumsq_tail_kernel<false>, tail_grid, dim3(256), 0, tail_st, a);
+  else hipLaunchKernelGGL(np_sumsq_tail_kernel<true>, tail_grid, dim3(256), 0, tail_st, a);
+  const int c = (variant == 7 || variant == 12) ? 3 : (variant == 0 || variant == 8 || variant == 13) ? 4 : 2;
+  const dim3 gc{uint32_t(uint64_t(a.n_chunks) * uint64_t((a.K + c - 1) / c))};
+  if (variant == 5) hipLaunchKernelGGL(np_sumsq_half_kernel, grid, dim3(256), 0, st, a);
+  else if (variant == 6) hipLaunchKernelGGL(np_sumsq_half4_kernel, grid, dim3(256), 0, st, a);
+  else if (variant == 7) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<3>, gc, dim3(256), 0, st, a);
+  else if (variant == 8 || variant == 0) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<4>, gc, dim3(256), 0, st, a);
+  else if (variant == 9) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<2>, gc, dim3(256), 0, st, a);
+  else if (variant == 12) hipLaunchKernelGGL((np_sumsq_half4xc_kernel<3, true>), gc, dim3(256), 0, st, a);
+  else if (variant == 13) hipLaunchKernelGGL((np_sumsq_half4xc_kernel<4, true>), gc, dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((np_sumsq_half4xc_kernel<2, true>), gc, dim3(256), 0, st, a);  // 10, 11, 14
 }
-[[maybe_unused]] constexpr int kNumSumsqVariants = 11;
-constexpr int kSumsqDefault = 0;  // two clients per workgroup + parallel-leaf tail: 1.05 ms on 128 ResNet-18 clients
+[[maybe_unused]] constexpr int kNumSumsqVariants = 15;
+constexpr int kSumsqDefault = 0;  // four clients per workgroup + side-stream parallel-leaf tail: 0.98 ms (128 ResNet-18)
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
                  float* d_out, hipStream_t stream);
+
+// A second stream per device (created on first use, never destroyed) with a fork / join event pair, so
+// that independent launches of one C-ABI call overlap: fork() makes the side stream wait for everything
+// the caller's stream has enqueued, join() makes the caller's stream wait for the side stream.  The
+// enqueue sequence runs under a per-device lock (the events are reused across calls; a wait captures an
+// event's state when it is enqueued), so concurrent callers stay ordered.
+struct SideStream {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  std::mutex mu;
+};
+SideStream* side_stream(int dev) {
+  static std::mutex mu;
+  static std::map<int, SideStream*> all;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = all.find(dev);
+  if (it != all.end()) return it->second;
+  auto* ss = new SideStream();  // process lifetime
+  if (hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) != hipSuccess) {
+    delete ss;
+    return nullptr;
+  }
+  all[dev] = ss;
+  return ss;
+}
 
 
 }  // namespace
@@ -1545,7 +1568,27 @@ int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_bas
   const uint64_t t1 = uint64_t(n_chunks) * uint64_t(K), t2 = uint64_t(n_pieces) * uint64_t(K);
   if (t1) {
     if (t1 > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "too many chunks");
-    launch_sumsq(variant, a, stream);
+    // the partial-chunk kernel (variants 0, 5-10) runs on a side stream beside the full-chunk kernel
+    // (0.23 ms of the launch when serialised after it, profiles/r05zzb kernel trace)
+    const bool tail = !(variant >= 1 && variant <= 4) && variant != 11;  // 11: the default, one stream
+    hipDevice_t dev = 0;
+    int cur = 0;
+    SideStream* ss = nullptr;
+    if (tail && hipStreamGetDevice(stream, &dev) == hipSuccess && hipGetDevice(&cur) == hipSuccess) {
+      if (cur != dev) (void)hipSetDevice(dev);
+      ss = side_stream(dev);
+    }
+    if (ss) {
+      std::lock_guard<std::mutex> lk(ss->mu);
+      (void)hipEventRecord(ss->fork, stream);
+      (void)hipStreamWaitEvent(ss->s, ss->fork, 0);
+      launch_sumsq(variant, a, stream, ss->s);
+      (void)hipEventRecord(ss->join, ss->s);
+      (void)hipStreamWaitEvent(stream, ss->join, 0);
+    } else {
+      launch_sumsq(variant, a, stream, stream);
+    }
+    if (tail && cur != int(dev)) (void)hipSetDevice(cur);
     if (int rc = check_launch("np_sumsq chunks launch")) return rc;
   }
   hipLaunchKernelGGL(np_sumsq_pieces_kernel, dim3(uint32_t((t2 + 255) / 256)), dim3(256), 0, stream, a);
