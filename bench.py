@@ -656,6 +656,11 @@ def main():
 # (scripts/micro/chain_b128.hip, profiles/r04_micro_chain_b128.log), the wave64 issue rate; the
 # round-1 micro's 6.0 (scripts/micro/fma_chain.hip) included a taken loop branch every 16 steps
 CHAIN_CYCLES = 4.0
+# the same chain fed from LDS by ds_read_b128 (4 steps per read, one s_waitcnt per block), no other
+# waves: 5.86-5.87 cycles per step (profiles/r04_micro_chain_b128.log).  Every chain kernel reads its
+# operands this way: register-resident operands need another wave's data, global-memory operands ran
+# 48-50 cycles per step (profiles/r05zf_micro_chain_global.log), so this is the rate the design can reach
+LDS_FED_CHAIN_CYCLES = 5.86
 CLOCK_HZ = 2.4e9
 
 
@@ -677,13 +682,14 @@ def variant_legs(dev, k: int, reps: int) -> dict:
     spec = model_spec("resnet18")
     slots = list(range(k))
 
-    def make_round(align):
+    def make_round(align, deltas=False):
         lay = ArenaLayout.from_shapes(spec, align=align)
         base = DeviceArena(lay, dev)
         fill_baseline(base, 0)
         baseline = lay.unpack(base.f32.cpu(), base.i64.cpu())
         eng = FedAvgEngine(dev)
         eng.layout_align = align
+        eng.delta_arenas = deltas
         rnd = eng.begin(baseline, k)
         rnd.put_baseline(baseline)
         torch.cuda.synchronize(dev)
@@ -693,6 +699,15 @@ def variant_legs(dev, k: int, reps: int) -> dict:
             rnd._pf[s], rnd._pi[s] = int(pf[0]), int(pi[0])
             rnd.staged[s] = True
         torch.cuda.synchronize(dev)
+        rnd.delta_ms_per_client = None
+        if deltas:  # what put_client does behind each client's H2D: the slot turned into x - b in place
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(rnd.stager.stream)
+            for s in range(k):
+                rnd._to_delta(s)
+            e1.record(rnd.stager.stream)
+            torch.cuda.synchronize(dev)
+            rnd.delta_ms_per_client = e0.elapsed_time(e1) / k
         return lay, base, rnd
 
     def measure(fn, rnd, keys):
@@ -709,22 +724,29 @@ def variant_legs(dev, k: int, reps: int) -> dict:
         return statistics.median(walls), {key: statistics.median(v) for key, v in kernel.items()}
 
     def entry(kernel_ms, nbytes, chain_steps=0):
-        floor = max(nbytes / (HBM_PEAK_GBS * 1e9) * 1e3, chain_steps * CHAIN_CYCLES / CLOCK_HZ * 1e3)
-        return {"kernel_ms": round(kernel_ms, 4), "algorithmic_bytes": int(nbytes),
-                "GBps": round(nbytes / (kernel_ms * 1e-3) / 1e9, 1), "serial_chain_steps": int(chain_steps),
-                "floor_ms": round(floor, 4), "frac_of_floor": round(floor / kernel_ms, 4)}
+        hbm = nbytes / (HBM_PEAK_GBS * 1e9) * 1e3
+        floor = max(hbm, chain_steps * CHAIN_CYCLES / CLOCK_HZ * 1e3)
+        res = {"kernel_ms": round(kernel_ms, 4), "algorithmic_bytes": int(nbytes),
+               "GBps": round(nbytes / (kernel_ms * 1e-3) / 1e9, 1), "serial_chain_steps": int(chain_steps),
+               "floor_ms": round(floor, 4), "frac_of_floor": round(floor / kernel_ms, 4)}
+        if chain_steps:  # the chain at the measured LDS-fed rate (LDS_FED_CHAIN_CYCLES), beside the 4-cycle floor
+            lds = max(hbm, chain_steps * LDS_FED_CHAIN_CYCLES / CLOCK_HZ * 1e3)
+            res.update(lds_fed_chain_floor_ms=round(lds, 4), frac_of_lds_fed_chain_floor=round(lds / kernel_ms, 4))
+        return res
 
     out = {"clients": k, "model": "resnet18", "reps": reps,
            "note": "HIP events around each engine launch (AggregationRound.timings); outside the headline's timed "
-                   "region; floor = max(algorithmic bytes at 8 TB/s, serial fma chain at 4 cycles/step, 2.4 GHz)"}
+                   "region; floor = max(algorithmic bytes at 8 TB/s, serial fma chain at 4 cycles/step, 2.4 GHz); "
+                   "lds_fed_chain_floor = the same with the chain at its measured LDS-fed rate, 5.86 cycles/step"}
     lay, base, rnd = make_round(None)
     n_f, n_i = lay.n_f32_data, lay.n_i64
     model_bytes = n_f * 4 + n_i * 8
     n_flat = n_f + n_i
     longest = max(e.numel for e in lay.entries if e.region == F32)
 
-    # FedAdp: global gradient (entrywise pass) + the fused gather/sdot kernel, aligned arenas
-    lay_a, _, rnd_a = make_round("fedadp")
+    # FedAdp: global gradient (entrywise pass) + the fused gather/sdot kernel, aligned arenas holding each
+    # client's delta (FedAdpServerMixin.arena_deltas: formed behind each client's H2D at staging)
+    lay_a, _, rnd_a = make_round("fedadp", deltas=True)
     w1 = np.full((len(lay_a.entries), k), 1.0 / k)
 
     def fedadp():
@@ -732,8 +754,9 @@ def variant_legs(dev, k: int, reps: int) -> dict:
         rnd_a.fedadp_dots(grads, slots, 0.01)
 
     wall, km = measure(fedadp, rnd_a, ["fedadp_dots"])
-    out["fedadp"] = dict(entry(km["fedadp_dots"], k * model_bytes + 3 * n_flat * 4, n_flat // 64),
-                         path_ms=round(wall, 3), kernel="plato_agg_fedadp_dots (prep + dots + finish)",
+    out["fedadp"] = dict(entry(km["fedadp_dots"], k * model_bytes + 2 * n_flat * 4, n_flat // 64),
+                         path_ms=round(wall, 3), kernel="plato_agg_fedadp_dots (prep + dots + finish), delta arenas",
+                         staging_delta_ms_per_client=round(rnd_a.delta_ms_per_client, 4),
                          reference="examples/server_aggregation/fedadp/fedadp_server.py:91-99")
     del rnd_a
     torch.cuda.empty_cache()

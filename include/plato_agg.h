@@ -405,6 +405,10 @@ int plato_agg_sdot_shared(const float* d_x, const float* const* d_y, int n_pairs
  * n_segs) bytes — chain sums, per-group descriptors, the finished values of
  * the groups that cross an entry boundary and the chain-group-major copy of x
  * and the flattened baseline the kernel streams.
+ * Delta arenas: d_base_f32 = d_base_i64 = NULL means the client arenas already
+ * hold x - b (fp32 differences, int64 wrapping differences: compute_weight_deltas,
+ * plato/algorithms/fedavg.py:13-27, formed when each payload was staged); the
+ * values and their order are the same, and the kernel streams no baseline.
  */
 size_t plato_agg_fedadp_dots_workspace(int n_pairs, int with_xx, size_t n_i64, size_t n_flat, uint32_t n_segs);
 int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64, int n_pairs,

@@ -118,6 +118,8 @@ int plato_agg_tune_fedavg_qsgd(int variant, const uint8_t* const* d_codes_f32, c
 int plato_agg_tune_num_fedadp_variants(void);
 /* 1 if that variant is a timing probe (results wrong by design), else 0. */
 int plato_agg_tune_fedadp_is_probe(int variant);
+/* 1 if the variant runs on delta arenas (pass a null baseline), else 0 */
+int plato_agg_tune_fedadp_is_delta(int variant);
 int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const* d_src_f32,
                                const void* const* d_src_i64, int n_pairs, const float* d_base_f32,
                                const int64_t* d_base_i64, const plato_agg_segment* d_segs, uint32_t n_segs,

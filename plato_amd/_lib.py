@@ -189,6 +189,7 @@ TUNE_SIGNATURES = {
                  _c_void_p]),
     "plato_agg_tune_num_fedadp_variants": (_c_int, []),
     "plato_agg_tune_fedadp_is_probe": (_c_int, [_c_int]),
+    "plato_agg_tune_fedadp_is_delta": (_c_int, [_c_int]),
     "plato_agg_tune_num_port_norms_variants": (_c_int, []),
     "plato_agg_tune_num_np_sumsq_variants": (_c_int, []),
     "plato_agg_tune_num_cosine_variants": (_c_int, []),

@@ -140,16 +140,19 @@ __device__ float adp_y_in(const AdpArgs& a, int pair, uint64_t p, uint32_t sidx)
   const plato_agg_segment sg = a.segs[sidx];
   const uint64_t e = sg.src_offset + (p - sg.flat_offset);
   const bool neg = sg.flags & PLATO_AGG_SEG_NEG_DIV;
-  if (sg.region) return adp_i64(a.xi[pair][e], a.base_i[e], neg, a.lr);
-  return adp_f32(a.xf[pair][e], a.base_f[e], neg, a.lr);
+  if (sg.region) return adp_i64(a.xi[pair][e], a.base_i ? a.base_i[e] : int64_t(0), neg, a.lr);
+  return adp_f32(a.xf[pair][e], a.base_f ? a.base_f[e] : 0.f, neg, a.lr);
 }
 __device__ float adp_y_at(const AdpArgs& a, int pair, uint64_t p) {
   return adp_y_in(a, pair, p, adp_find(a.segs, a.n_segs, p));
 }
 
 // Tuning flags (kF): client arenas read non-temporally, the division as a float64 product, x and
-// b from the chain-group-major buffer (else x from the flat vector and b from the baseline arena)
-constexpr int kFYnt = 1, kFDiv64 = 4, kFXB = 8;
+// b from the chain-group-major buffer (else x from the flat vector and b from the baseline arena);
+// kFDelta: the client arenas hold deltas (y - b, formed when each payload was staged), so the
+// producers load no b at all: y - 0 is y bit for bit (also -0, NaN), the same values as y - b formed
+// here, and each (cg, group) stage streams x and the client only
+constexpr int kFYnt = 1, kFDiv64 = 4, kFXB = 8, kFDelta = 16;
 
 // 32 of the 64 chains per workgroup; kS steps per stage; kW producer waves, kIt gather iterations
 // of one group (8 half-blocks x 32 positions) each per stage
@@ -216,7 +219,11 @@ __device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpDesc* desc,
     const __amdgpu_buffer_rsrc_t ry = bnd ? src.bnd : src.y;
     const uint32_t yo = bnd ? (d.off * 256u + uint32_t(lane) * 4u) * 4u : (p + d.off) * 4u;
     r.y[i] = bload4<(kF & kFYnt) ? 2 : 0>(ry, yo);
-    if constexpr ((kF & kFXB) != 0) {  // [cg][group][x: 256 | b: 256], lane l at 4 l
+    if constexpr ((kF & kFDelta) != 0) {
+      static_assert((kF & kFXB) != 0, "delta arenas use the chain-group-major x buffer");
+      r.x[i] = bload4<0>(src.x, (grp * 512u + uint32_t(lane) * 4u) * 4u);
+      r.b[i] = f4v{0.f, 0.f, 0.f, 0.f};
+    } else if constexpr ((kF & kFXB) != 0) {  // [cg][group][x: 256 | b: 256], lane l at 4 l
       const uint32_t q = (grp * 512u + uint32_t(lane) * 4u) * 4u;
       r.x[i] = bload4<0>(src.x, q);
       r.b[i] = bload4<0>(src.x, q + 1024u);
@@ -477,7 +484,7 @@ __global__ __launch_bounds__(256) void fedadp_prep_kernel(AdpArgs a, float* xb) 
       const uint64_t s = p / 64, c = p % 64;
       float* o = xb + ((c / 32) * a.ngroups + s / 8) * 512 + (s % 8) * 32 + (c % 32);
       o[0] = a.x[p];
-      o[256] = i64 ? 0.f : a.base_f[p - sg.flat_offset + sg.src_offset];
+      if (a.base_f) o[256] = i64 ? 0.f : a.base_f[p - sg.flat_offset + sg.src_offset];  // (delta arenas: no b)
     }
   }
 }
@@ -542,6 +549,7 @@ __global__ __launch_bounds__(64) void fedadp_finish_kernel(AdpArgs a, float* out
 struct AdpLaunch {
   void (*fn)(const AdpArgs&, hipStream_t);
   bool uses_xb;
+  bool delta;  // kFDelta: for delta arenas (null baseline)
 };
 
 template <int kS, int kW, int kIt, int kD, int kF, int kProbe>
@@ -552,7 +560,7 @@ void launch_adp_impl(const AdpArgs& a, hipStream_t st) {
 
 template <int kS, int kW, int kIt, int kD, int kF, int kProbe = 0>
 constexpr AdpLaunch adp_launch() {
-  return AdpLaunch{&launch_adp_impl<kS, kW, kIt, kD, kF, kProbe>, (kF & kFXB) != 0};
+  return AdpLaunch{&launch_adp_impl<kS, kW, kIt, kD, kF, kProbe>, (kF & kFXB) != 0, (kF & kFDelta) != 0};
 }
 
 // The product's shape: 192-step stages of 12 producer waves x 2 iterations, x and b from the
@@ -561,6 +569,8 @@ constexpr AdpLaunch adp_launch() {
 // arenas the buffer still pays for its prep launch: without it (x from the flat gradient, b from
 // the baseline arena) the whole call took 1.381 ms against 1.355 (profiles/r04v_fedadp.log).
 constexpr AdpLaunch kAdpDefault = adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB>();
+// Delta arenas (null baseline): the same shape without the b loads
+constexpr AdpLaunch kAdpDefaultDelta = adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB | kFDelta>();
 #ifdef PLATO_AGG_TUNE
 const AdpLaunch kAdpVariants[] = {
     kAdpDefault,                                            // 0: the default
@@ -572,6 +582,12 @@ const AdpLaunch kAdpVariants[] = {
     adp_launch<192, 12, 2, 2, kFYnt | kFXB>(),              // 6: the default with the IEEE division
     adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB, 1>(), // 7: probe: the default's chains alone
     adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB, 2>(), // 8: probe: the default's producers alone
+    kAdpDefaultDelta,                                        // 9: the default for delta arenas (null baseline)
+    adp_launch<128, 8, 2, 2, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 10: delta arenas, 128-step stages
+    adp_launch<256, 8, 4, 2, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 11: delta arenas, 256-step stages
+    adp_launch<128, 8, 2, 3, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 12: delta arenas, 3 stages in flight
+    adp_launch<192, 12, 2, 3, kFYnt | kFDiv64 | kFXB | kFDelta>(), // 13: delta arenas, 192 steps, 3 stages in flight
+    adp_launch<192, 6, 4, 2, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 14: delta arenas, 6 producer waves x 4
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)
@@ -620,8 +636,9 @@ int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const 
                           const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
                           uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
                           float* d_out_xy, float* d_out_yy, hipStream_t stream) {
-  return run_fedadp(kAdpDefault, d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32, d_base_i64, d_segs, n_segs, n_flat, n_f32,
-                    n_i64, lr, with_xx, d_workspace, d_out_xy, d_out_yy, stream);
+  return run_fedadp(d_base_f32 ? kAdpDefault : kAdpDefaultDelta, d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32,
+                    d_base_i64, d_segs, n_segs, n_flat, n_f32, n_i64, lr, with_xx, d_workspace, d_out_xy, d_out_yy,
+                    stream);
 }
 
 #ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
@@ -631,6 +648,10 @@ int plato_agg_tune_fedadp_is_probe(int variant) {
   for (int v : kAdpProbes)
     if (v == variant) return 1;
   return 0;
+}
+
+int plato_agg_tune_fedadp_is_delta(int variant) {
+  return (variant >= 0 && variant < kNumAdpVariants && kAdpVariants[variant].delta) ? 1 : 0;
 }
 
 int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const* d_src_f32,
@@ -653,9 +674,14 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
                float* d_out_xy, float* d_out_yy, hipStream_t stream) {
   if (n_pairs <= 0 || n_pairs > 65535) return set_error(PLATO_AGG_EINVAL, "n_pairs must be in [1, 65535]");
   if (with_xx != 0 && with_xx != 1) return set_error(PLATO_AGG_EINVAL, "with_xx must be 0 or 1");
-  if (!d_x || !d_src_f32 || !d_src_i64 || !d_base_f32 || !d_segs || !d_workspace || !d_out_xy || !d_out_yy ||
-      (n_i64 && !d_base_i64))
+  if (!d_x || !d_src_f32 || !d_src_i64 || !d_segs || !d_workspace || !d_out_xy || !d_out_yy ||
+      (d_base_f32 && n_i64 && !d_base_i64))
     return set_error(PLATO_AGG_EINVAL, "null pointer");
+  if (!d_base_f32 && d_base_i64) return set_error(PLATO_AGG_EINVAL, "int64 baseline without an fp32 baseline");
+  // a null baseline means the arenas hold deltas: only the delta shapes run on them, and only on them
+  if (fn.delta != (d_base_f32 == nullptr))
+    return set_error(PLATO_AGG_EINVAL, fn.delta ? "this variant takes delta arenas (null baseline)"
+                                                : "delta arenas (null baseline) need a delta variant");
   if ((reinterpret_cast<uintptr_t>(d_x) & 15u) || (reinterpret_cast<uintptr_t>(d_workspace) & 255u))
     return set_error(PLATO_AGG_EINVAL, "x must be 16-byte and the workspace 256-byte aligned");
   if (n_segs == 0 || n_segs >= (1u << 22)) return set_error(PLATO_AGG_EINVAL, "segment count must be in [1, 2^22)");

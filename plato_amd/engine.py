@@ -162,6 +162,9 @@ class FedAvgEngine:
     port_variant: int | None = None  # plato_agg_tune_port_norms shape (tests / tuning), None = the default
     #: arena alignment of the layouts this engine builds (arena.ALIGNMENTS; FedAdp servers: "fedadp")
     layout_align: str | None = None
+    #: native rounds hold each client as its delta x - b (``AggregationRound.deltas``): FedAdp's servers,
+    #: whose dot kernel then streams no baseline
+    delta_arenas: bool = False
 
     def __init__(self, device=None, variant: int | None = None):
         self.device = require_device(device)
@@ -589,6 +592,8 @@ class AggregationRound:
     reference regardless of the order payloads arrived in.
     """
 
+    deltas = False  # (set per round in __init__; decoded rounds hold decoded weights)
+
     def __init__(self, engine: FedAvgEngine, layout: ArenaLayout, capacity: int, codec: str = "native"):
         self.engine = engine
         self.layout = layout
@@ -612,6 +617,32 @@ class AggregationRound:
         self._k = 0
         self._decoded = None
         self._timers: list = []
+        # Delta arenas: every staged slot is turned into x - b in place on the copy stream as it is staged
+        # (compute_weight_deltas, plato/algorithms/fedavg.py:13-27, the same fp32 differences and int64
+        # wrapping differences the kernels would form), so the reductions that re-read the baseline per
+        # client (FedAdp's dots) stream no baseline.  The kernels then run in their deltas forms and the
+        # final update adds the baseline once (plato_agg_update_weights: b + acc, the fused epilogue's sum).
+        self.deltas = bool(getattr(engine, "delta_arenas", False)) and codec == "native"
+        self._converted: set = set()
+
+    def _to_delta(self, slot: int) -> None:
+        """Turn staged slot ``slot`` into its delta x - b, in place, on the copy stream (after its H2D)."""
+        if not self.has_baseline:
+            raise ValueError("delta arenas: stage the baseline before the clients")
+        key = (self._pf[slot], self._pi[slot])
+        if key in self._converted:
+            return
+        eng, lay = self.engine, self.layout
+        n_i = lay.n_i64
+        cs = self.stager.stream
+        _lib.call("plato_agg_compute_deltas", self._pf[slot], self._pi[slot] if n_i else None, _ptr(self._base.f32),
+                  _ptr(self._base.i64) if n_i else None, self._pf[slot], self._pi[slot] if n_i else None,
+                  lay.n_f32, n_i, _stream_handle(cs))
+        self._converted.add(key)
+
+    def _raw_only(self, what: str) -> None:
+        if self.deltas:
+            raise ValueError(f"{what} reads the clients' weights; this round holds deltas (engine.delta_arenas)")
 
     def _timed(self, name: str, stream) -> _KernelTimer:
         return _KernelTimer(self, name, stream)
@@ -630,6 +661,8 @@ class AggregationRound:
     def put_baseline(self, baseline: Mapping[str, torch.Tensor]) -> None:
         self.layout.check_compatible(baseline, "baseline_weights")
         eng = self.engine
+        if self.deltas and any(self.staged):
+            raise ValueError("delta arenas: the clients were staged as deltas of the previous baseline")
         eng._stager.put(baseline, eng._base.f32, eng._base.i64)
         self.has_baseline = True
         self._decoded = None
@@ -640,9 +673,14 @@ class AggregationRound:
             raise IndexError(f"slot {slot} outside [0, {self.capacity})")
         self.layout.check_compatible(payload, f"{what}[{slot}]", self.codec)
         self._coded_scales(slot, payload)
+        if self.deltas and not self.has_baseline:
+            raise ValueError("delta arenas: stage the baseline before the clients")
         self.stager.put(payload, self.slab.f32[slot], self.slab.i64[slot])
         pf, pi = self.slab.row_pointers([slot])
         self._pf[slot], self._pi[slot] = int(pf[0]), int(pi[0])
+        self._converted.discard((self._pf[slot], self._pi[slot]))  # fresh weights in the row
+        if self.deltas:
+            self._to_delta(slot)  # behind this client's H2D on the copy stream
         self.staged[slot] = True
         self._decoded = None  # decoded rows are per staged set
 
@@ -668,6 +706,8 @@ class AggregationRound:
             return False
         self._coded_scales(slot, payload)
         self._pf[slot], self._pi[slot] = hit
+        if self.deltas:  # the arrival row held the weights: its delta, in place (the row is this round's)
+            self._to_delta(slot)
         self.staged[slot] = True
         self._decoded = None  # decoded rows are per staged set
         return True
@@ -718,6 +758,15 @@ class AggregationRound:
             _lib.call("plato_agg_fedavg_weights_bf16", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w), _ptr(s),
                       len(order), _ptr(self._base.f32), _ptr(self._base.i64) if n_i else None, _ptr(out_f),
                       _ptr(out_i) if n_i else None, lay.n_f32, n_i, _stream_handle(stream))
+        elif self.deltas and not deltas:  # delta arenas: acc = sum_i d_i * w_i, then b + acc
+            acc_f = torch.empty_like(out_f)
+            acc_i = torch.empty_like(out_i)
+            eng.launch_fedavg(lay, tf, ti, w, s, len(order), None, None, acc_f, acc_i, stream)
+            n_i = lay.n_i64
+            _lib.call("plato_agg_update_weights", _ptr(self._base.f32), _ptr(self._base.i64) if n_i else None,
+                      _ptr(acc_f), _ptr(acc_i) if n_i else None, _ptr(out_f), _ptr(out_i) if n_i else None,
+                      lay.n_f32, n_i, _stream_handle(stream))
+            w = (w, acc_f, acc_i)
         else:
             eng.launch_fedavg(lay, tf, ti, w, s, len(order), None if deltas else self._base.f32,
                               None if deltas else self._base.i64, out_f, out_i, stream)
@@ -740,6 +789,8 @@ class AggregationRound:
         slots = self._check_slots(order)
         if not deltas and not self.has_baseline:
             raise ValueError("baseline not staged")
+        if not deltas:
+            self._raw_only("launch_w64")
         eng, lay = self.engine, self.layout
         self.timings["stage_ms"] = (time.perf_counter() - self._t0) * 1e3
         self._k = len(order)
@@ -864,6 +915,7 @@ class AggregationRound:
         numpy arrays, entries in layout order.
         """
         slots = self._check_slots(slots)
+        deltas = deltas or self.deltas  # delta arenas: the rows are the deltas
         if not deltas and not self.has_baseline:
             raise ValueError("baseline not staged")
         eng, lay = self.engine, self.layout
@@ -901,6 +953,7 @@ class AggregationRound:
         clients in ``slots`` order).
         """
         slots = self._check_slots(slots)
+        self._raw_only("entry_norms")
         if not self.has_baseline:
             raise ValueError("baseline not staged")
         eng, lay = self.engine, self.layout
@@ -973,6 +1026,10 @@ class AggregationRound:
         slots = self._check_slots(order)
         if not deltas and not self.has_baseline:
             raise ValueError("baseline not staged")
+        if self.deltas and not deltas:
+            if add_base:
+                self._raw_only("launch_entrywise(add_base=True)")
+            deltas = True  # the staged rows are the deltas the kernel would form
         if deltas and add_base:
             raise ValueError("add_base needs the baseline (deltas=False)")
         eng, lay = self.engine, self.layout
@@ -1095,8 +1152,11 @@ class AggregationRound:
                          dtype=torch.float32, device=eng.device)
         n_i = lay.n_i64
         with self._timed("fedadp_dots", stream):
+            # delta arenas: a null baseline selects the kernel that streams none (same values, same order)
+            base_f = None if self.deltas else _ptr(self._base.f32)
+            base_i = None if (self.deltas or not n_i) else _ptr(self._base.i64)
             _lib.call("plato_agg_fedadp_dots", g_flat.data_ptr(), ptrs.data_ptr(), ptrs.data_ptr() + 8 * k, k,
-                      _ptr(self._base.f32), _ptr(self._base.i64) if n_i else None, segs.data_ptr(), len(order), n_flat,
+                      base_f, base_i, segs.data_ptr(), len(order), n_flat,
                       lay.n_f32, n_i, float(lr), 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(), _stream_handle(stream))
         xy_h, yy_h = xy.cpu().numpy(), yy.cpu().numpy()  # stream-ordered D2H (syncs this stream)
         self._resolve_timers()
@@ -1112,6 +1172,7 @@ class AggregationRound:
         (scripts/bench_variant_paths.py).
         """
         slots = self._check_slots(slots)
+        self._raw_only("fedadp_dots_flat")
         if not self.has_baseline:
             raise ValueError("baseline not staged")
         eng, lay = self.engine, self.layout
@@ -1157,6 +1218,7 @@ class AggregationRound:
         Returns ``[K, E]`` float32 (entries in layout order; int64 entries 0).
         """
         slots = self._check_slots(slots)
+        self._raw_only("np_sumsq")
         if not self.has_baseline:
             raise ValueError("baseline not staged")
         eng, lay = self.engine, self.layout
@@ -1219,6 +1281,7 @@ class AggregationRound:
         cross-check.
         Returned as fp32 like the reference's 0-dim tensor.
         """
+        self._raw_only("model_similarities")
         if not self.has_baseline:
             raise ValueError("baseline not staged")
         slots = list(slots)

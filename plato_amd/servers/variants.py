@@ -227,6 +227,9 @@ class FedAdpWeights(_EngineHolder):
     #: every fp32 entry at an arena offset congruent to its flattened position (arena.FEDADP_ALIGN):
     #: the dot kernel's gathers then read whole 128-byte lines
     arena_alignment = "fedadp"
+    #: clients staged as deltas x - b (FedAvgEngine.delta_arenas): the dot kernel streams no baseline,
+    #: 1.08 against 1.44 ms for 128 ResNet-18 clients, bitwise equal (profiles/r05zzk_delta_probe.log)
+    arena_deltas = True
 
     #: FedAdp's alpha; None = Config().algorithm.alpha, else 5 (fedadp_server.py:112-114)
     fedadp_alpha = None

@@ -21,7 +21,7 @@ import torch
 
 from oracle import fedavg_oracle as ref
 from plato_amd.arena import ArenaLayout
-from plato_amd.engine import FedAvgEngine
+from plato_amd.engine import ClientSlab, FedAvgEngine
 from tests import golden_cases as G
 
 pytestmark = pytest.mark.gpu
@@ -250,11 +250,13 @@ def test_fedatt_algorithm_is_bit_exact(engine, name):
     assert G.sha(ref.trunc_to_int64(_flat(layout, updated, "i64"))) == exp["loaded_i64_sha256"]
 
 
+@pytest.mark.parametrize("deltas", [True, False])
 @pytest.mark.parametrize("align", [None, "fedadp"])
 @pytest.mark.parametrize("name", ["fedadp_lenet5_k6", "fedadp_resnet18_k8"])
-def test_fedadp_server_matches_reference(name, align):
-    """The product path (FedAdpServerMixin: arenas aligned to the flattened positions) and the packed
-    layout give the reference's weights, angles and model bit for bit."""
+def test_fedadp_server_matches_reference(name, align, deltas):
+    """The product path (FedAdpServerMixin: arenas aligned to the flattened positions, clients staged as
+    their deltas) and the packed layout / weight arenas give the reference's weights, angles and model
+    bit for bit."""
     from plato_amd.servers.variants import FedAdpServerMixin
 
     recipe, exp = CASES[name]["recipe"], CASES[name]["expected"]
@@ -264,10 +266,12 @@ def test_fedadp_server_matches_reference(name, align):
         aggregation_device = DEV
         fedadp_lr = 0.01
         arena_alignment = align
+        arena_deltas = deltas
 
     server = Server()
     engine = server.aggregation_engine()
     assert engine.layout_align == align
+    assert engine.delta_arenas is deltas
     server.current_round = recipe["current_round"]
     server.selected_clients = [c + 1 for c in G.order_of(recipe)]
     server.local_angles = {int(c): np.float32(float.fromhex(a)) for c, a in recipe.get("local_angles", {}).items()}
@@ -281,7 +285,9 @@ def test_fedadp_server_matches_reference(name, align):
     assert G.sha(ref.trunc_to_int64(_flat(layout, updated, "i64"))) == exp["loaded_i64_sha256"]
     ref_w = [float.fromhex(h) for h in exp["adaptive_weighting"]]
 
-    # global gradient (deltas pass, no baseline) bit-exact; model bit-exact given the reference's weights
+    # global gradient (deltas pass, no baseline) bit-exact; model bit-exact given the reference's weights;
+    # the materialised-flatten cross-check reads weight arenas
+    engine.delta_arenas = False
     rnd = engine.begin(base, recipe["k"])
     assert rnd.layout.align == align
     rnd.put_baseline(base)
@@ -310,6 +316,53 @@ def test_fedadp_server_matches_reference(name, align):
     again = rnd.result()
     assert G.sha(G.canon(_flat(layout, again, "f32"))) == exp["updated_f32_sha256"]
     assert G.sha(ref.trunc_to_int64(_flat(layout, again, "i64"))) == exp["loaded_i64_sha256"]
+
+
+@pytest.mark.parametrize("name", ["fedadp_lenet5_k6", "fedadp_resnet18_k8"])
+def test_delta_round_matches_weight_round(name):
+    """A round whose clients are staged as deltas (FedAvgEngine.delta_arenas: put_client and adopt turn each
+    slot into x - b in place) gives the weight round's global gradient, FedAdp dots and FedAvg result bit
+    for bit, refuses the reductions that need the clients' weights, and needs the baseline first."""
+    recipe = CASES[name]["recipe"]
+    layout, base, pays, _, updates = _host(recipe)
+    k = recipe["k"]
+    w1 = np.tile(np.asarray([u.report.num_samples for u in updates], dtype=np.float64)
+                 / sum(u.report.num_samples for u in updates), (len(layout.entries), 1))
+    weights = [float(u.report.num_samples) / sum(x.report.num_samples for x in updates) for u in updates]
+    got = {}
+    for deltas in (False, True):
+        eng = FedAvgEngine(DEV)
+        eng.layout_align = "fedadp"
+        eng.delta_arenas = deltas
+        rnd = eng.begin(base, k)
+        assert rnd.deltas is deltas
+        if deltas:
+            with pytest.raises(ValueError, match="baseline"):
+                rnd.put_client(0, pays[0])
+        rnd.put_baseline(base)
+        for i, p in enumerate(pays):
+            if i == 1 and deltas:  # one slot through the arrival path: prestaged weights, converted at adopt
+                assert eng.prestage(p, rnd.layout) and rnd.adopt(i, p)
+            else:
+                rnd.put_client(i, p)
+        g_f, g_i = rnd.launch_entrywise(w1, add_base=False, device=True)
+        dots = rnd.fedadp_dots((g_f, g_i), range(k), 0.01)
+        rnd.launch(weights)
+        res = rnd.result()
+        g_model = rnd.layout.unpack(g_f.cpu(), g_i.cpu())  # (the aligned arena has padding between entries)
+        got[deltas] = (_flat(layout, g_model, "f32").tobytes(), _flat(layout, g_model, "i64").tobytes(),
+                       [np.asarray(d).tobytes() for d in dots], _flat(layout, res, "f32").tobytes(),
+                       _flat(layout, res, "i64").tobytes())
+        if deltas:
+            for call in (lambda: rnd.entry_norms(range(k)), lambda: rnd.np_sumsq(range(k)),
+                         lambda: rnd.fedadp_dots_flat((g_f, g_i), range(k), 0.01),
+                         lambda: rnd.launch_entrywise(w1, add_base=True)):
+                with pytest.raises(ValueError, match="deltas"):
+                    call()
+            with pytest.raises(ValueError, match="deltas"):
+                rnd.put_baseline(base)
+        eng.release_arrivals()
+    assert got[True] == got[False]
 
 
 def test_polaris_server_matches_reference(engine):
@@ -363,19 +416,33 @@ def test_fedadp_dots_tile_shapes_agree_bitwise(name, align):
     order = rnd._fedadp_order()
     segs, n_flat = rnd._flat_segments(order, True)
     dev = torch.device(DEV)
+    # delta arenas (the delta variants, null baseline): compute_weight_deltas of every staged slot
+    dslab = ClientSlab(layout, k, dev)
+    h = torch.cuda.current_stream().cuda_stream
+    for i in range(k):
+        _lib.call("plato_agg_compute_deltas", rnd._pf[i], rnd._pi[i], engine._base.f32.data_ptr(),
+                  engine._base.i64.data_ptr(), dslab.f32[i].data_ptr(), dslab.i64[i].data_ptr(), layout.n_f32,
+                  layout.n_i64, h)
+    dpf, dpi = dslab.row_pointers(range(k))
+    dptrs = torch.from_numpy(np.concatenate([dpf, dpi]).astype(np.int64)).to(dev)
+    n_delta = 0
     for v in range(_lib.tune().plato_agg_tune_num_fedadp_variants()):
         if _lib.tune().plato_agg_tune_fedadp_is_probe(v):  # timing probes: wrong results by design
             continue
+        delta = bool(_lib.tune().plato_agg_tune_fedadp_is_delta(v))
+        n_delta += delta
+        p = dptrs if delta else ptrs
         xy = torch.full((k + 1,), float("nan"), device=dev)
         yy = torch.full((k + 1,), float("nan"), device=dev)
-        _lib.tune_call("plato_agg_tune_fedadp_dots", v, g_flat.data_ptr(), ptrs.data_ptr(), ptrs.data_ptr() + 8 * k, k,
-                       engine._base.f32.data_ptr(), engine._base.i64.data_ptr(), segs.data_ptr(), len(order), n_flat,
-                       layout.n_f32, layout.n_i64, 0.01, 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(),
-                       torch.cuda.current_stream().cuda_stream)
+        _lib.tune_call("plato_agg_tune_fedadp_dots", v, g_flat.data_ptr(), p.data_ptr(), p.data_ptr() + 8 * k, k,
+                       None if delta else engine._base.f32.data_ptr(), None if delta else engine._base.i64.data_ptr(),
+                       segs.data_ptr(), len(order), n_flat, layout.n_f32, layout.n_i64, 0.01, 1, ws.data_ptr(),
+                       xy.data_ptr(), yy.data_ptr(), h)
         torch.cuda.synchronize()
         assert xy.cpu().numpy()[:k].tobytes() == np.asarray(want[0]).tobytes(), v
         assert xy.cpu().numpy()[k:].tobytes() == np.float32(want[1]).tobytes(), v
         assert yy.cpu().numpy()[:k].tobytes() == np.asarray(want[2]).tobytes(), v
+    assert n_delta >= 1
 
 
 # ------------------------------------------------------- coded payloads reaching the variants
