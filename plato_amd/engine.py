@@ -30,7 +30,7 @@ import torch
 
 from . import _lib
 from .arena import CODECS, F32, I64, ArenaLayout, fedadp_order, payload_codec
-from .staging import HostPacker, PinnedRing, ResultPool, arena_source, payload_fingerprint
+from .staging import HostPacker, PinnedRing, ResultPool, arena_source, baseline_key, payload_fingerprint
 
 
 def fp32_weights(values: Sequence[float]) -> np.ndarray:
@@ -306,12 +306,17 @@ class FedAvgEngine:
     # ---------------------------------------------------- arrival staging
     ARRIVAL_CHUNK = 16  # rows per arrival slab; rows never move once staged
 
-    def prestage(self, payload: Mapping[str, torch.Tensor], baseline_layout: ArenaLayout) -> bool:
+    def prestage(self, payload: Mapping[str, torch.Tensor], baseline_layout: ArenaLayout,
+                 baseline: Mapping[str, torch.Tensor] | None = None) -> bool:
         """Copy one arriving payload to HBM now (H2D overlaps the other clients' arrival).
 
         The next aggregation round adopts it by identity (``AggregationRound.adopt``);
         the payload must not be modified after arrival.  Returns False if the
         payload does not fit the layout (it is then staged at aggregation time).
+        With :attr:`delta_arenas` and the server's current model as ``baseline`` (the
+        baseline of the round this payload will join), the row is turned into its delta
+        right behind its H2D; a round adopts it only if its own baseline is that model
+        unchanged (:func:`baseline_key`), else it stages the payload again.
         """
         codec = payload_codec(payload)
         try:
@@ -324,8 +329,9 @@ class FedAvgEngine:
             self._arrivals, self._arrival_free, self._arrival_slabs = {}, {}, {}
         if self._copy_stream is None:
             self._copy_stream = torch.cuda.Stream(self.device)
-        if codec not in self._stagers:
-            self._stagers[codec] = _Stager(self._layout, self.device, codec=codec, stream=self._copy_stream)
+        for c in {codec, "native"}:
+            if c not in self._stagers:
+                self._stagers[c] = _Stager(self._layout, self.device, codec=c, stream=self._copy_stream)
         free = self._arrival_free.setdefault(codec, [])
         if not free:
             slabs = self._arrival_slabs.setdefault(codec, [])
@@ -335,10 +341,35 @@ class FedAvgEngine:
         slab, row = free.pop()
         self._stagers[codec].put(payload, slab.f32[row], slab.i64[row])
         pf, pi = slab.row_pointers([row])
+        delta_key = None
+        if self.delta_arenas and codec == "native" and baseline is not None:
+            delta_key = self._arrival_baseline(baseline)
+            if delta_key is not None:  # x - b in place, behind this payload's H2D on the copy stream
+                n_i = self._layout.n_i64
+                _lib.call("plato_agg_compute_deltas", int(pf[0]), int(pi[0]) if n_i else None,
+                          _ptr(self._arrival_base.f32), _ptr(self._arrival_base.i64) if n_i else None, int(pf[0]),
+                          int(pi[0]) if n_i else None, self._layout.n_f32, n_i, _stream_handle(self._copy_stream))
         # keep the dict alive: its id() is the key; the fingerprint detects later edits
         self._arrivals[id(payload)] = (payload, codec, self._layout.signature, int(pf[0]), int(pi[0]), slab, row,
-                                       payload_fingerprint(payload))
+                                       payload_fingerprint(payload), delta_key)
         return True
+
+    def _arrival_baseline(self, baseline: Mapping[str, torch.Tensor]):
+        """The arrival baseline on the device (staged once per model version); its key, or None."""
+        key = baseline_key(baseline)
+        if key == getattr(self, "_arrival_base_key", None):
+            return key
+        try:
+            self._layout.check_compatible(baseline, "baseline")
+        except (KeyError, ValueError):
+            return None
+        if getattr(self, "_arrival_base", None) is None or self._arrival_base_layout is not self._layout:
+            self._arrival_base = DeviceArena(self._layout, self.device)
+            self._arrival_base_layout = self._layout
+        # stream order on the copy stream: rows converted against the previous model ran before this copy
+        self._stagers["native"].put(baseline, self._arrival_base.f32, self._arrival_base.i64)
+        self._arrival_base_key = key
+        return key
 
     def _arrival_rows(self, payload, layout: ArenaLayout, codec: str):
         hit = self._arrivals.get(id(payload))
@@ -346,7 +377,7 @@ class FedAvgEngine:
             return None
         if hit[7] != payload_fingerprint(payload):
             return None  # an entry was replaced or written after arrival: stage the current tensors
-        return hit[3], hit[4]
+        return hit[3], hit[4], hit[8]
 
     def drop_arrival(self, payload) -> None:
         """Return one payload's arrival slot (a multi-GPU prestage that failed on another device).
@@ -360,7 +391,7 @@ class FedAvgEngine:
 
     def release_arrivals(self) -> None:
         """Return every arrival slot (after the round that used them has completed, or failed)."""
-        for payload, codec, _, _, _, slab, row, _ in self._arrivals.values():
+        for payload, codec, _, _, _, slab, row, _, _ in self._arrivals.values():
             self._arrival_free.setdefault(codec, []).append((slab, row))
         self._arrivals = {}
 
@@ -665,6 +696,7 @@ class AggregationRound:
             raise ValueError("delta arenas: the clients were staged as deltas of the previous baseline")
         eng._stager.put(baseline, eng._base.f32, eng._base.i64)
         self.has_baseline = True
+        self._base_key = baseline_key(baseline)
         self._decoded = None
 
     def put_client(self, slot: int, payload: Mapping[str, torch.Tensor],
@@ -704,9 +736,14 @@ class AggregationRound:
         hit = self.engine._arrival_rows(payload, self.layout, self.codec)
         if hit is None:
             return False
+        pf, pi, delta_key = hit
+        if delta_key is not None and not (self.deltas and delta_key == getattr(self, "_base_key", None)):
+            return False  # a delta against another model (or a weight round): stage the payload again
         self._coded_scales(slot, payload)
-        self._pf[slot], self._pi[slot] = hit
-        if self.deltas:  # the arrival row held the weights: its delta, in place (the row is this round's)
+        self._pf[slot], self._pi[slot] = pf, pi
+        if delta_key is not None:
+            self._converted.add((pf, pi))  # turned into its delta at arrival, against this round's baseline
+        elif self.deltas:  # the arrival row holds the weights: its delta now, in place (the row is this round's)
             self._to_delta(slot)
         self.staged[slot] = True
         self._decoded = None  # decoded rows are per staged set

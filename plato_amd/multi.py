@@ -265,11 +265,14 @@ class MultiDeviceEngine:
             shard.copy_stream.wait_stream(torch.cuda.current_stream(shard.device))
         return (ClientRound if client_split else MultiRound)(self, layout, capacity, codec)
 
-    def prestage(self, payload: Mapping[str, torch.Tensor], baseline_layout: ArenaLayout) -> bool:
-        """Copy an arriving payload's buckets to their GPUs now (adopted by the next round)."""
+    def prestage(self, payload: Mapping[str, torch.Tensor], baseline_layout: ArenaLayout,
+                 baseline: Mapping[str, torch.Tensor] | None = None) -> bool:
+        """Copy an arriving payload's buckets to their GPUs now (adopted by the next round).
+
+        (``baseline``: for the first GPU's delta rounds only, FedAvgEngine.prestage.)"""
         codec = payload_codec(payload)
         if codec not in MULTI_CODECS:
-            return self.primary.prestage(payload, baseline_layout)
+            return self.primary.prestage(payload, baseline_layout, baseline)
         try:
             baseline_layout.check_compatible(payload, "arriving payload", codec)
         except (KeyError, ValueError):
@@ -569,7 +572,7 @@ class ClientShardedEngine:
     def begin(self, template, capacity: int, codec: str = "native") -> "ClientRound":
         return self.multi.begin(template, capacity, codec, client_split=True)
 
-    def prestage(self, payload, baseline_layout: ArenaLayout) -> bool:
+    def prestage(self, payload, baseline_layout: ArenaLayout, baseline=None) -> bool:
         return self.multi.prestage(payload, baseline_layout)
 
     def release_arrivals(self) -> None:
@@ -906,7 +909,7 @@ class EntryShardedEngine:
 
         return EntryRound(self, layout, [(g, names) for g, names in parts], self.each(start, parts), codec)
 
-    def prestage(self, payload, baseline_layout: ArenaLayout) -> bool:
+    def prestage(self, payload, baseline_layout: ArenaLayout, baseline=None) -> bool:
         """Copy each shard's entries of an arriving payload to its GPU now (adopted by the next round)."""
         codec = payload_codec(payload)
         try:

@@ -60,9 +60,8 @@ class _EngineHolder:
     #: every fp32 entry to its flattened position so the dot kernel reads whole lines
     arena_alignment = None
     #: stage each client as its delta x - b (FedAvgEngine.delta_arenas; FedAdp's servers): the
-    #: subtraction runs behind each client's H2D, and the reductions that re-read the baseline per
-    #: client stream none.  Off when payloads are staged at arrival (stage_on_arrival): their rows are
-    #: copied before the round's baseline is known, so the subtraction would land on the round itself.
+    #: subtraction runs behind each client's H2D (with stage_on_arrival: at arrival, against the
+    #: server's current model), and the reductions that re-read the baseline per client stream none
     arena_deltas = False
 
     def aggregation_engine(self):
@@ -79,7 +78,7 @@ class _EngineHolder:
                 device = f"cuda:{device}" if isinstance(device, int) else device
                 eng = FedAvgEngine(device, variant=self.aggregation_variant)
             eng.layout_align = self.arena_alignment
-            deltas = bool(self.arena_deltas) and not getattr(self, "stage_on_arrival", False)
+            deltas = bool(self.arena_deltas)
             # one GPU, or the first GPU of several (where FedAdp's rounds run unless split by client)
             target = eng if isinstance(eng, FedAvgEngine) else getattr(eng, "primary", None)
             if target is not None and not (target is not eng and self.client_split_rounds):

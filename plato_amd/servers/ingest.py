@@ -48,6 +48,19 @@ class WireIngestMixin:
         self._plato_amd_ingest_layout = layout
         return layout
 
+    def _arrival_baseline(self):
+        """The current model, for engines that stage arrivals as deltas (``arena_deltas``), else None.
+
+        It is the baseline of the round the arriving payload joins, unless the model changes before
+        that round aggregates; the round then sees a different key and stages the payload again.
+        """
+        if not getattr(self, "arena_deltas", False):
+            return None
+        try:
+            return self.algorithm.extract_weights()
+        except (AttributeError, TypeError):
+            return None
+
     def ingest_payload(self, payload):
         """Native ``pickle.loads`` of one payload (falls back for non-tensor payloads).
 
@@ -96,7 +109,7 @@ class WireIngestMixin:
         if self.stage_on_arrival and isinstance(payload, ingest.ArenaStateDict):
             layout = self._ingest_layout()
             if layout is not None:
-                self.round_engine(payload_codec(payload)).prestage(payload, layout)
+                self.round_engine(payload_codec(payload)).prestage(payload, layout, self._arrival_baseline())
 
         if self.wire_size_accounting and file_len is not None:
             payload_size = (file_len + sys.getsizeof(b"")) / 1024**2
@@ -128,7 +141,7 @@ class WireIngestMixin:
         if self.stage_on_arrival and isinstance(_data, ingest.ArenaStateDict):
             layout = self._ingest_layout()
             if layout is not None:
-                self.round_engine(payload_codec(_data)).prestage(_data, layout)
+                self.round_engine(payload_codec(_data)).prestage(_data, layout, self._arrival_baseline())
 
         if self.client_payload[sid] is None:
             self.client_payload[sid] = _data

@@ -81,6 +81,18 @@ def payload_fingerprint(state_dict) -> tuple:
             tuple((name, id(t), getattr(t, "_version", 0)) for name, t in state_dict.items()))
 
 
+def baseline_key(state_dict) -> tuple:
+    """Storage + in-place version of every tensor of a model's ``state_dict`` (delta arenas).
+
+    ``extract_weights`` returns fresh tensor objects over the model's storage on every call, so a
+    model is keyed by where its tensors live and their version counters: ``load_state_dict`` writes
+    them in place (the counters move), a replaced parameter moves its storage.  Rows staged as deltas
+    at arrival are adopted only by a round whose baseline has the same key.
+    """
+    return tuple((name, t.data_ptr(), getattr(t, "_version", 0), tuple(t.shape), str(t.dtype))
+                 for name, t in state_dict.items())
+
+
 def arena_source(state_dict, layout: ArenaLayout, codec: str):
     """The pinned arena regions of an ingested payload, or None if it must be packed."""
     arena_f = getattr(state_dict, "arena_f32", None)

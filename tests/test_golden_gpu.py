@@ -11,6 +11,7 @@ the way the reference's _process_reports does (plato/servers/fedavg.py:171-182).
 
 import asyncio
 import types
+from collections import OrderedDict
 
 import numpy as np
 import pytest
@@ -436,8 +437,13 @@ def test_weighted_sum_matches_sequential_loop(engine):
     assert got.tobytes() == exp.tobytes()
 
 
-def test_stage_on_arrival_then_adopt_matches_reference():
-    """Payloads staged to HBM as they arrive (any arrival order), summed in updates order."""
+@pytest.mark.parametrize("mode", ["weights", "deltas", "deltas_stale"])
+def test_stage_on_arrival_then_adopt_matches_reference(mode):
+    """Payloads staged to HBM as they arrive (any arrival order), summed in updates order.
+
+    "deltas": the server stages arrivals as deltas against its current model (arena_deltas), adopted by a
+    round on that model; "deltas_stale": the model the arrivals were turned into deltas against is another
+    one (other storage), so the round stages every payload again from its host tensors."""
     import pickle
 
     from plato_amd import ingest
@@ -447,13 +453,17 @@ def test_stage_on_arrival_then_adopt_matches_reference():
     recipe, exp = case["recipe"], case["expected"]
     layout, baseline, payloads = _host_payloads(recipe)
 
+    at_arrival = (OrderedDict((n, t.clone()) for n, t in baseline.items()) if mode == "deltas_stale"
+                  else baseline)
+
     class Algo:
         def extract_weights(self):
-            return baseline
+            return at_arrival
 
     class Server(WireIngestMixin, FusedAggregationMixin):
         aggregation_device = DEV
         stage_on_arrival = True
+        arena_deltas = mode != "weights"
 
         def __init__(self):
             self.algorithm = Algo()
@@ -470,6 +480,8 @@ def test_stage_on_arrival_then_adopt_matches_reference():
         arrived[c] = server.client_payload[sid]
     eng = server.aggregation_engine()
     assert len(eng._arrivals) == recipe["k"]
+    # the arrival rows hold deltas (keyed by the model they were formed against) exactly when asked
+    assert all((hit[8] is not None) == (mode != "weights") for hit in eng._arrivals.values())
     updates = _updates(recipe, [arrived[c] for c in range(recipe["k"])])
     updated = asyncio.run(server.aggregate_weights(updates, baseline, [u.payload for u in updates]))
     assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]

@@ -343,6 +343,9 @@ def test_delta_round_matches_weight_round(name):
         for i, p in enumerate(pays):
             if i == 1 and deltas:  # one slot through the arrival path: prestaged weights, converted at adopt
                 assert eng.prestage(p, rnd.layout) and rnd.adopt(i, p)
+            elif i == 2 and deltas:  # and one turned into its delta at arrival against the same model
+                assert eng.prestage(p, rnd.layout, baseline=base)
+                assert eng._arrivals[id(p)][8] is not None and rnd.adopt(i, p)
             else:
                 rnd.put_client(i, p)
         g_f, g_i = rnd.launch_entrywise(w1, add_base=False, device=True)
