@@ -16,6 +16,7 @@
 #   profile_variants   scripts/profile_variants.sh <tag>
 #   pmc=<counters>@<script+args>   one rocprofv3 --pmc pass (comma-separated counters) over python3 <script> <args>
 #                      (default script: scripts/bench_variants.py --reps 3)
+#   kt=<script+args>   rocprofv3 --kernel-trace --stats over python3 <script> <args>
 #   py=<script+args>   python <script> <args> (spaces as '+')
 # Libraries are built in-tree before the call (never on the GPU box).
 set -u
@@ -63,6 +64,12 @@ for step in "$@"; do
               -d "$GRAFT_REPO_ROOT/$out/pmc_$n" -o pmc -- python3 "$GRAFT_REPO_ROOT/$script" "$@") \
              > "$out/pmc_$n.log" 2>&1 || { rc=$?; echo "pmc pass $n rc=$rc"; tail -4 "$out/pmc_$n.log"; exit $rc; }
            echo "=== pmc_$n ok ($ctrs over $script $*)" ;;
+    kt=*) set -- $args
+          script=$1; shift
+          (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+             -d "$GRAFT_REPO_ROOT/$out/kt_$n" -o kt -- python3 "$GRAFT_REPO_ROOT/$script" "$@") \
+            > "$out/kt_$n.log" 2>&1 || { rc=$?; echo "kernel trace $n rc=$rc"; tail -4 "$out/kt_$n.log"; exit $rc; }
+          echo "=== kt_$n ok (kernel trace of $script $*)" ;;
     py=*) run py_$n 600 python -u $args ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
