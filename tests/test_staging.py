@@ -84,3 +84,17 @@ def test_result_pool_use_count():
     assert _in_use(t)
     del v
     assert not _in_use(t)
+
+
+def test_baseline_key_follows_storage_and_in_place_writes():
+    """staging.baseline_key (delta arenas at arrival): equal for the same model's state_dict taken twice,
+    different after an in-place write (load_state_dict's copy_) or for a copy of the same values."""
+    from plato_amd.staging import baseline_key
+
+    model = torch.nn.Sequential(torch.nn.Linear(4, 3), torch.nn.BatchNorm1d(3))
+    k0 = baseline_key(model.state_dict())
+    assert baseline_key(model.state_dict()) == k0  # fresh tensor objects, same storage and versions
+    clone = {n: t.clone() for n, t in model.state_dict().items()}
+    assert baseline_key(clone) != k0  # same values elsewhere: another model as far as arrivals go
+    model.load_state_dict({n: t + 1 if t.is_floating_point() else t for n, t in clone.items()})
+    assert baseline_key(model.state_dict()) != k0  # written in place: the version counters moved
