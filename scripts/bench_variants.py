@@ -48,6 +48,8 @@ def main():
     ap.add_argument("--ew-shapes", default=None,
                     help="comma-separated chunk:threads pairs of fedavg_entrywise to time through the tuning "
                          "library (plato_agg_tune_set_entrywise_block), e.g. 2048:256,512:64")
+    ap.add_argument("--deltas", action="store_true",
+                    help="client arenas hold x - b (delta arenas): entry norms run with a null baseline")
     ap.add_argument("--norm-order", default="longest", choices=["longest", "layout"],
                     help="entry order of the norms launch (longest first = the engine's)")
     args = ap.parse_args()
@@ -67,6 +69,13 @@ def main():
     fill_clients(slab, base, 0, k)
     stream = torch.cuda.current_stream(dev)
     h = stream.cuda_stream
+    if args.deltas:  # every client row turned into its delta in place (FedAvgEngine.delta_arenas)
+        for r in range(k):
+            _lib.call("plato_agg_compute_deltas", _ptr(slab.f32[r]), _ptr(slab.i64[r]), _ptr(base.f32),
+                      _ptr(base.i64), _ptr(slab.f32[r]), _ptr(slab.i64[r]), layout.n_f32, layout.n_i64, h)
+        torch.cuda.synchronize(dev)
+    nb_f = None if args.deltas else base.f32
+    nb_i = None if args.deltas else base.i64
     pf, pi = slab.row_pointers(range(k))
     tf = torch.from_numpy(pf).to(dev)
     ti = torch.from_numpy(pi).to(dev)
@@ -141,10 +150,10 @@ def main():
     def run_norms(variant=None):
         ef, ei = engine._norm_tables(layout) if args.norm_order == "longest" else chunks(1 << 32)
         if variant is None:
-            _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64), _ptr(ef),
+            _lib.call("plato_agg_entry_norms_f32", _ptr(tf), _ptr(ti), k, _ptr(nb_f), _ptr(nb_i), _ptr(ef),
                       ef.shape[0], _ptr(ei), ei.shape[0], n_e, n_f, n_i, _ptr(norms_out), h)
         else:
-            _lib.tune_call("plato_agg_tune_entry_norms", variant, _ptr(tf), _ptr(ti), k, _ptr(base.f32), _ptr(base.i64),
+            _lib.tune_call("plato_agg_tune_entry_norms", variant, _ptr(tf), _ptr(ti), k, _ptr(nb_f), _ptr(nb_i),
                       _ptr(ef), ef.shape[0], _ptr(ei), ei.shape[0], n_e, n_f, n_i, _ptr(norms_out), h)
 
     def run_fedavg():
