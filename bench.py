@@ -536,19 +536,20 @@ def main():
     torch.cuda.synchronize(dev)
     barrier(world)
     torch.cuda.synchronize(dev)
-    # HIP events on the launch stream.  N = 1: one event per step boundary, so a step's kernel time is
-    # the span between consecutive events (the launch gap included); each recorded event costs the
-    # stream ~3-4 us (profiles/r05c_anchor.log "launch_gaps": 0.9064 ms per launch with none, 0.9097
-    # with one, 0.9182 with the three per step of rounds 1-4).  N > 1: events around the kernels and
-    # around the assembly, which are timed apart.
+    # HIP events on the launch stream.  N = 1: one event before the first step and one after the last,
+    # so the kernel time is the span over the K back-to-back launches divided by K (launch gaps
+    # included); each event recorded between two launches costs the stream ~3-4 us
+    # (profiles/r05c_anchor.log "launch_gaps": 0.9064 ms per launch with none, 0.9097 with one, 0.9182
+    # with the three per step of rounds 1-4).  N > 1: events around the kernels and around the
+    # assembly, which are timed apart.
     if plan is None:
-        bounds = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+        bounds = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         t0 = time.perf_counter()
         bounds[0].record(stream)
         for i in range(args.steps):
             kernel()
             assemble()
-            bounds[i + 1].record(stream)
+        bounds[1].record(stream)
     else:
         marks = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
         t0 = time.perf_counter()
@@ -564,7 +565,7 @@ def main():
     t1 = time.perf_counter()
     wall = max_over_ranks(t1 - t0, world)
     if plan is None:
-        kernel_ms = statistics.fmean(a.elapsed_time(b) for a, b in zip(bounds, bounds[1:]))
+        kernel_ms = bounds[0].elapsed_time(bounds[1]) / args.steps
         assembly_ms = 0.0
     else:
         kernel_ms = statistics.fmean(m[0].elapsed_time(m[1]) for m in marks)
