@@ -761,6 +761,18 @@ def variant_legs(dev, k: int, reps: int) -> dict:
                          reference="examples/server_aggregation/fedadp/fedadp_server.py:91-99")
     del rnd_a
     torch.cuda.empty_cache()
+    # the same kernel on weight arenas (the baseline streamed beside every client), for comparison
+    _, _, rnd_w = make_round("fedadp")
+
+    def fedadp_w():
+        grads = rnd_w.launch_entrywise(w1, add_base=False, device=True)
+        rnd_w.fedadp_dots(grads, slots, 0.01)
+
+    wall, km = measure(fedadp_w, rnd_w, ["fedadp_dots"])
+    out["fedadp_weight_arenas"] = dict(entry(km["fedadp_dots"], k * model_bytes + 3 * n_flat * 4, n_flat // 64),
+                                       path_ms=round(wall, 3), kernel="plato_agg_fedadp_dots, weight arenas")
+    del rnd_w
+    torch.cuda.empty_cache()
 
     # Port: norms gathered from the arenas (8 torch-order chains per vector) + cosine sums
     prev = DeviceArena(lay, dev)

@@ -569,8 +569,10 @@ constexpr AdpLaunch adp_launch() {
 // arenas the buffer still pays for its prep launch: without it (x from the flat gradient, b from
 // the baseline arena) the whole call took 1.381 ms against 1.355 (profiles/r04v_fedadp.log).
 constexpr AdpLaunch kAdpDefault = adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB>();
-// Delta arenas (null baseline): the same shape without the b loads
-constexpr AdpLaunch kAdpDefaultDelta = adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB | kFDelta>();
+// Delta arenas (null baseline): the same shape without the b loads, three stages of loads in flight (the
+// registers the b loads held): 1.077 / 1.080 against 1.088 / 1.092 ms with two, interleaved on two leases
+// (profiles/r05zzu_delta_probe_shapes.log, r05zzm_delta_probe.log; 1.054 by rocprof with two, r05zzo)
+constexpr AdpLaunch kAdpDefaultDelta = adp_launch<192, 12, 2, 3, kFYnt | kFDiv64 | kFXB | kFDelta>();
 #ifdef PLATO_AGG_TUNE
 const AdpLaunch kAdpVariants[] = {
     kAdpDefault,                                            // 0: the default
@@ -582,12 +584,16 @@ const AdpLaunch kAdpVariants[] = {
     adp_launch<192, 12, 2, 2, kFYnt | kFXB>(),              // 6: the default with the IEEE division
     adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB, 1>(), // 7: probe: the default's chains alone
     adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB, 2>(), // 8: probe: the default's producers alone
-    kAdpDefaultDelta,                                        // 9: the default for delta arenas (null baseline)
+    adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 9: the default's shape on delta arenas
+                                                                     //    (null baseline), two stages in flight
     adp_launch<128, 8, 2, 2, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 10: delta arenas, 128-step stages
     adp_launch<256, 8, 4, 2, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 11: delta arenas, 256-step stages
     adp_launch<128, 8, 2, 3, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 12: delta arenas, 3 stages in flight
-    adp_launch<192, 12, 2, 3, kFYnt | kFDiv64 | kFXB | kFDelta>(), // 13: delta arenas, 192 steps, 3 stages in flight
+    kAdpDefaultDelta,                                        // 13: the default for delta arenas, 3 stages in flight
     adp_launch<192, 6, 4, 2, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 14: delta arenas, 6 producer waves x 4
+    adp_launch<192, 8, 3, 2, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 15: delta arenas, 8 producer waves x 3
+    adp_launch<192, 8, 3, 3, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 16: the same, 3 stages in flight
+    adp_launch<192, 12, 2, 4, kFYnt | kFDiv64 | kFXB | kFDelta>(), // 17: 12 waves x 2, 4 stages in flight
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)
