@@ -357,6 +357,8 @@ class FedAvgEngine:
     def _arrival_baseline(self, baseline: Mapping[str, torch.Tensor]):
         """The arrival baseline on the device (staged once per model version); its key, or None."""
         key = baseline_key(baseline)
+        if key is None:  # a model without version counters: arrivals stay weights
+            return None
         if key == getattr(self, "_arrival_base_key", None):
             return key
         try:

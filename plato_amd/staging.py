@@ -89,8 +89,10 @@ def baseline_key(state_dict) -> tuple:
     them in place (the counters move), a replaced parameter moves its storage.  Rows staged as deltas
     at arrival are adopted only by a round whose baseline has the same key.
     """
-    return tuple((name, t.data_ptr(), getattr(t, "_version", 0), tuple(t.shape), str(t.dtype))
-                 for name, t in state_dict.items())
+    try:
+        return tuple((name, t.data_ptr(), t._version, tuple(t.shape), str(t.dtype)) for name, t in state_dict.items())
+    except (AttributeError, RuntimeError):  # not tensors, or inference tensors (no version counter): no key
+        return None
 
 
 def arena_source(state_dict, layout: ArenaLayout, codec: str):

@@ -98,3 +98,6 @@ def test_baseline_key_follows_storage_and_in_place_writes():
     assert baseline_key(clone) != k0  # same values elsewhere: another model as far as arrivals go
     model.load_state_dict({n: t + 1 if t.is_floating_point() else t for n, t in clone.items()})
     assert baseline_key(model.state_dict()) != k0  # written in place: the version counters moved
+    with torch.inference_mode():
+        frozen = {"w": torch.ones(3)}
+    assert baseline_key(frozen) is None  # inference tensors keep no version counter: no key, no arrival deltas
