@@ -17,9 +17,10 @@
 // * plato_agg_torch_cosine_sum is the sum in F.cosine_similarity
 //   (port_server.py:50): q = (a/|a|)*(b/|b|) summed by PyTorch's CPU
 //   two-pass reduction over T OpenMP chunks, each a 4-level cascade of 8-wide
-//   vectors x 4 rows of ILP (ATen SumKernel.cpp).  A workgroup computes one
-//   (client, chunk): the level-0 groups in parallel, the higher levels in
-//   order; a second launch combines the T partials.  (The norms |a|, |b| are
+//   vectors x 4 rows of ILP (ATen SumKernel.cpp).  A workgroup computes two
+//   clients of one chunk (a staged once in LDS for both; one client per
+//   workgroup for chunks past 2^24 elements): the level-0 groups in parallel,
+//   the higher levels in order; a second launch combines the T partials.  (The norms |a|, |b| are
 //   plato_agg_entry_norms_f32 over the flattened vectors.)
 // Compiled with -ffp-contract=off: fmaf where the reference fuses, separate
 // roundings everywhere else; divisions are IEEE (correctly rounded).
@@ -724,6 +725,94 @@ __device__ float chunk_cascade(const Q& q, uint64_t b0, uint64_t size0, float* l
   return result;
 }
 
+// chunk_cascade for two clients of one chunk (L = 16, chunks of at most 2^24 elements), 512 threads: each
+// half (256 threads) runs one client's cascade exactly as chunk_cascade's common case (the same level-0
+// groups per thread, the same sums in the same order), and the shared vector a of each level-1 group is
+// loaded once for both into LDS (32 KB, 16 coalesced loads per thread) instead of once per client from L2.
+// Barriers are the whole workgroup's: both halves walk the same chunk, so they meet every one.
+template <int C, class Q>
+__device__ float chunk_cascade2(const Q& q, uint64_t b0, uint64_t size0, float* s0, float* a_lds) {
+  constexpr int kL = 16, kH = kSumThreads;  // threads per client
+  const uint64_t vec_size = size0 / 8;
+  const uint64_t size_ilp = vec_size / 4;
+  const uint64_t G0 = size_ilp / kL;  // full level-0 groups
+  const uint64_t G1 = G0 / kL;        // full level-1 groups
+  const int tid = int(threadIdx.x) & (kH - 1), wtid = int(threadIdx.x);
+  const int acc_id = tid & 31, gslot = tid >> 5;
+  float acc2 = 0.f, acc3 = 0.f;  // lanes 0..31 of the half's first wave
+  for (uint64_t g1 = 0; g1 < G1; ++g1) {
+    constexpr int kJ = 16 / (kH / 32), kA = kL * kL * 32 / (C * kH);  // 2 groups, 8192 / (C * 256) a values
+    const float* ag = q.a + b0 + g1 * (kL * kL * 32);
+    float av[kA], bv[kJ][kL];
+#pragma unroll
+    for (int j = 0; j < kA; ++j) av[j] = ag[j * C * kH + wtid];
+#pragma unroll
+    for (int jj = 0; jj < kJ; ++jj) {
+      const uint64_t row0 = (g1 * kL + uint64_t(gslot + jj * (kH / 32))) * kL;
+#pragma unroll
+      for (int i = 0; i < kL; ++i) bv[jj][i] = q.b[b0 + (row0 + uint64_t(i)) * 32 + uint64_t(acc_id)];
+    }
+#pragma unroll
+    for (int j = 0; j < kA; ++j) a_lds[j * C * kH + wtid] = av[j];
+    __syncthreads();  // the group's a in LDS (and the previous group's level-1 reads of s0 done)
+#pragma unroll
+    for (int jj = 0; jj < kJ; ++jj) {
+      const int g = gslot + jj * (kH / 32);
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < kL; ++i) s += q.av(a_lds[(g * kL + i) * 32 + acc_id]) * (bv[jj][i] / q.nb);
+      s0[g * 32 + acc_id] = s;
+    }
+    __syncthreads();  // s0 complete; every a_lds read done
+    if (tid < 32) {
+      float s1 = 0.f;
+      for (int j = 0; j < kL; ++j) s1 += s0[j * 32 + tid];
+      acc2 += s1;
+      if ((g1 + 1) % kL == 0) {
+        acc3 += acc2;
+        acc2 = 0.f;
+      }
+    }
+  }
+  // the partial level-1 group and the tails: chunk_cascade's code per half (a from global memory)
+  auto s0_of = [&](uint64_t g0) {
+    float s = 0.f;
+    const uint64_t row0 = g0 * kL;
+    for (uint64_t i = 0; i < uint64_t(kL); ++i) s += q(b0 + (row0 + i) * 32 + uint64_t(acc_id));
+    return s;
+  };
+  __syncthreads();  // lanes 0..31 have read the last pass's s0
+  const uint64_t rem0 = G0 - G1 * kL;
+  for (uint64_t j = uint64_t(gslot); j < rem0; j += kH / 32) s0[j * 32 + uint64_t(acc_id)] = s0_of(G1 * kL + j);
+  __syncthreads();
+  float result = 0.f;
+  if (tid < 32) {
+    float acc1 = 0.f;
+    for (uint64_t j = 0; j < rem0; ++j) acc1 += s0[j * 32 + uint64_t(tid)];
+    float acc0 = 0.f;  // the rows after the last complete level-0 group
+    for (uint64_t i = G0 * kL; i < size_ilp; ++i) acc0 += q(b0 + i * 32 + uint64_t(tid));
+    float ps = acc0;
+    ps += acc1;
+    ps += acc2;
+    ps += acc3;
+    s0[tid] = ps;  // ps[k][l] at k*8 + l
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float ps0[8];
+    for (int l = 0; l < 8; ++l) ps0[l] = s0[l];
+    for (uint64_t v = size_ilp * 4; v < vec_size; ++v)
+      for (int l = 0; l < 8; ++l) ps0[l] += q(b0 + v * 8 + uint64_t(l));
+    for (int k = 1; k < 4; ++k)
+      for (int l = 0; l < 8; ++l) ps0[l] += s0[k * 8 + l];
+    float final_acc = 0.f;
+    for (uint64_t e = vec_size * 8; e < size0; ++e) final_acc += q(b0 + e);
+    for (int l = 0; l < 8; ++l) final_acc += ps0[l];
+    result = final_acc;
+  }
+  return result;
+}
+
 // scalar_inner_sum / vectorized_inner_sum of a short array (single thread), W = 8 (n >= 8) or 1 lanes;
 // every accumulator index is a compile-time constant (unrolled k, l and level loops), so the 4 x 4 x 8
 // cascade stays in registers (the runtime-indexed form spilled 656 bytes per lane to scratch and took
@@ -883,6 +972,42 @@ __global__ __launch_bounds__(kSumThreads) void cosine_chunks_kernel(CosArgs a) {
     }
   }
   if (threadIdx.x == 0) a.partial[uint64_t(k) * a.T + t] = 0.f + r;
+}
+
+// Two clients of a chunk per 512-thread workgroup sharing the loads of a through LDS (chunk_cascade2);
+// chunks of at most 2^24 elements (L = 16).  A missing second client (K odd) recomputes client K - 1 in
+// its half without storing it.
+template <bool kScaled, int C = 2>
+__global__ __launch_bounds__(C * kSumThreads) void cosine_chunks2_kernel(CosArgs a, int K) {
+  __shared__ float s0_all[C][16 * 32];
+  __shared__ float a_lds[16 * 16 * 32];
+  const int half = int(threadIdx.x) / kSumThreads;
+  const int k_raw = int(blockIdx.x) * C + half, k = k_raw < K ? k_raw : K - 1;
+  const int t = blockIdx.y;
+  const uint64_t b0 = uint64_t(t) * a.chunk;
+  if (b0 >= a.n) return;  // workgroup-uniform
+  const uint64_t e0 = b0 + a.chunk < a.n ? b0 + a.chunk : a.n;
+  QSrcT<kScaled> q;
+  q.a = a.av;
+  q.b = sld(a.bv, k);
+  q.na = kScaled ? 1.f : a.norm_a[0];
+  q.nb = a.norm_b[k];
+  if (q.na < a.eps) q.na = a.eps;  // clamp_min_: NaN stays NaN
+  if (q.nb < a.eps) q.nb = a.eps;
+  const uint64_t size0 = e0 - b0;
+  const int tid = int(threadIdx.x) % kSumThreads;
+  float r;
+  if (size0 >= 8) {
+    r = chunk_cascade2<C>(q, b0, size0, s0_all[half], a_lds);
+  } else {
+    r = 0.f;
+    if (tid == 0) {
+      float tmp[8];
+      for (uint64_t e = 0; e < size0; ++e) tmp[e] = q(b0 + e);
+      r = small_inner_sum(tmp, int(size0));
+    }
+  }
+  if (tid == 0 && k_raw < K) a.partial[uint64_t(k) * a.T + t] = 0.f + r;
 }
 
 // a / max(|a|, eps) (F.cosine_similarity's x1 / x1_norm after clamp_min_), once for the K sums
@@ -1639,13 +1764,28 @@ int run_cosine(bool scaled, const float* d_a, const float* const* d_b, int K, si
   // variant (tuning only): 1 = one LDS buffer, two barriers per level-1 group (round 3).  Held to 64
   // VGPRs (eight waves per SIMD, the 2,048-workgroup grid in one round) the default spilled (2.23 ms)
   // and, loading one level-0 group at a time, ran 1.070 against 1.044 (profiles/r04zh_cosine.log).  Two
-  // clients of a chunk per workgroup sharing the loads of a (118 VGPRs, lanes 32c.. of wave 0 running client
-  // c's higher levels) ran 1.117 against 1.083, bitwise equal (profiles/r05z_cosine_variants.log); removed
+  // clients of a chunk per workgroup sharing the loads of a in registers (118 VGPRs, lanes 32c.. of wave 0
+  // running client c's higher levels) ran 1.117 against 1.083, bitwise equal (profiles/r05z_cosine_variants.log);
+  // removed.  Shared through LDS instead (cosine_chunks2_kernel), two clients win: the default below
   const dim3 grid{uint32_t(K), uint32_t(a.nt)};
+  // variant 0 (the default): two clients of a chunk per 512-thread workgroup, a shared through LDS
+  // (cosine_chunks2_kernel<2>), when every chunk has L = 16 (at most 2^24 elements) and K >= 2: 1.041 /
+  // 1.042 ms against 1.109 / 1.111 for the one-client kernel (variant 2, the round-4/5 default) in two
+  // interleaved runs, 1.056 / 1.074 against 1.093 / 1.101 on another lease (profiles/r05zzzb_cosine_shared_a.log,
+  // r05zzza_…), bitwise equal; four clients per workgroup (variant 3) 1.23-1.27.  Else the one-client kernel.
+  const bool two = a.chunk <= (uint64_t(1) << 24) && K >= 2;
   if (variant == 1) {
     if (scaled) hipLaunchKernelGGL((cosine_chunks_kernel<true, false>), grid, dim3(kSumThreads), 0, stream, a);
     else hipLaunchKernelGGL((cosine_chunks_kernel<false, false>), grid, dim3(kSumThreads), 0, stream, a);
-  } else {
+  } else if (variant == 0 && two) {
+    const dim3 g2{uint32_t((K + 1) / 2), uint32_t(a.nt)};
+    if (scaled) hipLaunchKernelGGL((cosine_chunks2_kernel<true, 2>), g2, dim3(2 * kSumThreads), 0, stream, a, K);
+    else hipLaunchKernelGGL((cosine_chunks2_kernel<false, 2>), g2, dim3(2 * kSumThreads), 0, stream, a, K);
+  } else if (variant == 3 && two) {  // four clients per workgroup
+    const dim3 g4{uint32_t((K + 3) / 4), uint32_t(a.nt)};
+    if (scaled) hipLaunchKernelGGL((cosine_chunks2_kernel<true, 4>), g4, dim3(4 * kSumThreads), 0, stream, a, K);
+    else hipLaunchKernelGGL((cosine_chunks2_kernel<false, 4>), g4, dim3(4 * kSumThreads), 0, stream, a, K);
+  } else {  // variant 2 and the fallback: one client per workgroup, double-buffered level-0 sums
     if (scaled) hipLaunchKernelGGL(cosine_chunks_kernel<true>, grid, dim3(kSumThreads), 0, stream, a);
     else hipLaunchKernelGGL(cosine_chunks_kernel<false>, grid, dim3(kSumThreads), 0, stream, a);
   }
@@ -1733,12 +1873,12 @@ int plato_agg_torch_cosine_sum_scaled(const float* d_a_scaled, const float* cons
 }
 
 #ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
-int plato_agg_tune_num_cosine_variants(void) { return 2; }
+int plato_agg_tune_num_cosine_variants(void) { return 4; }
 
 int plato_agg_tune_torch_cosine_sum_scaled(int variant, const float* d_a_scaled, const float* const* d_b, int K,
                                            size_t n, const float* d_norm_b, float eps, int threads,
                                            void* d_workspace, float* d_out, hipStream_t stream) {
-  if (variant < 0 || variant > 1) return set_error(PLATO_AGG_EINVAL, "bad cosine variant");
+  if (variant < 0 || variant > 3) return set_error(PLATO_AGG_EINVAL, "bad cosine variant");
   return run_cosine(true, d_a_scaled, d_b, K, n, nullptr, d_norm_b, eps, threads, d_workspace, d_out, stream,
                     variant);
 }
