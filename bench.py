@@ -71,7 +71,7 @@ def parse():
                    help="launcher check without a GPU: every rank joins a gloo group, rank 0 prints one JSON line")
     p.add_argument("--no-variants", action="store_true",
                    help="skip the variant servers' reductions leg (SURVEY.md §8(f), N=1 only)")
-    p.add_argument("--variant-reps", type=int, default=5)
+    p.add_argument("--variant-reps", type=int, default=10)
     p.add_argument("--engine-devices", type=int, default=0,
                    help="single-process multi-GPU engine (plato_amd.multi) over this many devices: host-inclusive "
                         "and device-resident timings of the server's own path (repeats cuda:0 on a 1-GPU box)")
