@@ -793,10 +793,18 @@ def variant_legs(dev, k: int, reps: int) -> dict:
     out["fedatt_norms"] = dict(entry(km["entry_norms"], (k + 1) * n_f * 4, longest // 8), path_ms=round(wall, 3),
                                kernel="plato_agg_entry_norms_f32",
                                reference="examples/server_aggregation/fedatt/fedatt_algorithm.py:34-39")
-    wall, km = measure(lambda: rnd.np_sumsq(slots), rnd, ["np_sumsq"])
-    out["polaris_sumsq"] = dict(entry(km["np_sumsq"], (k + 1) * n_f * 4), path_ms=round(wall, 3),
-                                kernel="plato_agg_np_sumsq",
+    wall_w, km_w = measure(lambda: rnd.np_sumsq(slots), rnd, ["np_sumsq"])
+    # Polaris' rounds stage deltas (PolarisWeights.arena_deltas): the sums on delta arenas, no baseline
+    _, _, rnd_p = make_round(None, deltas=True)
+    wall, km = measure(lambda: rnd_p.np_sumsq(slots), rnd_p, ["np_sumsq"])
+    out["polaris_sumsq"] = dict(entry(km["np_sumsq"], k * n_f * 4), path_ms=round(wall, 3),
+                                kernel="plato_agg_np_sumsq, delta arenas",
+                                staging_delta_ms_per_client=round(rnd_p.delta_ms_per_client, 4),
                                 reference="examples/client_selection/polaris/polaris_server.py:78-81")
+    out["polaris_sumsq_weight_arenas"] = dict(entry(km_w["np_sumsq"], (k + 1) * n_f * 4), path_ms=round(wall_w, 3),
+                                              kernel="plato_agg_np_sumsq, weight arenas")
+    del rnd_p
+    torch.cuda.empty_cache()
 
     # QSGD-coded FedAvg: one code byte per element through HBM, decoded in the kernel
     qslab = ClientSlab(lay, k, dev, codec="qsgd")

@@ -1225,16 +1225,17 @@ __device__ __forceinline__ NpTask np_task(const SumsqArgs& a, uint64_t t) {  // 
 }
 
 // kT threads per workgroup, kNpBuf / kT elements per lane: element q * kT + tid.
-template <int kT>
+// kB = false: delta arenas (a null baseline; the rows already hold x - b, so b = 0: x - 0 is x bit for bit)
+template <int kT, bool kB = true>
 __device__ __forceinline__ void np_load(const SumsqArgs& a, const NpTask& t, float (&xv)[kNpBuf / kT],
                                         float (&bv)[kNpBuf / kT]) {
   const float* x = a.x[t.k] + t.begin;
-  const float* b = a.base + t.begin;
+  const float* b = kB ? a.base + t.begin : nullptr;
 #pragma unroll
   for (int q = 0; q < int(kNpBuf / kT); ++q) {
     const uint32_t i = uint32_t(q * kT) + threadIdx.x;
     xv[q] = i < t.n ? __builtin_nontemporal_load(x + i) : 0.f;
-    bv[q] = i < t.n ? b[i] : 0.f;
+    bv[q] = (kB && i < t.n) ? b[i] : 0.f;
   }
 }
 
@@ -1410,6 +1411,7 @@ __global__ __launch_bounds__(256) void np_sumsq_half_kernel(SumsqArgs a) {
 // aligned).  A quarter of the load and LDS-write instructions of the dword form; the same leaves, the
 // same accumulators, the same order.
 typedef __attribute__((address_space(1))) const f4 gcf4;
+template <bool kB = true>
 __global__ __launch_bounds__(256) void np_sumsq_half4_kernel(SumsqArgs a) {
   __shared__ __attribute__((aligned(16))) float sq[kNpBuf / kPW / 2 * kLeafPitch];
   __shared__ float leaf_sum[kNpBuf / kPW];
@@ -1419,11 +1421,11 @@ __global__ __launch_bounds__(256) void np_sumsq_half4_kernel(SumsqArgs a) {
   const int tid = int(threadIdx.x);
   f4 xv[kQ], bv[kQ];
   const gcf4* x = (const gcf4*)(a.x[t.k] + t.begin) + tid;
-  const gcf4* b = (const gcf4*)(a.base + t.begin) + tid;
+  const gcf4* b = kB ? (const gcf4*)(a.base + t.begin) + tid : nullptr;
 #pragma unroll
   for (int q = 0; q < kQ; ++q) {
     xv[q] = __builtin_nontemporal_load(x + q * 256);
-    bv[q] = b[q * 256];
+    bv[q] = kB ? b[q * 256] : f4{0.f, 0.f, 0.f, 0.f};
   }
   const int leaf = tid >> 3, j = tid & 7;
 #pragma unroll
@@ -1459,7 +1461,7 @@ __global__ __launch_bounds__(256) void np_sumsq_half4_kernel(SumsqArgs a) {
 // all of them (the L2-served b re-reads take as many of a CU's in-flight read slots as the client
 // bytes), the clients' squares staged and summed one after the other through the same
 // half-chunk buffer.  A ragged last group (K mod C) loads and stores only its own clients.
-template <int C, bool kFirstThenRest = false>
+template <int C, bool kFirstThenRest = false, bool kB = true>
 __global__ __launch_bounds__(256) void np_sumsq_half4xc_kernel(SumsqArgs a) {
   __shared__ __attribute__((aligned(16))) float sq[kNpBuf / kPW / 2 * kLeafPitch];
   __shared__ float leaf_sum[C][kNpBuf / kPW];
@@ -1470,13 +1472,13 @@ __global__ __launch_bounds__(256) void np_sumsq_half4xc_kernel(SumsqArgs a) {
   constexpr int kQ = int(kNpBuf / 1024), kHalfQ = kQ / 2;
   const int tid = int(threadIdx.x);
   f4 xv[C][kQ], bv[kQ];
-  const gcf4* b = (const gcf4*)(a.base + t.begin) + tid;
+  const gcf4* b = kB ? (const gcf4*)(a.base + t.begin) + tid : nullptr;
   if constexpr (kFirstThenRest) {  // the first client and b, then the others: client 0's squares can be
                                    // staged while the later clients' loads are still in flight
 #pragma unroll
     for (int q = 0; q < kQ; ++q) {
       xv[0][q] = __builtin_nontemporal_load((const gcf4*)(a.x[t.k] + t.begin) + tid + q * 256);
-      bv[q] = b[q * 256];
+      bv[q] = kB ? b[q * 256] : f4{0.f, 0.f, 0.f, 0.f};
     }
 #pragma unroll
     for (int c = 1; c < C; ++c) {
@@ -1493,7 +1495,7 @@ __global__ __launch_bounds__(256) void np_sumsq_half4xc_kernel(SumsqArgs a) {
         const gcf4* x = (const gcf4*)(a.x[c < nc ? t.k + c : t.k] + t.begin) + tid;
         xv[c][q] = c < nc ? __builtin_nontemporal_load(x + q * 256) : f4{0.f, 0.f, 0.f, 0.f};  // nc is uniform
       }
-      bv[q] = b[q * 256];
+      bv[q] = kB ? b[q * 256] : f4{0.f, 0.f, 0.f, 0.f};
     }
   }
   const int leaf = tid >> 3, j = tid & 7;
@@ -1534,7 +1536,7 @@ __global__ __launch_bounds__(256) void np_sumsq_half4xc_kernel(SumsqArgs a) {
 
 // The partial last chunk of every (piece, client), through the full-staging path (kPar: its leaves
 // summed in parallel, np_partial_par).
-template <bool kPar = true>
+template <bool kPar = true, bool kB = true>
 __global__ __launch_bounds__(256) void np_sumsq_tail_kernel(SumsqArgs a) {
   __shared__ float sq[kNpBuf / kPW * kLeafPitch];
   __shared__ float leaf_sum[kNpBuf / kPW];
@@ -1544,7 +1546,7 @@ __global__ __launch_bounds__(256) void np_sumsq_tail_kernel(SumsqArgs a) {
   const NpTask t = np_task(a, uint64_t(c_end - 1) * uint64_t(a.K) + k);
   if (t.n == kNpBuf) return;  // workgroup-uniform: a whole last chunk went through the half kernel
   float xv[kNpBuf / 256], bv[kNpBuf / 256];
-  np_load<256>(a, t, xv, bv);
+  np_load<256, kB>(a, t, xv, bv);
   np_chunk<256, kPar>(a, t, xv, bv, sq, leaf_sum);
 }
 
@@ -1596,12 +1598,21 @@ void launch_sumsq(int variant, const SumsqArgs& a, hipStream_t st, hipStream_t t
     return;
   }
   // the partial last chunks first (on tail_st: beside the full chunks), then the full chunks
+  if (!a.base) {  // delta arenas (the default family only, run_np_sumsq): no baseline loads
+    hipLaunchKernelGGL((np_sumsq_tail_kernel<true, false>), tail_grid, dim3(256), 0, tail_st, a);
+    const int cd = variant == 6 ? 1 : variant == 14 ? 2 : 4;
+    const dim3 gd{uint32_t(uint64_t(a.n_chunks) * uint64_t((a.K + cd - 1) / cd))};
+    if (cd == 1) hipLaunchKernelGGL(np_sumsq_half4_kernel<false>, grid, dim3(256), 0, st, a);
+    else if (cd == 2) hipLaunchKernelGGL((np_sumsq_half4xc_kernel<2, true, false>), gd, dim3(256), 0, st, a);
+    else hipLaunchKernelGGL((np_sumsq_half4xc_kernel<4, false, false>), gd, dim3(256), 0, st, a);
+    return;
+  }
   if (variant == 10) hipLaunchKernelGGL(np_sumsq_tail_kernel<false>, tail_grid, dim3(256), 0, tail_st, a);
   else hipLaunchKernelGGL(np_sumsq_tail_kernel<true>, tail_grid, dim3(256), 0, tail_st, a);
   const int c = (variant == 7 || variant == 12) ? 3 : (variant == 0 || variant == 8 || variant == 13) ? 4 : 2;
   const dim3 gc{uint32_t(uint64_t(a.n_chunks) * uint64_t((a.K + c - 1) / c))};
   if (variant == 5) hipLaunchKernelGGL(np_sumsq_half_kernel, grid, dim3(256), 0, st, a);
-  else if (variant == 6) hipLaunchKernelGGL(np_sumsq_half4_kernel, grid, dim3(256), 0, st, a);
+  else if (variant == 6) hipLaunchKernelGGL(np_sumsq_half4_kernel<>, grid, dim3(256), 0, st, a);
   else if (variant == 7) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<3>, gc, dim3(256), 0, st, a);
   else if (variant == 8 || variant == 0) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<4>, gc, dim3(256), 0, st, a);
   else if (variant == 9) hipLaunchKernelGGL(np_sumsq_half4xc_kernel<2>, gc, dim3(256), 0, st, a);
@@ -1678,8 +1689,11 @@ int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_bas
                  float* d_out, hipStream_t stream) {
   if (K <= 0) return set_error(PLATO_AGG_EINVAL, "K must be >= 1");
   if (!n_pieces) return clear_error();
-  if (!d_x || !d_base || !d_pieces || !d_first_chunk || !d_workspace || !d_out)
+  if (!d_x || !d_pieces || !d_first_chunk || !d_workspace || !d_out)
     return set_error(PLATO_AGG_EINVAL, "null pointer");
+  // a null baseline: the client rows hold deltas (delta arenas) — the default's kernels (variants 0, 6, 14)
+  if (!d_base && variant != 0 && variant != 6 && variant != 14)
+    return set_error(PLATO_AGG_EINVAL, "a null baseline (delta arenas) needs variant 0, 6 or 14");
   SumsqArgs a{};
   a.x = d_x;
   a.base = d_base;

@@ -1257,7 +1257,6 @@ class AggregationRound:
         Returns ``[K, E]`` float32 (entries in layout order; int64 entries 0).
         """
         slots = self._check_slots(slots)
-        self._raw_only("np_sumsq")
         if not self.has_baseline:
             raise ValueError("baseline not staged")
         eng, lay = self.engine, self.layout
@@ -1287,7 +1286,9 @@ class AggregationRound:
                          device=eng.device)
         dev_out = torch.empty((k, n_p), dtype=torch.float32, device=eng.device)
         with self._timed("np_sumsq", stream):
-            _lib.call("plato_agg_np_sumsq", tf.data_ptr(), k, _ptr(self._base.f32), pieces.data_ptr(),
+            # delta arenas: a null baseline selects the kernels that load none (the rows hold x - b)
+            _lib.call("plato_agg_np_sumsq", tf.data_ptr(), k, None if self.deltas else _ptr(self._base.f32),
+                      pieces.data_ptr(),
                       first.data_ptr(), n_p, n_chunks, ws.data_ptr(), dev_out.data_ptr(), _stream_handle(stream))
         out[:, entry_of] = dev_out.cpu().numpy()
         self._resolve_timers()

@@ -281,6 +281,9 @@ class PolarisWeights(_EngineHolder):
 
     needs_staged_round = True
     entry_local_weights = True  # per-layer sums: sharded by whole entries over aggregation_devices
+    #: clients staged as deltas x - b (FedAvgEngine.delta_arenas): the sums load no baseline, 0.918-0.921
+    #: against 0.972-0.980 ms for 128 ResNet-18 clients, bitwise equal (profiles/r05zzzg_polaris_deltas.log)
+    arena_deltas = True
 
     def aggregation_weights(self, updates):
         weights, scales = super().aggregation_weights(updates)  # FedAvg n_i/N, sets total_samples

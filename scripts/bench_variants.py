@@ -48,6 +48,7 @@ def main():
     ap.add_argument("--ew-shapes", default=None,
                     help="comma-separated chunk:threads pairs of fedavg_entrywise to time through the tuning "
                          "library (plato_agg_tune_set_entrywise_block), e.g. 2048:256,512:64")
+    ap.add_argument("--sumsq-list", default=None, help="comma-separated np_sumsq variants to time")
     ap.add_argument("--deltas", action="store_true",
                     help="client arenas hold x - b (delta arenas): entry norms run with a null baseline")
     ap.add_argument("--norm-order", default="longest", choices=["longest", "layout"],
@@ -171,9 +172,13 @@ def main():
     sq_ws = torch.empty(max(1, engine.lib.plato_agg_np_sumsq_workspace(k, sq_chunks) // 4), device=dev)
     sq_out = torch.empty((k, len(sq_rows)), device=dev)
 
-    def run_sumsq():
-        _lib.call("plato_agg_np_sumsq", _ptr(tf), k, _ptr(base.f32), _ptr(sq_pieces), _ptr(sq_firsts), len(sq_rows),
-                  sq_chunks, _ptr(sq_ws), _ptr(sq_out), h)
+    def run_sumsq(variant=None):
+        if variant is None:
+            _lib.call("plato_agg_np_sumsq", _ptr(tf), k, _ptr(nb_f), _ptr(sq_pieces), _ptr(sq_firsts), len(sq_rows),
+                      sq_chunks, _ptr(sq_ws), _ptr(sq_out), h)
+        else:
+            _lib.tune_call("plato_agg_tune_np_sumsq", variant, _ptr(tf), k, _ptr(nb_f), _ptr(sq_pieces), _ptr(sq_firsts),
+                           len(sq_rows), sq_chunks, _ptr(sq_ws), _ptr(sq_out), h)
 
     kernels = {
         "qsgd": (run_qsgd, k * (n_f + n_i) + n_f * 8 + n_i * 12),
@@ -196,6 +201,9 @@ def main():
             cap, thr = (int(x) for x in pair.split(":"))
             kernels[f"entrywise_v{cap}x{thr}"] = ((lambda cap=cap, thr=thr: run_entrywise(cap, thr)),
                                                   kernels["entrywise"][1])
+    if args.sumsq_list:  # tuning: the listed plato_agg_tune_np_sumsq variants
+        for v in [int(x) for x in args.sumsq_list.split(",")]:
+            kernels[f"sumsq_v{v}"] = ((lambda v=v: run_sumsq(v)), kernels["sumsq"][1])
     if args.norm_variants or args.norm_list:  # tuning: every (or the listed) plato_agg_tune_entry_norms variant
         for v in ([int(x) for x in args.norm_list.split(",")] if args.norm_list
                   else range(_lib.tune().plato_agg_tune_num_entry_norms_variants())):

@@ -184,6 +184,25 @@ def test_np_sumsq_variants_agree_bitwise(k):
                        torch.cuda.current_stream().cuda_stream)
         torch.cuda.synchronize()
         assert out.cpu().numpy().tobytes() == want[:, entry_of].tobytes(), v
+    # delta arenas (null baseline): the default's kernels on the rows turned into x - b in place
+    h = torch.cuda.current_stream().cuda_stream
+    for c in range(k):
+        _lib.call("plato_agg_compute_deltas", rnd._pf[c], rnd._pi[c], rnd._base.f32.data_ptr(),
+                  rnd._base.i64.data_ptr(), rnd._pf[c], rnd._pi[c], layout.n_f32, layout.n_i64, h)
+    for v in (None, 0, 6, 14):
+        out = torch.full((k, int(entry_of.size)), float("nan"), device=DEV)
+        ws.fill_(float("nan"))
+        args = (tf.data_ptr(), k, None, pieces.data_ptr(), first.data_ptr(), int(entry_of.size), n_chunks,
+                ws.data_ptr(), out.data_ptr(), h)
+        if v is None:
+            _lib.call("plato_agg_np_sumsq", *args)
+        else:
+            _lib.tune_call("plato_agg_tune_np_sumsq", v, *args)
+        torch.cuda.synchronize()
+        assert out.cpu().numpy().tobytes() == want[:, entry_of].tobytes(), ("deltas", v)
+    with pytest.raises(ValueError, match="null baseline"):
+        _lib.tune_call("plato_agg_tune_np_sumsq", 5, tf.data_ptr(), k, None, pieces.data_ptr(), first.data_ptr(),
+                       int(entry_of.size), n_chunks, ws.data_ptr(), out.data_ptr(), h)
 
 
 def test_np_sumsq_equals_numpy_order():

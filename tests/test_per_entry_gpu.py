@@ -420,11 +420,12 @@ def test_delta_round_matches_weight_round(name):
         rnd.launch(weights)
         res = rnd.result()
         g_model = rnd.layout.unpack(g_f.cpu(), g_i.cpu())  # (the aligned arena has padding between entries)
-        got[deltas] = (_flat(layout, g_model, "f32").tobytes(), _flat(layout, g_model, "i64").tobytes(),
+        sumsq = rnd.np_sumsq(range(k))  # Polaris' sums: on delta arenas with a null baseline
+        got[deltas] = (sumsq.tobytes(), _flat(layout, g_model, "f32").tobytes(), _flat(layout, g_model, "i64").tobytes(),
                        [np.asarray(d).tobytes() for d in dots], _flat(layout, res, "f32").tobytes(),
                        _flat(layout, res, "i64").tobytes())
         if deltas:
-            for call in (lambda: rnd.entry_norms(range(k)), lambda: rnd.np_sumsq(range(k)),
+            for call in (lambda: rnd.entry_norms(range(k)),
                          lambda: rnd.fedadp_dots_flat((g_f, g_i), range(k), 0.01),
                          lambda: rnd.launch_entrywise(w1, add_base=True)):
                 with pytest.raises(ValueError, match="deltas"):
