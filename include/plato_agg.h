@@ -432,7 +432,9 @@ int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const 
  * d_lengths: null, or n_vectors lengths <= n_flat, vector v taking only its
  * first d_lengths[v] positions (FedAtt's per-(entry, client) norms,
  * fedatt_algorithm.py:34-39: one fp32 entry of one client per vector, the
- * pointers offset to the entry and one segment covering it).
+ * pointers offset to the entry and one segment covering it).  A null
+ * d_b_f32[v] (and d_b_i64[v]) means vector v's arenas already hold the
+ * difference (delta arenas): nothing is subtracted, the same values result.
  */
 #define PLATO_AGG_PORT_CAST_FIRST 1
 int plato_agg_port_norms(const void* const* d_x_f32, const void* const* d_x_i64, const void* const* d_b_f32,

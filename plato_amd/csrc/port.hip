@@ -90,8 +90,10 @@ __device__ __forceinline__ float pn_value(const PnArgs& a, const PnSeg* S, int& 
   while (idx + 1 < int(a.n_segs) && S[idx + 1].flat <= p) ++idx;
   const PnSeg sg = S[idx];
   const uint32_t e = p - sg.flat + sg.src;
-  if (!(sg.info & kSegI64)) return a.xf[v][e] - a.bf[v][e];
-  const int64_t x = a.xi[v][e], b = a.bi[v][e];
+  const float* bf = a.bf[v];  // null: vector v's arena already holds x - b (delta arenas)
+  if (!(sg.info & kSegI64)) return a.xf[v][e] - (bf ? bf[e] : 0.f);
+  const int64_t* bi = a.bi[v];
+  const int64_t x = a.xi[v][e], b = bi ? bi[e] : int64_t(0);
   if (v == 0 && a.cast_first) return float(x) - float(b);
   return float(int64_t(uint64_t(x) - uint64_t(b)));
 }
@@ -215,7 +217,10 @@ __global__ __launch_bounds__(64 * (1 + kWp)) void port_norms_kernel(PnArgs a_in)
   const uint32_t nbar = (ntiles + kD - 1) / kD * kD;  // barriers: whole trips of kD tiles
   if (wave > 0) {  // producer
     const int w = wave - 1;
-    const __amdgpu_buffer_rsrc_t rx = pn_rsrc(sld(a.xf, v), a.n_f32 * 4), rb = pn_rsrc(sld(a.bf, v), a.n_f32 * 4);
+    // a null subtrahend (delta arenas: the arena holds x - b): a zero-length buffer, whose loads return 0
+    // without a memory request, so x - 0 = x bit for bit
+    const float* bfv = sld(a.bf, v);
+    const __amdgpu_buffer_rsrc_t rx = pn_rsrc(sld(a.xf, v), a.n_f32 * 4), rb = pn_rsrc(bfv, bfv ? a.n_f32 * 4 : 0);
     PnCursor cur;
     pn_cursor_load(S, 0, cur);
     float* flat = a.flat ? sld(a.flat, v) : nullptr;

@@ -1321,7 +1321,6 @@ class AggregationRound:
         cross-check.
         Returned as fp32 like the reference's 0-dim tensor.
         """
-        self._raw_only("model_similarities")
         if not self.has_baseline:
             raise ValueError("baseline not staged")
         slots = list(slots)
@@ -1359,8 +1358,15 @@ class AggregationRound:
         if flat_norms:  # the round-2 path: flattened vectors, norms and sums over them
             cur, _ = self._flatten(_lib.PLATO_AGG_FLAT_CAST_DIFF, segs, n_segs, n_flat, [base[0]], [base[1]],
                                    (_ptr(prev.f32), _ptr(prev.i64)), 0.0, stream)
+            # (delta arenas: the rows minus a zero arena, x - 0 = x, int64 differences cast once as before)
+            zero = None
+            if self.deltas:
+                zero = DeviceArena(lay, eng.device)
+                zero.f32.zero_()
+                zero.i64.zero_()
+            sub = (_ptr(zero.f32), _ptr(zero.i64)) if self.deltas else base
             deltas, _ = self._flatten(_lib.PLATO_AGG_FLAT_DELTA, segs, n_segs, n_flat, [self._pf[i] for i in slots],
-                                      [self._pi[i] for i in slots], base, 0.0, stream)
+                                      [self._pi[i] for i in slots], sub, 0.0, stream)
             rows = [cur.data_ptr()] + [deltas.data_ptr() + r * stride * 4 for r in range(k)]
             tab = torch.from_numpy(np.asarray(rows, dtype=np.int64)).to(eng.device)
             chunk = torch.from_numpy(np.asarray([[0, 0, n_flat, 0]], dtype=np.uint32).view(np.int32)).to(eng.device)
@@ -1370,13 +1376,14 @@ class AggregationRound:
                       0, 1, stride, 0, norms.data_ptr(), h)
             _lib.call("plato_agg_torch_cosine_sum", cur.data_ptr(), tab.data_ptr() + 8, k, n_flat, norms.data_ptr(),
                       norms.data_ptr() + 4, float(eps), threads, ws.data_ptr(), out.data_ptr(), h)
-            keep = (cur, deltas, tab, chunk)
+            keep = (cur, deltas, tab, chunk, zero)
         else:  # norms straight from the arenas; the same kernel stores the flattened vectors for the sums
             flat = torch.empty((k + 1, stride), dtype=torch.float32, device=eng.device)
             vec = np.asarray([base[0]] + [self._pf[i] for i in slots]
                              + [base[1] or 0] + [self._pi[i] or 0 for i in slots]
-                             + [_ptr(prev.f32)] + [base[0]] * k
-                             + [_ptr(prev.i64) or 0] + [base[1] or 0] * k
+                             # client vectors subtract the baseline, or nothing on delta arenas (null)
+                             + [_ptr(prev.f32)] + [0 if self.deltas else base[0]] * k
+                             + [_ptr(prev.i64) or 0] + [0 if self.deltas else (base[1] or 0)] * k
                              + [flat.data_ptr() + r * stride * 4 for r in range(k + 1)], dtype=np.int64)
             vt = torch.from_numpy(vec).to(eng.device)
             v8, n1 = vt.data_ptr(), 8 * (k + 1)

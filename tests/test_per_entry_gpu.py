@@ -14,6 +14,7 @@
 
 import asyncio
 import types
+from collections import OrderedDict
 
 import numpy as np
 import pytest
@@ -421,7 +422,12 @@ def test_delta_round_matches_weight_round(name):
         res = rnd.result()
         g_model = rnd.layout.unpack(g_f.cpu(), g_i.cpu())  # (the aligned arena has padding between entries)
         sumsq = rnd.np_sumsq(range(k))  # Polaris' sums: on delta arenas with a null baseline
-        got[deltas] = (sumsq.tobytes(), _flat(layout, g_model, "f32").tobytes(), _flat(layout, g_model, "i64").tobytes(),
+        # Port's similarities against another model: gathered (null subtrahends) and flat-norms paths
+        other = OrderedDict((n_, (t_ * 0.5 if t_.is_floating_point() else t_)) for n_, t_ in base.items())
+        sims = [np.asarray(rnd.model_similarities(other, range(k), threads=4, flat_norms=f)).tobytes()
+                for f in (False, True)]
+        got[deltas] = (sims, sumsq.tobytes(), _flat(layout, g_model, "f32").tobytes(),
+                       _flat(layout, g_model, "i64").tobytes(),
                        [np.asarray(d).tobytes() for d in dots], _flat(layout, res, "f32").tobytes(),
                        _flat(layout, res, "i64").tobytes())
         if deltas:
