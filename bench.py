@@ -72,6 +72,20 @@ def parse():
     p.add_argument("--no-variants", action="store_true",
                    help="skip the variant servers' reductions leg (SURVEY.md §8(f), N=1 only)")
     p.add_argument("--variant-reps", type=int, default=10)
+    p.add_argument("--dist-timeout", type=float, default=180.0,
+                   help="N > 1: seconds any collective (and the rendezvous) may wait before the rank fails "
+                        "naming it; also the per-rank stall watchdog (+60 s)")
+    p.add_argument("--launch-timeout", type=float, default=900.0,
+                   help="N > 1 self-launch: wall-clock seconds for the whole rank tree; on expiry its process "
+                        "group is killed and each rank's last phase is printed (exit 124)")
+    p.add_argument("--no-engine-devices-leg", action="store_true",
+                   help="N > 1 strong scaling: skip the server's in-process multi-GPU leg (MultiDeviceEngine over "
+                        "the N GPUs, run by rank 0 in a child process after the ranks have finished)")
+    p.add_argument("--probe-stall-rank", type=int, default=-1,
+                   help="with --probe-launch: this rank sleeps instead of joining the collective (timeout tests)")
+    p.add_argument("--parity", action="store_true",
+                   help="with --engine-devices: check the host result and every GPU's gathered copy bit for bit "
+                        "against the one-GPU engine on the same payloads")
     p.add_argument("--engine-devices", type=int, default=0,
                    help="single-process multi-GPU engine (plato_amd.multi) over this many devices: host-inclusive "
                         "and device-resident timings of the server's own path (repeats cuda:0 on a 1-GPU box)")
@@ -103,44 +117,123 @@ def model_spec(name):
     }[name]()
 
 
-def self_launch(n: int, argv: list[str]) -> int:
+def self_launch(n: int, argv: list[str], limit_s: float) -> int:
     """``bench.py --gpus N`` started plainly: run it under torch.distributed.run, one rank per GPU.
 
     Called before anything touches the GPU (no torch.cuda call in this process): the N ranks are
-    a child process tree (never an exec of this one).  Rank 0's JSON line is forwarded to this
-    process's stdout; anything else the child writes on stdout goes to stderr, so the result line
-    stays the only stdout line.  Returns the child's exit code.
+    a child process tree in its own process group (never an exec of this one).  Rank 0's JSON line
+    is forwarded to this process's stdout; everything else the ranks write goes to stderr, so the
+    result line stays the only stdout line.  The tree gets ``limit_s`` seconds of wall clock: on
+    expiry its process group is killed and the last phase each rank announced (``[bench] rank r:
+    ...`` lines, which name the collective a rank entered) is printed; the exit code is then 124.
+    Returns the child's exit code otherwise.
     """
+    import collections
+    import signal
     import socket
     import subprocess
+    import threading
 
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *argv]
-    progress(f"--gpus {n} without a torch.distributed world: launching {n} ranks (port {port})")
-    child = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
-    for line in child.stdout:
-        if line.startswith("{"):
-            sys.stdout.write(line)
-            sys.stdout.flush()
-        else:
+    env = dict(os.environ, TORCH_NCCL_ASYNC_ERROR_HANDLING="1")
+    progress(f"--gpus {n} without a torch.distributed world: launching {n} ranks (port {port}, "
+             f"limit {limit_s:.0f} s)")
+    child = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, bufsize=1, env=env,
+                             start_new_session=True)
+    tail = collections.deque(maxlen=40)
+    phases: dict = {}
+
+    def pump_out():
+        for line in child.stdout:
+            if line.startswith("{"):
+                sys.stdout.write(line)
+                sys.stdout.flush()
+            else:
+                sys.stderr.write(line)
+
+    def pump_err():
+        for line in child.stderr:
             sys.stderr.write(line)
-    return child.wait()
+            tail.append(line.rstrip("\n"))
+            marker = line.find("[bench] rank ")
+            if marker >= 0:
+                head = line[marker + len("[bench] rank "):]
+                r = head.split(":", 1)[0].strip()
+                if r.isdigit():
+                    phases[int(r)] = head.split(":", 1)[1].strip() if ":" in head else head.strip()
+
+    readers = [threading.Thread(target=f, daemon=True) for f in (pump_out, pump_err)]
+    for t in readers:
+        t.start()
+    try:
+        code = child.wait(timeout=limit_s)
+    except subprocess.TimeoutExpired:
+        for sig, grace in ((signal.SIGTERM, 10), (signal.SIGKILL, 10)):
+            try:
+                os.killpg(child.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                child.wait(timeout=grace)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        for t in readers:
+            t.join(timeout=5)
+        print(f"[bench] TIMEOUT: the {n}-rank tree exceeded --launch-timeout {limit_s:.0f} s and was killed; "
+              "last phase per rank:", file=sys.stderr, flush=True)
+        for r in range(n):
+            print(f"[bench]   rank {r}: {phases.get(r, 'no phase reported (still starting)')}", file=sys.stderr,
+                  flush=True)
+        print("[bench] last stderr lines of the tree:", file=sys.stderr, flush=True)
+        for line in list(tail)[-15:]:
+            print(f"[bench]   | {line}", file=sys.stderr, flush=True)
+        return 124
+    for t in readers:
+        t.join(timeout=5)
+    return code
+
+
+def collective(rank: int, name: str, fn, *a, **kw):
+    """Run one collective of the N > 1 path: announce it (the self-launcher's per-rank phase) and turn a
+    failure (a peer gone, the --dist-timeout expired) into an error that names this rank and collective."""
+    progress(f"rank {rank}: {name}")
+    try:
+        return fn(*a, **kw)
+    except Exception as exc:  # torch.distributed raises RuntimeError / DistBackendError subclasses
+        raise RuntimeError(f"rank {rank}: collective {name!r} failed: {exc}") from exc
+
+
+def arm_watchdog(args, world: int) -> None:
+    """N > 1: a rank stalled outside any collective (a kernel or a host wait that never returns) dumps every
+    thread's Python stack to stderr and exits non-zero after --dist-timeout + 60 s (faulthandler; no exec)."""
+    if world > 1:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(args.dist_timeout + 60.0, exit=True)
 
 
 def probe_launch(args) -> None:
     """The launcher's plumbing on CPU: every rank joins a gloo group and sums its rank; rank 0 prints."""
     import torch.distributed as dist
 
+    import datetime
+
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world > 1:
-        dist.init_process_group("gloo")
+        progress(f"rank {rank}: init_process_group(gloo)")
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=args.dist_timeout))
     t = torch.tensor([float(rank)])
+    if rank == args.probe_stall_rank:
+        progress(f"rank {rank}: stalling before all_reduce (--probe-stall-rank)")
+        time.sleep(3600)
     if world > 1:
-        dist.all_reduce(t)
+        collective(rank, "all_reduce(rank_sum)", dist.all_reduce, t)
     if rank == 0:
         print(json.dumps({"probe": "launch", "n_gpus": world, "requested": args.gpus,
                           "rank_sum": float(t.item())}), flush=True)
@@ -164,30 +257,35 @@ def dist_setup(args):
         local = local % ndev  # rehearsal only: ranks share a GPU
     torch.cuda.set_device(local)
     if world > 1:
+        import datetime
+
         import torch.distributed as dist
 
+        arm_watchdog(args, world)
+        timeout = datetime.timedelta(seconds=args.dist_timeout)
         if backend == "nccl":  # RCCL over xGMI
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            collective(rank, "init_process_group(nccl)", dist.init_process_group, "nccl",
+                       device_id=torch.device("cuda", local), timeout=timeout)
         else:
-            dist.init_process_group(backend)
+            collective(rank, f"init_process_group({backend})", dist.init_process_group, backend, timeout=timeout)
     return world, rank, local
 
 
-def barrier(world):
+def barrier(world, what: str = "barrier"):
     if world > 1:
         import torch.distributed as dist
 
-        dist.barrier()
+        collective(dist.get_rank(), what, dist.barrier)
 
 
-def max_over_ranks(value: float, world: int) -> float:
+def max_over_ranks(value: float, world: int, what: str = "max over ranks") -> float:
     if world == 1:
         return value
     import torch.distributed as dist
 
     dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
     t = torch.tensor([value], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    collective(dist.get_rank(), f"all_reduce(MAX, {what})", dist.all_reduce, t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
 
@@ -248,19 +346,22 @@ def profile_roofline(summ, alg_bytes: int, kernel_ms: float, ms_per_step: float)
     """Roofline fields taken from the committed profile, and how they compare with this run."""
     if summ is None:
         return {"traffic": None, "traffic_source": None}
-    avg = summ.get("avg_duration_ms")
-    timed = summ.get("timed_avg_ms") or avg
+    # primary: the profile's timed-region dispatches (what ms_per_step covers); older summaries carried the
+    # rocprof stats average over every call (warm-up included) as avg_duration_ms
+    timed = summ.get("timed_avg_ms") or summ.get("avg_duration_ms")
+    every = summ.get("rocprof_stats_avg_ms") or summ.get("avg_duration_ms")
     out = {
         "traffic": summ["pmc"]["hbm_bytes"],
         "traffic_source": summ["path"],
         "traffic_source_current": summ["current_source"],
-        "traffic_profile_avg_ms": avg,
+        "traffic_profile_avg_ms": timed,
+        "traffic_profile_all_calls_avg_ms": every,
         # the profile's own roofline: algorithmic bytes / the rocprofv3 kernel-trace duration
-        "frac_profile": round(alg_bytes / (avg * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if avg else None,
-        "frac_profile_timed": round(alg_bytes / (timed * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if timed else None,
+        "frac_profile": round(alg_bytes / (timed * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if timed else None,
+        "frac_profile_all_calls": round(alg_bytes / (every * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if every else None,
         "profile_over_this_run_kernel_ms": round(timed / kernel_ms, 4) if timed else None,
         # a profile slower than this run's whole step was measured on another box / clock
-        "profile_avg_exceeds_ms_per_step": bool(avg and avg > ms_per_step),
+        "profile_avg_exceeds_ms_per_step": bool(timed and timed > ms_per_step),
         "profile_lease_bench": summ.get("bench_same_lease"),
     }
     return out
@@ -306,7 +407,7 @@ def cpu_model():
 def main():
     args = parse()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        sys.exit(self_launch(args.gpus, sys.argv[1:]))
+        sys.exit(self_launch(args.gpus, sys.argv[1:], args.launch_timeout))
     if args.probe_launch:
         return probe_launch(args)
     if args.anchor:
@@ -325,7 +426,7 @@ def main():
     scaling = args.scaling
     k = args.clients or k_default
     full_layout = ArenaLayout.from_shapes(model_spec(model))
-    plan = None
+    plan = xchg = None
     pieces = 1
     if scaling == "strong" and world > 1:
         # one model, parameter-bucket sharded and cut into `pieces` round-robin pieces: piece
@@ -337,6 +438,7 @@ def main():
         progress(f"rank {rank}: {pieces} pieces per rank "
                  + ("(--pieces)" if args.pieces else "(PIECES_BY_WORLD, from the one-GPU anchor)"))
         plan = PiecePlan.for_layout(full_layout, world, pieces)
+        xchg = plan.exchange(full_layout.n_i64)
         piece_n = [plan.piece_elements(rank, p) for p in range(pieces)]
         n_i64_loc = full_layout.n_i64 if rank == 0 else 0
         layout = ArenaLayout([], pieces * plan.length, n_i64_loc)
@@ -344,13 +446,21 @@ def main():
     else:
         layout = full_layout
         job_bytes = world * full_layout.algorithmic_bytes(k)
-    seed = args.seed + rank  # distinct synthetic data per bucket
+    # ONE job: every rank uses the same seed, so its pieces are slices of the one global baseline and
+    # client set (and every rank the same num_samples); weak scaling gives each rank the same job again
+    seed = args.seed
     engine = FedAvgEngine(dev, variant=args.variant)
 
     base = DeviceArena(layout, dev)
     slab = ClientSlab(layout, k, dev)
-    fill_baseline(base, seed)
-    fill_clients(slab, base, seed, k)
+    if plan is not None:
+        from plato_amd.synthetic import fill_slices
+
+        slices = [(p * plan.length, plan.piece_range(rank, p)[0], piece_n[p]) for p in range(pieces) if piece_n[p]]
+        fill_slices(base, slab, slices, n_i64_loc, seed, k)
+    else:
+        fill_baseline(base, seed)
+        fill_clients(slab, base, seed, k)
     if args.codec == "bf16":  # model_quantize'd payloads (every entry .to(bfloat16))
         slab16 = ClientSlab(layout, k, dev, codec="bf16")
         slab16.f32.copy_(slab.f32.to(torch.bfloat16))
@@ -374,15 +484,12 @@ def main():
     ti = torch.from_numpy(pi).to(dev)
     if plan is not None:
         # send buffer: [piece 0 | int64 results (meaningful on rank 0) | piece 1 | ... ]; the
-        # all-gather of piece p lands in gathered[goff[p]:], ranks in model order
+        # all-gather of piece p lands in gathered[goff[p]:], ranks in model order (PieceExchange)
         L = plan.length
-        ipad = -(-max(full_layout.n_i64, 1) // 64) * 64
-        send = torch.zeros(pieces * L + ipad, dtype=torch.float32, device=dev)
-        soff = [0] + [L + ipad + (p - 1) * L for p in range(1, pieces)]
-        slen = [L + ipad] + [L] * (pieces - 1)
-        goff = [0] + [world * (L + ipad) + (p - 1) * world * L for p in range(1, pieces)]
-        gathered = torch.empty(world * (pieces * L + ipad), dtype=torch.float32, device=dev)
-        out_i = send[L: L + ipad]
+        send = torch.zeros(xchg.send_numel, dtype=torch.float32, device=dev)
+        soff = xchg.soff
+        gathered = torch.empty(xchg.gathered_numel, dtype=torch.float32, device=dev)
+        out_i = send[xchg.int64_offset(): xchg.int64_offset() + xchg.ipad]
         # per piece: client-row pointers offset to the piece (rows are pieces * L long)
         piece_tf = [torch.from_numpy(pf + p * L * 4).to(dev) for p in range(pieces)]
         piece_lay = [ArenaLayout([], piece_n[p], layout.n_i64 if p == 0 else 0) for p in range(pieces)]
@@ -425,8 +532,8 @@ def main():
         and concurrent with the later pieces' kernels (async_op; waited for in assemble())."""
         import torch.distributed as dist
 
-        src = send[soff[p]: soff[p] + slen[p]]
-        dst = gathered[goff[p]: goff[p] + world * slen[p]]
+        src = xchg.send_slice(send, p)
+        dst = xchg.gather_slice(gathered, p)
         if rehearsal:  # gloo moves host tensors (ranks sharing one GPU)
             host = torch.empty(dst.numel(), dtype=torch.float32)
             dist.all_gather_into_tensor(host, src.cpu())
@@ -645,12 +752,167 @@ def main():
                                               args.config)
         result["parity"] = result["cpu_baseline"].pop("parity")
 
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    exit_code = 0
+    if plan is not None:
+        # outside the timed region: the model every rank gathered in the last step, in model order,
+        # must be the one-GPU fused kernel's result on the same global job (rank 0 recomputes it), bit
+        # for bit, and every rank must hold the same bits
+        torch.cuda.synchronize(dev)
+        got_f, got_i = xchg.assemble(gathered)
+        agree = ranks_agree(bits_digest(got_f, got_i), world)
+        if rank == 0:
+            progress(f"rank {rank}: parity check against the one-GPU kernel on the same job")
+            par = check_against_one_gpu(engine, full_layout, k, seed, w, got_f, got_i, dev, stream)
+            par["ranks_hold_identical_models"] = agree
+            if not agree:
+                par["parity"] = "MISMATCH: ranks gathered different models"
+            result["parity"] = par.pop("parity")
+            result["parity_detail"] = par
+            if not result["parity"].startswith("bit-exact"):
+                exit_code = 3
+        del got_f, got_i
+        barrier(world, "barrier after the parity check")
     if world > 1:
         import torch.distributed as dist
 
+        progress(f"rank {rank}: destroy_process_group")
         dist.destroy_process_group()
+    if rank == 0 and plan is not None and not args.no_engine_devices_leg and args.codec == "native":
+        # the server's own multi-GPU path (one process driving the N GPUs: MultiDeviceEngine, RCCL
+        # communicator from ncclCommInitAll), in a child process once the ranks are done
+        del slab, base, send, gathered
+        torch.cuda.empty_cache()
+        result["engine_devices"] = engine_devices_child(args, world)
+        if str(result["engine_devices"].get("parity", "")).startswith("MISMATCH"):
+            exit_code = 3
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if exit_code:
+        sys.exit(exit_code)
+
+
+def bits_digest(f: torch.Tensor, i: torch.Tensor) -> list[int]:
+    """Two order-sensitive int64 checksums of the bit patterns of (fp32 arena, int64-entry results)."""
+    out = []
+    for t in (f, i):
+        b = t.contiguous().view(torch.int32).to(torch.int64)
+        pos = torch.arange(b.numel(), device=b.device, dtype=torch.int64) % 65521 + 1
+        out.extend([int(b.sum()), int((b * pos).sum())])
+    return out
+
+
+def ranks_agree(digest: list[int], world: int) -> bool:
+    """Every rank's digest equal (all_reduce MAX and MIN)."""
+    if world == 1:
+        return True
+    import torch.distributed as dist
+
+    dev = "cpu" if dist.get_backend() == "gloo" else "cuda"
+    hi = torch.tensor(digest, dtype=torch.int64, device=dev)
+    lo = hi.clone()
+    rank = dist.get_rank()
+    collective(rank, "all_reduce(MAX, model digest)", dist.all_reduce, hi, op=dist.ReduceOp.MAX)
+    collective(rank, "all_reduce(MIN, model digest)", dist.all_reduce, lo, op=dist.ReduceOp.MIN)
+    return bool(torch.equal(hi, lo))
+
+
+def check_against_one_gpu(engine, full_layout, k: int, seed: int, w: torch.Tensor, got_f: torch.Tensor,
+                          got_i: torch.Tensor, dev, stream, budget: int | None = None) -> dict:
+    """The one-GPU fused kernel on the whole job (the same K clients of ``seed``), compared bit for bit.
+
+    The job is regenerated on this GPU by the same counter generator, in windows of the fp32 arena
+    sized to ``budget`` bytes of client + baseline + result (the whole C2 model in one window; C3's
+    1,024 clients in a few): every element is the same sequential-K chain whatever the window, so
+    each window's launch is the one-GPU result for its elements.  The int64 entries run with the
+    first window.
+    """
+    from plato_amd.arena import ROW_ALIGN, ArenaLayout
+    from plato_amd.engine import ClientSlab, DeviceArena
+    from plato_amd.synthetic import fill_slices
+
+    n_f, n_i = full_layout.n_f32, full_layout.n_i64
+    if budget is None:
+        free, _ = torch.cuda.mem_get_info(dev)
+        budget = min(free // 3, 24 << 30)
+    per_elem = (k + 2) * 4
+    win = max(ROW_ALIGN, min(max(n_f, 1), budget // per_elem) // ROW_ALIGN * ROW_ALIGN)
+    lay = ArenaLayout([], win, n_i)
+    base = DeviceArena(lay, dev)
+    slab = ClientSlab(lay, k, dev)
+    out_f = torch.empty(lay.row_f32, dtype=torch.float32, device=dev)
+    out_i = torch.empty(max(lay.row_i64, 1), dtype=torch.float32, device=dev)
+    pf, pi = slab.row_pointers(range(k))
+    tf, ti = torch.from_numpy(pf).to(dev), torch.from_numpy(pi).to(dev)
+
+    def run_window(lo, n, ni):
+        fill_slices(base, slab, [(0, lo, n)] if n > 0 else [], ni, seed, k, stream)
+        engine.launch_fedavg(ArenaLayout([], n, ni), tf, ti, w, None, k, base.f32, base.i64, out_f, out_i, stream)
+        return out_f[:n], out_i[:ni]
+
+    res = compare_windows(n_f, n_i, win, run_window, got_f, got_i)
+    torch.cuda.synchronize(dev)
+    res["reference"] = ("plato_agg_fedavg_weights on rank 0's GPU over the whole job, regenerated by "
+                        "plato_agg_fill_synth_*_at (same seed, same clients, same weights)")
+    return res
+
+
+def compare_windows(n_f: int, n_i: int, win: int, run_window, got_f: torch.Tensor, got_i: torch.Tensor) -> dict:
+    """Compare the gathered model with ``run_window(lo, n, ni) -> (fp32 results, int64-entry results)`` over
+    windows of ``win`` fp32 elements (the int64 entries with the first), bit for bit; the parity fields."""
+    mism, first_bad, windows = 0, None, 0
+    for lo in range(0, max(n_f, 1), win):
+        n = max(0, min(win, n_f - lo))
+        ni = n_i if lo == 0 else 0
+        if n == 0 and not ni:
+            break
+        ref_f, ref_i = run_window(lo, n, ni)
+        windows += 1
+        if n:
+            bad = (ref_f.view(torch.int32) != got_f[lo:lo + n].view(torch.int32)).nonzero()
+            if bad.numel():
+                mism += int(bad.numel())
+                first_bad = first_bad if first_bad is not None else lo + int(bad[0])
+        if ni:
+            bad_i = (ref_i.view(torch.int32) != got_i[:ni].view(torch.int32)).nonzero()
+            mism += int(bad_i.numel())
+            if bad_i.numel() and first_bad is None:
+                first_bad = f"int64 entry {int(bad_i[0])}"
+    return {"parity": "bit-exact vs 1-GPU kernel" if mism == 0 else "MISMATCH vs 1-GPU kernel",
+            "elements_checked": n_f + n_i, "mismatched_elements": mism, "first_mismatch": first_bad,
+            "windows": windows, "window_elements": win}
+
+
+def engine_devices_child(args, world: int) -> dict:
+    """``bench.py --engine-devices N --parity`` as a child process (spawned, never exec'd); its JSON line.
+
+    The child drives the N GPUs from one process (``MultiDeviceEngine``), as the Plato server does
+    (plato/servers/base.py:323-327), and checks its results against the one-GPU engine.  Bounded by
+    ``--launch-timeout``; a child that fails or times out is reported in the line, not retried.
+    """
+    import signal
+    import subprocess
+
+    env = {key: v for key, v in os.environ.items()
+           if key not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                          "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    cmd = [sys.executable, os.path.abspath(__file__), "--engine-devices", str(world), "--config", args.config,
+           "--steps", str(max(1, min(args.steps, 5))), "--warmup", "1", "--seed", str(args.seed), "--parity"]
+    if args.clients:
+        cmd += ["--clients", str(args.clients)]
+    progress(f"rank 0: engine-devices leg: {' '.join(cmd[1:])}")
+    child = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, start_new_session=True)
+    try:
+        out, _ = child.communicate(timeout=args.launch_timeout)
+    except subprocess.TimeoutExpired:
+        os.killpg(child.pid, signal.SIGKILL)
+        child.communicate()
+        return {"status": "timeout", "limit_s": args.launch_timeout, "command": " ".join(cmd[1:])}
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    if child.returncode != 0 or not lines:
+        return {"status": f"failed (exit {child.returncode})", "command": " ".join(cmd[1:])}
+    res = json.loads(lines[-1])
+    res["status"] = "ok"
+    return res
 
 
 # one dependent v_fmac_f32 step on MI355X: 4.04 shader cycles back to back from registers
@@ -1075,8 +1337,60 @@ def engine_devices_bench(args):
     }
     if args.client_split:
         out["client_split"] = client_split_leg(eng, baseline, payloads, k, args.steps)
+    if args.parity:
+        out.update(engine_devices_parity(eng, layout, baseline, payloads, weights))
+    out["rccl_communicator"] = eng._comm is not None  # ncclCommInitAll over distinct GPUs
     print(json.dumps(out), flush=True)
     eng.close()
+    if str(out.get("parity", "")).startswith("MISMATCH"):
+        sys.exit(3)
+
+
+def _same_bits(a: torch.Tensor, b: torch.Tensor) -> bool:
+    a, b = a.reshape(-1), b.reshape(-1)
+    if a.dtype != b.dtype:
+        return False
+    if a.dtype == torch.float32:
+        return torch.equal(a.view(torch.int32), b.view(torch.int32))
+    return torch.equal(a, b)
+
+
+def engine_devices_parity(eng, layout, baseline, payloads, weights) -> dict:
+    """MultiDeviceEngine's host result and every GPU's gathered copy against the one-GPU engine, bit for bit.
+
+    One more round of the multi-device engine with ``gather=True`` (RCCL all-gather over distinct GPUs,
+    device copies where devices repeat); the reference is ``FedAvgEngine`` on the first device with the
+    same baseline, payloads and weights — the product path at N = 1, which the golden fixtures pin.
+    """
+    from plato_amd.arena import F32
+    from plato_amd.engine import FedAvgEngine
+
+    one = FedAvgEngine(eng.devices[0]).aggregate_weights(baseline, payloads, weights)
+    rnd = eng.begin(baseline, len(payloads))
+    rnd.put_baseline(baseline)
+    for slot, p in enumerate(payloads):
+        rnd.put_client(slot, p)
+    rnd.launch(weights, gather=True)
+    host = rnd.result()
+    bad_host = [n for n in one if not _same_bits(one[n], host[n])]
+    bad_dev = []
+    for g in range(eng.world):
+        f, i = rnd.device_result(g)
+        f, i = f.cpu(), i.cpu()
+        for e in layout.entries:
+            ref = one[e.name].reshape(-1)
+            if e.region == F32:
+                ok = torch.equal(f[e.offset:e.offset + e.numel].view(torch.int32), ref.view(torch.int32))
+            else:  # the int64 entries' fp32 results, truncated as load_state_dict does
+                ok = torch.equal(i[e.offset:e.offset + e.numel].to(torch.int64), ref)
+            if not ok:
+                bad_dev.append((g, e.name))
+    exact = not bad_host and not bad_dev
+    return {"parity": "bit-exact vs 1-GPU engine (host result and every GPU's gathered copy)" if exact
+            else "MISMATCH vs 1-GPU engine",
+            "parity_detail": {"entries": len(layout.entries), "gathered_copies_checked": eng.world,
+                              "host_mismatched_entries": bad_host[:8],
+                              "device_mismatched": [f"gpu{g}:{n}" for g, n in bad_dev[:8]]}}
 
 
 def client_split_leg(eng, baseline, payloads, k: int, reps: int) -> dict:

@@ -302,6 +302,19 @@ int plato_agg_fill_synth_i64(int64_t* d_out, const int64_t* d_add, size_t n,
                              hipStream_t stream);
 
 /*
+ * The same streams from element ``first`` on: out[e] is element first + e of
+ * the stream (h = splitmix64(key + first + e)) and d_add[e] its addend.  A
+ * rank of the bucket-sharded bench fills its pieces as slices of the one
+ * global model and client set this way (bench.py, N > 1).
+ */
+int plato_agg_fill_synth_f32_at(float* d_out, const float* d_add, size_t n,
+                                uint64_t seed, uint64_t stream_id, uint64_t first,
+                                int scale_log2, hipStream_t stream);
+int plato_agg_fill_synth_i64_at(int64_t* d_out, const int64_t* d_add, size_t n,
+                                uint64_t seed, uint64_t stream_id, uint64_t first,
+                                uint64_t modulus, hipStream_t stream);
+
+/*
  * FedAvg with float64 weights on the fp32 entries (ABI 2): for every fp32
  * element, clients in order,
  *   d = x_i - b (fp32; d = x_i when d_base_* are NULL: deltas mode)

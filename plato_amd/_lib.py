@@ -76,6 +76,12 @@ SIGNATURES = {
     "plato_agg_fill_synth_i64": (
         _c_int, [_c_void_p, _c_void_p, _c_size_t, _c_u64, _c_u64, _c_u64, _c_void_p]
     ),
+    "plato_agg_fill_synth_f32_at": (
+        _c_int, [_c_void_p, _c_void_p, _c_size_t, _c_u64, _c_u64, _c_u64, _c_int, _c_void_p]
+    ),
+    "plato_agg_fill_synth_i64_at": (
+        _c_int, [_c_void_p, _c_void_p, _c_size_t, _c_u64, _c_u64, _c_u64, _c_u64, _c_void_p]
+    ),
     "plato_agg_client_dots_workspace": (_c_size_t, [_c_int, _c_size_t]),
     "plato_agg_client_dots": (
         _c_int,

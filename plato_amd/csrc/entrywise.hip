@@ -451,8 +451,9 @@ __device__ void ew_i64_chunk(const EwArgs& a, uint32_t cc) {
 }
 
 // The int64 chunks are the grid's first blocks (dispatched first, their K-client walks run beside the
-// stream instead of after it), the fp32 chunks follow.  B threads per chunk; the engine's chunk size is
-// B x 2 float4 groups (FedAvgEngine.ENTRYWISE_CHUNK).
+// stream instead of after it), the fp32 chunks follow.  B threads per chunk; the engine's chunk
+// (FedAvgEngine.ENTRYWISE_CHUNK = 256 elements) is B x 1 float4 group at the default B = 64; the
+// chunk loop strides by the block, so any chunk length is covered.
 template <bool HAS_BASE, int B>
 __global__ __launch_bounds__(B) void fedavg_entrywise_kernel(EwArgs a) {
   const uint32_t c = blockIdx.x;

@@ -832,10 +832,11 @@ dim3 grid_for(uint64_t work) {
   return dim3(uint32_t(b));
 }
 
-__global__ __launch_bounds__(kBlock) void deltas_kernel(const float* __restrict__ x, const int64_t* __restrict__ xi,
+// x / o (and xi / oi) may be the same arena: the delta arenas convert a staged row in place (x -= b),
+// so they carry no __restrict__; each element is read once, then written, by the same lane.
+__global__ __launch_bounds__(kBlock) void deltas_kernel(const float* x, const int64_t* xi,
                                                         const float* __restrict__ b, const int64_t* __restrict__ bi,
-                                                        float* __restrict__ o, int64_t* __restrict__ oi,
-                                                        uint64_t n_f32, uint64_t n_i64) {
+                                                        float* o, int64_t* oi, uint64_t n_f32, uint64_t n_i64) {
   const uint64_t n4 = n_f32 / 4;
   for (uint64_t k = gtid(); k < n4; k += gstride()) {
     reinterpret_cast<f4*>(o)[k] =
@@ -1334,25 +1335,36 @@ int plato_agg_mix_weights(const float* d_x_f32, const int64_t* d_x_i64, const fl
   return check_launch("mix launch");
 }
 
-int plato_agg_fill_synth_f32(float* d_out, const float* d_add, size_t n, uint64_t seed, uint64_t stream_id,
-                             int scale_log2, hipStream_t stream) {
+int plato_agg_fill_synth_f32_at(float* d_out, const float* d_add, size_t n, uint64_t seed, uint64_t stream_id,
+                                uint64_t first, int scale_log2, hipStream_t stream) {
   if (n == 0) return PLATO_AGG_OK;
   if (!d_out) return fail(PLATO_AGG_EINVAL, "null output");
   if (scale_log2 < -126 || scale_log2 > 100) return fail(PLATO_AGG_EINVAL, "scale_log2 out of range");
   const float scale = ldexpf(1.0f, scale_log2);
+  // element e of the slice is element first + e of the stream: h = splitmix64(key + first + e)
   hipLaunchKernelGGL(synth_f32_kernel, grid_for(n), dim3(kBlock), 0, stream, d_out, d_add, (uint64_t)n,
-                     synth_key(seed, stream_id), scale);
+                     synth_key(seed, stream_id) + first, scale);
   return check_launch("synth_f32 launch");
 }
 
-int plato_agg_fill_synth_i64(int64_t* d_out, const int64_t* d_add, size_t n, uint64_t seed, uint64_t stream_id,
-                             uint64_t modulus, hipStream_t stream) {
+int plato_agg_fill_synth_f32(float* d_out, const float* d_add, size_t n, uint64_t seed, uint64_t stream_id,
+                             int scale_log2, hipStream_t stream) {
+  return plato_agg_fill_synth_f32_at(d_out, d_add, n, seed, stream_id, 0, scale_log2, stream);
+}
+
+int plato_agg_fill_synth_i64_at(int64_t* d_out, const int64_t* d_add, size_t n, uint64_t seed, uint64_t stream_id,
+                                uint64_t first, uint64_t modulus, hipStream_t stream) {
   if (n == 0) return PLATO_AGG_OK;
   if (!d_out) return fail(PLATO_AGG_EINVAL, "null output");
   if (modulus == 0) return fail(PLATO_AGG_EINVAL, "modulus must be >= 1");
   hipLaunchKernelGGL(synth_i64_kernel, grid_for(n), dim3(kBlock), 0, stream, d_out, d_add, (uint64_t)n,
-                     synth_key(seed, stream_id), modulus);
+                     synth_key(seed, stream_id) + first, modulus);
   return check_launch("synth_i64 launch");
+}
+
+int plato_agg_fill_synth_i64(int64_t* d_out, const int64_t* d_add, size_t n, uint64_t seed, uint64_t stream_id,
+                             uint64_t modulus, hipStream_t stream) {
+  return plato_agg_fill_synth_i64_at(d_out, d_add, n, seed, stream_id, 0, modulus, stream);
 }
 
 }  // extern "C"

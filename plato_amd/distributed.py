@@ -175,11 +175,75 @@ class PiecePlan:
         """Where the all-gather of the p-th pieces starts in the assembled arena."""
         return p * self.world * self.length
 
+    def exchange(self, n_i64: int) -> "PieceExchange":
+        """The send / gather buffer layout of a rank whose piece 0 carries the int64 results (bench.py, N > 1)."""
+        return PieceExchange.make(self, n_i64)
+
     def gather_piece(self, p: int, piece: torch.Tensor, full: torch.Tensor, group=None, async_op: bool = False):
         """All-gather rank pieces p (``length`` elements each) into ``full`` (``world*pieces*length``)."""
         n = self.world * self.length
         dst = full[self.gather_offset(p): self.gather_offset(p) + n]
         return dist.all_gather_into_tensor(dst, piece[: self.length], group=group, async_op=async_op)
+
+
+@dataclass(frozen=True)
+class PieceExchange:
+    """Where a rank's pieces sit in its send buffer and in the all-gathered buffer.
+
+    Send buffer of every rank: ``[piece 0 | int64 results, ipad floats | piece 1 | ... ]`` (the
+    int64 results are meaningful on rank 0 only).  The all-gather of the p-th pieces of all ranks
+    (``slen[p]`` floats each) lands at ``goff[p]``, ranks in model order, so the gathered buffer
+    holds the model once the ``pieces`` all-gathers are done; :meth:`assemble` reads it back in
+    model order (fp32 arena, fp32 values of the int64 entries).
+    """
+
+    plan: PiecePlan
+    n_i64: int
+    ipad: int
+    soff: tuple
+    slen: tuple
+    goff: tuple
+
+    @classmethod
+    def make(cls, plan: PiecePlan, n_i64: int) -> "PieceExchange":
+        L, world, pieces = plan.length, plan.world, plan.pieces
+        ipad = -(-max(n_i64, 1) // ROW_ALIGN) * ROW_ALIGN
+        soff = (0,) + tuple(L + ipad + (p - 1) * L for p in range(1, pieces))
+        slen = (L + ipad,) + (L,) * (pieces - 1)
+        goff = (0,) + tuple(world * (L + ipad) + (p - 1) * world * L for p in range(1, pieces))
+        return cls(plan, n_i64, ipad, soff, slen, goff)
+
+    @property
+    def send_numel(self) -> int:
+        return self.plan.pieces * self.plan.length + self.ipad
+
+    @property
+    def gathered_numel(self) -> int:
+        return self.plan.world * self.send_numel
+
+    def int64_offset(self) -> int:
+        """Offset of the int64 results in a send buffer (and in the gathered one: rank 0 comes first)."""
+        return self.plan.length
+
+    def send_slice(self, send: torch.Tensor, p: int) -> torch.Tensor:
+        return send[self.soff[p]: self.soff[p] + self.slen[p]]
+
+    def gather_slice(self, gathered: torch.Tensor, p: int) -> torch.Tensor:
+        return gathered[self.goff[p]: self.goff[p] + self.plan.world * self.slen[p]]
+
+    def assemble(self, gathered: torch.Tensor) -> tuple[torch.Tensor, torch.Tensor]:
+        """(fp32 arena [n_f32], int64-entry results [n_i64]) of the model, from the gathered buffer."""
+        plan = self.plan
+        n_f32 = plan.buckets.n_f32
+        full = torch.empty(n_f32, dtype=gathered.dtype, device=gathered.device)
+        for p in range(plan.pieces):
+            for r in range(plan.world):
+                lo, hi = plan.piece_range(r, p)
+                if hi > lo:
+                    src = self.goff[p] + r * self.slen[p]
+                    full[lo:hi] = gathered[src: src + hi - lo]
+        i0 = self.int64_offset()
+        return full, gathered[i0: i0 + self.n_i64].clone()
 
 
 def gather_buckets(plan: BucketPlan, bucket_f32: torch.Tensor, bucket_i64f: torch.Tensor | None,

@@ -699,6 +699,7 @@ class AggregationRound:
         eng._stager.put(baseline, eng._base.f32, eng._base.i64)
         self.has_baseline = True
         self._base_key = baseline_key(baseline)
+        self._arrival_base_ok = None
         self._decoded = None
 
     def put_client(self, slot: int, payload: Mapping[str, torch.Tensor],
@@ -739,7 +740,8 @@ class AggregationRound:
         if hit is None:
             return False
         pf, pi, delta_key = hit
-        if delta_key is not None and not (self.deltas and delta_key == getattr(self, "_base_key", None)):
+        if delta_key is not None and not (self.deltas and delta_key == getattr(self, "_base_key", None)
+                                          and self._arrival_base_matches()):
             return False  # a delta against another model (or a weight round): stage the payload again
         self._coded_scales(slot, payload)
         self._pf[slot], self._pi[slot] = pf, pi
@@ -750,6 +752,29 @@ class AggregationRound:
         self.staged[slot] = True
         self._decoded = None  # decoded rows are per staged set
         return True
+
+    def _arrival_base_matches(self) -> bool:
+        """The model the arrivals were turned into deltas against has this round's baseline bits.
+
+        The keys (storage + version counters) already match; an in-place write that leaves the
+        counters alone (``.data`` writes in a hook) or a freed storage reused at the same address
+        would still let a stale delta in, so the two staged arenas are compared once per round on
+        the device, after both copies (copy stream).  A mismatch makes every arrival row of the
+        round staged again from its host tensors.
+        """
+        ok = getattr(self, "_arrival_base_ok", None)
+        if ok is None:
+            eng, lay = self.engine, self.layout
+            arr = getattr(eng, "_arrival_base", None)
+            if arr is None or eng._arrival_base_layout is not lay:
+                ok = False
+            else:
+                stream = torch.cuda.current_stream(eng.device)
+                stream.wait_stream(eng._copy_stream)
+                ok = (torch.equal(self._base.f32[: lay.n_f32].view(torch.int32), arr.f32[: lay.n_f32].view(torch.int32))
+                      and torch.equal(self._base.i64[: lay.n_i64], arr.i64[: lay.n_i64]))
+            self._arrival_base_ok = ok
+        return ok
 
     def launch(self, weights: Sequence[float], scales: Sequence[float] | None = None,
                order: Sequence[int] | None = None, deltas: bool = False) -> None:
@@ -1207,11 +1232,13 @@ class AggregationRound:
         """The same dots through materialised flat vectors (``plato_agg_flatten`` + ``plato_agg_sdot_shared``).
 
         The round-2 path, kept as an independent device cross-check of
-        :meth:`fedadp_dots` (tests) and for the before/after timing
-        (scripts/bench_variant_paths.py).
+        :meth:`fedadp_dots` (tests), for the before/after timing
+        (scripts/bench_variant_paths.py), and for models beyond the fused
+        kernel's limits (:meth:`fedadp_dots` falls back here).  On delta arenas
+        the rows are flattened against a zero arena: x - 0 = x for the fp32
+        deltas, and the int64 deltas are the exact int64 differences either way.
         """
         slots = self._check_slots(slots)
-        self._raw_only("fedadp_dots_flat")
         if not self.has_baseline:
             raise ValueError("baseline not staged")
         eng, lay = self.engine, self.layout
@@ -1229,8 +1256,15 @@ class AggregationRound:
         per = max(1, int(batch_bytes // (stride * 4)))
         ws = torch.empty(_lib.lib().plato_agg_sdot_shared_workspace(min(k, per), 1) // 4, dtype=torch.float32,
                          device=eng.device)
-        base = (_ptr(self._base.f32), _ptr(self._base.i64))
-        keep = []
+        zero = None
+        if self.deltas:  # the rows already hold x - b
+            zero = DeviceArena(lay, eng.device)
+            zero.f32.zero_()
+            zero.i64.zero_()
+            base = (_ptr(zero.f32), _ptr(zero.i64))
+        else:
+            base = (_ptr(self._base.f32), _ptr(self._base.i64))
+        keep = [zero]
         for s0 in range(0, k, per):
             part = slots[s0:s0 + per]
             locs, _ = self._flatten(_lib.PLATO_AGG_FLAT_DELTA, segs, len(order), n_flat,
@@ -1243,7 +1277,7 @@ class AggregationRound:
             keep.append((locs, ys))
             if s0 + per < k:
                 stream.synchronize()  # bound the flat buffers to one batch
-                keep = []
+                keep = [zero]
         stream.synchronize()
         xy_h, yy_h = xy.cpu().numpy(), yy.cpu().numpy()
         inner, g_sq, l_sq = xy_h[:k], xy_h[k], yy_h[:k]

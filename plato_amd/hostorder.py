@@ -147,27 +147,31 @@ def host_port_value(models: dict, threads: int) -> np.float32:
 
 
 # ---------------------------------------------------------------- device halves
-def _probe_round(device, models: dict, align: str | None = None, port_variant: int | None = None):
+def _probe_round(device, models: dict, align: str | None = None, port_variant: int | None = None,
+                 deltas: bool = False):
     """A one-client round of the probe model on a private engine (the server's engine keeps its layout).
 
-    ``align`` / ``port_variant``: the server engine's arena alignment and Port kernel shape, so the probe
-    takes the same descriptor / offset path as the rounds (FedAdp's servers run on aligned arenas)."""
+    ``align`` / ``port_variant`` / ``deltas``: the server engine's arena alignment, Port kernel shape and
+    delta arenas, so the probe takes the same descriptor / offset path and the same kernel as the rounds
+    (FedAdp's servers run on aligned delta arenas: the dot kernel's no-baseline form)."""
     from .engine import FedAvgEngine
 
     eng = FedAvgEngine(device)
     eng.layout_align = align
     eng.port_variant = port_variant
+    eng.delta_arenas = deltas
     rnd = eng.begin(models["baseline"], 1)
     rnd.put_baseline(models["baseline"])
     rnd.put_client(0, models["client"])
     return rnd
 
 
-def device_fedadp_values(device, models: dict, lr: float, align: str | None = None) -> np.ndarray:
+def device_fedadp_values(device, models: dict, lr: float, align: str | None = None,
+                         deltas: bool = False) -> np.ndarray:
     """The same three dots through ``AggregationRound.fedadp_dots`` (the product's ``plato_agg_fedadp_dots``)."""
     from .arena import F32
 
-    rnd = _probe_round(device, models, align)
+    rnd = _probe_round(device, models, align, deltas=deltas)
     lay = rnd.layout
     gf = torch.zeros(lay.row_f32, dtype=torch.float32)
     gi = torch.zeros(max(1, lay.row_i64), dtype=torch.float32)
@@ -196,19 +200,22 @@ def _report(key, ok: bool, msg: str, strict: bool) -> bool:
     return ok
 
 
-def check_fedadp(device, lr: float = PROBE_LR, strict: bool = False, align: str | None = None) -> bool:
-    """True if this host's numpy dots equal the device's bit for bit (checked once per device, lr and alignment).
+def check_fedadp(device, lr: float = PROBE_LR, strict: bool = False, align: str | None = None,
+                 deltas: bool = False) -> bool:
+    """True if this host's numpy dots equal the device's bit for bit (checked once per device, lr, alignment
+    and arena form).
 
-    ``align``: the server engine's arena alignment (FedAdp servers use "fedadp").  A mismatch is logged
-    once (``strict``: raises :class:`HostOrderError`).
+    ``align`` / ``deltas``: the server engine's arena alignment and delta arenas (FedAdp servers use
+    "fedadp" and deltas), so the probe runs the kernel the rounds run.  A mismatch is logged once
+    (``strict``: raises :class:`HostOrderError`).
     """
-    key = ("fedadp", str(device), float(lr), align)
+    key = ("fedadp", str(device), float(lr), align, bool(deltas))
     with _lock:
         if key in _checked and (_checked[key] or not strict):
             return _checked[key]
         models = probe_models(PROBE_N)
         want = host_fedadp_values(models, lr)
-        got = device_fedadp_values(device, models, lr, align)
+        got = device_fedadp_values(device, models, lr, align, deltas)
         msg = ("FedAdp: this host's numpy float32 dot order differs from the one the device reproduces "
                f"(OpenBLAS sdot_k_SKYLAKEX); probe np.inner/dot = {want.tolist()}, device {got.tolist()}. "
                f"{host_description()}. The reference's FedAdp weights on this host would differ in the last bits.")

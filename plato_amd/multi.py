@@ -51,7 +51,7 @@ from . import _lib
 from .arena import CODECS, ArenaLayout, payload_codec
 from .distributed import BucketPlan, EntryPlan
 from .engine import FedAvgEngine, fp32_weights, require_device
-from .staging import HostPacker, PinnedRing, ResultPool, arena_source, payload_fingerprint
+from .staging import HostPacker, PinnedRing, ResultPool, arena_source, baseline_key, payload_fingerprint
 
 MULTI_CODECS = ("native", "bf16")
 
@@ -96,6 +96,29 @@ class _Shard:
                 torch.empty((rows, max(self.ni, 1)), dtype=dt_i, device=self.device))
         self.arrival_slabs.setdefault(codec, []).append(slab)
         return slab
+
+    def arrival_base(self):
+        """This bucket of the model the arrivals are turned into deltas against (allocated on first use)."""
+        if getattr(self, "_arr", None) is None:
+            self._arr = (torch.empty(self.per, dtype=torch.float32, device=self.device),
+                         torch.empty(max(self.ni, 1), dtype=torch.int64, device=self.device))
+        return self._arr
+
+    def to_delta(self, row_f: torch.Tensor, row_i: torch.Tensor, base_f: torch.Tensor, base_i: torch.Tensor) -> None:
+        """row -= base for this bucket, in place, on the copy stream (behind the row's and the base's H2D)."""
+        if not (self.n or self.ni):
+            return
+        _lib.call("plato_agg_compute_deltas", _ptr(row_f) if self.n else None, _ptr(row_i) if self.ni else None,
+                  _ptr(base_f) if self.n else None, _ptr(base_i) if self.ni else None,
+                  _ptr(row_f) if self.n else None, _ptr(row_i) if self.ni else None, self.n, self.ni,
+                  self.copy_stream.cuda_stream)
+
+    def same_bits(self, a_f: torch.Tensor, a_i: torch.Tensor, b_f: torch.Tensor, b_i: torch.Tensor) -> bool:
+        """Whether two copies of this bucket hold the same bits (after this shard's copy stream)."""
+        with torch.cuda.device(self.device):
+            torch.cuda.current_stream(self.device).wait_stream(self.copy_stream)
+            return (torch.equal(a_f[: self.n].view(torch.int32), b_f[: self.n].view(torch.int32))
+                    and torch.equal(a_i[: self.ni], b_i[: self.ni]))
 
     def copy_in(self, host_f: torch.Tensor, host_i: torch.Tensor, dst_f: torch.Tensor, dst_i: torch.Tensor):
         """Bucket slice of a full host arena -> this GPU (on the copy stream)."""
@@ -152,6 +175,27 @@ class MultiDeviceEngine:
         self._clients: "ClientShardedEngine | None" = None
         self._client_engines: list[FedAvgEngine] = [self.primary]
         self._pool = None
+        self._delta_arenas = False
+        self._arrival_base_key = None
+
+    @property
+    def delta_arenas(self) -> bool:
+        """Stage clients as their deltas x - b (FedAvgEngine.delta_arenas) on every device of this engine.
+
+        Bucket rounds (and ClientRound's client-split reductions) then hold deltas, formed per bucket right
+        behind each H2D (at arrival with ``prestage(..., baseline)``); the entry shards' and the primary's
+        engines follow the same setting.
+        """
+        return self._delta_arenas
+
+    @delta_arenas.setter
+    def delta_arenas(self, on: bool) -> None:
+        self._delta_arenas = bool(on)
+        for eng in self._client_engines:
+            eng.delta_arenas = self._delta_arenas
+        if self._entries is not None:
+            for eng in self._entries._engines:
+                eng.delta_arenas = self._delta_arenas
 
     @property
     def world(self) -> int:
@@ -173,6 +217,7 @@ class MultiDeviceEngine:
         while len(self._client_engines) <= g:
             eng = FedAvgEngine(self.devices[len(self._client_engines)], variant=self.variant)
             eng.layout_align = self.layout_align
+            eng.delta_arenas = self._delta_arenas
             self._client_engines.append(eng)
         return self._client_engines[g]
 
@@ -219,6 +264,7 @@ class MultiDeviceEngine:
             self._rings, self._packers = {}, {}
             self._results = ResultPool(layout)
             self._arrivals, self._arrival_free = {}, {}
+            self._arrival_base_key = None
         return self._layout
 
     def _ring(self, codec: str) -> tuple[PinnedRing, HostPacker]:
@@ -269,7 +315,10 @@ class MultiDeviceEngine:
                  baseline: Mapping[str, torch.Tensor] | None = None) -> bool:
         """Copy an arriving payload's buckets to their GPUs now (adopted by the next round).
 
-        (``baseline``: for the first GPU's delta rounds only, FedAvgEngine.prestage.)"""
+        With :attr:`delta_arenas` and the server's current model as ``baseline``, each bucket of the
+        row is turned into its delta right behind its H2D, against that model's bucket on the same GPU
+        (FedAvgEngine.prestage, per bucket); a round adopts it only if its own baseline is that model
+        unchanged (its :func:`baseline_key`, and the staged bits compared on the device)."""
         codec = payload_codec(payload)
         if codec not in MULTI_CODECS:
             return self.primary.prestage(payload, baseline_layout, baseline)
@@ -284,10 +333,37 @@ class MultiDeviceEngine:
             free.extend((slabs, r) for r in range(self.ARRIVAL_CHUNK))
         slabs, row = free.pop()
         self._stage(payload, codec, [(f[row], i[row]) for f, i in slabs])
+        delta_key = None
+        if self._delta_arenas and codec == "native" and baseline is not None:
+            delta_key = self._arrival_baseline(baseline)
+            if delta_key is not None:  # x - b per bucket, in place, behind this payload's H2D
+                for s, (f, i) in zip(self._shards, slabs):
+                    af, ai = s.arrival_base()
+                    s.to_delta(f[row], i[row], af, ai)
         ptrs = [(_row_ptr(f, row), _row_ptr(i, row)) for f, i in slabs]
         self._arrivals[id(payload)] = (payload, codec, self._layout.signature, ptrs, slabs, row,
-                                       payload_fingerprint(payload))
+                                       payload_fingerprint(payload), delta_key)
         return True
+
+    def _arrival_baseline(self, baseline: Mapping[str, torch.Tensor]):
+        """The arrival baseline's buckets on their GPUs (staged once per model version); its key, or None."""
+        key = baseline_key(baseline)
+        if key is None:
+            return None
+        if key == self._arrival_base_key:
+            return key
+        try:
+            self._layout.check_compatible(baseline, "baseline")
+        except (KeyError, ValueError):
+            return None
+        # copy-stream order: rows converted against the previous model ran before this copy
+        self._stage(baseline, "native", [s.arrival_base() for s in self._shards])
+        self._arrival_base_key = key
+        return key
+
+    def _arrival_base_matches(self, shards_base) -> bool:
+        """The round's staged baseline (``[(base_f, base_i)]`` per shard) has the arrival baseline's bits."""
+        return all(s.same_bits(bf, bi, *s.arrival_base()) for s, (bf, bi) in zip(self._shards, shards_base))
 
     def _arrival_rows(self, payload, layout: ArenaLayout, codec: str):
         hit = self._arrivals.get(id(payload))
@@ -295,10 +371,10 @@ class MultiDeviceEngine:
             return None
         if hit[6] != payload_fingerprint(payload):
             return None  # edited after arrival: the round stages its current tensors
-        return hit[3], [(f[hit[5]], i[hit[5]]) for f, i in hit[4]]
+        return hit[3], [(f[hit[5]], i[hit[5]]) for f, i in hit[4]], hit[7]
 
     def release_arrivals(self) -> None:
-        for _, codec, _, _, slabs, row, _ in self._arrivals.values():
+        for _, codec, _, _, slabs, row, _, _ in self._arrivals.values():
             self._arrival_free.setdefault(codec, []).append((slabs, row))
         self._arrivals = {}
         self.primary.release_arrivals()
@@ -379,17 +455,37 @@ class MultiRound:
         self._t0 = time.perf_counter()
         self.timings: dict = {}
         self._k = 0
+        # delta arenas (MultiDeviceEngine.delta_arenas): every staged row holds x - b per bucket, formed on
+        # its shard's copy stream behind its H2D; the launch is the deltas-form kernel plus b + acc
+        self.deltas = bool(getattr(engine, "delta_arenas", False)) and codec == "native"
+        self._base_key = None
+        self._arrival_base_ok = None  # the device check of the arrival baseline, once per round
+        self._converted: set = set()
 
     def put_baseline(self, baseline: Mapping[str, torch.Tensor]) -> None:
         self.layout.check_compatible(baseline, "baseline_weights")
+        if self.deltas and any(self.staged):
+            raise ValueError("delta arenas: the clients were staged as deltas of the previous baseline")
         eng = self.engine
         eng._stage(baseline, "native", [(s.base_f, s.base_i) for s in eng._shards])
         self.has_baseline = True
+        self._base_key = baseline_key(baseline)
+        self._arrival_base_ok = None
+
+    def _to_delta(self, rows) -> None:
+        key = tuple(r[0].data_ptr() for r in rows)
+        if key in self._converted:
+            return
+        for s, (f, i) in zip(self.engine._shards, rows):
+            s.to_delta(f, i, s.base_f, s.base_i)
+        self._converted.add(key)
 
     def put_client(self, slot: int, payload, what: str = "weights_received") -> None:
         if not 0 <= slot < self.capacity:
             raise IndexError(f"slot {slot} outside [0, {self.capacity})")
         self.layout.check_compatible(payload, f"{what}[{slot}]", self.codec)
+        if self.deltas and not self.has_baseline:
+            raise ValueError("delta arenas: stage the baseline before the clients")
         eng = self.engine
         rows = []
         ptrs = []
@@ -398,6 +494,9 @@ class MultiRound:
             rows.append((f[slot], i[slot]))
             ptrs.append((_row_ptr(f, slot), _row_ptr(i, slot)))
         eng._stage(payload, self.codec, rows)
+        self._converted.discard(tuple(r[0].data_ptr() for r in rows))  # fresh weights in the rows
+        if self.deltas:
+            self._to_delta(rows)
         self._ptrs[slot] = ptrs
         self._rows[slot] = rows
         self.staged[slot] = True
@@ -408,7 +507,22 @@ class MultiRound:
         hit = self.engine._arrival_rows(payload, self.layout, self.codec)
         if hit is None:
             return False
-        self._ptrs[slot], self._rows[slot] = hit
+        ptrs, rows, delta_key = hit
+        if delta_key is not None:
+            if not (self.deltas and self.has_baseline and delta_key == self._base_key):
+                return False  # a delta against another model (or a weight round): stage the payload again
+            if self._arrival_base_ok is None:  # the key matched; the bits must too (an in-place write that
+                # left the version counters alone, a reused address): compared once per round, on the devices
+                self._arrival_base_ok = self.engine._arrival_base_matches([(s.base_f, s.base_i)
+                                                                            for s in self.engine._shards])
+            if not self._arrival_base_ok:
+                return False
+            self._converted.add(tuple(r[0].data_ptr() for r in rows))
+        elif self.deltas:
+            if not self.has_baseline:
+                raise ValueError("delta arenas: stage the baseline before the clients")
+            self._to_delta(rows)  # the arrival rows hold weights: their deltas now (the rows are this round's)
+        self._ptrs[slot], self._rows[slot] = ptrs, rows
         self.staged[slot] = True
         return True
 
@@ -427,6 +541,9 @@ class MultiRound:
             raise ValueError("deltas are fp32 (x - b promotes coded payloads); use the native codec")
         if scales is not None and len(scales) != len(weights):
             raise ValueError("scales must have one entry per client")
+        # delta arenas: acc = sum_i d_i * w_i per bucket (the deltas-form kernel), then b + acc
+        # (plato_agg_update_weights: the fused epilogue's sum)
+        update = self.deltas and not deltas
         eng = self.engine
         k = len(order)
         self._k = k
@@ -457,6 +574,15 @@ class MultiRound:
                     _lib.call("plato_agg_fedavg_weights_bf16", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w),
                               _ptr(sc), k, _ptr(s.base_f), _ptr(s.base_i) if n_i else None, _ptr(out_f),
                               _ptr(out_i) if n_i else None, s.n, n_i, h)
+                elif update:
+                    acc_f = torch.empty(s.per, dtype=torch.float32, device=s.device)
+                    acc_i = torch.empty(max(s.ni, 1), dtype=torch.float32, device=s.device)
+                    _lib.call("plato_agg_fedavg_deltas", _ptr(tf), _ptr(ti) if n_i else None, _ptr(w), _ptr(sc),
+                              k, _ptr(acc_f), _ptr(acc_i) if n_i else None, s.n, n_i, h)
+                    _lib.call("plato_agg_update_weights", _ptr(s.base_f), _ptr(s.base_i) if n_i else None,
+                              _ptr(acc_f), _ptr(acc_i) if n_i else None, _ptr(out_f), _ptr(out_i) if n_i else None,
+                              s.n, n_i, h)
+                    keep.extend((acc_f, acc_i))
                 elif eng.variant is not None:
                     _lib.tune_call("plato_agg_tune_fedavg", eng.variant, int(not deltas), _ptr(tf),
                               _ptr(ti) if n_i else None, _ptr(w), _ptr(sc), k,
@@ -573,7 +699,7 @@ class ClientShardedEngine:
         return self.multi.begin(template, capacity, codec, client_split=True)
 
     def prestage(self, payload, baseline_layout: ArenaLayout, baseline=None) -> bool:
-        return self.multi.prestage(payload, baseline_layout)
+        return self.multi.prestage(payload, baseline_layout, baseline)
 
     def release_arrivals(self) -> None:
         self.multi.release_arrivals()
@@ -649,6 +775,7 @@ class ClientRound(MultiRound):
                 r = e.begin(self._baseline_sd, max(1, len(mine)), "native")
                 if r.layout.signature != self.layout.signature:
                     raise RuntimeError("client engine built another arena layout")
+                r.deltas = self.deltas  # the assembled rows are what the bucket rows hold: deltas or weights
                 here = torch.cuda.current_stream(dev)
                 here.wait_stream(e._copy_stream)  # the previous round's copies into this engine's slab
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -710,6 +837,9 @@ class ClientRound(MultiRound):
             raise ValueError("client-split rounds offer the device-resident entrywise sum only (FedAdp)")
         if not self.has_baseline:
             raise ValueError("baseline not staged")
+        if self.deltas and add_base:
+            raise ValueError("launch_entrywise(add_base=True) reads the clients' weights; this round holds deltas")
+        rows_are_deltas = self.deltas  # the kernel's deltas form: no baseline read
         eng, lay = self.engine, self.layout
         n_e = len(lay.entries)
         order = list(range(np.asarray(weights).shape[1])) if order is None else list(order)
@@ -736,7 +866,8 @@ class ClientRound(MultiRound):
                 if ncf or nci:
                     _lib.call("plato_agg_fedavg_entrywise", _ptr(tf), _ptr(ti) if s.ni else None, k, _ptr(dw), n_e,
                               _ptr(dcf) if ncf else None, ncf, _ptr(dci) if nci else None, nci,
-                              _ptr(s.base_f), _ptr(s.base_i) if s.ni else None, None, None, float(scale),
+                              None if rows_are_deltas else _ptr(s.base_f),
+                              None if (rows_are_deltas or not s.ni) else _ptr(s.base_i), None, None, float(scale),
                               float(noise_scale), _lib.PLATO_AGG_ADD_BASE if add_base else 0, _ptr(out_f),
                               _ptr(out_i) if s.ni else None, s.n, s.ni, s.stream.cuda_stream)
                 outs.append((out_f, out_i))
@@ -862,6 +993,8 @@ class EntryShardedEngine:
         # staging layout, and the primary's (the whole model, for codecs staged on one GPU) and
         # shard 0's (its entries) would evict each other's arenas and arrivals every round
         self._engines = [FedAvgEngine(d, variant=multi.variant) for d in self.devices]
+        for eng in self._engines:
+            eng.delta_arenas = multi.delta_arenas
         self._plans: dict = {}
         self._arrivals: dict = {}
         self._pool = None
@@ -910,7 +1043,10 @@ class EntryShardedEngine:
         return EntryRound(self, layout, [(g, names) for g, names in parts], self.each(start, parts), codec)
 
     def prestage(self, payload, baseline_layout: ArenaLayout, baseline=None) -> bool:
-        """Copy each shard's entries of an arriving payload to its GPU now (adopted by the next round)."""
+        """Copy each shard's entries of an arriving payload to its GPU now (adopted by the next round).
+
+        ``baseline`` (the server's current model): with delta arenas each shard turns its entries into
+        deltas against that model's entries at arrival (FedAvgEngine.prestage per shard)."""
         codec = payload_codec(payload)
         try:
             baseline_layout.check_compatible(payload, "arriving payload", codec)
@@ -918,11 +1054,15 @@ class EntryShardedEngine:
             return False
         _, parts = self.plan(baseline_layout)
         subs = [_sub_payload(payload, names) for _, names in parts]
+        try:
+            bases = [None if baseline is None else OrderedDict((n, baseline[n]) for n in names) for _, names in parts]
+        except KeyError:  # not the model these payloads update: arrivals stay weights
+            bases = [None] * len(parts)
         done = []
-        for (g, names), sub in zip(parts, subs):
+        for (g, names), sub, base in zip(parts, subs, bases):
             lay = self._sub_layout(baseline_layout, names)
             with torch.cuda.device(self.devices[g]):
-                if not self._engines[g].prestage(sub, lay):
+                if not self._engines[g].prestage(sub, lay, base):
                     for g0, sub0 in done:  # no half-staged payload keeps slots on the other shards
                         self._engines[g0].drop_arrival(sub0)
                     return False

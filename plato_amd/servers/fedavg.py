@@ -78,11 +78,9 @@ class _EngineHolder:
                 device = f"cuda:{device}" if isinstance(device, int) else device
                 eng = FedAvgEngine(device, variant=self.aggregation_variant)
             eng.layout_align = self.arena_alignment
-            deltas = bool(self.arena_deltas)
-            # one GPU, or the first GPU of several (where FedAdp's rounds run unless split by client)
-            target = eng if isinstance(eng, FedAvgEngine) else getattr(eng, "primary", None)
-            if target is not None and not (target is not eng and self.client_split_rounds):
-                target.delta_arenas = deltas
+            # one GPU, or every engine of the multi-GPU one (its buckets, entry shards, client-split devices
+            # and first GPU): clients staged as deltas, at arrival against the server's current model
+            eng.delta_arenas = bool(self.arena_deltas)
             self._plato_amd_engine = eng
         return eng
 

@@ -258,7 +258,8 @@ class FedAdpWeights(_EngineHolder):
         check = hostorder.mode(self.host_order_check)
         if check:  # this host's numpy sdot order (a mismatch warns; "strict" refuses)
             self._plato_amd_host_order_ok = hostorder.check_fedadp(
-                rnd.engine.device, lr, strict=check == "strict", align=getattr(rnd.engine, "layout_align", None))
+                rnd.engine.device, lr, strict=check == "strict", align=getattr(rnd.engine, "layout_align", None),
+                deltas=bool(getattr(rnd, "deltas", False)))
         inner, g_sq, l_sq = rnd.fedadp_dots(grads, range(k), lr)
         angles = W.fedadp_angles_from_dots(inner, g_sq, l_sq)
         contribs = W.fedadp_contributions(angles, self.selected_clients, self.local_angles,

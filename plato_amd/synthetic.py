@@ -84,3 +84,33 @@ def fill_clients(slab: ClientSlab, base: DeviceArena, seed: int, k: int, stream=
         if lay.n_i64:
             _lib.call("plato_agg_fill_synth_i64", slab.i64[r].data_ptr(), base.i64.data_ptr(),
                       lay.n_i64, seed, c + 1, I64_CLIENT_MOD, _h(stream))
+
+
+def fill_slices(base: DeviceArena, slab: ClientSlab | None, slices, n_i64: int, seed: int, k: int,
+                stream=None) -> None:
+    """Arenas holding SLICES of the one global model and client set of ``seed``.
+
+    ``slices``: [(local offset, global first element, n)] of the fp32 region; the local
+    ``base.f32[off:off+n]`` gets baseline elements ``first..first+n-1`` and client row r's
+    the matching elements of client r (``plato_agg_fill_synth_*_at``), so the slices of
+    several arenas — a bucket-sharded rank's pieces, a window of a parity check — are
+    bit-identical to the same elements of :func:`fill_baseline` / :func:`fill_clients`
+    on the whole model.  The first ``n_i64`` int64 entries are filled whole (they are
+    never cut).
+    """
+    stream = stream or torch.cuda.current_stream(base.f32.device)
+    h = _h(stream)
+    b0, bi0 = base.f32.data_ptr(), base.i64.data_ptr()
+    for off, first, n in slices:
+        _lib.call("plato_agg_fill_synth_f32_at", b0 + off * 4, None, n, seed, 0, first, BASE_SCALE, h)
+    if n_i64:
+        _lib.call("plato_agg_fill_synth_i64_at", bi0, None, n_i64, seed, 0, 0, I64_BASE_MOD, h)
+    if slab is None:
+        return
+    for r in range(k):
+        rf, ri = slab.f32[r].data_ptr(), slab.i64[r].data_ptr()
+        for off, first, n in slices:
+            _lib.call("plato_agg_fill_synth_f32_at", rf + off * 4, b0 + off * 4, n, seed, r + 1, first,
+                      CLIENT_SCALE, h)
+        if n_i64:
+            _lib.call("plato_agg_fill_synth_i64_at", ri, bi0, n_i64, seed, r + 1, 0, I64_CLIENT_MOD, h)

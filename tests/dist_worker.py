@@ -1,6 +1,11 @@
 """Worker for the multi-process tests (launched by torch.distributed.run).
 
 Modes:
+  cpu-bench-strong
+               gloo, CPU: bench.py's N > 1 job (pieces filled as slices of one global
+               job, PieceExchange send/gather/assemble) with the oracle as the
+               per-piece compute; bench's parity fields must say bit-exact
+               (-corrupt: one flipped bit on the last rank must say MISMATCH).
   cpu-bucket   gloo, CPU: bucket sharding with the oracle as the per-bucket
                compute (the sequential-K kernel is elementwise, so each
                bucket's result is the oracle on that slice); gathered model
@@ -59,6 +64,56 @@ def cpu_pieces(rank, world, out):
     exp, _ = ref.fedavg_numpy(bf, bi, xs_f, xs_i, w)
     out["bit_exact"] = full[: layout.n_f32].numpy().tobytes() == exp.tobytes()
     out["pieces"], out["length"] = plan.pieces, L
+
+
+def cpu_bench_strong(rank, world, out, corrupt=False):
+    """bench.py's N > 1 job and its parity fields, with the oracle in the kernel's place.
+
+    Every rank generates ITS pieces as slices of the one global job (the counter generator from the
+    pieces' global offsets, as plato_agg_fill_synth_*_at does on the GPU), lays its results out in
+    the send buffer of PieceExchange, all-gathers piece by piece, and reads the model back with
+    PieceExchange.assemble; then bench.ranks_agree and, on rank 0, bench.compare_windows against the
+    whole job regenerated window by window.  ``corrupt``: rank world-1 flips one bit of its last piece.
+    """
+    import bench
+
+    layout = ArenaLayout.from_shapes(workloads.lenet5())
+    k, seed, pieces = 5, 31, 3
+    w = ref.fedavg_weights(synth.num_samples(k, seed))
+    plan = PiecePlan.for_layout(layout, world, pieces)
+    xchg = plan.exchange(layout.n_i64)
+
+    def job_slice(lo, n, ni):
+        b = synth.synth_f32(n, seed, 0, synth.BASE_SCALE, start=lo)
+        xs = [synth.synth_f32(n, seed, c + 1, synth.CLIENT_SCALE, add=b, start=lo) for c in range(k)]
+        bi = synth.synth_i64(ni, seed, 0, synth.I64_BASE_MOD)
+        xi = [synth.synth_i64(ni, seed, c + 1, synth.I64_CLIENT_MOD, add=bi) for c in range(k)]
+        f, i = ref.fedavg_numpy(b, bi, xs, xi, w)
+        return torch.from_numpy(f), torch.from_numpy(i)
+
+    send = torch.zeros(xchg.send_numel, dtype=torch.float32)
+    for p in range(pieces):
+        lo, hi = plan.piece_range(rank, p)
+        ni = layout.n_i64 if (rank == 0 and p == 0) else 0
+        f, i = job_slice(lo, hi - lo, ni)
+        send[xchg.soff[p]: xchg.soff[p] + (hi - lo)] = f
+        if ni:
+            send[xchg.int64_offset(): xchg.int64_offset() + ni] = i
+    if corrupt and rank == world - 1:
+        lo, hi = plan.piece_range(rank, pieces - 1)
+        if hi > lo:
+            send[xchg.soff[pieces - 1]: xchg.soff[pieces - 1] + 1].view(torch.int32).bitwise_xor_(1)
+    gathered = torch.empty(xchg.gathered_numel, dtype=torch.float32)
+    for p in range(pieces):
+        dist.all_gather_into_tensor(xchg.gather_slice(gathered, p), xchg.send_slice(send, p))
+    got_f, got_i = xchg.assemble(gathered)
+    out["ranks_agree"] = bench.ranks_agree(bench.bits_digest(got_f, got_i), world)
+    if rank == 0:
+        res = bench.compare_windows(layout.n_f32, layout.n_i64, 20000, job_slice, got_f, got_i)
+        out.update(res)
+        exp_f, exp_i = job_slice(0, layout.n_f32, layout.n_i64)
+        out["whole_job_bit_exact"] = (got_f.numpy().tobytes() == exp_f.numpy().tobytes()
+                                      and got_i.numpy().tobytes() == exp_i.numpy().tobytes())
 
 
 def cpu_bucket(rank, world, out):
@@ -153,7 +208,9 @@ def main():
         dist.init_process_group("gloo")
     rank, world = dist.get_rank(), dist.get_world_size()
     out = {"rank": rank, "world": world}
-    {"cpu-bucket": cpu_bucket, "cpu-pieces": cpu_pieces, "cpu-client": cpu_client, "gpu-bucket": gpu_bucket,
+    {"cpu-bench-strong": cpu_bench_strong,
+     "cpu-bench-strong-corrupt": lambda r, wd, o: cpu_bench_strong(r, wd, o, corrupt=True),
+     "cpu-bucket": cpu_bucket, "cpu-pieces": cpu_pieces, "cpu-client": cpu_client, "gpu-bucket": gpu_bucket,
      "gpu-rccl": gpu_rccl}[mode](rank, world, out)
     with open(os.path.join(out_dir, f"rank{rank}.json"), "w") as f:
         json.dump(out, f)

@@ -133,6 +133,24 @@ def test_piece_plan_covers_arena_once(n_f32, world, pieces):
     assert pos == n_f32
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_bench_strong_job_parity(tmp_path, world):
+    """bench.py's N > 1 job is ONE FedAvg job: each rank's pieces are slices of the same global inputs, and
+    the parity fields the bench reports (compare_windows, ranks_agree) say bit-exact against the whole job."""
+    outs = _run("cpu-bench-strong", world, tmp_path)
+    assert all(o["ranks_agree"] for o in outs)
+    r0 = outs[0]
+    assert r0["parity"] == "bit-exact vs 1-GPU kernel" and r0["mismatched_elements"] == 0, r0
+    assert r0["whole_job_bit_exact"] and r0["windows"] >= 3  # the windowed check covers the model in pieces
+
+
+def test_gloo_bench_strong_job_parity_catches_a_flipped_bit(tmp_path):
+    outs = _run("cpu-bench-strong-corrupt", 2, tmp_path)
+    r0 = outs[0]
+    assert r0["parity"] == "MISMATCH vs 1-GPU kernel" and r0["mismatched_elements"] == 1, r0
+    assert not r0["whole_job_bit_exact"]
+
+
 def test_gloo_client_sharding_normwise(tmp_path):
     outs = _run("cpu-client", 2, tmp_path)
     for o in outs:
@@ -177,6 +195,40 @@ def test_bench_self_launches_its_ranks():
     assert "launching 2 ranks" in err
 
 
+def _bench_fails(args, limit):
+    import time
+
+    env = dict(os.environ, OMP_NUM_THREADS="2", PLATO_BENCH_BACKEND="gloo")
+    env.pop("WORLD_SIZE", None)
+    t0 = time.monotonic()
+    proc = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *args], env=env, capture_output=True,
+                          text=True, timeout=limit)
+    return proc, time.monotonic() - t0
+
+
+def test_bench_collective_timeout_names_rank_and_collective():
+    """A rank that never joins: the waiting rank's collective fails after --dist-timeout, naming itself and the
+    collective, and ``python bench.py --gpus 2`` exits non-zero well before any outer limit."""
+    proc, took = _bench_fails(["--gpus", "2", "--probe-launch", "--probe-stall-rank", "1", "--dist-timeout", "8",
+                               "--launch-timeout", "240"], 280)
+    assert proc.returncode not in (0, 124), proc.stderr[-3000:]
+    assert "rank 0: collective 'all_reduce(rank_sum)' failed" in proc.stderr, proc.stderr[-3000:]
+    assert took < 200
+    assert not [ln for ln in proc.stdout.splitlines() if ln.strip()]  # no result line
+
+
+def test_bench_launch_timeout_kills_the_tree_and_reports_phases():
+    """The self-launcher's wall-clock limit: the rank tree is killed, each rank's last phase is printed
+    (the stalled rank and the collective the other one waits in), exit code 124."""
+    proc, took = _bench_fails(["--gpus", "2", "--probe-launch", "--probe-stall-rank", "1", "--dist-timeout", "600",
+                               "--launch-timeout", "45"], 200)
+    assert proc.returncode == 124, proc.stderr[-3000:]
+    err = proc.stderr
+    assert "TIMEOUT" in err and "rank 1: stalling before all_reduce" in err, err[-3000:]
+    assert "rank 0: all_reduce(rank_sum)" in err, err[-3000:]
+    assert took < 120
+
+
 @pytest.mark.gpu
 def test_bench_self_launch_two_ranks_on_gpu():
     """The N > 1 bench from a plain ``python bench.py --gpus 2`` on the one-GPU box (gloo rehearsal: the ranks share
@@ -188,3 +240,12 @@ def test_bench_self_launch_two_ranks_on_gpu():
     cfg = out["config"]
     assert cfg["algorithmic_bytes_per_step_per_gpu"] > 0 and cfg["pieces_per_rank"] >= 1
     assert out["roofline"]["frac"] > 0
+    # one FedAvg job: the gathered model is the one-GPU kernel's on the same inputs, bit for bit
+    assert out["parity"] == "bit-exact vs 1-GPU kernel", out.get("parity_detail")
+    assert out["parity_detail"]["ranks_hold_identical_models"]
+    assert out["parity_detail"]["elements_checked"] == 11183562 + 20
+    # the server's in-process multi-GPU path (MultiDeviceEngine over 2 devices, repeated on one GPU)
+    ed = out["engine_devices"]
+    assert ed["status"] == "ok" and ed["engine_devices"] == 2, ed
+    assert ed["parity"].startswith("bit-exact vs 1-GPU engine"), ed
+    assert ed["parity_detail"]["gathered_copies_checked"] == 2

@@ -437,17 +437,42 @@ def test_weighted_sum_matches_sequential_loop(engine):
     assert got.tobytes() == exp.tobytes()
 
 
-@pytest.mark.parametrize("mode", ["weights", "deltas", "deltas_stale"])
-def test_stage_on_arrival_then_adopt_matches_reference(mode):
+def _arrival_delta_keys(eng, kind: str, layout) -> list:
+    """Per arrived payload: the key of the model its rows were turned into deltas against (None: weights)."""
+    if kind == "single":
+        return [hit[8] for hit in eng._arrivals.values()]
+    if kind in ("multi", "clients"):
+        return [hit[7] for hit in eng._arrivals.values()]
+    ent = eng.entries
+    parts = ent.plan(layout)[1]
+    keys = []
+    for _, _, subs in ent._arrivals.values():
+        per = [ent._engines[g]._arrivals[id(sub)][8] for (g, _), sub in zip(parts, subs)]
+        keys.append(None if any(k is None for k in per) else tuple(per))
+    return keys
+
+
+def _arrivals_of(eng, kind: str) -> dict:
+    return eng.entries._arrivals if kind == "entry" else eng._arrivals
+
+
+@pytest.mark.parametrize("engine_kind", ["single", "multi", "entry", "clients"])
+@pytest.mark.parametrize("mode", ["weights", "deltas", "deltas_stale", "deltas_data_write"])
+def test_stage_on_arrival_then_adopt_matches_reference(mode, engine_kind):
     """Payloads staged to HBM as they arrive (any arrival order), summed in updates order.
 
     "deltas": the server stages arrivals as deltas against its current model (arena_deltas), adopted by a
     round on that model; "deltas_stale": the model the arrivals were turned into deltas against is another
-    one (other storage), so the round stages every payload again from its host tensors."""
+    one (other storage), so the round stages every payload again from its host tensors;
+    "deltas_data_write": the arrivals were turned into deltas while the model held other values, written
+    and then restored through ``.data`` (no version-counter bump: the keys still match), so only the
+    device-side comparison of the two staged baselines makes the round stage the payloads again.
+    ``engine_kind``: one GPU; the multi-GPU engine's bucket rounds, entry shards and client-split rounds
+    (two repeated devices on a one-GPU box)."""
     import pickle
 
-    from plato_amd import ingest
     from plato_amd.servers import FusedAggregationMixin, WireIngestMixin
+    from plato_amd.staging import baseline_key
 
     case = next(c for c in CASES if c["recipe"]["name"] == "resnet18_k16_permuted")
     recipe, exp = case["recipe"], case["expected"]
@@ -455,13 +480,22 @@ def test_stage_on_arrival_then_adopt_matches_reference(mode):
 
     at_arrival = (OrderedDict((n, t.clone()) for n, t in baseline.items()) if mode == "deltas_stale"
                   else baseline)
+    if mode == "deltas_data_write":
+        saved = OrderedDict((n, t.clone()) for n, t in baseline.items())
+        key0 = baseline_key(baseline)
+        for t in baseline.values():
+            t.data.add_(1)
 
     class Algo:
         def extract_weights(self):
             return at_arrival
 
     class Server(WireIngestMixin, FusedAggregationMixin):
-        aggregation_device = DEV
+        aggregation_device = DEV if engine_kind == "single" else None
+        aggregation_devices = None if engine_kind == "single" else [DEV, DEV]
+        needs_staged_round = engine_kind in ("entry", "clients")
+        entry_local_weights = engine_kind == "entry"
+        client_split_rounds = engine_kind == "clients"
         stage_on_arrival = True
         arena_deltas = mode != "weights"
 
@@ -479,14 +513,19 @@ def test_stage_on_arrival_then_adopt_matches_reference(mode):
         asyncio.run(server._client_payload_arrived(sid, c + 1))
         arrived[c] = server.client_payload[sid]
     eng = server.aggregation_engine()
-    assert len(eng._arrivals) == recipe["k"]
+    if mode == "deltas_data_write":
+        for n, t in baseline.items():
+            t.data.copy_(saved[n])
+        assert baseline_key(baseline) == key0  # the in-place writes left every key as it was
+    keys = _arrival_delta_keys(eng, engine_kind, layout)
+    assert len(keys) == recipe["k"]
     # the arrival rows hold deltas (keyed by the model they were formed against) exactly when asked
-    assert all((hit[8] is not None) == (mode != "weights") for hit in eng._arrivals.values())
+    assert all((key is not None) == (mode != "weights") for key in keys)
     updates = _updates(recipe, [arrived[c] for c in range(recipe["k"])])
     updated = asyncio.run(server.aggregate_weights(updates, baseline, [u.payload for u in updates]))
     assert G.sha(G.canon(_flat(layout, updated, "f32"))) == exp["updated_f32_sha256"]
     assert G.sha(G.canon(_flat(layout, updated, "i64"))) == exp["updated_i64f_sha256"]
-    assert len(eng._arrivals) == 0  # released after the round
+    assert len(_arrivals_of(eng, engine_kind)) == 0  # released after the round
 
 
 RL = [c for c in CASES if c["recipe"].get("mode") in ("rl", "rl_f32")]

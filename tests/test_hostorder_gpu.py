@@ -25,13 +25,17 @@ def _record_calls(monkeypatch):
     return seen
 
 
+@pytest.mark.parametrize("deltas", [False, True])
 @pytest.mark.parametrize("align", [None, "fedadp"])
 @pytest.mark.parametrize("lr", [0.01, 0.3])
-def test_fedadp_probe_passes_through_the_product_kernel(monkeypatch, lr, align):
-    """Also on the aligned arenas FedAdp's servers use (the probe takes the server engine's alignment)."""
+def test_fedadp_probe_passes_through_the_product_kernel(monkeypatch, lr, align, deltas):
+    """Also on the aligned delta arenas FedAdp's servers use (the probe takes the server engine's alignment and
+    arena form, so it runs the dot kernel the rounds run: with deltas, its no-baseline form)."""
     H._checked.clear()
     seen = _record_calls(monkeypatch)
-    assert H.check_fedadp(DEV, lr, strict=True, align=align)
+    assert H.check_fedadp(DEV, lr, strict=True, align=align, deltas=deltas)
+    if deltas:
+        assert "plato_agg_compute_deltas" in seen  # the probe's client row was staged as its delta
     # the round's own calls (engine.AggregationRound.fedadp_dots), not a stand-in kernel
     assert "plato_agg_fedadp_dots" in seen and "plato_agg_sdot_shared" not in seen
 

@@ -667,13 +667,21 @@ def _many_entries(n_entries, seed):
     return ArenaLayout.from_shapes(spec)
 
 
+@pytest.mark.parametrize("deltas", [False, True], ids=["weight_arenas", "delta_arenas"])
 @pytest.mark.parametrize("n_entries", [300, 2600])
-def test_fedadp_dots_many_entries_match_oracle(engine, n_entries):
+def test_fedadp_dots_many_entries_match_oracle(engine, n_entries, deltas):
     """More entries than the round-3 kernel's 2,048-entry segment map: every boundary group goes through
-    the boundary table; the dots equal numpy's sdot order (oracle) and the flatten + sdot path bit for bit."""
+    the boundary table; the dots equal numpy's sdot order (oracle) and the flatten + sdot path bit for bit.
+    ``delta_arenas``: the clients staged as deltas (FedAdp's servers' default), where the fallback to the
+    flat path for models past the fused kernel's limits flattens the delta rows against a zero arena."""
     from oracle import fedavg_oracle as FO
     from oracle import reductions as R
 
+    if deltas:
+        from plato_amd.engine import FedAvgEngine
+
+        engine = FedAvgEngine(engine.device)
+        engine.delta_arenas = True
     layout = _many_entries(n_entries, n_entries)
     rng = np.random.default_rng(7)
     k, lr = 3, 0.03
