@@ -908,10 +908,10 @@ def engine_devices_child(args, world: int) -> dict:
         child.communicate()
         return {"status": "timeout", "limit_s": args.launch_timeout, "command": " ".join(cmd[1:])}
     lines = [ln for ln in out.splitlines() if ln.startswith("{")]
-    if child.returncode != 0 or not lines:
-        return {"status": f"failed (exit {child.returncode})", "command": " ".join(cmd[1:])}
-    res = json.loads(lines[-1])
-    res["status"] = "ok"
+    res = json.loads(lines[-1]) if lines else {}
+    res["status"] = "ok" if child.returncode == 0 and lines else f"failed (exit {child.returncode})"
+    if child.returncode:
+        res["command"] = " ".join(cmd[1:])
     return res
 
 
@@ -1378,12 +1378,9 @@ def engine_devices_parity(eng, layout, baseline, payloads, weights) -> dict:
         f, i = rnd.device_result(g)
         f, i = f.cpu(), i.cpu()
         for e in layout.entries:
-            ref = one[e.name].reshape(-1)
-            if e.region == F32:
-                ok = torch.equal(f[e.offset:e.offset + e.numel].view(torch.int32), ref.view(torch.int32))
-            else:  # the int64 entries' fp32 results, truncated as load_state_dict does
-                ok = torch.equal(i[e.offset:e.offset + e.numel].to(torch.int64), ref)
-            if not ok:
+            # fp32 entries, and the int64 entries' fp32 results (update_weights' values, before load_weights)
+            got = (f if e.region == F32 else i)[e.offset:e.offset + e.numel]
+            if not _same_bits(got, one[e.name]):
                 bad_dev.append((g, e.name))
     exact = not bad_host and not bad_dev
     return {"parity": "bit-exact vs 1-GPU engine (host result and every GPU's gathered copy)" if exact

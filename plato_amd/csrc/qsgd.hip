@@ -96,8 +96,18 @@ __device__ __forceinline__ float term(float x, float b, float w, float s, bool t
   return t;
 }
 
-template <int kBlock, int kU, bool TWO, int kG = ::kG, bool kSM = false>
-__device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
+// kAbs: the decode table holds |zeta| = 0..127 only (128 entries per client) and the code's sign bit is
+// flipped into the decoded value's bit 31 (round-to-nearest is sign-symmetric: decode(128 + z) =
+// -decode(z) for z != 0).  Code 128 (zeta = -0, the integer 0) then decodes to -decode(0) instead of
+// decode(0): a zero of the other sign (or a NaN of the other sign when max_v is not finite), which
+// cannot change any result bit — x - b with x = -0 or +0 differs only for b = +-0, where it is +-0 again,
+// and the accumulator, which starts at +0 and only becomes zero again by an exact cancellation (+0),
+// absorbs a zero term of either sign (NaN payloads are not compared).  Halving the table
+// puts the frequent small |zeta| of both signs on one address (a broadcast) instead of two addresses in
+// one bank: the lookups' LDS bank conflicts fall from ~2.1 extra cycles per ds_read_b32 (SQ counters,
+// profiles/r06c_qsgd_pmc.json) to the ~0.5 a 128-entry table's random collisions cost.
+template <int kBlock, int kU, bool TWO, int kG = ::kG, bool kSM = false, bool kAbs = false>
+__device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[kAbs ? 128 : 256]) {
   static_assert(kG == 16 || kG == 8 || kG == 4, "one 16-, 8- or 4-byte code load per lane");
   const Chunk ch = load_chunk(a.tf, c, a.n_f32);
   const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
@@ -151,7 +161,7 @@ __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
         if (u < nu) {
           const float v = decode(uint32_t(z), sld(mrow, i0 + u), a.divisor);
           lut[u][z] = v;
-          lut[u][z + 128] = z ? -v : v;
+          if (!kAbs) lut[u][z + 128] = z ? -v : v;
         }
       }
       __syncthreads();
@@ -171,7 +181,13 @@ __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
 #pragma unroll
             for (int q = 0; q < kG; ++q) {
               const uint32_t word = code[u][q >> 2];
-              const float x = lut[u][(word >> (8 * (q & 3))) & 255u];
+              float x;
+              if (kAbs) {
+                const uint32_t sbit = (word << (24 - 8 * (q & 3))) & 0x80000000u;
+                x = __uint_as_float(__float_as_uint(lut[u][(word >> (8 * (q & 3))) & 127u]) ^ sbit);
+              } else {
+                x = lut[u][(word >> (8 * (q & 3))) & 255u];
+              }
               acc[q] = acc[q] + term(x, b[q], wu, su, TWO);
             }
           }
@@ -184,7 +200,12 @@ __device__ void qsgd_f32_chunk(const QArgs& a, uint32_t c, float (*lut)[256]) {
 #pragma unroll
           for (int q = 0; q < kG; ++q) {
             const uint64_t e = e0 + q;
-            if (e >= ch.begin && e < ch.end) acc[q] = acc[q] + term(lut[u][p[e]], b[q], wu, su, TWO);
+            if (e >= ch.begin && e < ch.end) {
+              const uint32_t byte = p[e];
+              const float x = kAbs ? __uint_as_float(__float_as_uint(lut[u][byte & 127u]) ^ ((byte & 128u) << 24))
+                                   : lut[u][byte];
+              acc[q] = acc[q] + term(x, b[q], wu, su, TWO);
+            }
           }
         }
       }
@@ -433,26 +454,159 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, 8))) 
   }
 }
 
-template <int kBlock, int kU, bool TWO, int kGE = kG, bool kSM = false>
+template <int kBlock, int kU, bool TWO, int kGE = kG, bool kSM = false, bool kAbs = false>
 __global__ __launch_bounds__(kBlock) void fedavg_qsgd_kernel(QArgs a) {
-  __shared__ float lut[kU][256];
+  __shared__ float lut[kU][kAbs ? 128 : 256];
   const uint32_t c = blockIdx.x;  // the int64 chunks first (qsgd_i64_chunk)
   if (c >= a.nci) {
-    qsgd_f32_chunk<kBlock, kU, TWO, kGE, kSM>(a, c - a.nci, lut);
+    qsgd_f32_chunk<kBlock, kU, TWO, kGE, kSM, kAbs>(a, c - a.nci, lut);
   } else {
     qsgd_i64_chunk<kBlock, TWO>(a, c);
   }
 }
 
+#ifdef PLATO_AGG_TUNE  // round-6 candidates (libplato_agg_tune.so)
+// ---------------------------------------------------------------------------
+// Arithmetic decode (no tables, no LDS, no barriers): x = RN32(p / divisor) as
+// RN32(RN64(p) * RN64(1 / divisor)) with p = RN32(|zeta| * max_v) — the exact float32 division's bits
+// for every float pair (the argument of fedadp.hip adp_div_lr_f64, tests/test_division.py: the float64
+// product lies within 2^-52 of the quotient, which is never that close to a float32 midpoint unless it
+// is one, and then it is a float64 the product rounds to exactly).  The sign is applied afterwards by
+// flipping bit 31 of the decoded value for codes with bit 7 set and |zeta| != 0: round-to-nearest is
+// sign-symmetric, so decode(128 + z) = -decode(z) for z != 0, and code 128 (zeta = -0, the integer 0)
+// decodes as code 0.  A lane owns kG consecutive elements (one kG-byte code load per client), clients in
+// batches of kU whose code loads are issued one batch ahead.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float decode_arith(uint32_t zabs, float max_v, double inv_div) {
+  const float p = float(zabs) * max_v;  // fp32(zeta * max_v): zeta exact in fp32 (v_cvt_f32_ubyte)
+  return float(double(p) * inv_div);     // fp32(p / divisor)
+}
+
+template <int kG, int kU, bool TWO>
+__device__ __forceinline__ void arith_batch(const QArgs& a, const float* mrow, int i0, int nu, double inv_div,
+                                            const CodeOf<kG> (&code)[kU], const float (&b)[kG], float (&acc)[kG]) {
+#pragma unroll
+  for (int u = 0; u < kU; ++u) {
+    if (u < nu) {
+      const float mv = sld(mrow, i0 + u);
+      const float wu = sld(a.w, i0 + u);
+      const float su = TWO ? sld(a.s, i0 + u) : 1.f;
+#pragma unroll
+      for (int j = 0; j < kG / 4; ++j) {
+        const uint32_t word = code[u][j];
+        const uint32_t mag = word & 0x7f7f7f7fu;
+        // bit 7 of each byte: set iff the code is negative and |zeta| != 0 (|zeta| + 127 carries into bit 7)
+        const uint32_t neg = word & (mag + 0x7f7f7f7fu) & 0x80808080u;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const float v = decode_arith((mag >> (8 * q)) & 0xffu, mv, inv_div);
+          const uint32_t sbit = (neg << (24 - 8 * q)) & 0x80000000u;
+          const float x = __uint_as_float(__float_as_uint(v) ^ sbit);
+          acc[4 * j + q] = acc[4 * j + q] + term(x, b[4 * j + q], wu, su, TWO);
+        }
+      }
+    }
+  }
+}
+
+template <int kBlock, int kG, int kU, bool TWO>
+__device__ void qsgd_f32_chunk_arith(const QArgs& a, uint32_t c) {
+  static_assert(kG == 16 || kG == 8 || kG == 4, "one 16-, 8- or 4-byte code load per lane");
+  const Chunk ch = load_chunk(a.tf, c, a.n_f32);
+  const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
+  const uint64_t g0 = ch.begin / kG, g1 = (uint64_t(ch.end) + kG - 1) / kG;
+  const int K = a.K;
+  const double inv_div = 1.0 / double(a.divisor);
+  for (uint64_t gp = g0; gp < g1; gp += kBlock) {
+    const uint64_t g = gp + threadIdx.x;
+    const bool have = g < g1;
+    const uint64_t e0 = g * kG;
+    const bool full = have && e0 >= ch.begin && e0 + kG <= ch.end;
+    float b[kG], acc[kG];
+#pragma unroll
+    for (int q = 0; q < kG; ++q) {
+      acc[q] = 0.f;
+      b[q] = 0.f;
+    }
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < kG / 4; ++q) {
+        const f4 v = *((gf4*)(a.base_f + e0) + q);
+        b[4 * q] = v.x;
+        b[4 * q + 1] = v.y;
+        b[4 * q + 2] = v.z;
+        b[4 * q + 3] = v.w;
+      }
+      CodeOf<kG> ca[kU], cb[kU];
+      load_codes<kU, kG>(a, 0, K, e0, ca);
+      for (int i0 = 0; i0 < K; i0 += 2 * kU) {  // two register sets, alternating by batch
+        if (i0 + kU < K) load_codes<kU, kG>(a, i0 + kU, K, e0, cb);
+        arith_batch<kG, kU, TWO>(a, mrow, i0, K - i0 < kU ? K - i0 : kU, inv_div, ca, b, acc);
+        if (i0 + kU >= K) break;
+        if (i0 + 2 * kU < K) load_codes<kU, kG>(a, i0 + 2 * kU, K, e0, ca);
+        arith_batch<kG, kU, TWO>(a, mrow, i0 + kU, K - i0 - kU < kU ? K - i0 - kU : kU, inv_div, cb, b, acc);
+      }
+#pragma unroll
+      for (int q = 0; q < kG / 4; ++q) {
+        const f4 v = f4{b[4 * q] + acc[4 * q], b[4 * q + 1] + acc[4 * q + 1], b[4 * q + 2] + acc[4 * q + 2],
+                        b[4 * q + 3] + acc[4 * q + 3]};
+        __builtin_nontemporal_store(v, (gf4w*)(a.out_f + e0) + q);
+      }
+    } else if (have) {  // a group cut by the chunk's ends: byte by byte
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const uint64_t e = e0 + q;
+        if (e >= ch.begin && e < ch.end) b[q] = a.base_f[e];
+      }
+      for (int i = 0; i < K; ++i) {
+        const uint8_t* p = sld(a.cf, i);
+        const float mv = sld(mrow, i), wu = sld(a.w, i), su = TWO ? sld(a.s, i) : 1.f;
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+          const uint64_t e = e0 + q;
+          if (e >= ch.begin && e < ch.end) {
+            const uint32_t byte = p[e];
+            const float v = decode_arith(byte & 127u, mv, inv_div);
+            const float x = (byte > 128u) ? -v : v;
+            acc[q] = acc[q] + term(x, b[q], wu, su, TWO);
+          }
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const uint64_t e = e0 + q;
+        if (e >= ch.begin && e < ch.end) a.out_f[e] = b[q] + acc[q];
+      }
+    }
+  }
+}
+
+template <int kBlock, int kG, int kU, bool TWO>
+__global__ __launch_bounds__(kBlock) void fedavg_qsgd_arith_kernel(QArgs a) {
+  const uint32_t c = blockIdx.x;  // the int64 chunks first (qsgd_i64_chunk)
+  if (c >= a.nci) {
+    qsgd_f32_chunk_arith<kBlock, kG, kU, TWO>(a, c - a.nci);
+  } else {
+    qsgd_i64_chunk<kBlock, TWO>(a, c);
+  }
+}
+#endif  // PLATO_AGG_TUNE
+
 using QFn = void (*)(const QArgs&, hipStream_t, uint32_t);
-template <int B, int U, bool TWO, int G = kG, bool SM = false>
+template <int B, int U, bool TWO, int G = kG, bool SM = false, bool ABS = false>
 void launch_q(const QArgs& a, hipStream_t st, uint32_t nc) {
-  hipLaunchKernelGGL((fedavg_qsgd_kernel<B, U, TWO, G, SM>), dim3(nc), dim3(B), 0, st, a);
+  hipLaunchKernelGGL((fedavg_qsgd_kernel<B, U, TWO, G, SM, ABS>), dim3(nc), dim3(B), 0, st, a);
 }
 template <int B, int U, bool TWO, int G, int P = 0>
 void launch_qp(const QArgs& a, hipStream_t st, uint32_t nc) {
   hipLaunchKernelGGL((fedavg_qsgd_pipe_kernel<B, U, TWO, G, P>), dim3(nc), dim3(B), 0, st, a);
 }
+#ifdef PLATO_AGG_TUNE
+template <int B, int G, int U, bool TWO>
+void launch_qa(const QArgs& a, hipStream_t st, uint32_t nc) {
+  hipLaunchKernelGGL((fedavg_qsgd_arith_kernel<B, G, U, TWO>), dim3(nc), dim3(B), 0, st, a);
+}
+#endif
 struct QVariant {
   int block, u, g;  // threads, clients per table batch, elements per lane
   QFn fn[2];        // [TWO]
@@ -471,6 +625,19 @@ const QVariant kQVariants[] = {
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 3>, &launch_qp<512, 4, true, 8, 3>}},  // 4: probe, neither
     {1024, 8, 8, {&launch_q<1024, 8, false, 8>, &launch_q<1024, 8, true, 8>}},       // 5: round 1 (vector max_v loads)
     {512, 8, 8, {&launch_q<512, 8, false, 8, true>, &launch_q<512, 8, true, 8, true>}},  // 6: the round-4 default
+    // round 6: arithmetic decode (float64 reciprocal product, no tables): {block, clients per batch, elements/lane}
+    {256, 4, 8, {&launch_qa<256, 8, 4, false>, &launch_qa<256, 8, 4, true>}},     // 7
+    {256, 8, 8, {&launch_qa<256, 8, 8, false>, &launch_qa<256, 8, 8, true>}},     // 8
+    {256, 4, 16, {&launch_qa<256, 16, 4, false>, &launch_qa<256, 16, 4, true>}},  // 9
+    {128, 4, 16, {&launch_qa<128, 16, 4, false>, &launch_qa<128, 16, 4, true>}},  // 10
+    {64, 4, 16, {&launch_qa<64, 16, 4, false>, &launch_qa<64, 16, 4, true>}},     // 11
+    {256, 2, 16, {&launch_qa<256, 16, 2, false>, &launch_qa<256, 16, 2, true>}},  // 12
+    // round 6: |zeta| tables (128 entries) with the sign flipped into bit 31 (kAbs)
+    {256, 8, 8, {&launch_q<256, 8, false, 8, true, true>, &launch_q<256, 8, true, 8, true, true>}},      // 13
+    {256, 16, 8, {&launch_q<256, 16, false, 8, true, true>, &launch_q<256, 16, true, 8, true, true>}},   // 14
+    {512, 8, 8, {&launch_q<512, 8, false, 8, true, true>, &launch_q<512, 8, true, 8, true, true>}},      // 15
+    {256, 8, 16, {&launch_q<256, 8, false, 16, true, true>, &launch_q<256, 8, true, 16, true, true>}},   // 16
+    {128, 8, 8, {&launch_q<128, 8, false, 8, true, true>, &launch_q<128, 8, true, 8, true, true>}},      // 17
 };
 #else  // libplato_agg.so: the default only
 // 256 threads: 0.309 against 0.320 ms for the round-4 512-thread form, interleaved (profiles/r05l_qsgd.log)

@@ -497,7 +497,7 @@ def test_entry_sharded_prestage_failure_keeps_no_slot():
     lay = ArenaLayout.from_state_dict(base)
     assert eng.prestage(pays[0], lay)
     assert len(eng._engines[0]._arrivals) == 1 and len(eng._engines[1]._arrivals) == 1
-    eng._engines[1].prestage = lambda payload, layout: False
+    eng._engines[1].prestage = lambda payload, layout, baseline=None: False
     assert not eng.prestage(pays[1], lay)
     assert len(eng._engines[0]._arrivals) == 1  # only the first payload's slot
     assert id(pays[1]) not in eng._arrivals

@@ -75,7 +75,7 @@ SPEC = [("a", (3,), "f32"), ("n0", (), "i64"), ("b", (17,), "f32"), ("c", (5, 7)
 # the product default (libplato_agg.so) and the tuning library's FedAvg shapes: 0 the default's plain
 # form, 1 the pipelined form of rounds 2-3, 5 the round-1 plain form, 6 a 256-thread shape; 2-4 are
 # timing probes (not the FedAvg)
-@pytest.mark.parametrize("variant", [None, 0, 1, 5, 6])
+@pytest.mark.parametrize("variant", [None, 0, 1, 5, 6, 7, 9, 12, 13, 14, 16])
 @pytest.mark.parametrize("cap,k,two", [(8, 3, False), (20, 9, True), (4096, 17, False), (64, 16, True), (1 << 20, 5, False)])
 def test_qsgd_kernel_matches_oracle(engine, monkeypatch, cap, k, two, variant):
     """Chunk pieces of every alignment (caps 8/20: partial 16-byte groups everywhere;
@@ -116,3 +116,44 @@ def test_qsgd_kernel_matches_oracle(engine, monkeypatch, cap, k, two, variant):
                                     [weights[i] for i in order], None if scales is None else [scales[i] for i in order])
     assert G.canon(_flat(layout, got, "f32")).tobytes() == G.canon(exp_f).tobytes()
     assert G.canon(_flat(layout, got, "i64")).tobytes() == G.canon(exp_i).tobytes()
+
+
+@pytest.mark.parametrize("variant", [None, 7, 9, 13, 16])
+def test_qsgd_decode_at_float32_extremes(engine, monkeypatch, variant):
+    """max_v at the ends of float32 (subnormal, tiny, huge, so that |zeta| * max_v / divisor overflows or
+    lands among the subnormals) and divisors of awkward quotients: the arithmetic decode (a float64
+    reciprocal product, variants 7 and 9) gives the float32 division's bits, like the table kernel."""
+    monkeypatch.setattr(engine, "qsgd_variant", variant)
+    spec = [("a", (4096,), "f32"), ("b", (333,), "f32"), ("c", (8192,), "f32"), ("n", (), "i64")]
+    layout = ArenaLayout.from_shapes(spec)
+    rng = np.random.default_rng(5)
+    bf = (rng.standard_normal(layout.n_f32) * 1e-3).astype(np.float32)
+    bi = rng.integers(-50, 50, layout.n_i64)
+    baseline = layout.unpack(torch.from_numpy(bf), torch.from_numpy(bi))
+    extremes = [1e-45, 3e-39, 1.1754944e-38, 7e-36, 2.5e37, 3.4e38, 0.37, 1.0, 1e-8]
+    k = len(extremes)
+    for level in (3, 64, 129):
+        proc = Processor(quantization_level=level)
+        wires = []
+        for c in range(k):
+            ents = {}
+            for e in layout.entries:
+                codes = rng.integers(0, 256, e.numel).astype(np.uint8)
+                ents[e.name] = Q.encode_layer(codes, np.float32(extremes[(c + len(ents)) % k]), e.shape)
+            wires.append(ents)
+        pays = [proc.process(w) for w in wires]
+        deq = []
+        for w in wires:
+            vals = {n: Q.decode_layer(b, level).reshape(-1) for n, b in w.items()}
+            deq.append((np.concatenate([vals[e.name] for e in layout.entries if e.region == "f32"]),
+                        np.concatenate([vals[e.name] for e in layout.entries if e.region == "i64"])))
+        weights = W.fedavg(list(range(1, k + 1)))
+        rnd = engine.begin(baseline, k, "qsgd")
+        rnd.put_baseline(baseline)
+        for slot in range(k):
+            rnd.put_client(slot, pays[slot])
+        rnd.launch(weights)
+        got = rnd.result()
+        exp_f, exp_i = ref.fedavg_numpy(bf, bi, [d[0] for d in deq], [d[1] for d in deq], weights)
+        assert G.canon(_flat(layout, got, "f32")).tobytes() == G.canon(exp_f).tobytes(), level
+        assert G.canon(_flat(layout, got, "i64")).tobytes() == G.canon(exp_i).tobytes(), level
