@@ -72,6 +72,9 @@ def parse():
     p.add_argument("--no-variants", action="store_true",
                    help="skip the variant servers' reductions leg (SURVEY.md §8(f), N=1 only)")
     p.add_argument("--variant-reps", type=int, default=10)
+    p.add_argument("--variants-first", action="store_true",
+                   help="N=1: run the variant reductions leg right after the headline's timed region, before the "
+                        "host-inclusive leg (which leaves another K-client slab allocated)")
     p.add_argument("--dist-timeout", type=float, default=180.0,
                    help="N > 1: seconds any collective (and the rendezvous) may wait before the rank fails "
                         "naming it; also the per-rank stall watchdog (+60 s)")
@@ -198,10 +201,18 @@ def self_launch(n: int, argv: list[str], limit_s: float) -> int:
     return code
 
 
+_WATCHDOG_S = None
+
+
 def collective(rank: int, name: str, fn, *a, **kw):
     """Run one collective of the N > 1 path: announce it (the self-launcher's per-rank phase) and turn a
-    failure (a peer gone, the --dist-timeout expired) into an error that names this rank and collective."""
+    failure (a peer gone, the --dist-timeout expired) into an error that names this rank and collective.
+    Re-arms the per-rank watchdog: it fires only when one phase outlasts it."""
     progress(f"rank {rank}: {name}")
+    if _WATCHDOG_S is not None:
+        import faulthandler
+
+        faulthandler.dump_traceback_later(_WATCHDOG_S, exit=True)
     try:
         return fn(*a, **kw)
     except Exception as exc:  # torch.distributed raises RuntimeError / DistBackendError subclasses
@@ -209,12 +220,24 @@ def collective(rank: int, name: str, fn, *a, **kw):
 
 
 def arm_watchdog(args, world: int) -> None:
-    """N > 1: a rank stalled outside any collective (a kernel or a host wait that never returns) dumps every
-    thread's Python stack to stderr and exits non-zero after --dist-timeout + 60 s (faulthandler; no exec)."""
+    """N > 1: a rank stalled between two collectives (a kernel or a host wait that never returns) dumps every
+    thread's Python stack to stderr and exits non-zero once --dist-timeout + 60 s pass without a new phase
+    (faulthandler, re-armed by every collective; no exec)."""
+    global _WATCHDOG_S
     if world > 1:
         import faulthandler
 
-        faulthandler.dump_traceback_later(args.dist_timeout + 60.0, exit=True)
+        _WATCHDOG_S = args.dist_timeout + 60.0
+        faulthandler.dump_traceback_later(_WATCHDOG_S, exit=True)
+
+
+def disarm_watchdog() -> None:
+    global _WATCHDOG_S
+    if _WATCHDOG_S is not None:
+        import faulthandler
+
+        faulthandler.cancel_dump_traceback_later()
+        _WATCHDOG_S = None
 
 
 def probe_launch(args) -> None:
@@ -735,6 +758,11 @@ def main():
 
     if args.codec != "native":
         args.no_host_inclusive = args.no_cpu_baseline = True
+    run_variants = rank == 0 and world == 1 and not args.no_variants and args.config == "C2" and args.codec == "native"
+    if run_variants and args.variants_first:
+        progress("variant reductions leg")
+        result["variants"] = variant_legs(dev, k, args.variant_reps)
+        run_variants = False
     if rank == 0 and world == 1 and not args.no_host_inclusive:
         progress("host-inclusive leg")
         result["host_inclusive"] = host_inclusive(engine, layout, base, slab, k, weights, dev)
@@ -742,7 +770,7 @@ def main():
     if rank == 0 and world == 1 and args.streaming:
         result["streaming"] = streaming(engine, layout, base, slab, k, weights, dev)
 
-    if rank == 0 and world == 1 and not args.no_variants and args.config == "C2" and args.codec == "native":
+    if run_variants:
         progress("variant reductions leg")
         result["variants"] = variant_legs(dev, k, args.variant_reps)
 
@@ -777,6 +805,7 @@ def main():
 
         progress(f"rank {rank}: destroy_process_group")
         dist.destroy_process_group()
+        disarm_watchdog()  # what follows is bounded on its own (the engine-devices leg's limit)
     if rank == 0 and plan is not None and not args.no_engine_devices_leg and args.codec == "native":
         # the server's own multi-GPU path (one process driving the N GPUs: MultiDeviceEngine, RCCL
         # communicator from ncclCommInitAll), in a child process once the ranks are done
@@ -882,6 +911,9 @@ def compare_windows(n_f: int, n_i: int, win: int, run_window, got_f: torch.Tenso
             "windows": windows, "window_elements": win}
 
 
+ENGINE_DEVICES_LIMIT_S = 300.0
+
+
 def engine_devices_child(args, world: int) -> dict:
     """``bench.py --engine-devices N --parity`` as a child process (spawned, never exec'd); its JSON line.
 
@@ -899,14 +931,17 @@ def engine_devices_child(args, world: int) -> dict:
            "--steps", str(max(1, min(args.steps, 5))), "--warmup", "1", "--seed", str(args.seed), "--parity"]
     if args.clients:
         cmd += ["--clients", str(args.clients)]
-    progress(f"rank 0: engine-devices leg: {' '.join(cmd[1:])}")
+    # bounded well inside the whole run's budget: the leg takes ~30-60 s (torch import, 128 host payloads,
+    # a few rounds); a hang in its first in-process RCCL communicator must not cost the line
+    limit = min(args.launch_timeout, ENGINE_DEVICES_LIMIT_S)
+    progress(f"rank 0: engine-devices leg (limit {limit:.0f} s): {' '.join(cmd[1:])}")
     child = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, env=env, start_new_session=True)
     try:
-        out, _ = child.communicate(timeout=args.launch_timeout)
+        out, _ = child.communicate(timeout=limit)
     except subprocess.TimeoutExpired:
         os.killpg(child.pid, signal.SIGKILL)
         child.communicate()
-        return {"status": "timeout", "limit_s": args.launch_timeout, "command": " ".join(cmd[1:])}
+        return {"status": "timeout", "limit_s": limit, "command": " ".join(cmd[1:])}
     lines = [ln for ln in out.splitlines() if ln.startswith("{")]
     res = json.loads(lines[-1]) if lines else {}
     res["status"] = "ok" if child.returncode == 0 and lines else f"failed (exit {child.returncode})"

@@ -40,6 +40,7 @@
 // is an explicit v_fma_f32.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 #include <string>
 
@@ -220,8 +221,9 @@ __device__ __forceinline__ void adp_issue(const AdpArgs& a, const AdpDesc* desc,
     const uint32_t yo = bnd ? (d.off * 256u + uint32_t(lane) * 4u) * 4u : (p + d.off) * 4u;
     r.y[i] = bload4<(kF & kFYnt) ? 2 : 0>(ry, yo);
     if constexpr ((kF & kFDelta) != 0) {
-      static_assert((kF & kFXB) != 0, "delta arenas use the chain-group-major x buffer");
-      r.x[i] = bload4<0>(src.x, (grp * 512u + uint32_t(lane) * 4u) * 4u);
+      // delta arenas: no b; x from the chain-group-major buffer, or (round 6) straight from the flat
+      // gradient: 8 lanes read one 128-byte run of a half-block, whole lines, 16-byte aligned (p = 0 mod 4)
+      r.x[i] = (kF & kFXB) ? bload4<0>(src.x, (grp * 512u + uint32_t(lane) * 4u) * 4u) : bload4<0>(src.x, p * 4u);
       r.b[i] = f4v{0.f, 0.f, 0.f, 0.f};
     } else if constexpr ((kF & kFXB) != 0) {  // [cg][group][x: 256 | b: 256], lane l at 4 l
       const uint32_t q = (grp * 512u + uint32_t(lane) * 4u) * 4u;
@@ -441,10 +443,9 @@ __global__ __launch_bounds__(256) void fedadp_rows_kernel(AdpArgs a) {
 // The boundary table: process_grad's values of every boundary group of every pair, in the lane
 // order of the stream (index u * 32 + v: block 8 group + u, position cg * 32 + v); 0 past the
 // last whole block
-__global__ __launch_bounds__(256) void fedadp_boundary_kernel(AdpArgs a) {
-  const uint32_t row = blockIdx.x;
+// One row of the boundary table for pair blockIdx.y (the body of the round-5 one-row-per-workgroup kernel).
+__device__ __forceinline__ void fedadp_boundary_row(const AdpArgs& a, uint32_t row) {
   const int pair = int(blockIdx.y);
-  if (row >= min(*a.n_bnd, a.max_bnd)) return;
   const uint32_t j = a.bnd_at[row];
   const uint32_t cg = j / a.ngroups, grp = j % a.ngroups;
   const uint32_t u = threadIdx.x / 32, v = threadIdx.x % 32;
@@ -462,6 +463,18 @@ __global__ __launch_bounds__(256) void fedadp_boundary_kernel(AdpArgs a) {
     val = adp_y_in(a, pair, p, idx);
   }
   a.bnd[(uint64_t(pair) * a.max_bnd + row) * 256 + threadIdx.x] = val;
+}
+
+// Rows are walked with a stride of gridDim.x (kBndRowGroups workgroups per pair): the row count is
+// known on the device only, and one workgroup per possible row (max_bnd of them, most returning at
+// once) cost ~25 us of launch for ResNet-18 (profiles/r06f_variant_legs_kernel_stats.csv).
+constexpr uint32_t kBndRowGroups = 16;
+__global__ __launch_bounds__(256) void fedadp_boundary_kernel(AdpArgs a) {
+  const uint32_t nrows = min(*a.n_bnd, a.max_bnd);
+  for (uint32_t row = blockIdx.x; row < nrows; row += gridDim.x) {
+    if (row != blockIdx.x) __syncthreads();  // the previous row's shared segment index is consumed
+    fedadp_boundary_row(a, row);
+  }
 }
 
 // The chain-group-major x / b buffer: xb[cg][grp][0..255] = x at the group's half-block positions
@@ -594,6 +607,10 @@ const AdpLaunch kAdpVariants[] = {
     adp_launch<192, 8, 3, 2, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 15: delta arenas, 8 producer waves x 3
     adp_launch<192, 8, 3, 3, kFYnt | kFDiv64 | kFXB | kFDelta>(),  // 16: the same, 3 stages in flight
     adp_launch<192, 12, 2, 4, kFYnt | kFDiv64 | kFXB | kFDelta>(), // 17: 12 waves x 2, 4 stages in flight
+    // round 6: delta arenas with x read straight from the flat gradient (no chain-group-major buffer, no prep launch)
+    adp_launch<192, 12, 2, 3, kFYnt | kFDiv64 | kFDelta>(),        // 18: the delta default's shape
+    adp_launch<192, 12, 2, 4, kFYnt | kFDiv64 | kFDelta>(),        // 19: 4 stages in flight
+    adp_launch<192, 12, 2, 2, kFYnt | kFDiv64 | kFDelta>(),        // 20: 2 stages in flight
 };
 constexpr int kNumAdpVariants = sizeof(kAdpVariants) / sizeof(kAdpVariants[0]);
 // timing probes of the table above: wrong results by design (tests skip them)
@@ -729,7 +746,8 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
     if (int rc = check_launch("fedadp_desc launch")) return rc;
     hipLaunchKernelGGL(fedadp_rows_kernel, dim3((2 * a.ngroups + 255) / 256), dim3(256), 0, stream, a);
     if (int rc = check_launch("fedadp_rows launch")) return rc;
-    hipLaunchKernelGGL(fedadp_boundary_kernel, dim3(a.max_bnd, uint32_t(n_pairs)), dim3(256), 0, stream, a);
+    hipLaunchKernelGGL(fedadp_boundary_kernel, dim3(std::min(a.max_bnd, kBndRowGroups), uint32_t(n_pairs)), dim3(256), 0,
+                       stream, a);
     if (int rc = check_launch("fedadp_boundary launch")) return rc;
     if (fn.uses_xb) {
       hipLaunchKernelGGL(fedadp_prep_kernel, dim3(uint32_t((a.nsteps * 64 + kPrepSpan - 1) / kPrepSpan)), dim3(256), 0,

@@ -336,6 +336,276 @@ __device__ __forceinline__ void load_weights(const QArgs& a, int i0, float (&wu)
   }
 }
 
+// The plain form with its lookups software-pipelined (round 6): the counters of the default
+// (profiles/r06c_qsgd_pmc.json) show each wave issuing one client's kG lookups, then waiting for all of
+// them (s_waitcnt lgkmcnt(0): the scalar weight loads between the clients share the counter) before its
+// arithmetic.  Here the batch's weights are loaded with its codes, ahead of the tables, so the lookups
+// are the only LDS-counter operations in the batch, and client u + 1's lookups are issued before client
+// u's arithmetic: each wait leaves the next client's kG reads in flight.
+template <int kG, bool kAbs>
+__device__ __forceinline__ void sp_lookup(const float* tab, const CodeOf<kG>& code, float (&x)[kG]) {
+#pragma unroll
+  for (int q = 0; q < kG; ++q) {
+    const uint32_t word = code[q >> 2];
+    if (kAbs) {
+      const uint32_t sbit = (word << (24 - 8 * (q & 3))) & 0x80000000u;
+      x[q] = __uint_as_float(__float_as_uint(tab[(word >> (8 * (q & 3))) & 127u]) ^ sbit);
+    } else {
+      x[q] = tab[(word >> (8 * (q & 3))) & 255u];
+    }
+  }
+}
+
+template <int kG, bool TWO>
+__device__ __forceinline__ void sp_sum(const float (&x)[kG], const float (&b)[kG], float w, float s, float (&acc)[kG]) {
+#pragma unroll
+  for (int q = 0; q < kG; ++q) acc[q] = acc[q] + term(x[q], b[q], w, s, TWO);
+}
+
+template <int kBlock, int kU, bool TWO, int kG, bool kAbs>
+__device__ void qsgd_f32_chunk_sp(const QArgs& a, uint32_t c, float (*lut)[kAbs ? 128 : 256]) {
+  static_assert(kG == 16 || kG == 8 || kG == 4, "one 16-, 8- or 4-byte code load per lane");
+  const Chunk ch = load_chunk(a.tf, c, a.n_f32);
+  const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
+  const uint64_t g0 = ch.begin / kG, g1 = (uint64_t(ch.end) + kG - 1) / kG;
+  const int K = a.K;
+  for (uint64_t gp = g0; gp < g1; gp += kBlock) {
+    const uint64_t g = gp + threadIdx.x;
+    const bool have = g < g1;
+    const uint64_t e0 = g * kG;
+    const bool full = have && e0 >= ch.begin && e0 + kG <= ch.end;
+    float b[kG], acc[kG];
+#pragma unroll
+    for (int q = 0; q < kG; ++q) {
+      acc[q] = 0.f;
+      b[q] = 0.f;
+    }
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < kG / 4; ++q) {
+        const f4 v = *((gf4*)(a.base_f + e0) + q);
+        b[4 * q] = v.x;
+        b[4 * q + 1] = v.y;
+        b[4 * q + 2] = v.z;
+        b[4 * q + 3] = v.w;
+      }
+    } else if (have) {
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const uint64_t e = e0 + q;
+        if (e >= ch.begin && e < ch.end) b[q] = a.base_f[e];
+      }
+    }
+    for (int i0 = 0; i0 < K; i0 += kU) {
+      const int nu = K - i0 < kU ? K - i0 : kU;
+      __syncthreads();  // previous batch's lookups are done
+      CodeOf<kG> code[kU];
+      if (full) load_codes<kU, kG>(a, i0, K, e0, code);  // in flight during the table build and barrier
+      float wu[kU], su[kU];
+      load_weights<kU, TWO>(a, i0, wu, su);
+      for (int t = threadIdx.x; t < kU * 128; t += kBlock) {
+        const int u = __builtin_amdgcn_readfirstlane(t >> 7), z = t & 127;  // wave-uniform: scalar max_v
+        if (u < nu) {
+          const float v = decode(uint32_t(z), sld(mrow, i0 + u), a.divisor);
+          lut[u][z] = v;
+          if (!kAbs) lut[u][z + 128] = z ? -v : v;
+        }
+      }
+      __syncthreads();
+      if (full && nu == kU) {
+        float xa[kG], xb[kG];
+        sp_lookup<kG, kAbs>(lut[0], code[0], xa);
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          if (u % 2 == 0) {
+            if (u + 1 < kU) sp_lookup<kG, kAbs>(lut[u + 1], code[u + 1], xb);
+            sp_sum<kG, TWO>(xa, b, wu[u], su[u], acc);
+          } else {
+            if (u + 1 < kU) sp_lookup<kG, kAbs>(lut[u + 1], code[u + 1], xa);
+            sp_sum<kG, TWO>(xb, b, wu[u], su[u], acc);
+          }
+        }
+      } else if (full) {  // a ragged last batch
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+          if (u < nu) {
+            float x[kG];
+            sp_lookup<kG, kAbs>(lut[u], code[u], x);
+            sp_sum<kG, TWO>(x, b, wu[u], su[u], acc);
+          }
+        }
+      } else if (have) {
+        for (int u = 0; u < nu; ++u) {
+          const uint8_t* p = sld(a.cf, i0 + u);
+#pragma unroll
+          for (int q = 0; q < kG; ++q) {
+            const uint64_t e = e0 + q;
+            if (e >= ch.begin && e < ch.end) {
+              const uint32_t byte = p[e];
+              const float x = kAbs ? __uint_as_float(__float_as_uint(lut[u][byte & 127u]) ^ ((byte & 128u) << 24))
+                                   : lut[u][byte];
+              acc[q] = acc[q] + term(x, b[q], wu[u], su[u], TWO);
+            }
+          }
+        }
+      }
+    }
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < kG / 4; ++q) {
+        const f4 v = f4{b[4 * q] + acc[4 * q], b[4 * q + 1] + acc[4 * q + 1], b[4 * q + 2] + acc[4 * q + 2],
+                        b[4 * q + 3] + acc[4 * q + 3]};
+        __builtin_nontemporal_store(v, (gf4w*)(a.out_f + e0) + q);
+      }
+    } else if (have) {
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        const uint64_t e = e0 + q;
+        if (e >= ch.begin && e < ch.end) a.out_f[e] = b[q] + acc[q];
+      }
+    }
+  }
+}
+
+// Round 6, the VALU side of the plain form: a wave64 VALU instruction holds a SIMD for 4 cycles, so the
+// default's 3.87 VALU instructions per 64 element-clients already keep the SIMDs ~53 % busy beside the
+// LDS array's ~60 % (profiles/r06c_qsgd_pmc.json).  Two levers on it:
+//  * kFastTab: the decode table built with the float64 reciprocal product (RN32(RN64(p) * RN64(1 / d))
+//    = RN32(p / d) for every float pair, tests/test_division.py; fedadp.hip adp_div_lr_f64) instead of the
+//    IEEE division's ~10-instruction sequence: the table build was ~a quarter of the VALU instructions;
+//  * kP element groups per lane: each table batch serves kP groups of kG elements (a kP-times longer chunk
+//    per workgroup), so the table build and its two barriers are paid once per kP groups.
+[[maybe_unused]] __device__ __forceinline__ float decode_tab(uint32_t z, float max_v, double inv_div) {
+  return float(double(float(z) * max_v) * inv_div);
+}
+
+template <int kBlock, int kU, bool TWO, int kG, int kP, bool kFastTab>
+__device__ void qsgd_f32_chunk_mp(const QArgs& a, uint32_t c, float (*lut)[256]) {
+  static_assert(kG == 16 || kG == 8 || kG == 4, "one 16-, 8- or 4-byte code load per lane");
+  const Chunk ch = load_chunk(a.tf, c, a.n_f32);
+  const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
+  const uint64_t g0 = ch.begin / kG, g1 = (uint64_t(ch.end) + kG - 1) / kG;
+  const int K = a.K;
+  const double inv_div = 1.0 / double(a.divisor);
+  for (uint64_t gp = g0; gp < g1; gp += uint64_t(kBlock) * kP) {
+    uint64_t e0[kP];
+    bool have[kP], full[kP];
+    float b[kP][kG], acc[kP][kG];
+#pragma unroll
+    for (int p = 0; p < kP; ++p) {
+      const uint64_t g = gp + uint64_t(p) * kBlock + threadIdx.x;
+      have[p] = g < g1;
+      e0[p] = g * kG;
+      full[p] = have[p] && e0[p] >= ch.begin && e0[p] + kG <= ch.end;
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        acc[p][q] = 0.f;
+        b[p][q] = 0.f;
+      }
+      if (full[p]) {
+#pragma unroll
+        for (int q = 0; q < kG / 4; ++q) {
+          const f4 v = *((gf4*)(a.base_f + e0[p]) + q);
+          b[p][4 * q] = v.x;
+          b[p][4 * q + 1] = v.y;
+          b[p][4 * q + 2] = v.z;
+          b[p][4 * q + 3] = v.w;
+        }
+      } else if (have[p]) {
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+          const uint64_t e = e0[p] + q;
+          if (e >= ch.begin && e < ch.end) b[p][q] = a.base_f[e];
+        }
+      }
+    }
+    for (int i0 = 0; i0 < K; i0 += kU) {
+      const int nu = K - i0 < kU ? K - i0 : kU;
+      __syncthreads();  // previous batch's lookups are done
+      CodeOf<kG> code[kP][kU];
+#pragma unroll
+      for (int p = 0; p < kP; ++p)
+        if (full[p]) load_codes<kU, kG>(a, i0, K, e0[p], code[p]);  // in flight during the table build
+      float wu[kU], su[kU];
+      load_weights<kU, TWO>(a, i0, wu, su);
+      for (int t = threadIdx.x; t < kU * 128; t += kBlock) {
+        const int u = __builtin_amdgcn_readfirstlane(t >> 7), z = t & 127;  // wave-uniform: scalar max_v
+        if (u < nu) {
+          const float mv = sld(mrow, i0 + u);
+          const float v = kFastTab ? decode_tab(uint32_t(z), mv, inv_div) : decode(uint32_t(z), mv, a.divisor);
+          lut[u][z] = v;
+          lut[u][z + 128] = z ? -v : v;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int p = 0; p < kP; ++p) {
+        if (full[p]) {
+#pragma unroll
+          for (int u = 0; u < kU; ++u) {
+            if (u < nu) {
+#pragma unroll
+              for (int q = 0; q < kG; ++q) {
+                const uint32_t word = code[p][u][q >> 2];
+                const float x = lut[u][(word >> (8 * (q & 3))) & 255u];
+                acc[p][q] = acc[p][q] + term(x, b[p][q], wu[u], su[u], TWO);
+              }
+            }
+          }
+        } else if (have[p]) {
+          for (int u = 0; u < nu; ++u) {
+            const uint8_t* ptr = sld(a.cf, i0 + u);
+#pragma unroll
+            for (int q = 0; q < kG; ++q) {
+              const uint64_t e = e0[p] + q;
+              if (e >= ch.begin && e < ch.end) acc[p][q] = acc[p][q] + term(lut[u][ptr[e]], b[p][q], wu[u], su[u], TWO);
+            }
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < kP; ++p) {
+      if (full[p]) {
+#pragma unroll
+        for (int q = 0; q < kG / 4; ++q) {
+          const f4 v = f4{b[p][4 * q] + acc[p][4 * q], b[p][4 * q + 1] + acc[p][4 * q + 1],
+                          b[p][4 * q + 2] + acc[p][4 * q + 2], b[p][4 * q + 3] + acc[p][4 * q + 3]};
+          __builtin_nontemporal_store(v, (gf4w*)(a.out_f + e0[p]) + q);
+        }
+      } else if (have[p]) {
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+          const uint64_t e = e0[p] + q;
+          if (e >= ch.begin && e < ch.end) a.out_f[e] = b[p][q] + acc[p][q];
+        }
+      }
+    }
+  }
+}
+
+template <int kBlock, int kU, bool TWO, int kG, int kP, bool kFastTab>
+__global__ __launch_bounds__(kBlock) void fedavg_qsgd_mp_kernel(QArgs a) {
+  __shared__ float lut[kU][256];
+  const uint32_t c = blockIdx.x;  // the int64 chunks first (qsgd_i64_chunk)
+  if (c >= a.nci) {
+    qsgd_f32_chunk_mp<kBlock, kU, TWO, kG, kP, kFastTab>(a, c - a.nci, lut);
+  } else {
+    qsgd_i64_chunk<kBlock, TWO>(a, c);
+  }
+}
+
+template <int kBlock, int kU, bool TWO, int kG, bool kAbs>
+__global__ __launch_bounds__(kBlock) void fedavg_qsgd_sp_kernel(QArgs a) {
+  __shared__ float lut[kU][kAbs ? 128 : 256];
+  const uint32_t c = blockIdx.x;  // the int64 chunks first (qsgd_i64_chunk)
+  if (c >= a.nci) {
+    qsgd_f32_chunk_sp<kBlock, kU, TWO, kG, kAbs>(a, c - a.nci, lut);
+  } else {
+    qsgd_i64_chunk<kBlock, TWO>(a, c);
+  }
+}
+
 // Timing probes of the pipelined kernel (kP; results are NOT the FedAvg, never a default, not
 // parity-tested): kP 1 without the code loads, 2 without the table lookups, 3 without either.
 // One batch of the pipelined loop: tables and codes of batch bi+1 go out, batch bi (codes in
@@ -607,6 +877,14 @@ void launch_qa(const QArgs& a, hipStream_t st, uint32_t nc) {
   hipLaunchKernelGGL((fedavg_qsgd_arith_kernel<B, G, U, TWO>), dim3(nc), dim3(B), 0, st, a);
 }
 #endif
+template <int B, int U, bool TWO, int G, bool ABS>
+void launch_qs(const QArgs& a, hipStream_t st, uint32_t nc) {
+  hipLaunchKernelGGL((fedavg_qsgd_sp_kernel<B, U, TWO, G, ABS>), dim3(nc), dim3(B), 0, st, a);
+}
+template <int B, int U, bool TWO, int G, int P, bool FT>
+void launch_qm(const QArgs& a, hipStream_t st, uint32_t nc) {
+  hipLaunchKernelGGL((fedavg_qsgd_mp_kernel<B, U, TWO, G, P, FT>), dim3(nc), dim3(B), 0, st, a);
+}
 struct QVariant {
   int block, u, g;  // threads, clients per table batch, elements per lane
   QFn fn[2];        // [TWO]
@@ -638,6 +916,28 @@ const QVariant kQVariants[] = {
     {512, 8, 8, {&launch_q<512, 8, false, 8, true, true>, &launch_q<512, 8, true, 8, true, true>}},      // 15
     {256, 8, 16, {&launch_q<256, 8, false, 16, true, true>, &launch_q<256, 8, true, 16, true, true>}},   // 16
     {128, 8, 8, {&launch_q<128, 8, false, 8, true, true>, &launch_q<128, 8, true, 8, true, true>}},      // 17
+    // round 6: software-pipelined lookups, weights loaded with the codes ({block, U, G}; ABS as 13-17)
+    {256, 8, 8, {&launch_qs<256, 8, false, 8, false>, &launch_qs<256, 8, true, 8, false>}},     // 18
+    {256, 8, 8, {&launch_qs<256, 8, false, 8, true>, &launch_qs<256, 8, true, 8, true>}},       // 19
+    {256, 16, 8, {&launch_qs<256, 16, false, 8, false>, &launch_qs<256, 16, true, 8, false>}},  // 20
+    {256, 8, 16, {&launch_qs<256, 8, false, 16, false>, &launch_qs<256, 8, true, 16, false>}},  // 21
+    {512, 8, 8, {&launch_qs<512, 8, false, 8, false>, &launch_qs<512, 8, true, 8, false>}},     // 22
+    {128, 8, 8, {&launch_qs<128, 8, false, 8, false>, &launch_qs<128, 8, true, 8, false>}},     // 23
+    // round 6: kP element groups per lane per table batch, float64-product table decode ({block, U, G * P})
+    {256, 8, 8, {&launch_qm<256, 8, false, 8, 1, true>, &launch_qm<256, 8, true, 8, 1, true>}},    // 24: P 1, fast tables
+    {256, 8, 16, {&launch_qm<256, 8, false, 8, 2, true>, &launch_qm<256, 8, true, 8, 2, true>}},   // 25: P 2, fast tables
+    {256, 8, 16, {&launch_qm<256, 8, false, 8, 2, false>, &launch_qm<256, 8, true, 8, 2, false>}}, // 26: P 2, IEEE tables
+    {128, 8, 16, {&launch_qm<128, 8, false, 8, 2, true>, &launch_qm<128, 8, true, 8, 2, true>}},   // 27: P 2, 128 threads
+    {256, 8, 32, {&launch_qm<256, 8, false, 8, 4, true>, &launch_qm<256, 8, true, 8, 4, true>}},   // 28: P 4
+    {256, 4, 16, {&launch_qm<256, 4, false, 8, 2, true>, &launch_qm<256, 4, true, 8, 2, true>}},   // 29: P 2, U 4
+    {256, 4, 8, {&launch_qm<256, 4, false, 8, 1, true>, &launch_qm<256, 4, true, 8, 1, true>}},    // 30: P 1, U 4
+    {256, 4, 16, {&launch_qm<256, 4, false, 8, 2, false>, &launch_qm<256, 4, true, 8, 2, false>}}, // 31: P 2, U 4, IEEE
+    {256, 4, 32, {&launch_qm<256, 4, false, 8, 4, true>, &launch_qm<256, 4, true, 8, 4, true>}},   // 32: P 4, U 4
+    {256, 2, 16, {&launch_qm<256, 2, false, 8, 2, true>, &launch_qm<256, 2, true, 8, 2, true>}},   // 33: P 2, U 2
+    {512, 4, 16, {&launch_qm<512, 4, false, 8, 2, true>, &launch_qm<512, 4, true, 8, 2, true>}},   // 34: P 2, U 4, 512
+    {128, 4, 16, {&launch_qm<128, 4, false, 8, 2, true>, &launch_qm<128, 4, true, 8, 2, true>}},   // 35: P 2, U 4, 128
+    {256, 4, 24, {&launch_qm<256, 4, false, 8, 3, true>, &launch_qm<256, 4, true, 8, 3, true>}},   // 36: P 3, U 4
+    {256, 4, 16, {&launch_qm<256, 4, false, 4, 4, true>, &launch_qm<256, 4, true, 4, 4, true>}},   // 37: G 4 x P 4, U 4
 };
 #else  // libplato_agg.so: the default only
 // 256 threads: 0.309 against 0.320 ms for the round-4 512-thread form, interleaved (profiles/r05l_qsgd.log)

@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--fedadp-kernel", action="store_true",
                     help="HIP-event time of plato_agg_fedadp_dots alone (+ bitwise check against the flat path)")
     ap.add_argument("--fedadp-only", action="store_true", help="only the fedadp kernel timing (for PMC passes)")
+    ap.add_argument("--fedadp-variants", default=None, help="comma-separated fedadp_dots tuning variants to time (default all)")
     ap.add_argument("--port-only", action="store_true", help="only the port path (for kernel traces)")
     ap.add_argument("--fedadp-align", default="fedadp", help="arena alignment of the FedAdp rounds ('' = packed)")
     ap.add_argument("--only", default=None, help="comma-separated paths to time")
@@ -157,7 +158,8 @@ def main():
                           "min_bytes": int(nbytes), "GBps_of_min_bytes": round(nbytes / (med * 1e-3) / 1e9, 1),
                           "serial_chain_steps": int(chain), "what": what}), flush=True)
     if args.fedadp_kernel:
-        fedadp_kernel(dev, rnd_adp, slots, rnd_adp.layout, args.reps)
+        fedadp_kernel(dev, rnd_adp, slots, rnd_adp.layout, args.reps,
+                      None if not args.fedadp_variants else {int(v) for v in args.fedadp_variants.split(",")})
     if args.sdot:
         sdot_kernels(dev, k, n_f + n_i, args.reps)
     if args.port_norms:
@@ -170,7 +172,7 @@ def main():
         cosine_variants(dev, k, n_f + n_i, args.reps, args.threads or torch.get_num_threads())
 
 
-def fedadp_kernel(dev, rnd, slots, layout, reps):
+def fedadp_kernel(dev, rnd, slots, layout, reps, only=None):
     """plato_agg_fedadp_dots alone (HIP events on the launch stream), against the flatten + sdot_shared path."""
     from plato_amd import _lib
 
@@ -187,16 +189,35 @@ def fedadp_kernel(dev, rnd, slots, layout, reps):
     yy = torch.empty(k + 1, device=dev)
     h = torch.cuda.current_stream(dev).cuda_stream
 
-    runs = {"default": lambda: _lib.call("plato_agg_fedadp_dots", g_flat.data_ptr(), ptrs.data_ptr(),
-                                         ptrs.data_ptr() + 8 * k, k, eng._base.f32.data_ptr(),
-                                         eng._base.i64.data_ptr(), segs.data_ptr(), len(order), n_flat,
-                                         layout.n_f32, layout.n_i64, 0.01, 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(), h)}
+    # delta arenas for the delta variants (null baseline): every slot's x - b in a second slab
+    from plato_amd.engine import ClientSlab
+
+    dslab = ClientSlab(layout, k, dev)
+    for i, j in enumerate(slots):
+        _lib.call("plato_agg_compute_deltas", rnd._pf[j], rnd._pi[j], eng._base.f32.data_ptr(),
+                  eng._base.i64.data_ptr(), dslab.f32[i].data_ptr(), dslab.i64[i].data_ptr(), layout.n_f32,
+                  layout.n_i64, h)
+    dpf, dpi = dslab.row_pointers(range(k))
+    dptrs = torch.from_numpy(np.concatenate([dpf, dpi]).astype(np.int64)).to(dev)
+
+    def call(name, v, delta):
+        p = dptrs if delta else ptrs
+        base_f = None if delta else eng._base.f32.data_ptr()
+        base_i = None if delta else eng._base.i64.data_ptr()
+        args = (g_flat.data_ptr(), p.data_ptr(), p.data_ptr() + 8 * k, k, base_f, base_i, segs.data_ptr(),
+                len(order), n_flat, layout.n_f32, layout.n_i64, 0.01, 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(), h)
+        if v is None:
+            _lib.call(name, *args)
+        else:
+            _lib.tune_call(name, v, *args)
+
+    runs = {"default": lambda: call("plato_agg_fedadp_dots", None, False),
+            "default_delta": lambda: call("plato_agg_fedadp_dots", None, True)}
     for v in range(_lib.tune().plato_agg_tune_num_fedadp_variants()):
-        runs[f"v{v}"] = (lambda v=v: _lib.tune_call("plato_agg_tune_fedadp_dots", v, g_flat.data_ptr(), ptrs.data_ptr(),
-                                                    ptrs.data_ptr() + 8 * k, k, eng._base.f32.data_ptr(),
-                                                    eng._base.i64.data_ptr(), segs.data_ptr(), len(order), n_flat,
-                                                    layout.n_f32, layout.n_i64, 0.01, 1, ws.data_ptr(), xy.data_ptr(),
-                                                    yy.data_ptr(), h))
+        if only is not None and v not in only:
+            continue
+        delta = bool(_lib.tune().plato_agg_tune_fedadp_is_delta(v))
+        runs[f"v{v}{'_delta' if delta else ''}"] = (lambda v=v, d=delta: call("plato_agg_tune_fedadp_dots", v, d))
     # unique bytes: each client's fp32 arena + int64 counters once, the baseline and g_flat once
     uniq = k * (layout.n_f32 * 4 + layout.n_i64 * 8) + 2 * layout.n_f32 * 4 + n_flat * 4
     oks = {}
