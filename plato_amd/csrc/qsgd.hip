@@ -42,11 +42,12 @@ typedef __attribute__((address_space(1))) const u1 gu1;
 // Kernel shape (tuning space, plato_agg_tune_fedavg_qsgd): B threads per
 // workgroup share each batch's decode tables, U clients per table batch, G
 // elements per lane (one 16/8/4-byte code load per client).  The default
-// (variant 0) is the plain form (two barriers per table batch) at B = 512, U = 8, G = 8 (4,096-element
-// chunks) with max_v by scalar loads and each batch's codes issued before its table build: 0.306 ms
-// interleaved on one box against 0.333 for the round-1 plain form (B = 1,024, vector max_v loads,
-// codes after the barrier; variant 5) and 0.373 for the pipelined form of rounds 2-3 (variant 1);
-// DESIGN.md §11, §14.
+// (round 6, tuning variant 29) is the plain form (two barriers per table batch) at B = 256, U = 4 and
+// two 8-element groups per lane (4,096-element chunks), tables built with the float64 reciprocal
+// product, max_v by scalar loads and each batch's codes issued before its table build: 0.290 ms
+// interleaved on one box against 0.308 for the round-5 default (B = 256, U = 8, one group; variant 0),
+// 0.333 for the round-1 plain form (variant 5) and 0.373 for the pipelined form of rounds 2-3
+// (variant 1); DESIGN.md §11, §14, §15.
 constexpr int kG = 16;      // elements per lane group of the plain kernel's template default
 
 template <class T>
@@ -584,6 +585,142 @@ __device__ void qsgd_f32_chunk_mp(const QArgs& a, uint32_t c, float (*lut)[256])
   }
 }
 
+// kP element groups per lane with the next batch's codes in flight (round 6): the codes of batch i0 + kU
+// are issued right after batch i0's table barrier, so their HBM latency runs under batch i0's lookups and
+// batch i0 + kU's table build instead of stalling every wave after its own table build.  Two register
+// sets of codes alternate by batch (a copy would wait for the loads).
+template <int kBlock, int kU, bool TWO, int kG, int kP, bool kFastTab>
+__device__ __forceinline__ void mpf_batch(const QArgs& a, const float* mrow, int i0, double inv_div,
+                                          const bool (&full)[kP], const bool (&have)[kP], const uint64_t (&e0)[kP],
+                                          const Chunk& ch, const CodeOf<kG> (&cur)[kP][kU],
+                                          CodeOf<kG> (&nxt)[kP][kU], float (*lut)[256], const float (&b)[kP][kG],
+                                          float (&acc)[kP][kG]) {
+  const int K = a.K;
+  const int nu = K - i0 < kU ? K - i0 : kU;
+  __syncthreads();  // previous batch's lookups are done
+  float wu[kU], su[kU];
+  load_weights<kU, TWO>(a, i0, wu, su);
+  for (int t = threadIdx.x; t < kU * 128; t += kBlock) {
+    const int u = __builtin_amdgcn_readfirstlane(t >> 7), z = t & 127;  // wave-uniform: scalar max_v
+    if (u < nu) {
+      const float mv = sld(mrow, i0 + u);
+      const float v = kFastTab ? decode_tab(uint32_t(z), mv, inv_div) : decode(uint32_t(z), mv, a.divisor);
+      lut[u][z] = v;
+      lut[u][z + 128] = z ? -v : v;
+    }
+  }
+  __syncthreads();
+  if (i0 + kU < K) {
+#pragma unroll
+    for (int p = 0; p < kP; ++p)
+      if (full[p]) load_codes<kU, kG>(a, i0 + kU, K, e0[p], nxt[p]);
+  }
+#pragma unroll
+  for (int p = 0; p < kP; ++p) {
+    if (full[p]) {
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        if (u < nu) {
+#pragma unroll
+          for (int q = 0; q < kG; ++q) {
+            const uint32_t word = cur[p][u][q >> 2];
+            const float x = lut[u][(word >> (8 * (q & 3))) & 255u];
+            acc[p][q] = acc[p][q] + term(x, b[p][q], wu[u], su[u], TWO);
+          }
+        }
+      }
+    } else if (have[p]) {
+      for (int u = 0; u < nu; ++u) {
+        const uint8_t* ptr = sld(a.cf, i0 + u);
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+          const uint64_t e = e0[p] + q;
+          if (e >= ch.begin && e < ch.end) acc[p][q] = acc[p][q] + term(lut[u][ptr[e]], b[p][q], wu[u], su[u], TWO);
+        }
+      }
+    }
+  }
+}
+
+template <int kBlock, int kU, bool TWO, int kG, int kP, bool kFastTab>
+__device__ void qsgd_f32_chunk_mpf(const QArgs& a, uint32_t c, float (*lut)[256]) {
+  static_assert(kG == 16 || kG == 8 || kG == 4, "one 16-, 8- or 4-byte code load per lane");
+  const Chunk ch = load_chunk(a.tf, c, a.n_f32);
+  const float* mrow = a.mv + uint64_t(ch.entry) * a.K;
+  const uint64_t g0 = ch.begin / kG, g1 = (uint64_t(ch.end) + kG - 1) / kG;
+  const int K = a.K;
+  const double inv_div = 1.0 / double(a.divisor);
+  for (uint64_t gp = g0; gp < g1; gp += uint64_t(kBlock) * kP) {
+    uint64_t e0[kP];
+    bool have[kP], full[kP];
+    float b[kP][kG], acc[kP][kG];
+    CodeOf<kG> ca[kP][kU], cb[kP][kU];
+#pragma unroll
+    for (int p = 0; p < kP; ++p) {
+      const uint64_t g = gp + uint64_t(p) * kBlock + threadIdx.x;
+      have[p] = g < g1;
+      e0[p] = g * kG;
+      full[p] = have[p] && e0[p] >= ch.begin && e0[p] + kG <= ch.end;
+      if (full[p]) load_codes<kU, kG>(a, 0, K, e0[p], ca[p]);  // batch 0's codes, ahead of the baseline
+#pragma unroll
+      for (int q = 0; q < kG; ++q) {
+        acc[p][q] = 0.f;
+        b[p][q] = 0.f;
+      }
+      if (full[p]) {
+#pragma unroll
+        for (int q = 0; q < kG / 4; ++q) {
+          const f4 v = *((gf4*)(a.base_f + e0[p]) + q);
+          b[p][4 * q] = v.x;
+          b[p][4 * q + 1] = v.y;
+          b[p][4 * q + 2] = v.z;
+          b[p][4 * q + 3] = v.w;
+        }
+      } else if (have[p]) {
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+          const uint64_t e = e0[p] + q;
+          if (e >= ch.begin && e < ch.end) b[p][q] = a.base_f[e];
+        }
+      }
+    }
+    for (int i0 = 0; i0 < K; i0 += 2 * kU) {
+      mpf_batch<kBlock, kU, TWO, kG, kP, kFastTab>(a, mrow, i0, inv_div, full, have, e0, ch, ca, cb, lut, b, acc);
+      if (i0 + kU < K)
+        mpf_batch<kBlock, kU, TWO, kG, kP, kFastTab>(a, mrow, i0 + kU, inv_div, full, have, e0, ch, cb, ca, lut, b,
+                                                     acc);
+    }
+#pragma unroll
+    for (int p = 0; p < kP; ++p) {
+      if (full[p]) {
+#pragma unroll
+        for (int q = 0; q < kG / 4; ++q) {
+          const f4 v = f4{b[p][4 * q] + acc[p][4 * q], b[p][4 * q + 1] + acc[p][4 * q + 1],
+                          b[p][4 * q + 2] + acc[p][4 * q + 2], b[p][4 * q + 3] + acc[p][4 * q + 3]};
+          __builtin_nontemporal_store(v, (gf4w*)(a.out_f + e0[p]) + q);
+        }
+      } else if (have[p]) {
+#pragma unroll
+        for (int q = 0; q < kG; ++q) {
+          const uint64_t e = e0[p] + q;
+          if (e >= ch.begin && e < ch.end) a.out_f[e] = b[p][q] + acc[p][q];
+        }
+      }
+    }
+  }
+}
+
+template <int kBlock, int kU, bool TWO, int kG, int kP, bool kFastTab>
+__global__ __launch_bounds__(kBlock) void fedavg_qsgd_mpf_kernel(QArgs a) {
+  __shared__ float lut[kU][256];
+  const uint32_t c = blockIdx.x;  // the int64 chunks first (qsgd_i64_chunk)
+  if (c >= a.nci) {
+    qsgd_f32_chunk_mpf<kBlock, kU, TWO, kG, kP, kFastTab>(a, c - a.nci, lut);
+  } else {
+    qsgd_i64_chunk<kBlock, TWO>(a, c);
+  }
+}
+
 template <int kBlock, int kU, bool TWO, int kG, int kP, bool kFastTab>
 __global__ __launch_bounds__(kBlock) void fedavg_qsgd_mp_kernel(QArgs a) {
   __shared__ float lut[kU][256];
@@ -885,6 +1022,10 @@ template <int B, int U, bool TWO, int G, int P, bool FT>
 void launch_qm(const QArgs& a, hipStream_t st, uint32_t nc) {
   hipLaunchKernelGGL((fedavg_qsgd_mp_kernel<B, U, TWO, G, P, FT>), dim3(nc), dim3(B), 0, st, a);
 }
+template <int B, int U, bool TWO, int G, int P, bool FT>
+void launch_qf(const QArgs& a, hipStream_t st, uint32_t nc) {
+  hipLaunchKernelGGL((fedavg_qsgd_mpf_kernel<B, U, TWO, G, P, FT>), dim3(nc), dim3(B), 0, st, a);
+}
 struct QVariant {
   int block, u, g;  // threads, clients per table batch, elements per lane
   QFn fn[2];        // [TWO]
@@ -896,7 +1037,7 @@ struct QVariant {
 // form of rounds 2-3 and its timing probes.
 #ifdef PLATO_AGG_TUNE  // libplato_agg_tune.so (scripts/bench_variants.py, tests/test_qsgd_gpu.py)
 const QVariant kQVariants[] = {
-    {256, 8, 8, {&launch_q<256, 8, false, 8, true>, &launch_q<256, 8, true, 8, true>}},  // 0 (default, round 5)
+    {256, 8, 8, {&launch_q<256, 8, false, 8, true>, &launch_q<256, 8, true, 8, true>}},  // 0 (round-5 default)
     {512, 4, 8, {&launch_qp<512, 4, false, 8>, &launch_qp<512, 4, true, 8>}},        // 1: pipelined (rounds 2-3)
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 1>, &launch_qp<512, 4, true, 8, 1>}},  // 2: probe, no code loads
     {512, 4, 8, {&launch_qp<512, 4, false, 8, 2>, &launch_qp<512, 4, true, 8, 2>}},  // 3: probe, no lookups
@@ -929,7 +1070,7 @@ const QVariant kQVariants[] = {
     {256, 8, 16, {&launch_qm<256, 8, false, 8, 2, false>, &launch_qm<256, 8, true, 8, 2, false>}}, // 26: P 2, IEEE tables
     {128, 8, 16, {&launch_qm<128, 8, false, 8, 2, true>, &launch_qm<128, 8, true, 8, 2, true>}},   // 27: P 2, 128 threads
     {256, 8, 32, {&launch_qm<256, 8, false, 8, 4, true>, &launch_qm<256, 8, true, 8, 4, true>}},   // 28: P 4
-    {256, 4, 16, {&launch_qm<256, 4, false, 8, 2, true>, &launch_qm<256, 4, true, 8, 2, true>}},   // 29: P 2, U 4
+    {256, 4, 16, {&launch_qm<256, 4, false, 8, 2, true>, &launch_qm<256, 4, true, 8, 2, true>}},   // 29: P 2, U 4 (default)
     {256, 4, 8, {&launch_qm<256, 4, false, 8, 1, true>, &launch_qm<256, 4, true, 8, 1, true>}},    // 30: P 1, U 4
     {256, 4, 16, {&launch_qm<256, 4, false, 8, 2, false>, &launch_qm<256, 4, true, 8, 2, false>}}, // 31: P 2, U 4, IEEE
     {256, 4, 32, {&launch_qm<256, 4, false, 8, 4, true>, &launch_qm<256, 4, true, 8, 4, true>}},   // 32: P 4, U 4
@@ -938,11 +1079,19 @@ const QVariant kQVariants[] = {
     {128, 4, 16, {&launch_qm<128, 4, false, 8, 2, true>, &launch_qm<128, 4, true, 8, 2, true>}},   // 35: P 2, U 4, 128
     {256, 4, 24, {&launch_qm<256, 4, false, 8, 3, true>, &launch_qm<256, 4, true, 8, 3, true>}},   // 36: P 3, U 4
     {256, 4, 16, {&launch_qm<256, 4, false, 4, 4, true>, &launch_qm<256, 4, true, 4, 4, true>}},   // 37: G 4 x P 4, U 4
+    // round 6: as 24-37 with the next batch's codes in flight during the current batch ({block, U, G * P})
+    {256, 4, 16, {&launch_qf<256, 4, false, 8, 2, true>, &launch_qf<256, 4, true, 8, 2, true>}},   // 38: P 2, U 4
+    {256, 8, 16, {&launch_qf<256, 8, false, 8, 2, true>, &launch_qf<256, 8, true, 8, 2, true>}},   // 39: P 2, U 8
+    {256, 4, 8, {&launch_qf<256, 4, false, 8, 1, true>, &launch_qf<256, 4, true, 8, 1, true>}},    // 40: P 1, U 4
+    {256, 2, 16, {&launch_qf<256, 2, false, 8, 2, true>, &launch_qf<256, 2, true, 8, 2, true>}},   // 41: P 2, U 2
+    {512, 4, 16, {&launch_qf<512, 4, false, 8, 2, true>, &launch_qf<512, 4, true, 8, 2, true>}},   // 42: P 2, U 4, 512
 };
 #else  // libplato_agg.so: the default only
-// 256 threads: 0.309 against 0.320 ms for the round-4 512-thread form, interleaved (profiles/r05l_qsgd.log)
+// = tuning variant 29 (round 6): two 8-element groups per lane per table batch of 4 clients, tables by
+// the float64 reciprocal product: 0.290 against 0.308 ms for the round-5 default (tuning variant 0),
+// interleaved on one box (profiles/r06g_qsgd_variants.log)
 const QVariant kQVariants[] = {
-    {256, 8, 8, {&launch_q<256, 8, false, 8, true>, &launch_q<256, 8, true, 8, true>}},  // 0 (default)
+    {256, 4, 16, {&launch_qm<256, 4, false, 8, 2, true>, &launch_qm<256, 4, true, 8, 2, true>}},  // 0 (default)
 };
 #endif
 constexpr int kNumQVariants = sizeof(kQVariants) / sizeof(kQVariants[0]);

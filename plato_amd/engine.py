@@ -225,7 +225,7 @@ class FedAvgEngine:
 
     # per-entry kernels: chunk capacity (elements) per workgroup
     STATS_CHUNK = 4096      # entry_stats: 256 lanes x 4 float4 groups
-    QSGD_CHUNK = 2048       # fedavg_qsgd: 256 lanes x 8 one-byte codes (plato_agg_tune_qsgd_chunk(0))
+    QSGD_CHUNK = 4096       # fedavg_qsgd: 256 lanes x 2 x 8 one-byte codes (plato_agg_tune_qsgd_chunk(29))
     ENTRYWISE_CHUNK = 256  # fedavg_entrywise: 64 lanes x 1 float4 group (round 5: 0.891 vs 0.917 ms for 256 x 2, r05i_entrywise.log)
 
     def _chunks(self, layout: ArenaLayout, cap: int):

@@ -75,7 +75,7 @@ SPEC = [("a", (3,), "f32"), ("n0", (), "i64"), ("b", (17,), "f32"), ("c", (5, 7)
 # the product default (libplato_agg.so) and the tuning library's FedAvg shapes: 0 the default's plain
 # form, 1 the pipelined form of rounds 2-3, 5 the round-1 plain form, 6 a 256-thread shape; 2-4 are
 # timing probes (not the FedAvg)
-@pytest.mark.parametrize("variant", [None, 0, 1, 5, 6, 7, 13, 18, 24, 25, 29, 31, 32, 33, 36, 37])
+@pytest.mark.parametrize("variant", [None, 0, 1, 5, 6, 7, 13, 18, 24, 25, 29, 31, 32, 33, 36, 37, 38, 39, 40, 41, 42])
 @pytest.mark.parametrize("cap,k,two", [(8, 3, False), (20, 9, True), (4096, 17, False), (64, 16, True), (1 << 20, 5, False)])
 def test_qsgd_kernel_matches_oracle(engine, monkeypatch, cap, k, two, variant):
     """Chunk pieces of every alignment (caps 8/20: partial 16-byte groups everywhere;
