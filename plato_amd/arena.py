@@ -102,6 +102,25 @@ class ArenaLayout:
         """fp32 entries back to back (no alignment padding)."""
         return self.n_f32 == self.n_f32_data
 
+    def f32_padding(self, device) -> torch.Tensor | None:
+        """Bool mask over the fp32 region, True at alignment padding (None for a packed region).
+
+        The padding of a staged arena holds whatever its host staging buffer held there (the
+        packer writes entries only), so two stagings of one model agree on the entries alone.
+        """
+        if self.packed:
+            return None
+        key = ("f32_padding", str(device))
+        mask = self._cache.get(key)
+        if mask is None:
+            mask = torch.ones(self.n_f32, dtype=torch.bool)
+            for e in self.entries:
+                if e.region == F32:
+                    mask[e.offset:e.offset + e.numel] = False
+            mask = self._cache[key] = mask.to(device)
+        return mask
+
+
     # ------------------------------------------------------------------ build
     @classmethod
     def _build(cls, items, align: str | None) -> "ArenaLayout":
@@ -280,3 +299,11 @@ class ArenaLayout:
 
 def _round_up(x: int, m: int) -> int:
     return (x + m - 1) // m * m
+
+
+def same_f32_bits(a: torch.Tensor, b: torch.Tensor, padding: torch.Tensor | None) -> bool:
+    """Whether two fp32 arena regions (device tensors of one length) hold the same bits outside ``padding``."""
+    a, b = a.view(torch.int32), b.view(torch.int32)
+    if padding is None:
+        return torch.equal(a, b)
+    return not bool(torch.any((a != b) & ~padding))

@@ -29,7 +29,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .arena import CODECS, F32, I64, ArenaLayout, fedadp_order, payload_codec
+from .arena import CODECS, F32, I64, ArenaLayout, fedadp_order, payload_codec, same_f32_bits
 from .staging import HostPacker, PinnedRing, ResultPool, arena_source, baseline_key, payload_fingerprint
 
 
@@ -766,12 +766,12 @@ class AggregationRound:
         if ok is None:
             eng, lay = self.engine, self.layout
             arr = getattr(eng, "_arrival_base", None)
-            if arr is None or eng._arrival_base_layout is not lay:
+            if arr is None or eng._arrival_base_layout.signature != lay.signature:
                 ok = False
             else:
                 stream = torch.cuda.current_stream(eng.device)
                 stream.wait_stream(eng._copy_stream)
-                ok = (torch.equal(self._base.f32[: lay.n_f32].view(torch.int32), arr.f32[: lay.n_f32].view(torch.int32))
+                ok = (same_f32_bits(self._base.f32[: lay.n_f32], arr.f32[: lay.n_f32], lay.f32_padding(eng.device))
                       and torch.equal(self._base.i64[: lay.n_i64], arr.i64[: lay.n_i64]))
             self._arrival_base_ok = ok
         return ok

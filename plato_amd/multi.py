@@ -48,7 +48,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from .arena import CODECS, ArenaLayout, payload_codec
+from .arena import CODECS, ArenaLayout, payload_codec, same_f32_bits
 from .distributed import BucketPlan, EntryPlan
 from .engine import FedAvgEngine, fp32_weights, require_device
 from .staging import HostPacker, PinnedRing, ResultPool, arena_source, baseline_key, payload_fingerprint
@@ -113,11 +113,14 @@ class _Shard:
                   _ptr(row_f) if self.n else None, _ptr(row_i) if self.ni else None, self.n, self.ni,
                   self.copy_stream.cuda_stream)
 
-    def same_bits(self, a_f: torch.Tensor, a_i: torch.Tensor, b_f: torch.Tensor, b_i: torch.Tensor) -> bool:
-        """Whether two copies of this bucket hold the same bits (after this shard's copy stream)."""
+    def same_bits(self, a_f: torch.Tensor, a_i: torch.Tensor, b_f: torch.Tensor, b_i: torch.Tensor,
+                  layout: ArenaLayout | None = None) -> bool:
+        """Whether two copies of this bucket hold the same bits (after this shard's copy stream); with the
+        full model's ``layout``, outside its alignment padding (ArenaLayout.f32_padding)."""
         with torch.cuda.device(self.device):
             torch.cuda.current_stream(self.device).wait_stream(self.copy_stream)
-            return (torch.equal(a_f[: self.n].view(torch.int32), b_f[: self.n].view(torch.int32))
+            pad = None if layout is None else layout.f32_padding(self.device)
+            return (same_f32_bits(a_f[: self.n], b_f[: self.n], None if pad is None else pad[self.lo:self.hi])
                     and torch.equal(a_i[: self.ni], b_i[: self.ni]))
 
     def copy_in(self, host_f: torch.Tensor, host_i: torch.Tensor, dst_f: torch.Tensor, dst_i: torch.Tensor):
@@ -363,7 +366,8 @@ class MultiDeviceEngine:
 
     def _arrival_base_matches(self, shards_base) -> bool:
         """The round's staged baseline (``[(base_f, base_i)]`` per shard) has the arrival baseline's bits."""
-        return all(s.same_bits(bf, bi, *s.arrival_base()) for s, (bf, bi) in zip(self._shards, shards_base))
+        return all(s.same_bits(bf, bi, *s.arrival_base(), layout=self._layout)
+                   for s, (bf, bi) in zip(self._shards, shards_base))
 
     def _arrival_rows(self, payload, layout: ArenaLayout, codec: str):
         hit = self._arrivals.get(id(payload))

@@ -67,3 +67,28 @@ def test_from_state_dict_alignment_matches_from_shapes():
     assert [(e.name, e.offset) for e in a.entries] == [(e.name, e.offset) for e in b.entries]
     with pytest.raises(ValueError):
         ArenaLayout.from_shapes(spec, align="sideways")
+
+
+def test_padding_mask_ignores_only_alignment_padding():
+    """Two stagings of one model agree on the entries; their padding may hold different host bytes
+    (AggregationRound._arrival_base_matches compares the arrival baseline with the round's outside it)."""
+    from collections import OrderedDict
+
+    from plato_amd.arena import same_f32_bits
+
+    sd = OrderedDict([("w", torch.zeros(50)), ("n", torch.zeros(4, dtype=torch.int64)), ("b", torch.zeros(70)),
+                      ("c", torch.zeros(33))])
+    assert ArenaLayout.from_state_dict(sd).f32_padding("cpu") is None  # packed: nothing to mask
+    lay = ArenaLayout.from_state_dict(sd, align="fedadp")
+    pad = lay.f32_padding("cpu")
+    assert int((~pad).sum()) == lay.n_f32_data and pad.numel() == lay.n_f32
+    a = torch.randn(lay.n_f32)
+    b = a.clone()
+    b[pad] = 123.0
+    assert same_f32_bits(a, b, pad) and not same_f32_bits(a, b, None)
+    for name in ("w", "b", "c"):
+        e = lay._by_name[name]
+        for at in (e.offset, e.offset + e.numel - 1):
+            c = b.clone()
+            c[at] = -c[at] if c[at] != 0 else 1.0
+            assert not same_f32_bits(a, c, pad)
