@@ -93,6 +93,7 @@ struct AdpArgs {
   uint32_t* n_bnd;               // number of boundary rows
   uint32_t* cnt;                 // [ceil(2 ngroups / 256)]: boundary groups per descriptor block
   float* bnd;                    // [n_pairs][max_bnd][256]: process_grad's values of the boundary groups
+  uint32_t* bsrc;                // [max_bnd][256]: the source word of each boundary value (fedadp_bndsrc_kernel)
   uint32_t n_segs;
   uint32_t ngroups;              // 8-block groups: ceil(nsteps / 8)
   uint32_t max_bnd;              // >= boundary groups (adp_max_bnd)
@@ -442,10 +443,18 @@ __global__ __launch_bounds__(256) void fedadp_rows_kernel(AdpArgs a) {
 
 // The boundary table: process_grad's values of every boundary group of every pair, in the lane
 // order of the stream (index u * 32 + v: block 8 group + u, position cg * 32 + v); 0 past the
-// last whole block
-// One row of the boundary table for pair blockIdx.y (the body of the round-5 one-row-per-workgroup kernel).
-__device__ __forceinline__ void fedadp_boundary_row(const AdpArgs& a, uint32_t row) {
-  const int pair = int(blockIdx.y);
+// last whole block.  Two launches: the positions' sources depend on the layout only, so one
+// workgroup per boundary row finds them once (segment search and walk) and packs each into a
+// word; the per-pair launch then costs one source word and one client load per value, R rows per
+// workgroup with their loads in flight together.  (Round 5 ran the search per (row, pair), one row
+// per workgroup: 25 us for ResNet-18 at K = 128; walking the rows with 16 workgroups per pair made
+// the searches serial, 49 us, profiles/r06l_kernel_stats.csv.)
+// Source word: the arena element (bits 0-29; both regions are < 2^30 elements, run_fedadp), bit 30
+// the int64 region, bit 31 the division by -lr; kBndNone past the last whole block.
+constexpr uint32_t kBndI64 = 1u << 30, kBndNeg = 1u << 31, kBndNone = 0xffffffffu;
+__global__ __launch_bounds__(256) void fedadp_bndsrc_kernel(AdpArgs a) {
+  const uint32_t row = blockIdx.x;
+  if (row >= min(*a.n_bnd, a.max_bnd)) return;
   const uint32_t j = a.bnd_at[row];
   const uint32_t cg = j / a.ngroups, grp = j % a.ngroups;
   const uint32_t u = threadIdx.x / 32, v = threadIdx.x % 32;
@@ -455,25 +464,42 @@ __device__ __forceinline__ void fedadp_boundary_row(const AdpArgs& a, uint32_t r
   __shared__ uint32_t first;
   if (threadIdx.x == 0) first = adp_find(a.segs, a.n_segs, uint64_t(grp) * 512 + cg * 32);
   __syncthreads();
-  float val = 0.f;
+  uint32_t word = kBndNone;
   if (s < a.nsteps) {
     const uint64_t p = s * 64 + cg * 32 + v;
     uint32_t idx = first;
     while (idx + 1 < a.n_segs && a.segs[idx + 1].flat_offset <= p) ++idx;
-    val = adp_y_in(a, pair, p, idx);
+    const plato_agg_segment sg = a.segs[idx];
+    word = uint32_t(sg.src_offset + (p - sg.flat_offset)) | (sg.region ? kBndI64 : 0u) |
+           ((sg.flags & PLATO_AGG_SEG_NEG_DIV) ? kBndNeg : 0u);
   }
-  a.bnd[(uint64_t(pair) * a.max_bnd + row) * 256 + threadIdx.x] = val;
+  a.bsrc[uint64_t(row) * 256 + threadIdx.x] = word;
 }
 
-// Rows are walked with a stride of gridDim.x (kBndRowGroups workgroups per pair): the row count is
-// known on the device only, and one workgroup per possible row (max_bnd of them, most returning at
-// once) cost ~25 us of launch for ResNet-18 (profiles/r06f_variant_legs_kernel_stats.csv).
-constexpr uint32_t kBndRowGroups = 16;
+constexpr uint32_t kBndRows = 4;  // boundary rows per workgroup of the per-pair launch
 __global__ __launch_bounds__(256) void fedadp_boundary_kernel(AdpArgs a) {
+  const int pair = int(blockIdx.y);
   const uint32_t nrows = min(*a.n_bnd, a.max_bnd);
-  for (uint32_t row = blockIdx.x; row < nrows; row += gridDim.x) {
-    if (row != blockIdx.x) __syncthreads();  // the previous row's shared segment index is consumed
-    fedadp_boundary_row(a, row);
+  const uint32_t row0 = blockIdx.x * kBndRows;
+  if (row0 >= nrows) return;
+  const float* xf = sld(a.xf, pair);
+  const int64_t* xi = sld(a.xi, pair);
+  uint32_t word[kBndRows];
+#pragma unroll
+  for (uint32_t r = 0; r < kBndRows; ++r)
+    word[r] = row0 + r < nrows ? a.bsrc[uint64_t(row0 + r) * 256 + threadIdx.x] : kBndNone;
+#pragma unroll
+  for (uint32_t r = 0; r < kBndRows; ++r) {
+    if (row0 + r >= nrows) break;
+    float val = 0.f;
+    const uint32_t w = word[r];
+    if (w != kBndNone) {
+      const uint32_t e = w & (kBndI64 - 1u);
+      const bool neg = (w & kBndNeg) != 0;
+      val = (w & kBndI64) ? adp_i64(xi[e], a.base_i ? a.base_i[e] : int64_t(0), neg, a.lr)
+                          : adp_f32(xf[e], a.base_f ? a.base_f[e] : 0.f, neg, a.lr);
+    }
+    a.bnd[(uint64_t(pair) * a.max_bnd + row0 + r) * 256 + threadIdx.x] = val;
   }
 }
 
@@ -622,7 +648,7 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
                uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
                float* d_out_xy, float* d_out_yy, hipStream_t stream);
 
-// workspace: [chain sums][descriptors][boundary rows + count][block counts][boundary table][xb],
+// workspace: [chain sums][descriptors][boundary rows + count][block counts][boundary table][xb][boundary sources],
 // 256-byte aligned parts
 size_t align256(size_t v) { return (v + 255) / 256 * 256; }
 // Boundary groups per chain group: one ends at (and so holds) each segment start — at most n_segs
@@ -630,7 +656,7 @@ size_t align256(size_t v) { return (v + 255) / 256 * 256; }
 // int64 positions: at most n_i64 / 256
 size_t adp_max_bnd(uint32_t n_segs, size_t n_i64) { return 2 * (size_t(n_segs) + n_i64 / 256 + 1); }
 struct AdpWs {
-  size_t chains, desc, bnd_at, cnt, bnd, xb, total;
+  size_t chains, desc, bnd_at, cnt, bnd, xb, bsrc, total;
 };
 AdpWs adp_ws(int n_pairs, int with_xx, size_t n_i64, size_t n_flat, uint32_t n_segs) {
   const size_t k = size_t(n_pairs > 0 ? n_pairs : 0);
@@ -643,7 +669,8 @@ AdpWs adp_ws(int n_pairs, int with_xx, size_t n_i64, size_t n_flat, uint32_t n_s
   w.cnt = align256(w.bnd_at + (max_bnd + 1) * sizeof(uint32_t));
   w.bnd = align256(w.cnt + (2 * ngroups + 255) / 256 * sizeof(uint32_t));
   w.xb = align256(w.bnd + k * max_bnd * 256 * sizeof(float));
-  w.total = w.xb + 2 * ngroups * 512 * sizeof(float);
+  w.bsrc = align256(w.xb + 2 * ngroups * 512 * sizeof(float));
+  w.total = w.bsrc + max_bnd * 256 * sizeof(uint32_t);
   return w;
 }
 
@@ -737,6 +764,7 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
   a.cnt = reinterpret_cast<uint32_t*>(ws + w.cnt);
   a.bnd = reinterpret_cast<float*>(ws + w.bnd);
   a.xb = reinterpret_cast<const float*>(ws + w.xb);
+  a.bsrc = reinterpret_cast<uint32_t*>(ws + w.bsrc);
   a.n_i64 = n_i64;
   a.n_f32 = n_f32;
   a.n_pairs = n_pairs;
@@ -746,8 +774,10 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
     if (int rc = check_launch("fedadp_desc launch")) return rc;
     hipLaunchKernelGGL(fedadp_rows_kernel, dim3((2 * a.ngroups + 255) / 256), dim3(256), 0, stream, a);
     if (int rc = check_launch("fedadp_rows launch")) return rc;
-    hipLaunchKernelGGL(fedadp_boundary_kernel, dim3(std::min(a.max_bnd, kBndRowGroups), uint32_t(n_pairs)), dim3(256), 0,
-                       stream, a);
+    hipLaunchKernelGGL(fedadp_bndsrc_kernel, dim3(a.max_bnd), dim3(256), 0, stream, a);
+    if (int rc = check_launch("fedadp_bndsrc launch")) return rc;
+    hipLaunchKernelGGL(fedadp_boundary_kernel, dim3((a.max_bnd + kBndRows - 1) / kBndRows, uint32_t(n_pairs)),
+                       dim3(256), 0, stream, a);
     if (int rc = check_launch("fedadp_boundary launch")) return rc;
     if (fn.uses_xb) {
       hipLaunchKernelGGL(fedadp_prep_kernel, dim3(uint32_t((a.nsteps * 64 + kPrepSpan - 1) / kPrepSpan)), dim3(256), 0,
