@@ -76,7 +76,7 @@
 extern "C" {
 #endif
 
-#define PLATO_AGG_ABI_VERSION 3
+#define PLATO_AGG_ABI_VERSION 4
 
 #define PLATO_AGG_OK 0
 #define PLATO_AGG_EINVAL (-1)   /* bad argument (null, misaligned, K <= 0) */
@@ -428,6 +428,23 @@ int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const 
                           const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
                           uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
                           float* d_out_xy, float* d_out_yy, hipStream_t stream);
+
+/*
+ * plato_agg_fedadp_dots with flags (ABI 4).  PLATO_AGG_FEDADP_TABLES_READY: d_workspace
+ * already holds the layout-only tables (per-group descriptors, boundary rows and their
+ * source positions) of an earlier call with the same d_segs contents, n_segs, n_flat,
+ * n_i64, n_pairs and with_xx, completed on or ordered before `stream`; they depend on
+ * the segment map only, so a server whose layout is unchanged between rounds builds
+ * them once (replaces nothing in the reference: the same dots as plato_agg_fedadp_dots,
+ * examples/server_aggregation/fedadp/fedadp_server.py:91-99).  flags = 0 is
+ * plato_agg_fedadp_dots.
+ */
+#define PLATO_AGG_FEDADP_TABLES_READY 1
+int plato_agg_fedadp_dots_ex(const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64,
+                             int n_pairs, const float* d_base_f32, const int64_t* d_base_i64,
+                             const plato_agg_segment* d_segs, uint32_t n_segs, size_t n_flat, size_t n_f32,
+                             size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy, float* d_out_yy,
+                             hipStream_t stream, int flags);
 
 /*
  * Port's vector norms gathered from the arenas (replaces the flatten + norm of

@@ -14,7 +14,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libplato_agg.so")
 TUNE_LIB_PATH = os.path.join(_HERE, "libplato_agg_tune.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 PLATO_AGG_OK = 0
 PLATO_AGG_EINVAL = -1
@@ -26,6 +26,7 @@ PLATO_AGG_FLAT_CAST_DIFF = 1
 PLATO_AGG_FLAT_RAW = 2
 PLATO_AGG_PORT_CAST_FIRST = 1
 PLATO_AGG_SEG_NEG_DIV = 1
+PLATO_AGG_FEDADP_TABLES_READY = 1
 PLATO_AGG_DECODE = {"native": 0, "bf16": 1, "qsgd": 2}
 
 _c_void_p = ctypes.c_void_p
@@ -132,6 +133,10 @@ SIGNATURES = {
         _c_int,
         [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,
          _c_size_t, _c_size_t, _c_float, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p]),
+    "plato_agg_fedadp_dots_ex": (
+        _c_int,
+        [_c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,
+         _c_size_t, _c_size_t, _c_float, _c_int, _c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int]),
     "plato_agg_port_norms": (
         _c_int,
         [_c_void_p, _c_void_p, _c_void_p, _c_void_p, _c_int, _c_void_p, _c_void_p, ctypes.c_uint32, _c_size_t,

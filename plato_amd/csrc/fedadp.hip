@@ -646,7 +646,7 @@ constexpr int kAdpProbes[] = {7, 8};
 int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64,
                int n_pairs, const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
                uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
-               float* d_out_xy, float* d_out_yy, hipStream_t stream);
+               float* d_out_xy, float* d_out_yy, hipStream_t stream, int flags);
 
 // workspace: [chain sums][descriptors][boundary rows + count][block counts][boundary table][xb][boundary sources],
 // 256-byte aligned parts
@@ -688,7 +688,18 @@ int plato_agg_fedadp_dots(const float* d_x, const void* const* d_src_f32, const 
                           float* d_out_xy, float* d_out_yy, hipStream_t stream) {
   return run_fedadp(d_base_f32 ? kAdpDefault : kAdpDefaultDelta, d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32,
                     d_base_i64, d_segs, n_segs, n_flat, n_f32, n_i64, lr, with_xx, d_workspace, d_out_xy, d_out_yy,
-                    stream);
+                    stream, 0);
+}
+
+int plato_agg_fedadp_dots_ex(const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64,
+                             int n_pairs, const float* d_base_f32, const int64_t* d_base_i64,
+                             const plato_agg_segment* d_segs, uint32_t n_segs, size_t n_flat, size_t n_f32,
+                             size_t n_i64, float lr, int with_xx, void* d_workspace, float* d_out_xy, float* d_out_yy,
+                             hipStream_t stream, int flags) {
+  if (flags & ~PLATO_AGG_FEDADP_TABLES_READY) return set_error(PLATO_AGG_EINVAL, "unknown fedadp_dots flags");
+  return run_fedadp(d_base_f32 ? kAdpDefault : kAdpDefaultDelta, d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32,
+                    d_base_i64, d_segs, n_segs, n_flat, n_f32, n_i64, lr, with_xx, d_workspace, d_out_xy, d_out_yy,
+                    stream, flags);
 }
 
 #ifdef PLATO_AGG_TUNE  // include/plato_agg_tune.h
@@ -711,7 +722,7 @@ int plato_agg_tune_fedadp_dots(int variant, const float* d_x, const void* const*
                                float* d_out_yy, hipStream_t stream) {
   if (variant < 0 || variant >= kNumAdpVariants) return set_error(PLATO_AGG_EINVAL, "bad fedadp_dots variant");
   return run_fedadp(kAdpVariants[variant], d_x, d_src_f32, d_src_i64, n_pairs, d_base_f32, d_base_i64, d_segs, n_segs, n_flat,
-                    n_f32, n_i64, lr, with_xx, d_workspace, d_out_xy, d_out_yy, stream);
+                    n_f32, n_i64, lr, with_xx, d_workspace, d_out_xy, d_out_yy, stream, 0);
 }
 #endif  // PLATO_AGG_TUNE
 
@@ -721,7 +732,7 @@ namespace {
 int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f32, const void* const* d_src_i64,
                int n_pairs, const float* d_base_f32, const int64_t* d_base_i64, const plato_agg_segment* d_segs,
                uint32_t n_segs, size_t n_flat, size_t n_f32, size_t n_i64, float lr, int with_xx, void* d_workspace,
-               float* d_out_xy, float* d_out_yy, hipStream_t stream) {
+               float* d_out_xy, float* d_out_yy, hipStream_t stream, int flags) {
   if (n_pairs <= 0 || n_pairs > 65535) return set_error(PLATO_AGG_EINVAL, "n_pairs must be in [1, 65535]");
   if (with_xx != 0 && with_xx != 1) return set_error(PLATO_AGG_EINVAL, "with_xx must be 0 or 1");
   if (!d_x || !d_src_f32 || !d_src_i64 || !d_segs || !d_workspace || !d_out_xy || !d_out_yy ||
@@ -770,12 +781,14 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
   a.n_pairs = n_pairs;
   a.with_xx = with_xx;
   if (a.nsteps) {
-    hipLaunchKernelGGL(fedadp_desc_kernel, dim3((2 * a.ngroups + 255) / 256), dim3(256), 0, stream, a);
-    if (int rc = check_launch("fedadp_desc launch")) return rc;
-    hipLaunchKernelGGL(fedadp_rows_kernel, dim3((2 * a.ngroups + 255) / 256), dim3(256), 0, stream, a);
-    if (int rc = check_launch("fedadp_rows launch")) return rc;
-    hipLaunchKernelGGL(fedadp_bndsrc_kernel, dim3(a.max_bnd), dim3(256), 0, stream, a);
-    if (int rc = check_launch("fedadp_bndsrc launch")) return rc;
+    if (!(flags & PLATO_AGG_FEDADP_TABLES_READY)) {  // the layout-only tables (descriptors, rows, sources)
+      hipLaunchKernelGGL(fedadp_desc_kernel, dim3((2 * a.ngroups + 255) / 256), dim3(256), 0, stream, a);
+      if (int rc = check_launch("fedadp_desc launch")) return rc;
+      hipLaunchKernelGGL(fedadp_rows_kernel, dim3((2 * a.ngroups + 255) / 256), dim3(256), 0, stream, a);
+      if (int rc = check_launch("fedadp_rows launch")) return rc;
+      hipLaunchKernelGGL(fedadp_bndsrc_kernel, dim3(a.max_bnd), dim3(256), 0, stream, a);
+      if (int rc = check_launch("fedadp_bndsrc launch")) return rc;
+    }
     hipLaunchKernelGGL(fedadp_boundary_kernel, dim3((a.max_bnd + kBndRows - 1) / kBndRows, uint32_t(n_pairs)),
                        dim3(256), 0, stream, a);
     if (int rc = check_launch("fedadp_boundary launch")) return rc;

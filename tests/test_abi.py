@@ -93,6 +93,8 @@ def test_argument_errors_are_raised_without_gpu_work():
     with pytest.raises(ValueError, match="boundary table"):
         _lib.call("plato_agg_fedadp_dots", a, a, a, 1, a, None, a, (1 << 21) - 1, 1 << 20, 1 << 20, 0, 0.01, 1,
                   a, a, a, None)
+    with pytest.raises(ValueError, match="flags"):  # only PLATO_AGG_FEDADP_TABLES_READY is defined
+        _lib.call("plato_agg_fedadp_dots_ex", a, a, a, 1, a, None, a, 1, 64, 64, 0, 0.01, 1, a, a, a, None, 2)
     from plato_amd.engine import AggregationRound
 
     assert AggregationRound.fedadp_boundary_rows((1 << 21) - 1, 0) >= AggregationRound.FEDADP_MAX_BND

@@ -37,7 +37,7 @@ def test_fedadp_probe_passes_through_the_product_kernel(monkeypatch, lr, align, 
     if deltas:
         assert "plato_agg_compute_deltas" in seen  # the probe's client row was staged as its delta
     # the round's own calls (engine.AggregationRound.fedadp_dots), not a stand-in kernel
-    assert "plato_agg_fedadp_dots" in seen and "plato_agg_sdot_shared" not in seen
+    assert "plato_agg_fedadp_dots_ex" in seen and "plato_agg_sdot_shared" not in seen
 
 
 @pytest.mark.parametrize("threads", [1, 8, 16, 64])

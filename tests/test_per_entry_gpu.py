@@ -470,6 +470,48 @@ def test_polaris_server_matches_reference(engine):
     assert sorted(set(range(1024)) - set(server.unexplored_clients)) == sorted(c for c in G.order_of(recipe))
 
 
+@pytest.mark.parametrize("deltas", [False, True])
+def test_fedadp_layout_tables_reused_across_rounds(deltas):
+    """The second round of one layout and K reuses the workspace's layout-only tables
+    (plato_agg_fedadp_dots_ex, PLATO_AGG_FEDADP_TABLES_READY) and gives the first round's dots bit for bit;
+    another K builds them again; both equal the flatten + sdot path."""
+    from plato_amd import _lib
+
+    recipe = CASES["fedadp_resnet18_k8"]["recipe"]
+    _, base, pays, _, _ = _host(recipe)
+    k = recipe["k"]
+    engine = FedAvgEngine(DEV)
+    engine.layout_align = "fedadp"
+    engine.delta_arenas = deltas
+    seen = []
+    real = _lib.call
+
+    def spy(name, *args):
+        if name == "plato_agg_fedadp_dots_ex":
+            seen.append(args[-1])
+        return real(name, *args)
+
+    got = []
+    for kk in (k, k, k - 3, k - 3):
+        rnd = engine.begin(base, kk)
+        rnd.put_baseline(base)
+        for i in range(kk):
+            rnd.put_client(i, pays[i])
+        w1 = np.tile(np.full(kk, 1.0 / kk), (len(rnd.layout.entries), 1))
+        grads = rnd.launch_entrywise(w1, add_base=False, device=True)
+        _lib.call = spy
+        try:
+            dots = rnd.fedadp_dots(grads, range(kk), 0.01)
+        finally:
+            _lib.call = real
+        want = rnd.fedadp_dots_flat(grads, range(kk), 0.01)
+        assert [np.asarray(d).tobytes() for d in dots] == [np.asarray(d).tobytes() for d in want]
+        got.append([np.asarray(d).tobytes() for d in dots])
+        engine.release_arrivals()
+    assert seen == [0, _lib.PLATO_AGG_FEDADP_TABLES_READY, 0, _lib.PLATO_AGG_FEDADP_TABLES_READY]
+    assert got[0] == got[1] and got[2] == got[3]
+
+
 @pytest.mark.parametrize("align", [None, "fedadp"])
 @pytest.mark.parametrize("name", ["fedadp_lenet5_k6", "fedadp_resnet18_k8"])
 def test_fedadp_dots_tile_shapes_agree_bitwise(name, align):
