@@ -133,7 +133,7 @@ def test_piece_plan_covers_arena_once(n_f32, world, pieces):
     assert pos == n_f32
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_gloo_bench_strong_job_parity(tmp_path, world):
     """bench.py's N > 1 job is ONE FedAvg job: each rank's pieces are slices of the same global inputs, and
     the parity fields the bench reports (compare_windows, ranks_agree) say bit-exact against the whole job."""
