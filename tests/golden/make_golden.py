@@ -206,6 +206,10 @@ def apply_overrides(bf, bi, xs_f, xs_i, overrides):
 
 
 def make_model(name):
+    if name in HF_MODELS:
+        if name not in _HF_BUILT:  # built before boot_reference (see main)
+            _HF_BUILT[name] = HF_MODELS[name]()
+        return _HF_BUILT[name]
     from plato.models import lenet5, resnet
 
     if name == "lenet5":
@@ -215,6 +219,28 @@ def make_model(name):
     if name == "resnet50_200":
         return resnet.Model.get("resnet_50", num_classes=200)
     raise ValueError(name)
+
+
+def _vit_large_hf():
+    """C5's ViT-L/16 classifier as the reference's models/vit.py builds it from HuggingFace
+    (AutoModelForImageClassification; here from its config, offline: random init, the same module
+    and state_dict layout as the installed transformers gives)."""
+    from transformers import ViTConfig, ViTForImageClassification
+
+    return ViTForImageClassification(ViTConfig(hidden_size=1024, num_hidden_layers=24, num_attention_heads=16,
+                                               intermediate_size=4096, image_size=224, patch_size=16, num_labels=10))
+
+
+def _gpt2_medium_hf():
+    """C5's GPT-2-medium as the reference's models/huggingface.py builds it (AutoModelForCausalLM), from its
+    config, offline; its state_dict lists the tied lm_head beside transformer.wte."""
+    from transformers import GPT2Config, GPT2LMHeadModel
+
+    return GPT2LMHeadModel(GPT2Config(n_embd=1024, n_layer=24, n_head=16, n_positions=1024, vocab_size=50257))
+
+
+HF_MODELS = {"vit_large_hf": _vit_large_hf, "gpt2_medium_hf": _gpt2_medium_hf}
+_HF_BUILT: dict = {}
 
 
 def make_updates(num_samples, payloads, order, staleness):
@@ -411,6 +437,15 @@ def run_case(case):
     xs_f = [x[0] for x in xs]
     xs_i = [x[1] for x in xs]
     apply_overrides(bf, bi, xs_f, xs_i, case.get("overrides", []))
+    # tied weights (GPT-2's lm_head = transformer.wte): the model's state_dict holds one storage under both
+    # keys, so a real baseline and real payloads carry equal values there (the baseline is read back from
+    # the server's model after load_weights, where the later key's copy wins)
+    by_name = {n: (r, o, c) for n, r, o, c, _ in entries}
+    for dst, src in case.get("tied", []):
+        (rd, od, nd), (rs, os_, ns_) = by_name[dst], by_name[src]
+        assert rd == rs == "f32" and nd == ns_
+        for arr in [bf, *xs_f]:
+            arr[od:od + nd] = arr[os_:os_ + ns_]
     baseline = unpack(entries, torch.from_numpy(bf), torch.from_numpy(bi))
     payloads = [unpack(entries, torch.from_numpy(xs_f[c]), torch.from_numpy(xs_i[c]))
                 for c in range(k)]
@@ -707,6 +742,11 @@ def cases():
              num_samples=synth.num_samples(5, 31), encrypt_indices=list(range(0, 61706, 97)), full=True),
         dict(name="he_plain_resnet18_k3", model="resnet18", k=3, seed=32, mode="he",
              num_samples=synth.num_samples(3, 32), encrypt_indices=list(range(100, 2000))),
+        # C5: the transformer models at full size, a few clients (the reference's CPU
+        # aggregation of K = 32 would need ~80 GB here); the kernel's arithmetic does not depend on K
+        dict(name="C5_vit_large_hf_k3", model="vit_large_hf", k=3, seed=40, num_samples=synth.num_samples(3, 40)),
+        dict(name="C5_gpt2_medium_hf_k2", model="gpt2_medium_hf", k=2, seed=41,
+             num_samples=synth.num_samples(2, 41), tied=[["transformer.wte.weight", "lm_head.weight"]]),
     ]
 
 
@@ -747,8 +787,8 @@ def run_gan_case(case):
     return out, None
 
 
-def dump_shapes(out_dir):
-    for name in ("lenet5", "resnet18", "resnet50_200"):
+def dump_shapes(out_dir, names=("lenet5", "resnet18", "resnet50_200", "vit_large_hf", "gpt2_medium_hf")):
+    for name in names:
         sd = make_model(name).state_dict()
         spec = [[k, list(v.shape), "f32" if v.dtype == torch.float32 else "i64"] for k, v in sd.items()]
         with open(os.path.join(out_dir, f"shapes_{name}.json"), "w") as f:
@@ -804,6 +844,11 @@ def main():
     ap.add_argument("--only", default=None)
     args = ap.parse_args()
     workdir = tempfile.mkdtemp(prefix="golden_")
+    # transformers' import-time version checks must see the real packages, before boot_reference's stub
+    # finder turns the missing ones into mocks: build the HuggingFace models first
+    for case in cases():
+        if case.get("model") in HF_MODELS and (not args.only or case["name"] == args.only):
+            make_model(case["model"])
     boot_reference(args.reference, workdir)
     os.chdir(workdir)
     if not args.only:
@@ -823,6 +868,8 @@ def main():
     for case in cases():
         if args.only and case["name"] != args.only:
             continue
+        if args.only and case.get("model") in HF_MODELS:
+            dump_shapes(HERE, (case["model"],))
         print("case", case["name"], flush=True)
         runner = {"gan": run_gan_case, "he": run_he_case}.get(case.get("mode"), run_case)
         out, _ = runner(case)

@@ -108,6 +108,9 @@ def model_spec(name):
         "lenet5": lambda: workloads.lenet5(10),
         "resnet18": lambda: workloads.resnet(18, 10),
         "resnet50_200": lambda: workloads.resnet(50, 200),
+        # C5: the layouts of the HuggingFace modules the generator built (shapes_*.json, recorded with the case)
+        "vit_large_hf": lambda: load_shapes("vit_large_hf"),
+        "gpt2_medium_hf": lambda: load_shapes("gpt2_medium_hf"),
     }[name]()
 
 
@@ -119,6 +122,26 @@ def apply_overrides(bf, bi, xs_f, xs_i, overrides):
         else:
             arr = bi if tgt == "base" else xs_i[tgt]
             arr[idx] = np.int64(int(val))
+
+
+def tied_ranges(recipe, layout):
+    """[(dst_offset, src_offset, numel)] of the recipe's tied fp32 entries (``tied``: [[dst, src]] names).
+
+    A model with tied weights (GPT-2's lm_head and transformer.wte) lists both keys in its state_dict
+    over one storage, so the server's baseline and every client's payload hold the same values under
+    both: the generator copies src's values over dst's in the baseline and in every client."""
+    out = []
+    for dst, src in recipe.get("tied", []):
+        d, s = layout[dst], layout[src]
+        assert d.numel == s.numel and d.region == s.region == "f32"
+        out.append((d.offset, s.offset, d.numel))
+    return out
+
+
+def apply_tied(bf, xs_f, ranges):
+    for dst, src, n in ranges:
+        for arr in [bf, *xs_f]:
+            arr[dst:dst + n] = arr[src:src + n]
 
 
 def case_size(recipe):

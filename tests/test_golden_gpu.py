@@ -49,6 +49,9 @@ def _device_inputs(recipe):
         else:
             v = torch.tensor([int(val)], dtype=torch.int64, device=dev)
             (base.i64 if tgt == "base" else slab.i64[tgt])[idx : idx + 1].copy_(v)
+    for dst, src, n in G.tied_ranges(recipe, layout):  # tied weights: one storage under two keys
+        for arr in [base.f32, *slab.f32]:
+            arr[dst:dst + n].copy_(arr[src:src + n])
     torch.cuda.synchronize()
     return layout, base, slab
 

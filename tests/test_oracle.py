@@ -54,6 +54,7 @@ def _inputs(recipe):
     xs_f = [x[0] for x in xs]
     xs_i = [x[1] for x in xs]
     G.apply_overrides(bf, bi, xs_f, xs_i, recipe.get("overrides", []))
+    G.apply_tied(bf, xs_f, G.tied_ranges(recipe, layout))
     if recipe.get("codec") == "bf16":
         xs_f = [ref.bf16_roundtrip(x) for x in xs_f]
         xs_i = [ref.bf16_roundtrip(x) for x in xs_i]
