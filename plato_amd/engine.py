@@ -1213,14 +1213,16 @@ class AggregationRound:
         xy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         yy = torch.empty(k + 1, dtype=torch.float32, device=eng.device)
         # The workspace's layout-only tables (descriptors, boundary rows and their sources) depend on the
-        # segment map alone (cached on the layout beside it): the last workspace is kept on the layout and
-        # the next round of the same shape skips building them (PLATO_AGG_FEDADP_TABLES_READY)
-        ws_key = ("fedadp_ws", tuple(order), k, str(eng.device))
-        held = lay._cache.get("fedadp_ws")
-        if held is not None and held[0] == ws_key:
-            ws, flags = held[1], _lib.PLATO_AGG_FEDADP_TABLES_READY
+        # segment map alone (`segs`, cached on the layout): the engine keeps its last workspace, and its next
+        # round of the same layout and K skips building them (PLATO_AGG_FEDADP_TABLES_READY).  Per engine,
+        # not per layout: an engine runs one round at a time, while several engines (a client-split round's
+        # devices, repeated devices in tests) may reduce the same layout concurrently.
+        ws_key = (id(lay), lay.signature, tuple(order), k, segs.data_ptr())
+        held = getattr(eng, "_fedadp_ws", None)
+        if held is not None and held[0] == ws_key and held[1] is lay:
+            ws, flags = held[2], _lib.PLATO_AGG_FEDADP_TABLES_READY
         else:
-            lay._cache.pop("fedadp_ws", None)  # one workspace per layout (K varies between async rounds)
+            eng._fedadp_ws = None  # one workspace per engine (K varies between async rounds)
             ws = torch.empty(-(-_lib.lib().plato_agg_fedadp_dots_workspace(k, 1, lay.n_i64, n_flat, len(order)) // 4),
                              dtype=torch.float32, device=eng.device)
             flags = 0
@@ -1234,7 +1236,7 @@ class AggregationRound:
                       lay.n_f32, n_i, float(lr), 1, ws.data_ptr(), xy.data_ptr(), yy.data_ptr(), _stream_handle(stream),
                       flags)
         xy_h, yy_h = xy.cpu().numpy(), yy.cpu().numpy()  # stream-ordered D2H (syncs this stream)
-        lay._cache["fedadp_ws"] = (ws_key, ws)  # its tables are built (this stream has passed the call)
+        eng._fedadp_ws = (ws_key, lay, ws)  # its tables are built (this stream has passed the call)
         self._resolve_timers()
         self._keep_flat = (g_flat, ptrs, ws)
         return xy_h[:k], xy_h[k], yy_h[:k]
