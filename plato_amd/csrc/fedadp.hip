@@ -24,7 +24,7 @@
 //     fedadp_boundary_kernel fills per pair before the launch — the same one 16-byte load per
 //     lane, so the stream never waits on a per-position lookup.
 //   * x (the flattened global gradient) and b (the baseline, flattened once per round by
-//     fedadp_prep_kernel) come from one chain-group-major buffer: per (cg, group) the 256 x values
+//     fedadp_prep_span) come from one chain-group-major buffer: per (cg, group) the 256 x values
 //     then the 256 b values — every x or b load of a wave is 1 KiB contiguous and 16-byte aligned.
 //     (Gathered from the arena, b's 16-byte loads start 4-12 bytes off a 16-byte boundary wherever
 //     an entry's arena offset and flat position differ mod 4, half of ResNet-18's elements;
@@ -82,7 +82,7 @@ struct AdpDesc {
 
 struct AdpArgs {
   const float* x;                // flattened global gradient (process_grad(g)), >= nsteps * 64 floats
-  const float* xb;               // [2][ngroups][512]: chain-group-major x and b (fedadp_prep_kernel)
+  const float* xb;               // [2][ngroups][512]: chain-group-major x and b (fedadp_prep_span)
   const float* const* xf;        // client fp32 arenas
   const int64_t* const* xi;      // client int64 arenas
   const float* base_f;
@@ -477,10 +477,9 @@ __global__ __launch_bounds__(256) void fedadp_bndsrc_kernel(AdpArgs a) {
 }
 
 constexpr uint32_t kBndRows = 4;  // boundary rows per workgroup of the per-pair launch
-__global__ __launch_bounds__(256) void fedadp_boundary_kernel(AdpArgs a) {
-  const int pair = int(blockIdx.y);
+__device__ __forceinline__ void fedadp_boundary_rows(const AdpArgs& a, int pair, uint32_t bx) {
   const uint32_t nrows = min(*a.n_bnd, a.max_bnd);
-  const uint32_t row0 = blockIdx.x * kBndRows;
+  const uint32_t row0 = bx * kBndRows;
   if (row0 >= nrows) return;
   const float* xf = sld(a.xf, pair);
   const int64_t* xi = sld(a.xi, pair);
@@ -502,6 +501,9 @@ __global__ __launch_bounds__(256) void fedadp_boundary_kernel(AdpArgs a) {
     a.bnd[(uint64_t(pair) * a.max_bnd + row0 + r) * 256 + threadIdx.x] = val;
   }
 }
+__global__ __launch_bounds__(256) void fedadp_boundary_kernel(AdpArgs a) {
+  fedadp_boundary_rows(a, int(blockIdx.y), blockIdx.x);
+}
 
 // The chain-group-major x / b buffer: xb[cg][grp][0..255] = x at the group's half-block positions
 // (block 8 grp + u, position cg * 32 + v at index u * 32 + v), xb[cg][grp][256..511] = b at the
@@ -510,9 +512,9 @@ __global__ __launch_bounds__(256) void fedadp_boundary_kernel(AdpArgs a) {
 // segments overlapping them (workgroup-uniform), consecutive positions on consecutive lanes:
 // coalesced reads of x and of each entry's baseline run, 128-byte runs of writes.
 constexpr int kPrepSpan = 2048;
-__global__ __launch_bounds__(256) void fedadp_prep_kernel(AdpArgs a, float* xb) {
+__device__ __forceinline__ void fedadp_prep_span(const AdpArgs& a, float* xb, uint32_t span) {
   const uint64_t np = a.nsteps * 64;  // whole blocks only
-  const uint64_t b0 = uint64_t(blockIdx.x) * kPrepSpan;
+  const uint64_t b0 = uint64_t(span) * kPrepSpan;
   const uint64_t b1 = min(b0 + kPrepSpan, np);
   for (uint32_t sidx = adp_find(a.segs, a.n_segs, b0); sidx < a.n_segs; ++sidx) {
     const plato_agg_segment sg = a.segs[sidx];
@@ -525,6 +527,17 @@ __global__ __launch_bounds__(256) void fedadp_prep_kernel(AdpArgs a, float* xb) 
       o[0] = a.x[p];
       if (a.base_f) o[256] = i64 ? 0.f : a.base_f[p - sg.flat_offset + sg.src_offset];  // (delta arenas: no b)
     }
+  }
+}
+// The prep spans and the per-pair boundary rows in one launch (they are independent): the boundary
+// table's ~11 us of dependent loads run beside the prep copy instead of after it (round 6).
+__global__ __launch_bounds__(256) void fedadp_prep_boundary_kernel(AdpArgs a, float* xb, uint32_t n_spans,
+                                                                   uint32_t nbx) {
+  if (blockIdx.x < n_spans) {
+    fedadp_prep_span(a, xb, blockIdx.x);
+  } else {
+    const uint32_t b = blockIdx.x - n_spans;
+    fedadp_boundary_rows(a, int(b / nbx), b % nbx);
   }
 }
 
@@ -789,13 +802,15 @@ int run_fedadp(const AdpLaunch& fn, const float* d_x, const void* const* d_src_f
       hipLaunchKernelGGL(fedadp_bndsrc_kernel, dim3(a.max_bnd), dim3(256), 0, stream, a);
       if (int rc = check_launch("fedadp_bndsrc launch")) return rc;
     }
-    hipLaunchKernelGGL(fedadp_boundary_kernel, dim3((a.max_bnd + kBndRows - 1) / kBndRows, uint32_t(n_pairs)),
-                       dim3(256), 0, stream, a);
-    if (int rc = check_launch("fedadp_boundary launch")) return rc;
-    if (fn.uses_xb) {
-      hipLaunchKernelGGL(fedadp_prep_kernel, dim3(uint32_t((a.nsteps * 64 + kPrepSpan - 1) / kPrepSpan)), dim3(256), 0,
-                         stream, a, reinterpret_cast<float*>(ws + w.xb));
-      if (int rc = check_launch("fedadp_prep launch")) return rc;
+    const uint32_t nbx = (a.max_bnd + kBndRows - 1) / kBndRows;
+    if (fn.uses_xb) {  // the chain-group-major x (and b) and the boundary table, one launch
+      const uint32_t n_spans = uint32_t((a.nsteps * 64 + kPrepSpan - 1) / kPrepSpan);
+      hipLaunchKernelGGL(fedadp_prep_boundary_kernel, dim3(n_spans + nbx * uint32_t(n_pairs)), dim3(256), 0, stream,
+                         a, reinterpret_cast<float*>(ws + w.xb), n_spans, nbx);
+      if (int rc = check_launch("fedadp_prep_boundary launch")) return rc;
+    } else {
+      hipLaunchKernelGGL(fedadp_boundary_kernel, dim3(nbx, uint32_t(n_pairs)), dim3(256), 0, stream, a);
+      if (int rc = check_launch("fedadp_boundary launch")) return rc;
     }
     fn.fn(a, stream);
     if (int rc = check_launch("fedadp_dots launch")) return rc;
