@@ -1550,15 +1550,27 @@ __global__ __launch_bounds__(256) void np_sumsq_tail_kernel(SumsqArgs a) {
   np_chunk<256, kPar>(a, t, xv, bv, sq, leaf_sum);
 }
 
+// One wave per (client, piece): numpy's outer loop adds the inner loops' pairwise sums one after the
+// other (out = ((0 + s_0) + s_1) + ...), a serial chain of dependent adds.  The wave loads 64 chunk sums at
+// a time (one per lane, independent loads) and folds them in order from lane 0 up (readlane: the chain
+// runs on wave-uniform values), instead of one thread walking the chunks with a dependent load per
+// add (up to 288 L2 round trips for ResNet-18's longest entries: ~30 us, round 5).
 __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
-  const uint64_t t = uint64_t(blockIdx.x) * 256 + threadIdx.x;
-  if (t >= uint64_t(a.n_pieces) * uint64_t(a.K)) return;
-  const uint32_t k = uint32_t(t / a.n_pieces), pc = uint32_t(t % a.n_pieces);
+  // wave-uniform task index (the launch checks n_pieces * K < 2^32)
+  const uint32_t t = blockIdx.x * 4u + uint32_t(__builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)));
+  if (t >= a.n_pieces * uint32_t(a.K)) return;
+  const int lane = int(threadIdx.x & 63);
+  const uint32_t k = t / a.n_pieces, pc = t % a.n_pieces;
   const uint32_t c0 = a.first_chunk[pc];
   const uint32_t c1 = pc + 1 < a.n_pieces ? a.first_chunk[pc + 1] : a.n_chunks;
+  const float* sums = a.chunk_sums + uint64_t(k) * a.n_chunks;
   float out = 0.f;  // the reduction's identity, then out += pairwise(chunk) per inner loop
-  for (uint32_t c = c0; c < c1; ++c) out += a.chunk_sums[uint64_t(k) * a.n_chunks + c];
-  a.out[uint64_t(k) * a.n_pieces + pc] = out;
+  for (uint32_t b = c0; b < c1; b += 64) {
+    const uint32_t n = c1 - b < 64u ? c1 - b : 64u;
+    const float v = uint32_t(lane) < n ? sums[b + uint32_t(lane)] : 0.f;
+    for (uint32_t j = 0; j < n; ++j) out = out + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), int(j)));
+  }
+  if (lane == 0) a.out[uint64_t(k) * a.n_pieces + pc] = out;
 }
 
 // variant 0 (the default): four clients of a chunk per workgroup sharing the baseline loads
@@ -1730,7 +1742,8 @@ int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_bas
     if (tail && cur != int(dev)) (void)hipSetDevice(cur);
     if (int rc = check_launch("np_sumsq chunks launch")) return rc;
   }
-  hipLaunchKernelGGL(np_sumsq_pieces_kernel, dim3(uint32_t((t2 + 255) / 256)), dim3(256), 0, stream, a);
+  if (t2 > 0x7fffffffull) return set_error(PLATO_AGG_EINVAL, "too many pieces");
+  hipLaunchKernelGGL(np_sumsq_pieces_kernel, dim3(uint32_t((t2 + 3) / 4)), dim3(256), 0, stream, a);
   return check_launch("np_sumsq pieces launch");
 }
 }  // namespace
