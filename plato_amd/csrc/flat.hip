@@ -36,6 +36,8 @@
 
 using plato_agg_internal::clear_error;
 using plato_agg_internal::set_error;
+using plato_agg_internal::side_stream;
+using plato_agg_internal::SideStream;
 
 namespace {
 
@@ -1566,9 +1568,11 @@ __global__ __launch_bounds__(256) void np_sumsq_pieces_kernel(SumsqArgs a) {
   const float* sums = a.chunk_sums + uint64_t(k) * a.n_chunks;
   float out = 0.f;  // the reduction's identity, then out += pairwise(chunk) per inner loop
   for (uint32_t b = c0; b < c1; b += 64) {
-    const uint32_t n = c1 - b < 64u ? c1 - b : 64u;
-    const float v = uint32_t(lane) < n ? sums[b + uint32_t(lane)] : 0.f;
-    for (uint32_t j = 0; j < n; ++j) out = out + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), int(j)));
+    // lanes past the piece's last chunk hold +0: every sum here is >= +0 (sums of squares, from +0), so
+    // adding +0 leaves its bits as they are, and the fold runs unrolled with constant lane indices
+    const float v = b + uint32_t(lane) < c1 ? sums[b + uint32_t(lane)] : 0.f;
+#pragma unroll
+    for (int j = 0; j < 64; ++j) out = out + __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
   }
   if (lane == 0) a.out[uint64_t(k) * a.n_pieces + pc] = out;
 }
@@ -1637,34 +1641,6 @@ constexpr int kSumsqDefault = 0;  // four clients per workgroup + side-stream pa
 int run_np_sumsq(int variant, const float* const* d_x, int K, const float* d_base, const plato_agg_chunk* d_pieces,
                  const uint32_t* d_first_chunk, uint32_t n_pieces, uint32_t n_chunks, void* d_workspace,
                  float* d_out, hipStream_t stream);
-
-// A second stream per device (created on first use, never destroyed) with a fork / join event pair, so
-// that independent launches of one C-ABI call overlap: fork() makes the side stream wait for everything
-// the caller's stream has enqueued, join() makes the caller's stream wait for the side stream.  The
-// enqueue sequence runs under a per-device lock (the events are reused across calls; a wait captures an
-// event's state when it is enqueued), so concurrent callers stay ordered.
-struct SideStream {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  std::mutex mu;
-};
-SideStream* side_stream(int dev) {
-  static std::mutex mu;
-  static std::map<int, SideStream*> all;
-  std::lock_guard<std::mutex> lk(mu);
-  auto it = all.find(dev);
-  if (it != all.end()) return it->second;
-  auto* ss = new SideStream();  // process lifetime
-  if (hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) != hipSuccess) {
-    delete ss;
-    return nullptr;
-  }
-  all[dev] = ss;
-  return ss;
-}
-
 
 }  // namespace
 
@@ -1922,3 +1898,24 @@ int plato_agg_scale_by_norm(const float* d_a, size_t n, const float* d_norm, flo
 }
 
 }  // extern "C"
+
+namespace plato_agg_internal {
+
+SideStream* side_stream(int dev) {
+  static std::mutex mu;
+  static std::map<int, SideStream*> all;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = all.find(dev);
+  if (it != all.end()) return it->second;
+  auto* ss = new SideStream();  // process lifetime
+  if (hipStreamCreateWithFlags(&ss->s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ss->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ss->join, hipEventDisableTiming) != hipSuccess) {
+    delete ss;
+    return nullptr;
+  }
+  all[dev] = ss;
+  return ss;
+}
+
+}  // namespace plato_agg_internal
