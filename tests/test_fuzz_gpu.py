@@ -170,3 +170,57 @@ def test_bf16_kernel_random_shapes_match_oracle(seed):
     assert bad.size == 0, f"K={k} n_f32={n_f}: {bad.size} mismatches, first at {bad[0]}"
     bad_i = np.nonzero(G.canon(got_i).view(np.uint32) != G.canon(want_i).view(np.uint32))[0]
     assert bad_i.size == 0, f"K={k} n_i64={n_i}: int64-entry mismatches at {bad_i[:5]}"
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_qsgd_kernel_random_layouts_match_oracle(seed):
+    """plato_agg_fedavg_qsgd through the QSGD processor (model_dequantize_qsgd.py:34-60 restated by
+    oracle/qsgd.py) on random layouts (tests/test_fuzz_variants_gpu.py), random quantization levels,
+    every code byte, and per-entry max_v that is negative, zero, subnormal, huge, inf or NaN."""
+    from oracle import qsgd as Q
+    from plato_amd import weights as W
+    from plato_amd.processors.qsgd import Processor
+    from tests.test_fuzz_variants_gpu import _spec
+
+    spec, k = _spec(100 + seed)
+    # the wire header holds each dimension as a big-endian int16 (model_quantize_qsgd.py:130-139)
+    spec = [(n, (8, -(-shape[0] // 8)) if len(shape) == 1 and shape[0] > 32767 else shape, r) for n, shape, r in spec]
+    layout = ArenaLayout.from_shapes(spec)
+    rng = np.random.default_rng(seed)
+    level = int(rng.choice([2, 3, 16, 64, 128, 129]))
+    bf = (rng.standard_normal(layout.n_f32) * 0.05).astype(np.float32)
+    bi = rng.integers(-50, 50, layout.n_i64)
+    baseline = layout.unpack(torch.from_numpy(bf), torch.from_numpy(bi))
+    max_vs = np.array([0.37, 1.0, 2.5, -0.75, 0.0, 1e-45, 3e38, np.inf, np.nan], dtype=np.float32)
+    proc = Processor(quantization_level=level)
+    wires = []
+    for _ in range(k):
+        wires.append({e.name: Q.encode_layer(rng.integers(0, 256, e.numel).astype(np.uint8),
+                                             np.float32(rng.choice(max_vs) if rng.random() < 0.3 else rng.uniform(0.01, 3)),
+                                             e.shape) for e in layout.entries})
+    deq = []
+    for w in wires:
+        vals = {n: Q.decode_layer(b, level).reshape(-1) for n, b in w.items()}
+        parts_f = [vals[e.name] for e in layout.entries if e.region == "f32"]
+        parts_i = [vals[e.name] for e in layout.entries if e.region == "i64"]
+        deq.append((np.concatenate(parts_f) if parts_f else np.zeros(0, np.float32),
+                    np.concatenate(parts_i) if parts_i else np.zeros(0, np.float32)))
+    weights = W.fedavg(list(rng.integers(1, 1000, k)))
+    order = list(rng.permutation(k))
+    engine = FedAvgEngine(DEV)
+    rnd = engine.begin(baseline, k, "qsgd")
+    rnd.put_baseline(baseline)
+    for slot in range(k):
+        rnd.put_client(slot, proc.process(wires[slot]))
+    rnd.launch([weights[i] for i in order], order=order)
+    got = rnd.result()
+    with np.errstate(over="ignore", invalid="ignore"):
+        exp_f, exp_i = ref.fedavg_numpy(bf, bi, [deq[i][0] for i in order], [deq[i][1] for i in order],
+                                        [weights[i] for i in order])
+
+    def flat(sd, region):
+        parts = [sd[e.name].reshape(-1).float() for e in layout.entries if e.region == region]
+        return torch.cat(parts).numpy() if parts else np.zeros(0, np.float32)
+
+    assert G.canon(flat(got, "f32")).tobytes() == G.canon(exp_f).tobytes(), (level, k)
+    assert G.canon(flat(got, "i64")).tobytes() == G.canon(exp_i).tobytes(), (level, k)
