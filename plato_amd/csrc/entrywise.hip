@@ -751,7 +751,7 @@ __device__ __forceinline__ uint64_t pc_ntiles(const Chunk ch) {
 // 1 / 2 = one s_waitcnt per 16- / 32-step block (4 / 8 reads), the next block's reads in flight.  Each
 // ds_read_b128 costs the chain wave ~5 issue cycles and each s_waitcnt ~3.7 beside the 4 of a
 // dependent v_fmac_f32 (scripts/micro/chain_b128.hip, profiles/r04_micro_chain_b128.log).
-template <int T, bool TR, int kOW = 0>
+template <int T, bool TR, int kOW = 0, int kLanes = kNormLanes>
 __device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstride, uint64_t nbar) {
   constexpr int kRT = T, kTS = DTile<T, TR>::kTS;
   const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
@@ -840,7 +840,7 @@ __device__ float pc_chain(const Chunk ch, int lane, const float* dtile, int dstr
 #pragma unroll
         for (int q = 0; q < kCB; ++q) cur[q] = nxt[q];
       }
-    } else if (lane < kNormLanes) {
+    } else if (lane < kLanes) {  // the first and the ragged last tile (kLanes: the lanes that own a chain)
       for (int u = 0; u < kRT / kNormLanes; ++u) {
         const int64_t st = s0 + u;
         if (st >= 0 && st < s_end) {
@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rs_kernel(NormArgs a
 // pairs of one entry have the same tile count).  A ragged last group (K mod C) recomputes client
 // K - 1 in its idle chain waves and does not store it.
 // ---------------------------------------------------------------------------
-template <int T, int P, int D, int C, bool HAS_BASE>
+template <int T, int P, int D, int C, bool HAS_BASE, int kCS = 2 * DTile<T, true>::kSize>
 __device__ void rsc_produce(const NormArgs& a, const Chunk ch, const gf4* const (&xs)[C], int w, int lane,
                             float* dbuf, uint64_t ntiles, uint64_t nbar) {
   constexpr int kTS = DTile<T, true>::kTS, kSize = DTile<T, true>::kSize;
@@ -1070,7 +1070,7 @@ __device__ void rsc_produce(const NormArgs& a, const Chunk ch, const gf4* const 
       wait_vmcnt<(D - 1) * kIt * kOps>();  // tile tt's loads (the later trips stay in flight)
 #pragma unroll
       for (int c = 0; c < C; ++c) {
-        float* dt = dbuf + (2 * c + int(tt & 1)) * kSize;
+        float* dt = dbuf + c * kCS + int(tt & 1) * kSize;  // client c's two-slot ring
 #pragma unroll
         for (int it = 0; it < kIt; ++it) {
           f4 dv = xr[j][it][c];
@@ -1119,6 +1119,58 @@ __global__ __launch_bounds__(64 * (C + P)) void entry_norms_rsc_kernel(NormArgs 
   pc_chain_prio<PRIO>(a, ch);
   const float acc = pc_chain<T, true, kOW>(ch, lane, dbuf + 2 * wave * kSize, kSize, nbar);
   if (i < a.K) pc_finish<HAS_BASE>(a, ch, i, x, lane, acc);
+}
+
+// C clients of one entry in ONE chain wave (round 6): lane l runs chain l & 7 of client (l >> 3) % C
+// (lanes 8 C .. 63 duplicate lanes 0 .. 8 C - 1), over that client's tile ring, so a workgroup holds one
+// chain wave instead of C: the chain waves that share a SIMD's issue halve, and no chain waits at the
+// tile barrier for a second chain wave.  Client rings kCS = 32 (mod 64) floats apart: a ds_read_b128 lane
+// group's rows then fall on 16 different 4-bank slots (the 8 chains of a tile on slots 4 j, the clients
+// 32 banks apart).  The epilogue of client c runs on lane 8 c.
+template <bool HAS_BASE, int C>
+__device__ __forceinline__ void pc_finish_folded(const NormArgs& a, const Chunk ch, int i0, int lane, float acc) {
+  const int cl = (lane >> 3) % C, base = 8 * cl;
+  float s = __shfl(acc, base, 64);
+  for (int l = 1; l < kNormLanes; ++l) s = s + __shfl(acc, base + l, 64);
+  const int i = i0 + cl;
+  if (lane >= 8 * C || (lane & 7) || i >= a.K) return;
+  const uint64_t n = ch.end - ch.begin, m = n - n % kNormLanes;
+  const float* x = sld(a.xf, i);
+  for (uint64_t e = m; e < n; ++e) {
+    const uint64_t idx = ch.begin + e;
+    const float v = HAS_BASE ? x[idx] - a.base_f[idx] : x[idx];
+    s = torch_norm_tail_step(s, v, e, m, n);
+  }
+  if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
+}
+
+template <int T, int P, int D, int C, bool HAS_BASE, int PRIO, int kOW>
+__global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rscf_kernel(NormArgs a) {
+  static_assert(8 * C <= 64, "C clients' chains in one wave");
+  constexpr int kSize = DTile<T, true>::kSize;
+  constexpr int kCS = 2 * kSize + (96 - (2 * kSize) % 64) % 64;  // client stride, = 32 (mod 64)
+  static_assert(kCS % 64 == 32 && kCS % 4 == 0, "client rings 32 banks apart, 16-byte aligned");
+  __shared__ __attribute__((aligned(16))) float dbuf[C * kCS];
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
+  const uint32_t groups = uint32_t((a.K + C - 1) / C);
+  const uint32_t ent = blockIdx.x / groups;  // entry-major over the (longest-first) fp32 table
+  const int i0 = int(blockIdx.x % groups) * C;
+  const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
+  if (uint64_t(ch.end) > (a.n_f32 & ~3ull)) return;  // the arena's partial last float4 group: per-wave launch
+  const uint64_t ntiles = pc_ntiles<T>(ch), nbar = (ntiles + D - 1) / D * D;
+  if (wave >= 1) {
+    __builtin_amdgcn_s_setprio(0);
+    if (!ntiles) return;
+    const gf4* xs[C];
+#pragma unroll
+    for (int c = 0; c < C; ++c) xs[c] = (const gf4*)sld(a.xf, i0 + c < a.K ? i0 + c : a.K - 1);
+    rsc_produce<T, P, D, C, HAS_BASE, kCS>(a, ch, xs, wave - 1, lane, dbuf, ntiles, nbar);
+    return;
+  }
+  const int cl = (lane >> 3) % C;
+  pc_chain_prio<PRIO>(a, ch);
+  const float acc = pc_chain<T, true, kOW, 8 * C>(ch, lane, dbuf + cl * kCS, kSize, nbar);
+  pc_finish_folded<HAS_BASE, C>(a, ch, i0, lane, acc);
 }
 
 bool misaligned(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) != 0; }
@@ -1320,6 +1372,23 @@ void launch_rsc_split(const NormArgs& a, bool hb, dim3, hipStream_t st) {
         else hipLaunchKernelGGL((entry_norms_kernel<false, true>), g2, dim3(kBlock), 0, s, a);
       });
 }
+template <int T, int P, int D, int C, int PRIO = -1, int kOW = 2>
+void launch_rscf_split(const NormArgs& a, bool hb, dim3, hipStream_t st) {
+  const dim3 g1{uint32_t(uint64_t(a.nef) * uint64_t((a.K + C - 1) / C))};
+  const uint64_t waves = (uint64_t(a.nef) + a.nei) * uint64_t(a.K);
+  const dim3 g2{uint32_t((waves + kBlock / 64 - 1) / (kBlock / 64))};
+  launch_beside(
+      st,
+      [&](hipStream_t s) {
+        if (!a.nef) return;
+        if (hb) hipLaunchKernelGGL((entry_norms_rscf_kernel<T, P, D, C, true, PRIO, kOW>), g1, dim3(64 * (1 + P)), 0, s, a);
+        else hipLaunchKernelGGL((entry_norms_rscf_kernel<T, P, D, C, false, PRIO, kOW>), g1, dim3(64 * (1 + P)), 0, s, a);
+      },
+      [&](hipStream_t s) {
+        if (hb) hipLaunchKernelGGL((entry_norms_kernel<true, true>), g2, dim3(kBlock), 0, s, a);
+        else hipLaunchKernelGGL((entry_norms_kernel<false, true>), g2, dim3(kBlock), 0, s, a);
+      });
+}
 #ifdef PLATO_AGG_TUNE
 void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
   const uint64_t threads = (uint64_t(a.nef) + a.nei) * uint64_t(a.K) * 64;  // a wave per pair
@@ -1351,15 +1420,21 @@ void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
 // runs ~10 % slower.  The default picks by K.  Measured and dropped: four clients per workgroup (1.18-1.26
 // at K = 128), three (1.19), and the long entries kept at one client per workgroup (1.18 at K = 128:
 // their ten-wave workgroups crowd the short pairs out; 0.86 at K = 32).
-constexpr int kNormShareK = 96;
+// Round 6: the clients of a workgroup folded into one chain wave (entry_norms_rscf_kernel), interleaved on
+// three leases (profiles/r06zi-zk_norms_fold.log): two clients 1.039 / 1.095 ms against 1.078 / 1.128 for
+// the two-wave form at K = 128 and 0.966 against 1.006 at K = 96; four clients 1.849 against 2.024 at K = 256
+// and 1.393 against 1.49-1.97 at K = 192, but 1.11 at K = 128.  Below K = 96 the one-client shape stays.
+constexpr int kNormShareK = 96, kNormFold4K = 192;
 void launch_norms_default(const NormArgs& a, bool hb, dim3 g, hipStream_t st) {
-  if (a.K >= kNormShareK) launch_rsc_split<2048, 8, 2, 2>(a, hb, g, st);
+  if (a.K >= kNormFold4K) launch_rscf_split<2048, 8, 2, 4>(a, hb, g, st);
+  else if (a.K >= kNormShareK) launch_rscf_split<2048, 8, 2, 2>(a, hb, g, st);
   else launch_rs_split<2048, 4, 2, -1, 2>(a, hb, g, st);
 }
 constexpr NormFn kNormDefault = &launch_norms_default;
 #ifdef PLATO_AGG_TUNE
 const NormFn kNormVariants[] = {
-    &launch_norms_default,         // 0: the default: one client per workgroup below K = 96, two from 96
+    &launch_norms_default,         // 0: the default: one client per workgroup below K = 96, two folded from 96,
+                                   //    four folded from 192
     &launch_rs<2048, 2, 2>,        // 1: 2 producer waves, one launch (the first round-4 default)
     &launch_rs<2048, 2, 3, -2>,    // 2: 3 tiles in flight, the long entries' producers at priority 2
     &launch_pc<1024, 5>,           // 3: LDS-DMA producer / consumer, 1,024-element tiles (round 3, > 6,144 pairs)
@@ -1372,10 +1447,17 @@ const NormFn kNormVariants[] = {
                                           //    in flight, the per-wave pairs (int64, partial last group) in a
                                           //    second launch, one s_waitcnt per 32 chain steps): the default below
                                           //    K = 96, rounds 4-5's default at every K
-    &launch_rsc_split<2048, 8, 2, 2>,     // 9: two clients per workgroup, 8 producer waves: the default from K = 96
+    &launch_rsc_split<2048, 8, 2, 2>,     // 9: two clients per workgroup (two chain waves), 8 producer waves: round
+                                          //    5's default from K = 96
     &launch_rsc_split<2048, 4, 2, 2>,     // 10: two clients, 4 producer waves
     &launch_rsc_split<2048, 8, 3, 2>,     // 11: two clients, 3 tiles of loads in flight
     &launch_rsc_split<2048, 8, 2, 4>,     // 12: four clients, 8 producer waves
+    // round 6: the clients of a workgroup folded into one chain wave (entry_norms_rscf_kernel)
+    &launch_rscf_split<2048, 8, 2, 2>,    // 13: two clients, 8 producer waves: the default from K = 96
+    &launch_rscf_split<2048, 4, 2, 2>,    // 14: two clients, 4 producer waves
+    &launch_rscf_split<2048, 8, 2, 4>,    // 15: four clients, 8 producer waves: the default from K = 192
+    &launch_rscf_split<2048, 4, 2, 4>,    // 16: four clients, 4 producer waves
+    &launch_rscf_split<2048, 8, 3, 2>,    // 17: two clients, 8 producer waves, 3 tiles in flight
 };
 constexpr int kNumNormVariants = sizeof(kNormVariants) / sizeof(kNormVariants[0]);
 #endif

@@ -168,10 +168,11 @@ def test_entry_norm_kernels_agree_bitwise(engine, k, deltas):
             assert outs[0][:, e_i].tobytes() == ref.torch_cpu_norm_f32(np.ascontiguousarray(rows)).tobytes(), e.name
 
 
-@pytest.mark.parametrize("k,deltas", [(96, False), (97, False), (129, True)])
+@pytest.mark.parametrize("k,deltas", [(96, False), (97, False), (129, True), (193, False), (255, True)])
 def test_entry_norms_default_from_k96_matches_oracle(engine, k, deltas):
     """The product entry point at K >= 96 (two clients of one entry per workgroup sharing the baseline
-    tiles; an odd K leaves a one-client last group) == torch CPU order, both arena tails."""
+    tiles, four from K = 192, in one chain wave; a ragged K leaves a partial last group) == torch CPU
+    order, both arena tails."""
     from plato_amd import _lib
 
     for spec in (RING_SPEC, RING_SPEC[:-1] + [("z", (12291,), "f32")]):
