@@ -1457,7 +1457,9 @@ const NormFn kNormVariants[] = {
     &launch_rscf_split<2048, 4, 2, 2>,    // 14: two clients, 4 producer waves
     &launch_rscf_split<2048, 8, 2, 4>,    // 15: four clients, 8 producer waves: the default from K = 192
     &launch_rscf_split<2048, 4, 2, 4>,    // 16: four clients, 4 producer waves
-    &launch_rscf_split<2048, 8, 3, 2>,    // 17: two clients, 8 producer waves, 3 tiles in flight
+    // measured and dropped (K = 128, interleaved, profiles/r06zm_norms_fold_shapes.log, against 1.110 for the
+    // default): two clients with 3 tiles in flight 1.152, 4,096-element tiles 1.895, three clients 1.166,
+    // 1,024-element tiles 1.282 ms
 };
 constexpr int kNumNormVariants = sizeof(kNormVariants) / sizeof(kNormVariants[0]);
 #endif
