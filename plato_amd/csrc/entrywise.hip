@@ -1144,7 +1144,10 @@ __device__ __forceinline__ void pc_finish_folded(const NormArgs& a, const Chunk 
   if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
 }
 
-template <int T, int P, int D, int C, bool HAS_BASE, int PRIO, int kOW>
+// kSpread > 1: dispatched workgroup b runs grid item (b % kSpread) * ceil(G / kSpread) + b / kSpread, so
+// consecutive dispatches take items a kSpread-th of the (longest-first) grid apart and the long entries'
+// workgroups are not dispatched back to back onto one CU's free slots (items >= G: padding, exit).
+template <int T, int P, int D, int C, bool HAS_BASE, int PRIO, int kOW, int kSpread = 1>
 __global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rscf_kernel(NormArgs a) {
   static_assert(8 * C <= 64, "C clients' chains in one wave");
   constexpr int kSize = DTile<T, true>::kSize;
@@ -1153,8 +1156,14 @@ __global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rscf_kernel(NormArgs
   __shared__ __attribute__((aligned(16))) float dbuf[C * kCS];
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const uint32_t groups = uint32_t((a.K + C - 1) / C);
-  const uint32_t ent = blockIdx.x / groups;  // entry-major over the (longest-first) fp32 table
-  const int i0 = int(blockIdx.x % groups) * C;
+  uint32_t item = blockIdx.x;
+  if constexpr (kSpread > 1) {
+    const uint32_t g = a.nef * groups, per = (g + kSpread - 1) / kSpread;
+    item = (blockIdx.x % kSpread) * per + blockIdx.x / kSpread;
+    if (item >= g) return;  // padding (before any barrier)
+  }
+  const uint32_t ent = item / groups;  // entry-major over the (longest-first) fp32 table
+  const int i0 = int(item % groups) * C;
   const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
   if (uint64_t(ch.end) > (a.n_f32 & ~3ull)) return;  // the arena's partial last float4 group: per-wave launch
   const uint64_t ntiles = pc_ntiles<T>(ch), nbar = (ntiles + D - 1) / D * D;
@@ -1372,17 +1381,18 @@ void launch_rsc_split(const NormArgs& a, bool hb, dim3, hipStream_t st) {
         else hipLaunchKernelGGL((entry_norms_kernel<false, true>), g2, dim3(kBlock), 0, s, a);
       });
 }
-template <int T, int P, int D, int C, int PRIO = -1, int kOW = 2>
+template <int T, int P, int D, int C, int PRIO = -1, int kOW = 2, int kSpread = 1>
 void launch_rscf_split(const NormArgs& a, bool hb, dim3, hipStream_t st) {
-  const dim3 g1{uint32_t(uint64_t(a.nef) * uint64_t((a.K + C - 1) / C))};
+  const uint64_t items = uint64_t(a.nef) * uint64_t((a.K + C - 1) / C);
+  const dim3 g1{uint32_t((items + kSpread - 1) / kSpread * kSpread)};
   const uint64_t waves = (uint64_t(a.nef) + a.nei) * uint64_t(a.K);
   const dim3 g2{uint32_t((waves + kBlock / 64 - 1) / (kBlock / 64))};
   launch_beside(
       st,
       [&](hipStream_t s) {
         if (!a.nef) return;
-        if (hb) hipLaunchKernelGGL((entry_norms_rscf_kernel<T, P, D, C, true, PRIO, kOW>), g1, dim3(64 * (1 + P)), 0, s, a);
-        else hipLaunchKernelGGL((entry_norms_rscf_kernel<T, P, D, C, false, PRIO, kOW>), g1, dim3(64 * (1 + P)), 0, s, a);
+        if (hb) hipLaunchKernelGGL((entry_norms_rscf_kernel<T, P, D, C, true, PRIO, kOW, kSpread>), g1, dim3(64 * (1 + P)), 0, s, a);
+        else hipLaunchKernelGGL((entry_norms_rscf_kernel<T, P, D, C, false, PRIO, kOW, kSpread>), g1, dim3(64 * (1 + P)), 0, s, a);
       },
       [&](hipStream_t s) {
         if (hb) hipLaunchKernelGGL((entry_norms_kernel<true, true>), g2, dim3(kBlock), 0, s, a);
@@ -1421,10 +1431,13 @@ void launch_per_wave(const NormArgs& a, bool hb, dim3, hipStream_t st) {
 // at K = 128), three (1.19), and the long entries kept at one client per workgroup (1.18 at K = 128:
 // their ten-wave workgroups crowd the short pairs out; 0.86 at K = 32).
 // Round 6: the clients of a workgroup folded into one chain wave (entry_norms_rscf_kernel), interleaved on
-// three leases (profiles/r06zi-zk_norms_fold.log): two clients 1.039 / 1.095 ms against 1.078 / 1.128 for
-// the two-wave form at K = 128 and 0.966 against 1.006 at K = 96; four clients 1.849 against 2.024 at K = 256
-// and 1.393 against 1.49-1.97 at K = 192, but 1.11 at K = 128.  Below K = 96 the one-client shape stays.
-constexpr int kNormShareK = 96, kNormFold4K = 192;
+// five leases (profiles/r06zi-zk_norms_fold.log, r06zm, r06zp, r06zq): two clients 0.95-0.97 ms against 1.006
+// for the two-wave form at K = 96; at K = 128 every two-client form runs in two modes from launch to launch
+// (samples ~1.03 or ~1.25 ms; medians 1.04-1.26 for both forms), while four clients hold 1.10-1.12 on every
+// lease — the better expected time, and four clients win outright at K = 192 (1.393 against 1.49-1.97) and
+// 256 (1.849 against 2.024).  At K = 112 four clients 1.059 against 1.042 (two-client samples to 1.23).
+// Below K = 96 the one-client shape stays (four clients 0.962, two 0.902 against 0.894 ms at K = 64).
+constexpr int kNormShareK = 96, kNormFold4K = 128;
 void launch_norms_default(const NormArgs& a, bool hb, dim3 g, hipStream_t st) {
   if (a.K >= kNormFold4K) launch_rscf_split<2048, 8, 2, 4>(a, hb, g, st);
   else if (a.K >= kNormShareK) launch_rscf_split<2048, 8, 2, 2>(a, hb, g, st);
@@ -1434,7 +1447,7 @@ constexpr NormFn kNormDefault = &launch_norms_default;
 #ifdef PLATO_AGG_TUNE
 const NormFn kNormVariants[] = {
     &launch_norms_default,         // 0: the default: one client per workgroup below K = 96, two folded from 96,
-                                   //    four folded from 192
+                                   //    four folded from 128
     &launch_rs<2048, 2, 2>,        // 1: 2 producer waves, one launch (the first round-4 default)
     &launch_rs<2048, 2, 3, -2>,    // 2: 3 tiles in flight, the long entries' producers at priority 2
     &launch_pc<1024, 5>,           // 3: LDS-DMA producer / consumer, 1,024-element tiles (round 3, > 6,144 pairs)
@@ -1453,13 +1466,15 @@ const NormFn kNormVariants[] = {
     &launch_rsc_split<2048, 8, 3, 2>,     // 11: two clients, 3 tiles of loads in flight
     &launch_rsc_split<2048, 8, 2, 4>,     // 12: four clients, 8 producer waves
     // round 6: the clients of a workgroup folded into one chain wave (entry_norms_rscf_kernel)
-    &launch_rscf_split<2048, 8, 2, 2>,    // 13: two clients, 8 producer waves: the default from K = 96
+    &launch_rscf_split<2048, 8, 2, 2>,    // 13: two clients, 8 producer waves: the default for K = 96 .. 127
     &launch_rscf_split<2048, 4, 2, 2>,    // 14: two clients, 4 producer waves
-    &launch_rscf_split<2048, 8, 2, 4>,    // 15: four clients, 8 producer waves: the default from K = 192
+    &launch_rscf_split<2048, 8, 2, 4>,    // 15: four clients, 8 producer waves: the default from K = 128
     &launch_rscf_split<2048, 4, 2, 4>,    // 16: four clients, 4 producer waves
     // measured and dropped (K = 128, interleaved, profiles/r06zm_norms_fold_shapes.log, against 1.110 for the
     // default): two clients with 3 tiles in flight 1.152, 4,096-element tiles 1.895, three clients 1.166,
-    // 1,024-element tiles 1.282 ms
+    // 1,024-element tiles 1.282 ms; the dispatch order spread by 4 / 8 (consecutive workgroups a quarter /
+    // an eighth of the grid apart: the long entries start late) 3.11 / 5.69 ms, four clients spread by 4
+    // 2.39 ms (profiles/r06zp_norms_spread.log)
 };
 constexpr int kNumNormVariants = sizeof(kNormVariants) / sizeof(kNormVariants[0]);
 #endif
