@@ -1144,10 +1144,7 @@ __device__ __forceinline__ void pc_finish_folded(const NormArgs& a, const Chunk 
   if (ch.entry < a.n_entries) a.out[uint64_t(i) * a.n_entries + ch.entry] = sqrtf(s);
 }
 
-// kSpread > 1: dispatched workgroup b runs grid item (b % kSpread) * ceil(G / kSpread) + b / kSpread, so
-// consecutive dispatches take items a kSpread-th of the (longest-first) grid apart and the long entries'
-// workgroups are not dispatched back to back onto one CU's free slots (items >= G: padding, exit).
-template <int T, int P, int D, int C, bool HAS_BASE, int PRIO, int kOW, int kSpread = 1>
+template <int T, int P, int D, int C, bool HAS_BASE, int PRIO, int kOW>
 __global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rscf_kernel(NormArgs a) {
   static_assert(8 * C <= 64, "C clients' chains in one wave");
   constexpr int kSize = DTile<T, true>::kSize;
@@ -1156,14 +1153,8 @@ __global__ __launch_bounds__(64 * (1 + P)) void entry_norms_rscf_kernel(NormArgs
   __shared__ __attribute__((aligned(16))) float dbuf[C * kCS];
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6)), lane = threadIdx.x & 63;
   const uint32_t groups = uint32_t((a.K + C - 1) / C);
-  uint32_t item = blockIdx.x;
-  if constexpr (kSpread > 1) {
-    const uint32_t g = a.nef * groups, per = (g + kSpread - 1) / kSpread;
-    item = (blockIdx.x % kSpread) * per + blockIdx.x / kSpread;
-    if (item >= g) return;  // padding (before any barrier)
-  }
-  const uint32_t ent = item / groups;  // entry-major over the (longest-first) fp32 table
-  const int i0 = int(item % groups) * C;
+  const uint32_t ent = blockIdx.x / groups;  // entry-major over the (longest-first) fp32 table
+  const int i0 = int(blockIdx.x % groups) * C;
   const Chunk ch = load_chunk(a.ef, ent, a.n_f32);
   if (uint64_t(ch.end) > (a.n_f32 & ~3ull)) return;  // the arena's partial last float4 group: per-wave launch
   const uint64_t ntiles = pc_ntiles<T>(ch), nbar = (ntiles + D - 1) / D * D;
@@ -1381,18 +1372,17 @@ void launch_rsc_split(const NormArgs& a, bool hb, dim3, hipStream_t st) {
         else hipLaunchKernelGGL((entry_norms_kernel<false, true>), g2, dim3(kBlock), 0, s, a);
       });
 }
-template <int T, int P, int D, int C, int PRIO = -1, int kOW = 2, int kSpread = 1>
+template <int T, int P, int D, int C, int PRIO = -1, int kOW = 2>
 void launch_rscf_split(const NormArgs& a, bool hb, dim3, hipStream_t st) {
-  const uint64_t items = uint64_t(a.nef) * uint64_t((a.K + C - 1) / C);
-  const dim3 g1{uint32_t((items + kSpread - 1) / kSpread * kSpread)};
+  const dim3 g1{uint32_t(uint64_t(a.nef) * uint64_t((a.K + C - 1) / C))};
   const uint64_t waves = (uint64_t(a.nef) + a.nei) * uint64_t(a.K);
   const dim3 g2{uint32_t((waves + kBlock / 64 - 1) / (kBlock / 64))};
   launch_beside(
       st,
       [&](hipStream_t s) {
         if (!a.nef) return;
-        if (hb) hipLaunchKernelGGL((entry_norms_rscf_kernel<T, P, D, C, true, PRIO, kOW, kSpread>), g1, dim3(64 * (1 + P)), 0, s, a);
-        else hipLaunchKernelGGL((entry_norms_rscf_kernel<T, P, D, C, false, PRIO, kOW, kSpread>), g1, dim3(64 * (1 + P)), 0, s, a);
+        if (hb) hipLaunchKernelGGL((entry_norms_rscf_kernel<T, P, D, C, true, PRIO, kOW>), g1, dim3(64 * (1 + P)), 0, s, a);
+        else hipLaunchKernelGGL((entry_norms_rscf_kernel<T, P, D, C, false, PRIO, kOW>), g1, dim3(64 * (1 + P)), 0, s, a);
       },
       [&](hipStream_t s) {
         if (hb) hipLaunchKernelGGL((entry_norms_kernel<true, true>), g2, dim3(kBlock), 0, s, a);
@@ -1472,9 +1462,9 @@ const NormFn kNormVariants[] = {
     &launch_rscf_split<2048, 4, 2, 4>,    // 16: four clients, 4 producer waves
     // measured and dropped (K = 128, interleaved, profiles/r06zm_norms_fold_shapes.log, against 1.110 for the
     // default): two clients with 3 tiles in flight 1.152, 4,096-element tiles 1.895, three clients 1.166,
-    // 1,024-element tiles 1.282 ms; the dispatch order spread by 4 / 8 (consecutive workgroups a quarter /
-    // an eighth of the grid apart: the long entries start late) 3.11 / 5.69 ms, four clients spread by 4
-    // 2.39 ms (profiles/r06zp_norms_spread.log)
+    // 1,024-element tiles 1.282 ms; the dispatch order spread by 4 / 8 (dispatched workgroup b running
+    // grid item (b mod 4) ceil(G / 4) + b / 4: the long entries start late) 3.11 / 5.69 ms, four clients
+    // spread by 4 2.39 ms (profiles/r06zp_norms_spread.log)
 };
 constexpr int kNumNormVariants = sizeof(kNormVariants) / sizeof(kNormVariants[0]);
 #endif
